@@ -1,0 +1,168 @@
+#!/usr/bin/env python3
+"""Benchmark: FVENS second-order residual sweep (FlowFV::compute_residual with local time steps)
+on MI355X, Mfaces/s and achieved HBM GB/s of the dominant kernel.
+
+Workload (BASELINE.json north_star target): the C4 mesh of SURVEY.md 8(d) — NACA0012 hybrid O-grid,
+Ntheta = 2048, 256 quad + 864 triangle-split layers = 4,063,232 cells, 6,359,040 faces — with
+Roe flux + weighted-least-squares gradients + MUSCL/Van Albada reconstruction, M 0.8, 1.25 deg.
+One step = one full residual evaluation (primitive conversion, BC ghosts, WLS gradients, fused
+reconstruction/flux/scatter/time-step sweep) with the state resident in HBM.
+Multi-GPU: one process per GPU; each rank sweeps its own C4-size mesh (weak scaling, no data-path
+collective yet: the partitioned halo-exchange path is not built in this round — DESIGN.md).
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, "tests"))
+
+HBM_PEAK_GBS = 8000.0   # MI355X HBM3E spec (MI355X_MICROARCH.md)
+
+
+def c4_mesh(fa, scale):
+    nt = 2048 // scale
+    nq = 256 // scale
+    ntri = 864 // scale
+    return fa.UMesh.naca_ogrid(nt, nq, ntri, 20.0, 1e-5), dict(ntheta=nt, nquad=nq, ntri=ntri)
+
+
+def sweep_algorithmic_bytes(N, F, Fb):
+    """32 B/face (L,R 8 + nx,ny,len 24) + 144 B/cell (prim 32 + grad 64 + centre 16
+    + residual write 32) + 48 B/boundary face (ghost centre 16 + ghost state 32) + 16 B/cell for the
+    time step (area read 8 + dtm write 8)."""
+    return 32 * F + 144 * N + 48 * Fb + 16 * N
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--scale", type=int, default=1, help="divide the C4 mesh dimensions (debug)")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-sweeps", type=int, default=3)
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    import torch
+    if world > 1:
+        import torch.distributed as dist
+        torch.cuda.set_device(local_rank)
+        dist.init_process_group("nccl", init_method="env://")
+    else:
+        dist = None
+        torch.cuda.set_device(0)
+
+    import fvens_amd as fa
+    import cases
+
+    t0 = time.time()
+    mesh, dims = c4_mesh(fa, args.scale)
+    p = cases.physics("naca")
+    n = cases.numerics("ROE", "LEASTSQUARES", "VANALBADA")
+    u = cases.state(mesh, p, seed=42)
+    sp = fa.FlowFV(mesh, p, n, device=torch.cuda.current_device())
+    perm = sp.permutation()
+    t_setup = time.time() - t0
+
+    N, F, Fb = mesh.nelem, mesh.naface, mesh.nbface
+    du = torch.tensor(u[perm], device="cuda")
+    dr = torch.empty((N, 4), dtype=torch.float64, device="cuda")
+    ddt = torch.empty(N, dtype=torch.float64, device="cuda")
+    torch.cuda.synchronize()
+
+    def step():
+        sp.compute_residual_device(du.data_ptr(), dr.data_ptr(), ddt.data_ptr(), True, True)
+
+    for _ in range(args.warmup):
+        step()
+    sp.synchronize()
+
+    def barrier():
+        if dist is not None:
+            dist.barrier()
+        torch.cuda.synchronize()
+        sp.synchronize()
+
+    barrier()
+    t1 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    sp.synchronize()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t1
+    if dist is not None:
+        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+        dist.barrier()
+    ms_per_step = 1e3 * elapsed / args.steps
+
+    # per-kernel durations with HIP events on the library's stream (separate pass)
+    sp.profile(True)
+    for _ in range(args.steps):
+        step()
+    kt = sp.kernel_times()
+    sp.profile(False)
+    sweep_name = [k for k in kt if k.startswith("k_sweep")]
+    sweep_ms = kt[sweep_name[0]][0] / kt[sweep_name[0]][1] if sweep_name else float("nan")
+    kernels_ms = {k: v[0] / v[1] for k, v in kt.items()}
+
+    ab = sweep_algorithmic_bytes(N, F, Fb)
+    achieved = ab / (sweep_ms * 1e-3) / 1e9
+    value = world * F / (ms_per_step * 1e-3) / 1e6
+
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        import _oracle as orc
+        om = orc.OracleMesh.from_raw(mesh.raw())
+        ref = orc.OracleSpatial(om, p, n)
+        secs = ref.time_residual(np.ascontiguousarray(u), args.cpu_sweeps, True)
+        cpu = {"value": F / secs / 1e6, "unit": "Mfaces/s", "cores": 1, "kind": "port",
+               "sample": f"{args.cpu_sweeps} full second-order residual sweeps (+1 warm-up) of the same "
+                         f"{N}-cell mesh and state by the single-threaded C++ restatement "
+                         f"(oracle/, -O2, no FMA): {secs:.3f} s per sweep"}
+        del ref, om
+
+    if rank == 0:
+        stats = sp.layout_stats()
+        out = {
+            "metric": "Mfaces/s (flux+residual sweep) + achieved HBM GB/s, 1/2/4/8 MI355X",
+            "value": round(value, 3),
+            "unit": "Mfaces/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(ms_per_step, 5),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "f64",
+            "data": "synthetic (generated C4 NACA0012 hybrid O-grid; seeded perturbed free stream)",
+            "config": {"workload": "C4 mesh, Roe + WLS gradients + MUSCL/Van Albada, 2nd-order residual "
+                                   "sweep with local time steps (explicit pseudo-time step)",
+                       "cells": N, "faces": F, "boundary_faces": Fb, **dims,
+                       "parallelism": f"replicas x{world}" if world > 1 else "single GPU",
+                       "layout": stats, "setup_s": round(t_setup, 2)},
+            "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
+                         "kernel": sweep_name[0] if sweep_name else None,
+                         "kernel_ms": round(sweep_ms, 5), "algorithmic_bytes": ab},
+            "kernels_ms": {k: round(v, 5) for k, v in kernels_ms.items()},
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(out))
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

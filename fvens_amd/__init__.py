@@ -1,0 +1,261 @@
+"""fvens_amd: MI355X-native FVENS face-flux / residual sweep.
+
+Host-side mirror of the reference's operator interface for the hot path (paths relative to
+/root/reference/src):
+
+  FlowPhysicsConfig / FlowNumericsConfig / FlowBCConfig   spatial/flow_spatial.hpp:33-55, abc.hpp
+  create_flow_spatial(mesh, pconf, nconf)                 utilities/afactory.cpp:251-276
+  FlowFV.compute_residual(u, r, gettimesteps, dtm)        spatial/flow_spatial.cpp:636-816
+  FlowFV.getGradients(u)                                  spatial/flow_spatial.cpp:95-112
+  UMesh (Gmsh-2 reader + face-indexing contract)          mesh/meshreaders.cpp, mesh/mesh.cpp
+
+Every call goes through libfvhip.so (include/fvhip.h); there is no CPU fallback.
+"""
+from dataclasses import dataclass, field
+import ctypes
+from typing import List, Optional
+
+import numpy as np
+
+from . import _ffi
+from ._ffi import check, dptr, iptr
+
+# string tables mirror the reference factories (upper-cased control-file strings)
+FLUXES = {"LLF": 0, "VANLEER": 1, "AUSM": 2, "AUSMPLUS": 3, "ROE": 4, "HLL": 5, "HLLC": 6}
+GRADIENTS = {"NONE": 0, "ZERO": 0, "GREENGAUSS": 1, "LEASTSQUARES": 2}
+RECONSTRUCTIONS = {"NONE": 0, "WENO": 1, "VANALBADA": 2, "BARTHJESPERSEN": 3, "VENKATAKRISHNAN": 4}
+BCTYPES = {"slipwall": 0, "farfield": 1, "inflowoutflow": 2, "subsonic_inflow": 3, "extrapolation": 4,
+           "periodic": 5, "isothermalwall": 6, "adiabaticwall": 7}
+
+
+@dataclass
+class FlowBCConfig:
+    """FlowBCConfig (spatial/abc.hpp): bc_type string as in bcTypeMap (abctypemap.cpp:14-28)"""
+    bc_type: str
+    bc_tag: int
+    bc_vals: List[float] = field(default_factory=list)
+
+
+@dataclass
+class FlowPhysicsConfig:
+    """spatial/flow_spatial.hpp:33-44. Inviscid runs use Tinf=298, Reinf=inf, Pr=nan like
+    controlparser.cpp:133-138."""
+    gamma: float = 1.4
+    Minf: float = 0.5
+    Tinf: float = 298.0
+    Reinf: float = float("inf")
+    Pr: float = float("nan")
+    aoa: float = 0.0            # radians
+    viscous_sim: bool = False
+    const_visc: bool = False
+    bcconf: List[FlowBCConfig] = field(default_factory=list)
+
+
+@dataclass
+class FlowNumericsConfig:
+    """spatial/flow_spatial.hpp:47-55 (limiter_param must be given: the reference never parses it)"""
+    conv_numflux: str = "ROE"
+    conv_numflux_jac: str = "ROE"
+    gradientscheme: str = "LEASTSQUARES"
+    reconstruction: str = "VANALBADA"
+    limiter_param: float = 20.0
+    order2: bool = True
+
+
+class UMesh:
+    """Reference-indexed mesh built natively (mesh/mesh.hpp accessors as numpy arrays)."""
+
+    def __init__(self, handle):
+        self._h = ctypes.c_void_p(handle)
+        v = _ffi.FvMeshView()
+        check(_ffi.lib().fvmesh_view(self._h, ctypes.byref(v)))
+        self.view = v
+        self.nelem, self.npoin, self.nbface = v.nelem, v.npoin, v.nbface
+        self.naface, self.nconnface, self.maxnnode = v.naface, v.nconnface, v.maxnnode
+        self.maxnfael, self.nbtag = v.maxnfael, v.nbtag
+        self.ninface = self.naface - self.nbface - self.nconnface
+
+        def arr(p, n, dt):
+            return np.ctypeslib.as_array(p, shape=(n,)).astype(dt, copy=True)
+        N, F, nb = self.nelem, self.naface, self.nbface
+        self.coords = arr(v.coords, 2 * self.npoin, np.float64).reshape(-1, 2)
+        self.inpoel = arr(v.inpoel, N * self.maxnnode, np.int32).reshape(N, -1)
+        self.nnode = arr(v.nnode, N, np.int32)
+        self.esuel = arr(v.esuel, N * self.maxnfael, np.int32).reshape(N, -1)
+        self.elemface = arr(v.elemface, N * self.maxnfael, np.int32).reshape(N, -1)
+        self.intfac = arr(v.intfac, 4 * F, np.int32).reshape(F, 4)
+        self.btags = arr(v.btags, nb * self.nbtag, np.int32).reshape(nb, -1)
+        self.facemetric = arr(v.facemetric, 3 * F, np.float64).reshape(F, 3)
+        self.area = arr(v.area, N, np.float64)
+        self.rc = arr(v.rc, 2 * (N + self.nconnface), np.float64).reshape(-1, 2)
+        self.rcbp = arr(v.rcbp, 2 * nb, np.float64).reshape(-1, 2)
+        self.gr = arr(v.gr, 2 * F, np.float64).reshape(F, 2)
+
+    @classmethod
+    def read_gmsh(cls, path):
+        h = ctypes.c_void_p()
+        check(_ffi.lib().fvmesh_read_gmsh(str(path).encode(), ctypes.byref(h)))
+        return cls(h.value)
+
+    @classmethod
+    def naca_ogrid(cls, ntheta, nquad, ntri, rfar=20.0, wallspacing=1e-4):
+        h = ctypes.c_void_p()
+        check(_ffi.lib().fvmesh_generate(0, ntheta, nquad, ntri, rfar, wallspacing, 0.0, ctypes.byref(h)))
+        return cls(h.value)
+
+    @classmethod
+    def cylinder_ogrid(cls, ntheta, nr, r0=0.5, r1=20.0):
+        h = ctypes.c_void_p()
+        check(_ffi.lib().fvmesh_generate(1, ntheta, nr, 0, r0, r1, 0.0, ctypes.byref(h)))
+        return cls(h.value)
+
+    @classmethod
+    def flat_plate(cls, nx, ny, xlead=0.25, height=0.5, wallspacing=1e-4):
+        h = ctypes.c_void_p()
+        check(_ffi.lib().fvmesh_generate(2, nx, ny, 0, xlead, height, wallspacing, ctypes.byref(h)))
+        return cls(h.value)
+
+    def raw(self):
+        """Pre-topology arrays (as read/generated): coords, inpoel, nnode, bface, nbtag"""
+        info = np.zeros(5, np.int32)
+        check(_ffi.lib().fvmesh_raw_info(self._h, iptr(info)))
+        npoin, nelem, maxnnode, nbface, nbtag = [int(x) for x in info]
+        coords = np.zeros(2 * npoin)
+        inpoel = np.zeros(nelem * maxnnode, np.int32)
+        nnode = np.zeros(nelem, np.int32)
+        bface = np.zeros(nbface * (2 + nbtag), np.int32)
+        check(_ffi.lib().fvmesh_raw_arrays(self._h, dptr(coords), iptr(inpoel), iptr(nnode), iptr(bface)))
+        return dict(npoin=npoin, nelem=nelem, maxnnode=maxnnode, nbface=nbface, nbtag=nbtag,
+                    coords=coords, inpoel=inpoel, nnode=nnode, bface=bface)
+
+    def write_gmsh(self, path):
+        check(_ffi.lib().fvmesh_write_gmsh(self._h, str(path).encode()))
+
+    def __del__(self):
+        try:
+            if self._h:
+                _ffi.lib().fvmesh_destroy(self._h)
+                self._h = None
+        except Exception:
+            pass
+
+
+def _config_struct(pconf: FlowPhysicsConfig, nconf: FlowNumericsConfig):
+    n = len(pconf.bcconf)
+    types = np.array([BCTYPES[b.bc_type.lower()] for b in pconf.bcconf], np.int32)
+    tags = np.array([b.bc_tag for b in pconf.bcconf], np.int32)
+    vals = np.zeros(2 * max(n, 1))
+    for i, b in enumerate(pconf.bcconf):
+        for j, x in enumerate(b.bc_vals[:2]):
+            vals[2 * i + j] = x
+    c = _ffi.FvFlowConfig()
+    c.gamma, c.Minf, c.Tinf, c.Reinf, c.Pr, c.aoa = (pconf.gamma, pconf.Minf, pconf.Tinf, pconf.Reinf,
+                                                     pconf.Pr, pconf.aoa)
+    c.viscous_sim, c.const_visc = int(pconf.viscous_sim), int(pconf.const_visc)
+    c.conv_numflux = FLUXES[nconf.conv_numflux.upper()]
+    c.conv_numflux_jac = FLUXES[nconf.conv_numflux_jac.upper()]
+    grad = nconf.gradientscheme.upper()
+    c.gradientscheme = GRADIENTS.get(grad, 0)
+    c.reconstruction = RECONSTRUCTIONS[nconf.reconstruction.upper()]
+    c.limiter_param = nconf.limiter_param
+    c.order2 = int(nconf.order2 and grad != "NONE")       # controlparser.cpp:180-181
+    c.nbc = n
+    keep = (types, tags, vals)
+    c.bc_type, c.bc_tag, c.bc_vals = iptr(types), iptr(tags), dptr(vals)
+    return c, keep
+
+
+class FlowFV:
+    """Device-resident FlowFV<freal,order2,constVisc> (spatial/flow_spatial.hpp:174-320)."""
+
+    def __init__(self, mesh: UMesh, pconf: FlowPhysicsConfig, nconf: FlowNumericsConfig, device: int = 0):
+        self.mesh, self.pconf, self.nconf = mesh, pconf, nconf
+        cfg, self._keep = _config_struct(pconf, nconf)
+        h = ctypes.c_void_p()
+        check(_ffi.lib().fvhip_create(ctypes.byref(mesh.view), ctypes.byref(cfg), device, ctypes.byref(h)))
+        self._h = h
+
+    # --- reference-ordered host interface -----------------------------------------------------
+    def compute_residual(self, u, r, gettimesteps=False, dtm=None):
+        """Adds -r(u) into r (flow_spatial.hpp:73-87); fills dtm if gettimesteps."""
+        N = self.mesh.nelem
+        assert u.shape == (N + self.mesh.nconnface, 4) and r.shape == (N, 4)
+        if gettimesteps:
+            assert dtm is not None and dtm.shape == (N,)
+        check(_ffi.lib().fvhip_compute_residual(self._h, dptr(u), dptr(r), int(gettimesteps),
+                                                dptr(dtm) if gettimesteps else None))
+        return r
+
+    def getGradients(self, u):
+        """GradBlock_t array [nelem][4 vars][2 dims] of conserved-variable gradients"""
+        g = np.zeros((self.mesh.nelem, 4, 2))
+        check(_ffi.lib().fvhip_get_gradients(self._h, dptr(u), dptr(g)))
+        return g
+
+    # --- device-resident interface (internal cell order) -----------------------------------------
+    def compute_residual_device(self, d_u, d_r, d_dtm=None, gettimesteps=False, overwrite=True):
+        check(_ffi.lib().fvhip_compute_residual_device(self._h, ctypes.c_void_p(d_u), ctypes.c_void_p(d_r),
+                                                       int(gettimesteps), ctypes.c_void_p(d_dtm or 0),
+                                                       1 if overwrite else 0))
+
+    def permutation(self):
+        p = np.zeros(self.mesh.nelem, np.int32)
+        check(_ffi.lib().fvhip_get_permutation(self._h, iptr(p)))
+        return p
+
+    def stream(self):
+        return _ffi.lib().fvhip_stream(self._h)
+
+    def synchronize(self):
+        check(_ffi.lib().fvhip_synchronize(self._h))
+
+    def profile(self, enable=True):
+        check(_ffi.lib().fvhip_profile(self._h, int(enable)))
+
+    def kernel_times(self):
+        maxk, nl = 32, 64
+        names = ctypes.create_string_buffer(maxk * nl)
+        ms = np.zeros(maxk)
+        cnt = np.zeros(maxk, np.int32)
+        n = _ffi.lib().fvhip_kernel_times(self._h, maxk, names, nl, dptr(ms), iptr(cnt))
+        if n < 0:
+            raise RuntimeError(_ffi.lib().fvhip_last_error().decode())
+        out = {}
+        for i in range(n):
+            nm = names.raw[i * nl:(i + 1) * nl].split(b"\0")[0].decode()
+            out[nm] = (float(ms[i]), int(cnt[i]))
+        return out
+
+    def layout_stats(self):
+        s = (ctypes.c_longlong * 6)()
+        check(_ffi.lib().fvhip_layout_stats(self._h, s))
+        keys = ("cells", "faces", "slots", "patches", "max_slots", "bfaces")
+        return dict(zip(keys, [int(x) for x in s]))
+
+    def close(self):
+        if getattr(self, "_h", None):
+            _ffi.lib().fvhip_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def create_flow_spatial(mesh, pconf, nconf, device=0):
+    """create_const_flowSpatialDiscretization (afactory.cpp:251-276)"""
+    return FlowFV(mesh, pconf, nconf, device)
+
+
+def local_flux(flux, gas, ul, ur, n):
+    """InviscidFlux::get_flux on the device for arrays of faces; gas = (g, Minf, Tinf, Reinf, Pr)"""
+    ul = np.ascontiguousarray(ul, np.float64)
+    ur = np.ascontiguousarray(ur, np.float64)
+    n = np.ascontiguousarray(n, np.float64)
+    out = np.zeros_like(ul)
+    g = np.array(gas, np.float64)
+    check(_ffi.lib().fvhip_local_flux(FLUXES[flux.upper()] if isinstance(flux, str) else flux, dptr(g),
+                                      ul.shape[0], dptr(ul), dptr(ur), dptr(n), dptr(out)))
+    return out

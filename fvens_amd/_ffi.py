@@ -1,0 +1,114 @@
+"""ctypes binding of libfvhip.so (include/fvhip.h).
+
+This is the Python face of the C-ABI; it mirrors what a reference-side binding would do
+(INTEGRATION.md). The library must be present: there is no CPU fallback for the product path.
+"""
+import ctypes
+import os
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libfvhip.so")
+
+c_int_p = ctypes.POINTER(ctypes.c_int)
+c_dbl_p = ctypes.POINTER(ctypes.c_double)
+
+
+class FvMeshView(ctypes.Structure):
+    _fields_ = [(n, ctypes.c_int) for n in
+                ("nelem", "npoin", "nbface", "naface", "nconnface", "maxnnode", "maxnfael", "nbtag")] + [
+        ("coords", c_dbl_p), ("inpoel", c_int_p), ("nnode", c_int_p), ("esuel", c_int_p),
+        ("elemface", c_int_p), ("intfac", c_int_p), ("btags", c_int_p), ("facemetric", c_dbl_p),
+        ("area", c_dbl_p), ("rc", c_dbl_p), ("rcbp", c_dbl_p), ("gr", c_dbl_p)]
+
+
+class FvFlowConfig(ctypes.Structure):
+    _fields_ = [("gamma", ctypes.c_double), ("Minf", ctypes.c_double), ("Tinf", ctypes.c_double),
+                ("Reinf", ctypes.c_double), ("Pr", ctypes.c_double), ("aoa", ctypes.c_double),
+                ("viscous_sim", ctypes.c_int), ("const_visc", ctypes.c_int),
+                ("conv_numflux", ctypes.c_int), ("conv_numflux_jac", ctypes.c_int),
+                ("gradientscheme", ctypes.c_int), ("reconstruction", ctypes.c_int),
+                ("limiter_param", ctypes.c_double), ("order2", ctypes.c_int), ("nbc", ctypes.c_int),
+                ("bc_type", c_int_p), ("bc_tag", c_int_p), ("bc_vals", c_dbl_p)]
+
+
+# name -> (restype, argtypes); kept in sync with include/fvhip.h (tests check every symbol)
+_SIGS = {
+    "fvhip_last_error": (ctypes.c_char_p, []),
+    "fvhip_version": (ctypes.c_char_p, []),
+    "fvhip_device_count": (ctypes.c_int, []),
+    "fvhip_create": (ctypes.c_int, [ctypes.POINTER(FvMeshView), ctypes.POINTER(FvFlowConfig), ctypes.c_int,
+                                    ctypes.POINTER(ctypes.c_void_p)]),
+    "fvhip_destroy": (ctypes.c_int, [ctypes.c_void_p]),
+    "fvhip_compute_residual": (ctypes.c_int, [ctypes.c_void_p, c_dbl_p, c_dbl_p, ctypes.c_int, c_dbl_p]),
+    "fvhip_compute_residual_device": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                                                     ctypes.c_int, ctypes.c_void_p, ctypes.c_int]),
+    "fvhip_get_gradients": (ctypes.c_int, [ctypes.c_void_p, c_dbl_p, c_dbl_p]),
+    "fvhip_assemble_jacobian": (ctypes.c_int, [ctypes.c_void_p, c_dbl_p, c_dbl_p, c_dbl_p, c_dbl_p]),
+    "fvhip_matfree_set_state": (ctypes.c_int, [ctypes.c_void_p, c_dbl_p, c_dbl_p, c_dbl_p]),
+    "fvhip_matfree_apply": (ctypes.c_int, [ctypes.c_void_p, c_dbl_p, c_dbl_p]),
+    "fvhip_matfree_set_eps": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_double]),
+    "fvhip_to_internal": (ctypes.c_int, [ctypes.c_void_p, c_dbl_p, ctypes.c_void_p, ctypes.c_int]),
+    "fvhip_from_internal": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, c_dbl_p, ctypes.c_int]),
+    "fvhip_get_permutation": (ctypes.c_int, [ctypes.c_void_p, c_int_p]),
+    "fvhip_device_alloc": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_ulonglong, ctypes.POINTER(ctypes.c_void_p)]),
+    "fvhip_device_free": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p]),
+    "fvhip_synchronize": (ctypes.c_int, [ctypes.c_void_p]),
+    "fvhip_stream": (ctypes.c_void_p, [ctypes.c_void_p]),
+    "fvhip_profile": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int]),
+    "fvhip_kernel_times": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_char_p, ctypes.c_int,
+                                          c_dbl_p, c_int_p]),
+    "fvhip_layout_stats": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(ctypes.c_longlong)]),
+    "fvhip_local_flux": (ctypes.c_int, [ctypes.c_int, c_dbl_p, ctypes.c_int, c_dbl_p, c_dbl_p, c_dbl_p, c_dbl_p]),
+    "fvhip_local_flux_jacobian": (ctypes.c_int, [ctypes.c_int, c_dbl_p, ctypes.c_int, c_dbl_p, c_dbl_p, c_dbl_p,
+                                                 c_dbl_p, c_dbl_p]),
+    "fvmesh_read_gmsh": (ctypes.c_int, [ctypes.c_char_p, ctypes.POINTER(ctypes.c_void_p)]),
+    "fvmesh_generate": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_double,
+                                       ctypes.c_double, ctypes.c_double, ctypes.POINTER(ctypes.c_void_p)]),
+    "fvmesh_write_gmsh": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_char_p]),
+    "fvmesh_destroy": (ctypes.c_int, [ctypes.c_void_p]),
+    "fvmesh_view": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(FvMeshView)]),
+    "fvmesh_raw_info": (ctypes.c_int, [ctypes.c_void_p, c_int_p]),
+    "fvmesh_raw_arrays": (ctypes.c_int, [ctypes.c_void_p, c_dbl_p, c_int_p, c_int_p, c_int_p]),
+}
+
+_lib = None
+
+
+def lib():
+    """Loads libfvhip.so (raises if it has not been built: the product has no fallback)."""
+    global _lib
+    if _lib is None:
+        # One HIP runtime per process: torch bundles its own libamdhip64.so.7 (same soname as
+        # /opt/rocm's). Loading torch first makes libfvhip bind to that copy, so a process that also
+        # uses torch.cuda / torch.distributed never holds two HSA runtimes.
+        try:
+            import torch  # noqa: F401
+        except ImportError:
+            pass
+        if not os.path.exists(LIB_PATH):
+            raise RuntimeError(f"{LIB_PATH} is missing; build it with __graft_entry__.build()")
+        L = ctypes.CDLL(LIB_PATH)
+        for name, (res, args) in _SIGS.items():
+            f = getattr(L, name)
+            f.restype = res
+            f.argtypes = args
+        _lib = L
+    return _lib
+
+
+def check(rc):
+    if rc != 0:
+        raise RuntimeError(lib().fvhip_last_error().decode())
+    return rc
+
+
+def dptr(a):
+    assert a.dtype == np.float64 and a.flags.c_contiguous
+    return a.ctypes.data_as(c_dbl_p)
+
+
+def iptr(a):
+    assert a.dtype == np.int32 and a.flags.c_contiguous
+    return a.ctypes.data_as(c_int_p)

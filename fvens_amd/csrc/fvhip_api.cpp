@@ -1,0 +1,479 @@
+/** \file fvhip_api.cpp
+ * \brief Implementation of the C-ABI in include/fvhip.h: device-resident discretisation,
+ *   host<->device plumbing with the reference's cell numbering, kernel timing, mesh builder.
+ * No exception crosses the ABI; errors become a nonzero return and fvhip_last_error().
+ */
+#include "../../include/fvhip.h"
+#include "layout.hpp"
+#include "kernels.hpp"
+#include "mesh.hpp"
+
+#include <hip/hip_runtime.h>
+#include <cstring>
+#include <cmath>
+#include <string>
+#include <vector>
+#include <map>
+#include <stdexcept>
+#include <memory>
+
+using namespace fvhip;
+
+namespace {
+
+thread_local std::string g_err;
+
+struct HipError : std::runtime_error { using std::runtime_error::runtime_error; };
+
+inline void hipCheck(hipError_t e, const char* what) {
+	if(e != hipSuccess) throw HipError(std::string(what) + ": " + hipGetErrorString(e));
+}
+#define HC(x) hipCheck((x), #x)
+
+template <typename F>
+int guard(F&& f) {
+	try { f(); return 0; }
+	catch(const std::exception& e) { g_err = e.what(); return 1; }
+	catch(...) { g_err = "unknown error"; return 1; }
+}
+
+template <typename T>
+T* upload(const std::vector<T>& v, std::vector<void*>& owned) {
+	if(v.empty()) return nullptr;
+	void* p = nullptr;
+	HC(hipMalloc(&p, v.size()*sizeof(T)));
+	HC(hipMemcpy(p, v.data(), v.size()*sizeof(T), hipMemcpyHostToDevice));
+	owned.push_back(p);
+	return static_cast<T*>(p);
+}
+
+double* dalloc(size_t n, std::vector<void*>& owned) {
+	if(n == 0) n = 1;
+	void* p = nullptr;
+	HC(hipMalloc(&p, n*sizeof(double)));
+	owned.push_back(p);
+	return static_cast<double*>(p);
+}
+
+/// interleave int pairs / 4-tuples for vector loads
+std::vector<int> pack2(const std::vector<int>& a, const std::vector<int>& b) {
+	std::vector<int> o(2*a.size());
+	for(size_t i = 0; i < a.size(); i++) { o[2*i] = a[i]; o[2*i+1] = b[i]; }
+	return o;
+}
+
+}
+
+struct fvhip_ctx
+{
+	int device = 0;
+	hipStream_t stream = nullptr;
+	fvhip_flow_config cfg{};
+	std::vector<int> bc_type, bc_tag;
+	std::vector<double> bc_vals;
+	Layout L;
+	DevMesh M{};
+	DevPhys P{};
+	std::vector<void*> owned;
+	int* d_perm = nullptr;
+	// state scratch
+	double *d_u = nullptr, *d_up = nullptr, *d_grad = nullptr, *d_lgrad = nullptr, *d_phi = nullptr;
+	double *d_ubc = nullptr, *d_ug = nullptr, *d_r = nullptr, *d_dtm = nullptr;
+	// mat-free state
+	double *d_mf_u = nullptr, *d_mf_r = nullptr, *d_mf_mdt = nullptr, *d_mf_aux = nullptr, *d_mf_y = nullptr;
+	double mf_eps = 1e-7;
+	std::vector<double> h_stage;
+	// profiling
+	bool prof = false;
+	struct Rec { std::string name; hipEvent_t a, b; };
+	std::vector<Rec> recs;
+	std::map<std::string, std::pair<double,int>> acc;
+
+	~fvhip_ctx() {
+		(void)hipSetDevice(device);
+		for(auto& r : recs) { (void)hipEventDestroy(r.a); (void)hipEventDestroy(r.b); }
+		for(void* p : owned) (void)hipFree(p);
+		if(stream) (void)hipStreamDestroy(stream);
+	}
+
+	template <typename F>
+	void timed(const std::string& name, F&& launch) {
+		if(!prof) { launch(); return; }
+		Rec r; r.name = name;
+		HC(hipEventCreate(&r.a)); HC(hipEventCreate(&r.b));
+		HC(hipEventRecord(r.a, stream));
+		launch();
+		HC(hipEventRecord(r.b, stream));
+		recs.push_back(r);
+	}
+	void collect() {
+		HC(hipStreamSynchronize(stream));
+		for(auto& r : recs) {
+			float ms = 0;
+			HC(hipEventElapsedTime(&ms, r.a, r.b));
+			auto& a = acc[r.name]; a.first += ms; a.second += 1;
+			(void)hipEventDestroy(r.a); (void)hipEventDestroy(r.b);
+		}
+		recs.clear();
+	}
+
+	int recKind() const {
+		if(!cfg.order2) return SR_FIRST;
+		return cfg.reconstruction == FVHIP_REC_VANALBADA ? SR_MUSCL : SR_LINEAR;
+	}
+	int viscKind() const {
+		if(!cfg.viscous_sim) return SV_NONE;
+		return cfg.const_visc ? SV_CONST : SV_SUTHERLAND;
+	}
+
+	/// the device sweep: -r(u) added (or written) into r, time steps into dtm
+	void residual(const double* u, double* r, bool dt, double* dtm, bool overwrite) {
+		const int rk = recKind();
+		SweepBuffers B{};
+		B.u = u; B.r = r; B.dtm = dtm; B.overwrite = overwrite ? 1 : 0;
+		if(rk != SR_FIRST) {
+			timed("k_prep", [&]{ launch_prep(M, P, u, d_up, d_ubc, d_ug, true, stream); });
+			switch(cfg.gradientscheme) {
+				case FVHIP_GRAD_LEASTSQUARES: timed("k_grad_wls", [&]{ launch_grad_wls(M, d_up, d_ug, d_grad, stream); }); break;
+				case FVHIP_GRAD_GREENGAUSS: timed("k_grad_gg", [&]{ launch_grad_gg(M, d_up, d_ug, d_grad, stream); }); break;
+				default: launch_fill(d_grad, 0.0, 8LL*L.ncell, stream);
+			}
+			B.up = d_up; B.grad = d_grad; B.rgrad = d_grad; B.ubc = d_ubc; B.ug = d_ug;
+			if(cfg.reconstruction == FVHIP_REC_BARTHJESPERSEN || cfg.reconstruction == FVHIP_REC_VENKATAKRISHNAN) {
+				const int venk = cfg.reconstruction == FVHIP_REC_VENKATAKRISHNAN;
+				timed("k_limiter", [&]{ launch_limiter(M, P, venk, d_up, d_ug, d_grad, d_phi, stream); });
+				B.phi = d_phi;
+			}
+			if(cfg.reconstruction == FVHIP_REC_WENO) {
+				timed("k_weno", [&]{ launch_weno(M, P, d_grad, d_lgrad, stream); });
+				B.rgrad = d_lgrad;
+			}
+		}
+		const char* nm = nullptr;
+		// name is only known after launch; record under a generic label then rename
+		timed("k_sweep", [&]{ nm = launch_sweep(M, P, B, cfg.conv_numflux, rk, viscKind(), dt, stream); });
+		if(prof && !recs.empty() && recs.back().name == "k_sweep" && nm) recs.back().name = nm;
+		HC(hipGetLastError());
+	}
+};
+
+extern "C" {
+
+const char* fvhip_last_error(void) { return g_err.c_str(); }
+const char* fvhip_version(void) { return "fvhip 0.1 (gfx950)"; }
+int fvhip_device_count(void) {
+	int n = 0;
+	if(hipGetDeviceCount(&n) != hipSuccess) return 0;
+	return n;
+}
+
+int fvhip_create(const fvhip_mesh* mesh, const fvhip_flow_config* cfg, int device, fvhip_handle* out)
+{
+	return guard([&] {
+		if(!mesh || !cfg || !out) throw std::invalid_argument("null argument");
+		if(cfg->nbc > MAXBC) throw std::invalid_argument("too many boundary conditions");
+		if(cfg->conv_numflux < 0 || cfg->conv_numflux > 6) throw std::invalid_argument("unknown flux"); // afactory.cpp:78-80
+		for(int i = 0; i < cfg->nbc; i++) {
+			const int t = cfg->bc_type[i];
+			if(t == FVHIP_BC_PERIODIC || t < 0 || t > 7) throw std::invalid_argument("BC type not implemented yet!"); // abc.cpp:493-494
+		}
+		std::unique_ptr<fvhip_ctx> h(new fvhip_ctx());
+		h->device = device;
+		HC(hipSetDevice(device));
+		HC(hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking));
+		h->cfg = *cfg;
+		h->bc_type.assign(cfg->bc_type, cfg->bc_type + cfg->nbc);
+		h->bc_tag.assign(cfg->bc_tag, cfg->bc_tag + cfg->nbc);
+		h->bc_vals.assign(cfg->bc_vals, cfg->bc_vals + 2*cfg->nbc);
+		h->cfg.bc_type = h->bc_type.data(); h->cfg.bc_tag = h->bc_tag.data(); h->cfg.bc_vals = h->bc_vals.data();
+
+		h->L = buildLayout(*mesh, h->cfg, true);
+		Layout& L = h->L;
+		auto& o = h->owned;
+		DevMesh& M = h->M;
+		M.ncell = L.ncell; M.nbface = L.nbface;
+		M.npatch = static_cast<int>(L.patch_cell.size()) - 1;
+		M.nslot = static_cast<int>(L.slot_L.size());
+		M.patch_cell = upload(L.patch_cell, o);
+		M.patch_slot = upload(L.patch_slot, o);
+		M.slot_LR = reinterpret_cast<const int2*>(upload(pack2(L.slot_L, L.slot_R), o));
+		M.slot_n = reinterpret_cast<const double2*>(upload(L.slot_n, o));
+		M.slot_len = upload(L.slot_len, o);
+		M.slot_gr = reinterpret_cast<const double2*>(upload(L.slot_gr, o));
+		M.cell_slots = reinterpret_cast<const int4*>(upload(L.cell_slots, o));
+		M.cell_nbr = reinterpret_cast<const int4*>(upload(L.cell_nbr_local, o));
+		M.cell_face = reinterpret_cast<const int4*>(upload(L.cell_face_local, o));
+		M.rc = reinterpret_cast<const double2*>(upload(L.rc, o));
+		M.area = upload(L.area, o);
+		M.wls_V = reinterpret_cast<const double4*>(upload(L.wls_V, o));
+		M.venk_eps2 = upload(L.venk_eps2, o);
+		M.bf_L = upload(L.bf_L, o);
+		M.bf_bc = upload(L.bf_bc, o);
+		M.bf_n = reinterpret_cast<const double2*>(upload(L.bf_n, o));
+		M.bf_rcbp = reinterpret_cast<const double2*>(upload(L.bf_rcbp, o));
+		h->d_perm = upload(L.perm, o);
+
+		DevPhys& P = h->P;
+		P.gas = gd::Gas{cfg->gamma, cfg->Minf, cfg->Tinf, cfg->Reinf, cfg->Pr, 110.5};
+		// free stream, aphysics.cpp:43-58 (sideslip 0)
+		const double beta = 0;
+		P.uinf[0] = 1.0;
+		P.uinf[1] = std::cos(cfg->aoa)*std::cos(beta);
+		P.uinf[2] = std::sin(cfg->aoa)*std::cos(beta);
+		const double pinf = (1.0/(cfg->gamma*cfg->Minf*cfg->Minf));
+		P.uinf[3] = pinf/(cfg->gamma-1.0) + 0.5*1.0*1.0;
+		P.nbc = cfg->nbc;
+		for(int i = 0; i < cfg->nbc; i++) P.bc[i] = gd::BCDev{cfg->bc_type[i], cfg->bc_vals[2*i], cfg->bc_vals[2*i+1]};
+		P.limiter_param = cfg->limiter_param;
+
+		const size_t N = static_cast<size_t>(L.ncell), nb = static_cast<size_t>(L.nbface);
+		h->d_u = dalloc(4*N, o); h->d_r = dalloc(4*N, o); h->d_dtm = dalloc(N, o);
+		h->d_up = dalloc(4*N, o); h->d_grad = dalloc(8*N, o);
+		h->d_ubc = dalloc(4*nb, o); h->d_ug = dalloc(4*nb, o);
+		if(cfg->reconstruction == FVHIP_REC_WENO) h->d_lgrad = dalloc(8*N, o);
+		if(cfg->reconstruction == FVHIP_REC_BARTHJESPERSEN || cfg->reconstruction == FVHIP_REC_VENKATAKRISHNAN)
+			h->d_phi = dalloc(4*N, o);
+		h->h_stage.resize(8*N);
+		*out = h.release();
+	});
+}
+
+int fvhip_destroy(fvhip_handle h) { return guard([&]{ delete h; }); }
+
+int fvhip_compute_residual_device(fvhip_handle h, const double* d_u, double* d_r, int gettimesteps,
+                                  double* d_dtm, int flags)
+{
+	return guard([&] {
+		HC(hipSetDevice(h->device));
+		h->residual(d_u, d_r, gettimesteps != 0, d_dtm, (flags & FVHIP_RES_OVERWRITE) != 0);
+	});
+}
+
+static void toInternal(fvhip_ctx* h, const double* src, double* dst, int width) {
+	const int N = h->L.ncell;
+	for(int c = 0; c < N; c++)
+		std::memcpy(dst + static_cast<size_t>(c)*width, src + static_cast<size_t>(h->L.perm[c])*width, width*sizeof(double));
+}
+static void fromInternal(fvhip_ctx* h, const double* src, double* dst, int width) {
+	const int N = h->L.ncell;
+	for(int c = 0; c < N; c++)
+		std::memcpy(dst + static_cast<size_t>(h->L.perm[c])*width, src + static_cast<size_t>(c)*width, width*sizeof(double));
+}
+
+int fvhip_compute_residual(fvhip_handle h, const double* u, double* r, int gettimesteps, double* dtm)
+{
+	return guard([&] {
+		HC(hipSetDevice(h->device));
+		const size_t N = static_cast<size_t>(h->L.ncell);
+		std::vector<double>& st = h->h_stage;
+		toInternal(h, u, st.data(), 4);
+		HC(hipMemcpyAsync(h->d_u, st.data(), 4*N*sizeof(double), hipMemcpyHostToDevice, h->stream));
+		HC(hipStreamSynchronize(h->stream));
+		toInternal(h, r, st.data(), 4);
+		HC(hipMemcpyAsync(h->d_r, st.data(), 4*N*sizeof(double), hipMemcpyHostToDevice, h->stream));
+		h->residual(h->d_u, h->d_r, gettimesteps != 0, h->d_dtm, false);
+		HC(hipMemcpyAsync(st.data(), h->d_r, 4*N*sizeof(double), hipMemcpyDeviceToHost, h->stream));
+		HC(hipStreamSynchronize(h->stream));
+		fromInternal(h, st.data(), r, 4);
+		if(gettimesteps) {
+			HC(hipMemcpyAsync(st.data(), h->d_dtm, N*sizeof(double), hipMemcpyDeviceToHost, h->stream));
+			HC(hipStreamSynchronize(h->stream));
+			fromInternal(h, st.data(), dtm, 1);
+		}
+	});
+}
+
+int fvhip_get_gradients(fvhip_handle h, const double* u, double* grads)
+{
+	return guard([&] {
+		HC(hipSetDevice(h->device));
+		const size_t N = static_cast<size_t>(h->L.ncell);
+		std::vector<double>& st = h->h_stage;
+		toInternal(h, u, st.data(), 4);
+		HC(hipMemcpyAsync(h->d_u, st.data(), 4*N*sizeof(double), hipMemcpyHostToDevice, h->stream));
+		// ghost states from cell values, then the gradient scheme on CONSERVED variables
+		launch_prep(h->M, h->P, h->d_u, h->d_up, h->d_ubc, h->d_ug, false, h->stream);
+		switch(h->cfg.gradientscheme) {
+			case FVHIP_GRAD_LEASTSQUARES: launch_grad_wls(h->M, h->d_u, h->d_ubc, h->d_grad, h->stream); break;
+			case FVHIP_GRAD_GREENGAUSS: launch_grad_gg(h->M, h->d_u, h->d_ubc, h->d_grad, h->stream); break;
+			default: launch_fill(h->d_grad, 0.0, 8LL*h->L.ncell, h->stream);
+		}
+		HC(hipGetLastError());
+		HC(hipMemcpyAsync(st.data(), h->d_grad, 8*N*sizeof(double), hipMemcpyDeviceToHost, h->stream));
+		HC(hipStreamSynchronize(h->stream));
+		fromInternal(h, st.data(), grads, 8);
+	});
+}
+
+int fvhip_assemble_jacobian(fvhip_handle h, const double* u, double* diag, double* lower, double* upper)
+{
+	return guard([&] { throw std::runtime_error("fvhip_assemble_jacobian: not built yet"); });
+}
+int fvhip_matfree_set_state(fvhip_handle h, const double* u, const double* r, const double* mdt)
+{
+	return guard([&] { throw std::runtime_error("fvhip_matfree_set_state: not built yet"); });
+}
+int fvhip_matfree_apply(fvhip_handle h, const double* x, double* y)
+{
+	return guard([&] { throw std::runtime_error("fvhip_matfree_apply: not built yet"); });
+}
+int fvhip_matfree_set_eps(fvhip_handle h, double eps) { return guard([&] { h->mf_eps = eps; }); }
+
+int fvhip_to_internal(fvhip_handle h, const double* host_ref, double* d_internal, int width)
+{
+	return guard([&] {
+		HC(hipSetDevice(h->device));
+		std::vector<double> st(static_cast<size_t>(h->L.ncell)*width);
+		toInternal(h, host_ref, st.data(), width);
+		HC(hipMemcpy(d_internal, st.data(), st.size()*sizeof(double), hipMemcpyHostToDevice));
+	});
+}
+int fvhip_from_internal(fvhip_handle h, const double* d_internal, double* host_ref, int width)
+{
+	return guard([&] {
+		HC(hipSetDevice(h->device));
+		HC(hipStreamSynchronize(h->stream));
+		std::vector<double> st(static_cast<size_t>(h->L.ncell)*width);
+		HC(hipMemcpy(st.data(), d_internal, st.size()*sizeof(double), hipMemcpyDeviceToHost));
+		fromInternal(h, st.data(), host_ref, width);
+	});
+}
+int fvhip_get_permutation(fvhip_handle h, int* perm)
+{
+	return guard([&] { std::memcpy(perm, h->L.perm.data(), h->L.perm.size()*sizeof(int)); });
+}
+int fvhip_device_alloc(fvhip_handle h, unsigned long long bytes, void** ptr)
+{
+	return guard([&] { HC(hipSetDevice(h->device)); HC(hipMalloc(ptr, bytes)); });
+}
+int fvhip_device_free(fvhip_handle h, void* ptr)
+{
+	return guard([&] { HC(hipSetDevice(h->device)); HC(hipFree(ptr)); });
+}
+int fvhip_synchronize(fvhip_handle h)
+{
+	return guard([&] { HC(hipSetDevice(h->device)); HC(hipStreamSynchronize(h->stream)); });
+}
+void* fvhip_stream(fvhip_handle h) { return h ? static_cast<void*>(h->stream) : nullptr; }
+
+int fvhip_profile(fvhip_handle h, int enable)
+{
+	return guard([&] {
+		if(!enable && h->prof) h->collect();
+		h->prof = enable != 0;
+		if(enable) { h->collect(); h->acc.clear(); }
+	});
+}
+
+int fvhip_kernel_times(fvhip_handle h, int maxk, char* names, int namelen, double* ms, int* counts)
+{
+	int n = 0;
+	const int rc = guard([&] {
+		h->collect();
+		for(auto& kv : h->acc) {
+			if(n >= maxk) break;
+			std::strncpy(names + static_cast<size_t>(n)*namelen, kv.first.c_str(), namelen-1);
+			names[static_cast<size_t>(n)*namelen + namelen-1] = '\0';
+			ms[n] = kv.second.first; counts[n] = kv.second.second;
+			n++;
+		}
+	});
+	return rc ? -1 : n;
+}
+
+int fvhip_layout_stats(fvhip_handle h, long long* s)
+{
+	return guard([&] {
+		s[0] = h->L.ncell; s[1] = h->L.naface; s[2] = static_cast<long long>(h->L.slot_L.size());
+		s[3] = static_cast<long long>(h->L.patch_cell.size()) - 1; s[4] = h->L.max_slots; s[5] = h->L.nbface;
+	});
+}
+
+int fvhip_local_flux(int flux_type, const double* gas5, int nf, const double* ul, const double* ur,
+                     const double* n, double* flux)
+{
+	return guard([&] {
+		gd::Gas G{gas5[0], gas5[1], gas5[2], gas5[3], gas5[4], 110.5};
+		double *a, *b, *c, *d;
+		HC(hipMalloc(&a, 4*sizeof(double)*nf + 8)); HC(hipMalloc(&b, 4*sizeof(double)*nf + 8));
+		HC(hipMalloc(&c, 2*sizeof(double)*nf + 8)); HC(hipMalloc(&d, 4*sizeof(double)*nf + 8));
+		HC(hipMemcpy(a, ul, 4*sizeof(double)*nf, hipMemcpyHostToDevice));
+		HC(hipMemcpy(b, ur, 4*sizeof(double)*nf, hipMemcpyHostToDevice));
+		HC(hipMemcpy(c, n, 2*sizeof(double)*nf, hipMemcpyHostToDevice));
+		launch_local_flux(flux_type, G, nf, a, b, c, d, nullptr);
+		HC(hipGetLastError());
+		HC(hipMemcpy(flux, d, 4*sizeof(double)*nf, hipMemcpyDeviceToHost));
+		(void)hipFree(a); (void)hipFree(b); (void)hipFree(c); (void)hipFree(d);
+	});
+}
+
+int fvhip_local_flux_jacobian(int flux_type, const double* gas5, int nf, const double* ul,
+                              const double* ur, const double* n, double* dfdl, double* dfdr)
+{
+	return guard([&] { throw std::runtime_error("fvhip_local_flux_jacobian: not built yet"); });
+}
+
+// ------------------------------------------------------------------------------------------------
+// mesh builder
+// ------------------------------------------------------------------------------------------------
+struct fvmesh_s { MeshData raw; Mesh mesh; };
+
+int fvmesh_read_gmsh(const char* path, fvmesh_handle* out)
+{
+	return guard([&] {
+		std::unique_ptr<fvmesh_s> m(new fvmesh_s());
+		m->raw = readGmsh2(path);
+		m->mesh = buildMesh(m->raw);
+		*out = m.release();
+	});
+}
+
+int fvmesh_generate(int kind, int a, int b, int c, double x, double y, double z, fvmesh_handle* out)
+{
+	return guard([&] {
+		std::unique_ptr<fvmesh_s> m(new fvmesh_s());
+		if(kind == 0) m->raw = generateNacaOgrid(a, b, c, x, y);
+		else if(kind == 1) m->raw = generateCylinderOgrid(a, b, x, y);
+		else if(kind == 2) m->raw = generateFlatPlate(a, b, x, y, z);
+		else throw std::invalid_argument("unknown mesh kind");
+		m->mesh = buildMesh(m->raw);
+		*out = m.release();
+	});
+}
+
+int fvmesh_write_gmsh(fvmesh_handle m, const char* path) { return guard([&] { writeGmsh2(m->raw, path); }); }
+int fvmesh_destroy(fvmesh_handle m) { return guard([&] { delete m; }); }
+
+int fvmesh_view(fvmesh_handle h, fvhip_mesh* v)
+{
+	return guard([&] {
+		const Mesh& M = h->mesh;
+		v->nelem = M.md.nelem; v->npoin = M.md.npoin; v->nbface = M.md.nbface; v->naface = M.naface;
+		v->nconnface = M.nconnface; v->maxnnode = M.md.maxnnode; v->maxnfael = M.md.maxnfael; v->nbtag = M.md.nbtag;
+		v->coords = M.md.coords.data(); v->inpoel = M.md.inpoel.data(); v->nnode = M.md.nnode.data();
+		v->esuel = M.esuel.data(); v->elemface = M.elemface.data(); v->intfac = M.intfac.data();
+		v->btags = M.btags.data(); v->facemetric = M.facemetric.data(); v->area = M.area.data();
+		v->rc = M.rc.data(); v->rcbp = M.rcbp.data(); v->gr = M.gr.data();
+	});
+}
+
+int fvmesh_raw_info(fvmesh_handle h, int* info)
+{
+	return guard([&] {
+		info[0] = h->raw.npoin; info[1] = h->raw.nelem; info[2] = h->raw.maxnnode;
+		info[3] = h->raw.nbface; info[4] = h->raw.nbtag;
+	});
+}
+
+int fvmesh_raw_arrays(fvmesh_handle h, double* coords, int* inpoel, int* nnode, int* bface)
+{
+	return guard([&] {
+		const MeshData& r = h->raw;
+		std::memcpy(coords, r.coords.data(), r.coords.size()*sizeof(double));
+		std::memcpy(inpoel, r.inpoel.data(), r.inpoel.size()*sizeof(int));
+		std::memcpy(nnode, r.nnode.data(), r.nnode.size()*sizeof(int));
+		std::memcpy(bface, r.bface.data(), r.bface.size()*sizeof(int));
+	});
+}
+
+}

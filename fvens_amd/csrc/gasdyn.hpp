@@ -1,0 +1,479 @@
+/** \file gasdyn.hpp
+ * \brief Point-wise gas dynamics for the MI355X face sweep: ideal-gas relations, the seven
+ *   numerical inviscid fluxes, boundary ghost states and the viscous face flux.
+ *
+ * Every expression keeps the reference's operation order and association, so that with
+ * -ffp-contract=off the device reproduces the reference's IEEE results (division and sqrt are
+ * correctly rounded on gfx950 in the default float mode). Sources (under /root/reference/src):
+ *   physics/aphysics_defs.hpp:13-487     ideal-gas relations
+ *   spatial/anumericalflux.cpp:40-61, 202-250, 264-315, 479-553, 667-732, 973-1007, 1069-1228
+ *   spatial/anumericalflux.hpp:175-189   Roe averages
+ *   spatial/abc.cpp:41-437               boundary ghost states
+ *   physics/viscousphysics.cpp:14-122, spatial/aspatial.cpp:172-205   viscous face flux
+ * Marked __host__ __device__ so the same code is also compiled into the host self-check.
+ */
+#ifndef FVHIP_GASDYN_HPP
+#define FVHIP_GASDYN_HPP
+
+#include <hip/hip_runtime.h>
+#include <cmath>
+
+#define FVHIP_HD __host__ __device__ __forceinline__
+
+namespace fvhip {
+namespace gd {
+
+/// Gas constants (IdealGasPhysics members, aphysics.hpp; sC = 110.5, aphysics.cpp:19)
+struct Gas {
+	double g, Minf, Tinf, Reinf, Pr, sC;
+};
+
+FVHIP_HD double dot2(const double* a, const double* b) { double d = 0; d += a[0]*b[0]; d += a[1]*b[1]; return d; }
+
+FVHIP_HD void directional_flux(const Gas& G, const double* uc, const double* n, double vn, double p, double* f) {
+	f[0] = vn*uc[0];
+	f[1] = vn*uc[1] + p*n[0];
+	f[2] = vn*uc[2] + p*n[1];
+	f[3] = vn*(uc[3] + p);
+}
+
+/// getVarsFromConserved: velocity, normal velocity, pressure, total enthalpy
+FVHIP_HD void flow_vars(const Gas& G, const double* uc, const double* n, double* v, double& vn, double& p, double& H) {
+	v[0] = uc[1]/uc[0];
+	v[1] = uc[2]/uc[0];
+	vn = dot2(v,n);
+	const double vm2 = dot2(v,v);
+	p = (G.g-1.0)*(uc[3] - 0.5*uc[0]*vm2);
+	H = (uc[3]+p)/uc[0];
+}
+
+FVHIP_HD double pressure_cons(const Gas& G, const double* uc) {
+	return (G.g-1.0)*(uc[3] - 0.5*dot2(&uc[1],&uc[1])/uc[0]);
+}
+FVHIP_HD double sound_speed(const Gas& G, double rho, double p) { return sqrt(G.g * p/rho); }
+FVHIP_HD double sound_speed_cons(const Gas& G, const double* uc) { return sound_speed(G, uc[0], pressure_cons(G, uc)); }
+FVHIP_HD double temperature(const Gas& G, double rho, double p) { return p/rho * G.g*G.Minf*G.Minf; }
+FVHIP_HD double energy_from_pressure(const Gas& G, double p, double d, double vm2) { return p/(G.g-1.0) + 0.5*d*vm2; }
+FVHIP_HD double energy_from_temperature(const Gas& G, double T, double d, double vm2) {
+	return d * (T/(G.g*(G.g-1.0)*G.Minf*G.Minf) + 0.5*vm2);
+}
+FVHIP_HD double freestream_pressure(const Gas& G) { return (1.0/(G.g*G.Minf*G.Minf)); }
+
+/// conserved -> (rho, vx, vy, p); in-place safe
+FVHIP_HD void cons2prim(const Gas& G, const double* uc, double* up) {
+	const double rho = uc[0];
+	const double p = pressure_cons(G, uc);
+	const double vx = uc[1]/rho, vy = uc[2]/rho;
+	up[0] = rho; up[1] = vx; up[2] = vy; up[3] = p;
+}
+/// (rho, vx, vy, p) -> conserved; in-place safe
+FVHIP_HD void prim2cons(const Gas& G, const double* up, double* uc) {
+	const double rhoE = energy_from_pressure(G, up[3], up[0], dot2(&up[1],&up[1]));
+	const double r = up[0];
+	uc[0] = r; uc[1] = r*up[1]; uc[2] = r*up[2]; uc[3] = rhoE;
+}
+/// conserved -> (rho, vx, vy, T)
+FVHIP_HD void cons2prim2(const Gas& G, const double* uc, double* up) {
+	const double p = pressure_cons(G, uc);
+	up[0] = uc[0]; up[1] = uc[1]/uc[0]; up[2] = uc[2]/uc[0];
+	up[3] = temperature(G, uc[0], p);
+}
+FVHIP_HD double grad_temperature(const Gas& G, double rho, double grho, double p, double gp) {
+	return (gp*rho - p*grho) / (rho*rho) * G.g*G.Minf*G.Minf;
+}
+FVHIP_HD double sutherland(const Gas& G, const double* uc) {
+	const double T = temperature(G, uc[0], pressure_cons(G, uc));
+	return (1.0+G.sC/G.Tinf)/(T+G.sC/G.Tinf) * pow(T,1.5) / G.Reinf;
+}
+
+/// Roe averages (anumericalflux.hpp:175-189)
+struct RoeAvg { double R, rho, v[2], vm2, vn, H, c; };
+FVHIP_HD RoeAvg roe_average(const Gas& G, const double* ul, const double* ur, const double* n,
+                            const double* vi, double Hi, const double* vj, double Hj) {
+	RoeAvg a;
+	a.R = sqrt(ur[0]/ul[0]);
+	a.rho = a.R*ul[0];
+	a.v[0] = (a.R*vj[0] + vi[0])/(a.R + 1.0);
+	a.v[1] = (a.R*vj[1] + vi[1])/(a.R + 1.0);
+	a.H = (a.R*Hj + Hi)/(a.R + 1.0);
+	a.vm2 = dot2(a.v,a.v);
+	a.vn = dot2(a.v,n);
+	a.c = sqrt( (G.g-1.0)*(a.H - a.vm2*0.5) );
+	return a;
+}
+
+// ---------------------------------------------------------------------------------------------
+// Numerical fluxes. Output: flux per unit length along unit normal n (L -> R).
+// ---------------------------------------------------------------------------------------------
+
+FVHIP_HD void flux_llf(const Gas& G, const double* ul, const double* ur, const double* n, double* f) {
+	double vi[2], vj[2], vni, vnj, pi, pj, Hi, Hj;
+	flow_vars(G, ul, n, vi, vni, pi, Hi);
+	flow_vars(G, ur, n, vj, vnj, pj, Hj);
+	const double ci = sound_speed(G, ul[0], pi), cj = sound_speed(G, ur[0], pj);
+	const double si = fabs(vni)+ci, sj = fabs(vnj)+cj;
+	const double eig = si > sj ? si : sj;
+	// getDirectionalFluxFromConserved recomputes vn and p from the conserved state (aphysics.cpp:28-35)
+	double fl[4], fr[4];
+	{
+		const double vn = dot2(&ul[1],n)/ul[0];
+		const double p = (G.g-1.0)*(ul[3] - 0.5*dot2(&ul[1],&ul[1])/ul[0]);
+		directional_flux(G, ul, n, vn, p, fl);
+	}
+	{
+		const double vn = dot2(&ur[1],n)/ur[0];
+		const double p = (G.g-1.0)*(ur[3] - 0.5*dot2(&ur[1],&ur[1])/ur[0]);
+		directional_flux(G, ur, n, vn, p, fr);
+	}
+	for(int k = 0; k < 4; k++) f[k] = 0.5*( fl[k] + fr[k] - eig*(ur[k]-ul[k]) );
+}
+
+FVHIP_HD double sq(double x) { return x*x; }   // std::pow(x,2) folds to x*x
+
+FVHIP_HD void flux_vanleer(const Gas& G, const double* ul, const double* ur, const double* n, double* f) {
+	const double g = G.g;
+	double vi[2], vj[2], vni, vnj, pi, pj, Hi, Hj;
+	flow_vars(G, ul, n, vi, vni, pi, Hi);
+	flow_vars(G, ur, n, vj, vnj, pj, Hj);
+	const double ci = sound_speed(G, ul[0], pi), cj = sound_speed(G, ur[0], pj);
+	const double Mni = vni/ci, Mnj = vnj/cj;
+	double fp[4], fm[4];
+	if(Mni < -1.0) { fp[0] = fp[1] = fp[2] = fp[3] = 0; }
+	else if(Mni > 1.0) directional_flux(G, ul, n, vni, pi, fp);
+	else {
+		const double vmags = sq(ul[1]/ul[0]) + sq(ul[2]/ul[0]);
+		fp[0] = ul[0]*ci*sq(Mni+1)/4.0;
+		fp[1] = fp[0] * (ul[1]/ul[0] + n[0]*(2.0*ci - vni)/g);
+		fp[2] = fp[0] * (ul[2]/ul[0] + n[1]*(2.0*ci - vni)/g);
+		fp[3] = fp[0] * ( (vmags - vni*vni)/2.0 + sq((g-1)*vni+2*ci)/(2*(g*g-1)) );
+	}
+	if(Mnj > 1.0) { fm[0] = fm[1] = fm[2] = fm[3] = 0; }
+	else if(Mnj < -1.0) directional_flux(G, ur, n, vnj, pj, fm);
+	else {
+		const double vmags = sq(ur[1]/ur[0]) + sq(ur[2]/ur[0]);
+		fm[0] = -ur[0]*cj*sq(Mnj-1)/4.0;
+		fm[1] = fm[0] * (ur[1]/ur[0] + n[0]*(-2.0*cj - vnj)/g);
+		fm[2] = fm[0] * (ur[2]/ur[0] + n[1]*(-2.0*cj - vnj)/g);
+		fm[3] = fm[0] * ( (vmags - vnj*vnj)/2.0 + sq((g-1)*vnj-2*cj)/(2*(g*g-1)) );
+	}
+	for(int k = 0; k < 4; k++) f[k] = fp[k] + fm[k];
+}
+
+FVHIP_HD void flux_ausm(const Gas& G, const double* ul, const double* ur, const double* n, double* f) {
+	double vi[2], vj[2], vni, vnj, pi, pj, Hi, Hj;
+	flow_vars(G, ul, n, vi, vni, pi, Hi);
+	flow_vars(G, ur, n, vj, vnj, pj, Hj);
+	const double ci = sound_speed(G, ul[0], pi), cj = sound_speed(G, ur[0], pj);
+	const double Mni = vni/ci, Mnj = vnj/cj;
+	double ML, MR, pL, pR;
+	if(fabs(Mni) <= 1.0) { ML = 0.25*(Mni+1)*(Mni+1); pL = ML*pi*(2.0-Mni); }
+	else if(Mni < -1.0) { ML = 0; pL = 0; }
+	else { ML = Mni; pL = pi; }
+	if(fabs(Mnj) <= 1.0) { MR = -0.25*(Mnj-1)*(Mnj-1); pR = -MR*pj*(2.0+Mnj); }
+	else if(Mnj < -1.0) { MR = Mnj; pR = pj; }
+	else { MR = 0; pR = 0; }
+	const double Mh = ML+MR, ph = pL+pR;
+	f[0] = Mh/2.0*(ul[0]*ci+ur[0]*cj) -fabs(Mh)/2.0*(ur[0]*cj-ul[0]*ci);
+	f[1] = Mh/2.0*(ul[1]*ci+ur[1]*cj) -fabs(Mh)/2.0*(ur[1]*cj-ul[1]*ci) + ph*n[0];
+	f[2] = Mh/2.0*(ul[2]*ci+ur[2]*cj) -fabs(Mh)/2.0*(ur[2]*cj-ul[2]*ci) + ph*n[1];
+	f[3] = Mh/2.0*(ci*(ul[3]+pi)+cj*(ur[3]+pj)) -fabs(Mh)/2.0*(cj*(ur[3]+pj)-ci*(ul[3]+pi));
+}
+
+FVHIP_HD void flux_ausmplus(const Gas& G, const double* ul, const double* ur, const double* n, double* f) {
+	const double g = G.g;
+	double vi[2], vj[2], vni, vnj, pi, pj, Hi, Hj;
+	flow_vars(G, ul, n, vi, vni, pi, Hi);
+	flow_vars(G, ur, n, vj, vnj, pj, Hj);
+	const double ci = sound_speed(G, ul[0], pi), cj = sound_speed(G, ur[0], pj);
+	const double vm2i = dot2(vi,vi), vm2j = dot2(vj,vj);
+	double csi = sqrt((ci*ci/(g-1.0)+0.5*vm2i)*2.0*(g-1.0)/(g+1.0));
+	double csj = sqrt((cj*cj/(g-1.0)+0.5*vm2j)*2.0*(g-1.0)/(g+1.0));
+	const double ki = csi > vni ? csi : vni;
+	const double kj = csj > -vnj ? csj : -vnj;
+	csi = csi*csi/ki;
+	csj = csj*csj/kj;
+	const double ch = (csi < csj) ? csi : csj;
+	const double Mni = vni/ch, Mnj = vnj/ch;
+	double ML, MR, pL, pR;
+	if(fabs(Mni) <= 1.0) {
+		ML = 0.25*(Mni+1)*(Mni+1) + 1.0/8.0*(Mni*Mni-1.0)*(Mni*Mni-1.0);
+		pL = pi*(0.25*(Mni+1)*(Mni+1)*(2.0-Mni) + 3.0/16*Mni*(Mni*Mni-1.0)*(Mni*Mni-1.0));
+	}
+	else if(Mni < -1.0) { ML = 0; pL = 0; }
+	else { ML = Mni; pL = pi; }
+	if(fabs(Mnj) <= 1.0) {
+		MR = -0.25*(Mnj-1)*(Mnj-1) - 1.0/8.0*(Mnj*Mnj-1.0)*(Mnj*Mnj-1.0);
+		pR = pj*(0.25*(Mnj-1)*(Mnj-1)*(2.0+Mnj) - 3.0/16*Mnj*(Mnj*Mnj-1.0)*(Mnj*Mnj-1.0));
+	}
+	else if(Mnj < -1.0) { MR = Mnj; pR = pj; }
+	else { MR = 0; pR = 0; }
+	const double Mh = ML+MR, ph = pL+pR;
+	f[0] = ch* (Mh/2.0*(ul[0]+ur[0]) -fabs(Mh)/2.0*(ur[0]-ul[0]));
+	f[1] = ch* (Mh/2.0*(ul[1]+ur[1]) -fabs(Mh)/2.0*(ur[1]-ul[1])) + ph*n[0];
+	f[2] = ch* (Mh/2.0*(ul[2]+ur[2]) -fabs(Mh)/2.0*(ur[2]-ul[2])) + ph*n[1];
+	f[3] = ch* (Mh/2.0*(ul[3]+pi+ur[3]+pj) -fabs(Mh)/2.0*((ur[3]+pj)-(ul[3]+pi)));
+}
+
+FVHIP_HD void flux_roe(const Gas& G, const double* ul, const double* ur, const double* n, double* f) {
+	double vi[2], vj[2], vni, vnj, pi, pj, Hi, Hj;
+	flow_vars(G, ul, n, vi, vni, pi, Hi);
+	flow_vars(G, ur, n, vj, vnj, pj, Hj);
+	const RoeAvg a = roe_average(G, ul, ur, n, vi, Hi, vj, Hj);
+	// |eigenvalues| with Harten's entropy fix, delta = 1e-4 c (anumericalflux.cpp:664, 686-692)
+	double l0 = fabs(a.vn-a.c), l1 = fabs(a.vn), l3 = fabs(a.vn+a.c);
+	const double delta = 1.0e-4*a.c;
+	if(l0 < delta) l0 = (l0*l0 + delta*delta)/(2.0*delta);
+	if(l1 < delta) l1 = (l1*l1 + delta*delta)/(2.0*delta);
+	if(l3 < delta) l3 = (l3*l3 + delta*delta)/(2.0*delta);
+	const double devn = vnj-vni, dep = pj-pi, derho = ur[0]-ul[0];
+	const double a0 = l0*(dep-a.rho*a.c*devn)/(2.0*a.c*a.c);
+	const double a1 = l1*(derho - dep/(a.c*a.c));
+	const double a2 = l1*a.rho;
+	const double a3 = l3*(dep+a.rho*a.c*devn)/(2.0*a.c*a.c);
+	double d0 = a0, d1 = a0*(a.v[0]-a.c*n[0]), d2 = a0*(a.v[1]-a.c*n[1]), d3 = a0*(a.H-a.c*a.vn);
+	d0 += a1;
+	d1 += a1*a.v[0] +      a2*(vj[0]-vi[0] - devn*n[0]);
+	d2 += a1*a.v[1] +      a2*(vj[1]-vi[1] - devn*n[1]);
+	d3 += a1*a.vm2/2.0 + a2 *(a.v[0]*(vj[0]-vi[0]) +a.v[1]*(vj[1]-vi[1]) -a.vn*devn);
+	d0 += a3;
+	d1 += a3*(a.v[0]+a.c*n[0]);
+	d2 += a3*(a.v[1]+a.c*n[1]);
+	d3 += a3*(a.H+a.c*a.vn);
+	double fi[4], fj[4];
+	directional_flux(G, ul, n, vni, pi, fi);
+	directional_flux(G, ur, n, vnj, pj, fj);
+	f[0] = 0.5*(fi[0]+fj[0] - d0);
+	f[1] = 0.5*(fi[1]+fj[1] - d1);
+	f[2] = 0.5*(fi[2]+fj[2] - d2);
+	f[3] = 0.5*(fi[3]+fj[3] - d3);
+}
+
+FVHIP_HD void einfeldt(double vni, double ci, double vnj, double cj, const RoeAvg& a, double& sl, double& sr) {
+	sl = vni - ci;
+	if(sl > a.vn-a.c) sl = a.vn-a.c;
+	sr = vnj+cj;
+	if(sr < a.vn+a.c) sr = a.vn+a.c;
+}
+
+FVHIP_HD void flux_hll(const Gas& G, const double* ul, const double* ur, const double* n, double* f) {
+	double vi[2], vj[2], vni, vnj, pi, pj, Hi, Hj;
+	flow_vars(G, ul, n, vi, vni, pi, Hi);
+	flow_vars(G, ur, n, vj, vnj, pj, Hj);
+	const double ci = sound_speed(G, ul[0], pi), cj = sound_speed(G, ur[0], pj);
+	const RoeAvg a = roe_average(G, ul, ur, n, vi, Hi, vj, Hj);
+	double sl, sr;
+	einfeldt(vni, ci, vnj, cj, a, sl, sr);
+	const double sr0 = sr > 0 ? 0 : sr;
+	const double sl0 = sl > 0 ? 0 : sl;
+	const double t1 = (sr0 - sl0)/(sr-sl); const double t2 = 1.0 - t1;
+	const double t3 = 0.5*(sr*fabs(sl)-sl*fabs(sr))/(sr-sl);
+	f[0] = t1*vnj*ur[0] + t2*vni*ul[0]                     - t3*(ur[0]-ul[0]);
+	f[1] = t1*(vnj*ur[1]+pj*n[0]) + t2*(vni*ul[1]+pi*n[0]) - t3*(ur[1]-ul[1]);
+	f[2] = t1*(vnj*ur[2]+pj*n[1]) + t2*(vni*ul[2]+pi*n[1]) - t3*(ur[2]-ul[2]);
+	f[3] = t1*(vnj*ur[0]*Hj) + t2*(vni*ul[0]*Hi)           - t3*(ur[3]-ul[3]);
+}
+
+/// HLLC star state (anumericalflux.cpp:1069-1081), returned as the flux correction s*(u* - u)
+FVHIP_HD void hllc_side(const double* u, const double* n, double vn, double p, double ss, double sm, double* f) {
+	const double pstar = u[0]*(vn-ss)*(vn-sm) + p;
+	const double us0 = u[0] * (ss - vn)/(ss-sm);
+	const double us1 = ( (ss-vn)*u[1] + (pstar-p)*n[0] )/(ss-sm);
+	const double us2 = ( (ss-vn)*u[2] + (pstar-p)*n[1] )/(ss-sm);
+	const double us3 = ( (ss-vn)*u[3] - p*vn + pstar*sm )/(ss-sm);
+	f[0] += ss * (us0 - u[0]);
+	f[1] += ss * (us1 - u[1]);
+	f[2] += ss * (us2 - u[2]);
+	f[3] += ss * (us3 - u[3]);
+}
+
+FVHIP_HD void flux_hllc(const Gas& G, const double* ul, const double* ur, const double* n, double* f) {
+	double vi[2], vj[2], vni, vnj, pi, pj, Hi, Hj;
+	flow_vars(G, ul, n, vi, vni, pi, Hi);
+	flow_vars(G, ur, n, vj, vnj, pj, Hj);
+	const double ci = sound_speed(G, ul[0], pi), cj = sound_speed(G, ur[0], pj);
+	const RoeAvg a = roe_average(G, ul, ur, n, vi, Hi, vj, Hj);
+	double sl, sr;
+	einfeldt(vni, ci, vnj, cj, a, sl, sr);
+	const double sm = ( ur[0]*vnj*(sr-vnj) - ul[0]*vni*(sl-vni) + pi-pj )
+		/ ( ur[0]*(sr-vnj) - ul[0]*(sl-vni) );
+	if(sl > 0)
+		directional_flux(G, ul, n, vni, pi, f);
+	else if(sl <= 0 && sm > 0) {
+		directional_flux(G, ul, n, vni, pi, f);
+		hllc_side(ul, n, vni, pi, sl, sm, f);
+	}
+	else if(sm <= 0 && sr >= 0) {
+		directional_flux(G, ur, n, vnj, pj, f);
+		hllc_side(ur, n, vnj, pj, sr, sm, f);
+	}
+	else
+		directional_flux(G, ur, n, vnj, pj, f);
+}
+
+template <int FLUX>
+FVHIP_HD void inviscid_flux(const Gas& G, const double* ul, const double* ur, const double* n, double* f) {
+	switch(FLUX) {
+		case 0: flux_llf(G, ul, ur, n, f); break;
+		case 1: flux_vanleer(G, ul, ur, n, f); break;
+		case 2: flux_ausm(G, ul, ur, n, f); break;
+		case 3: flux_ausmplus(G, ul, ur, n, f); break;
+		case 4: flux_roe(G, ul, ur, n, f); break;
+		case 5: flux_hll(G, ul, ur, n, f); break;
+		default: flux_hllc(G, ul, ur, n, f); break;
+	}
+}
+
+FVHIP_HD void inviscid_flux_rt(int type, const Gas& G, const double* ul, const double* ur, const double* n, double* f) {
+	switch(type) {
+		case 0: flux_llf(G, ul, ur, n, f); break;
+		case 1: flux_vanleer(G, ul, ur, n, f); break;
+		case 2: flux_ausm(G, ul, ur, n, f); break;
+		case 3: flux_ausmplus(G, ul, ur, n, f); break;
+		case 4: flux_roe(G, ul, ur, n, f); break;
+		case 5: flux_hll(G, ul, ur, n, f); break;
+		default: flux_hllc(G, ul, ur, n, f); break;
+	}
+}
+
+// ---------------------------------------------------------------------------------------------
+// Boundary ghost states (abc.cpp). bc = {type, vals[0], vals[1]}; uinf = free stream.
+// ---------------------------------------------------------------------------------------------
+struct BCDev { int type; double v0, v1; };
+
+FVHIP_HD void ghost_state(const Gas& G, const BCDev& bc, const double* uinf, const double* ins,
+                          const double* n, double* gs) {
+	switch(bc.type) {
+	case 2: {  // INFLOW_OUTFLOW (abc.cpp:46-81)
+		const double vni = dot2(&ins[1],n)/ins[0];
+		const double ci = sound_speed_cons(G, ins);
+		const double Mni = vni/ci;
+		if(Mni <= 0) { gs[0] = uinf[0]; gs[1] = uinf[1]; gs[2] = uinf[2]; gs[3] = uinf[3]; }
+		else if(Mni < 1) {
+			const double pinf = freestream_pressure(G);
+			const double e = energy_from_pressure(G, pinf, ins[0], dot2(&ins[1],&ins[1])/(ins[0]*ins[0]));
+			gs[0] = ins[0]; gs[1] = ins[1]; gs[2] = ins[2]; gs[3] = e;
+		}
+		else { gs[0] = ins[0]; gs[1] = ins[1]; gs[2] = ins[2]; gs[3] = ins[3]; }
+		break;
+	}
+	case 3: {  // SUBSONIC_INFLOW (abc.cpp:145-175)
+		const double g = G.g, ptotal = bc.v0, ttotal = bc.v1;
+		const double ci = sound_speed_cons(G, ins);
+		const double Rm = dot2(&ins[1],n)/ins[0] - ci/(2*g - 1.0);
+		const double co2 = ci*ci + (g-1.0)/2.0 * dot2(&ins[1],&ins[1])/(ins[0]*ins[0]);
+		const double q = sqrt((g+1)*co2/((g-1)*Rm*Rm) - (g-1)/2.0);
+		const double cg = -Rm*(g-1)/(g+1) * (1.0 + q);
+		const double tg = ttotal*cg*cg/co2;
+		const double pg = ptotal * pow(tg/ttotal, g/(g-1.0));
+		const double rho = g*G.Minf*G.Minf*pg/tg;
+		const double vm = sqrt(2.0/(g-1.0)*(co2 - cg*cg));
+		const double vx = vm*1.0*n[0], vy = vm*1.0*n[1];
+		gs[0] = rho; gs[1] = rho*vx; gs[2] = rho*vy;
+		gs[3] = energy_from_pressure(G, pg, rho, vm*vm);
+		break;
+	}
+	case 1:    // FARFIELD
+		gs[0] = uinf[0]; gs[1] = uinf[1]; gs[2] = uinf[2]; gs[3] = uinf[3];
+		break;
+	case 0: {  // SLIP_WALL (abc.cpp:219-229)
+		const double vni = dot2(&ins[1],n)/ins[0];
+		const double r = ins[0], e = ins[3];
+		const double m0 = ins[1] - 2.0*vni*n[0]*ins[0];
+		const double m1 = ins[2] - 2.0*vni*n[1]*ins[0];
+		gs[0] = r; gs[1] = m0; gs[2] = m1; gs[3] = e;
+		break;
+	}
+	case 7: {  // ADIABATIC_WALL -> Adiabaticwall2D (abc.cpp:278-287, factory :486-488)
+		const double tm = bc.v0 * ins[0];
+		const double r = ins[0], e = ins[3];
+		const double m0 =  2.0*tm*n[1] - ins[1];
+		const double m1 = -2.0*tm*n[0] - ins[2];
+		gs[0] = r; gs[1] = m0; gs[2] = m1; gs[3] = e;
+		break;
+	}
+	case 6: {  // ISOTHERMAL_WALL (abc.cpp:349-366)
+		const double p = pressure_cons(G, ins);
+		const double gtemp = 2.0*bc.v1 - temperature(G, ins[0], p);
+		const double r = ins[0];
+		const double m0 = r*( 2.0*bc.v0*n[1] - ins[1]/ins[0]);
+		const double m1 = r*(-2.0*bc.v0*n[0] - ins[2]/ins[0]);
+		double mm[2] = {m0, m1};
+		const double vm2 = dot2(mm,mm)/(r*r);
+		gs[0] = r; gs[1] = m0; gs[2] = m1; gs[3] = energy_from_temperature(G, gtemp, r, vm2);
+		break;
+	}
+	default:   // EXTRAPOLATION (and anything else, rejected at setup)
+		gs[0] = ins[0]; gs[1] = ins[1]; gs[2] = ins[2]; gs[3] = ins[3];
+		break;
+	}
+}
+
+// ---------------------------------------------------------------------------------------------
+// Viscous face flux (flow_spatial.cpp:348-395, aspatial.cpp:172-205, viscousphysics.cpp:14-122)
+// gl, gr: primitive gradients in GradBlock layout [var][dim]; zero-gradient first order if !order2
+// ---------------------------------------------------------------------------------------------
+template <bool ORDER2, bool CONSTVISC>
+FVHIP_HD void viscous_flux(const Gas& G, const double* n, const double* rcl, const double* rcr,
+                           const double* ucl, const double* ucr, const double* gl, const double* grr,
+                           const double* ul, const double* ur, double* vf) {
+	double tl[4], tr[4], gL[8], gR[8];          // gL[dim*4 + var]
+	if(ORDER2) {
+		for(int i = 0; i < 2; i++) for(int j = 0; j < 4; j++) { gL[i*4+j] = gl[j*2+i]; gR[i*4+j] = grr[j*2+i]; }
+		cons2prim(G, ucl, tl);
+		cons2prim(G, ucr, tr);
+		for(int j = 0; j < 2; j++) {
+			gL[j*4+3] = grad_temperature(G, tl[0], gL[j*4], tl[3], gL[j*4+3]);
+			gR[j*4+3] = grad_temperature(G, tr[0], gR[j*4], tr[3], gR[j*4+3]);
+		}
+		tl[3] = temperature(G, tl[0], tl[3]);
+		tr[3] = temperature(G, tr[0], tr[3]);
+	} else {
+		cons2prim2(G, ucl, tl);
+		cons2prim2(G, ucr, tr);
+		for(int i = 0; i < 8; i++) { gL[i] = 0; gR[i] = 0; }
+	}
+	double grad[2][4];
+	{
+		double dr[2], dist = 0;
+		dr[0] = rcr[0]-rcl[0]; dist += dr[0]*dr[0];
+		dr[1] = rcr[1]-rcl[1]; dist += dr[1]*dr[1];
+		dist = sqrt(dist);
+		dr[0] /= dist; dr[1] /= dist;
+		for(int i = 0; i < 4; i++) {
+			double davg[2];
+			davg[0] = 0.5*(gL[i] + gR[i]);
+			davg[1] = 0.5*(gL[4+i] + gR[4+i]);
+			const double corr = (tr[i]-tl[i])/dist;
+			const double ddr = dot2(davg,dr);
+			grad[0][i] = davg[0] - ddr*dr[0] + corr*dr[0];
+			grad[1][i] = davg[1] - ddr*dr[1] + corr*dr[1];
+		}
+	}
+	const double muRe = CONSTVISC ? 1.0/G.Reinf : 0.5*( sutherland(G, ul) + sutherland(G, ur) );
+	const double kd = muRe / (G.Minf*G.Minf*(G.g-1.0)*G.Pr);
+	double ldiv = 0;
+	ldiv += grad[0][1]; ldiv += grad[1][2];
+	ldiv *= 2.0/3.0*muRe;
+	double s[2][2];
+	s[0][0] = muRe*(grad[0][1] + grad[0][1]); s[0][1] = muRe*(grad[0][2] + grad[1][1]);
+	s[0][0] -= ldiv;
+	s[1][0] = muRe*(grad[1][1] + grad[0][2]); s[1][1] = muRe*(grad[1][2] + grad[1][2]);
+	s[1][1] -= ldiv;
+	vf[0] = 0;
+	for(int i = 0; i < 2; i++) { double t = 0; t -= s[i][0]*n[0]; t -= s[i][1]*n[1]; vf[i+1] = t; }
+	double va[2];
+	va[0] = 0.5*( ul[1]/ul[0] + ur[1]/ur[0] );
+	va[1] = 0.5*( ul[2]/ul[0] + ur[2]/ur[0] );
+	double e = 0;
+	for(int i = 0; i < 2; i++) {
+		double comp = 0;
+		comp += s[i][0]*va[0]; comp += s[i][1]*va[1];
+		comp += kd*grad[i][3];
+		e -= comp * n[i];
+	}
+	vf[3] = e;
+}
+
+}
+}
+#endif

@@ -1,0 +1,566 @@
+/** \file kernels.hip
+ * \brief HIP kernels of the MI355X face sweep (gfx950, wave64).
+ *
+ * Pipeline of one residual evaluation (FlowFV::compute_residual, flow_spatial.cpp:636-816):
+ *   k_prep_cells   conserved -> primitive cell states                     (:697-699)
+ *   k_prep_bfaces  boundary ghost state of the cell value, and its primitive (:679-695)
+ *   k_grad_*       cell-centred primitive gradients (WLS / Green-Gauss)   (:704-708)
+ *   k_limiter/k_weno  per-cell limiter values for limited reconstructions (:720-723)
+ *   k_sweep        THE HOT KERNEL: per patch, every touching face is reconstructed, converted,
+ *                  given its BC ghost if on the boundary, its inviscid (+viscous) flux and
+ *                  spectral radii computed into LDS; then every cell of the patch sums its faces
+ *                  from LDS in ascending reference face index and writes -r and the time step
+ *                  (:731-812 incl. compute_fluxes :488-563 and compute_max_timestep :565-634).
+ * No atomics: the per-cell sum order is the reference's single-thread order, so results are
+ * deterministic and, with -ffp-contract=off, bitwise equal to it.
+ */
+#include "kernels.hpp"
+#include "layout.hpp"
+
+namespace fvhip {
+
+using namespace gd;
+
+__device__ __forceinline__ void ld4(const double* p, int i, double* o) {
+	const double4 v = reinterpret_cast<const double4*>(p)[i];
+	o[0] = v.x; o[1] = v.y; o[2] = v.z; o[3] = v.w;
+}
+__device__ __forceinline__ void st4(double* p, int i, const double* o) {
+	reinterpret_cast<double4*>(p)[i] = make_double4(o[0], o[1], o[2], o[3]);
+}
+__device__ __forceinline__ void ld8(const double* p, int i, double* o) {
+	const double4* q = reinterpret_cast<const double4*>(p) + 2*static_cast<size_t>(i);
+	const double4 a = q[0], b = q[1];
+	o[0] = a.x; o[1] = a.y; o[2] = a.z; o[3] = a.w; o[4] = b.x; o[5] = b.y; o[6] = b.z; o[7] = b.w;
+}
+__device__ __forceinline__ void st8(double* p, int i, const double* o) {
+	double4* q = reinterpret_cast<double4*>(p) + 2*static_cast<size_t>(i);
+	q[0] = make_double4(o[0], o[1], o[2], o[3]); q[1] = make_double4(o[4], o[5], o[6], o[7]);
+}
+
+// ------------------------------------------------------------------------------------------------
+// preparation
+// ------------------------------------------------------------------------------------------------
+__global__ void __launch_bounds__(256) k_prep_cells(int N, Gas G, const double* __restrict__ u, double* __restrict__ up)
+{
+	const int c = blockIdx.x*blockDim.x + threadIdx.x;
+	if(c >= N) return;
+	double a[4], b[4];
+	ld4(u, c, a);
+	cons2prim(G, a, b);
+	st4(up, c, b);
+}
+
+__global__ void __launch_bounds__(256) k_prep_bfaces(DevMesh M, DevPhys P, const double* __restrict__ u,
+                                                     double* __restrict__ ubc, double* __restrict__ ug)
+{
+	const int f = blockIdx.x*blockDim.x + threadIdx.x;
+	if(f >= M.nbface) return;
+	double a[4], g[4], p[4];
+	ld4(u, M.bf_L[f], a);
+	const double2 nn = M.bf_n[f];
+	const double n[2] = {nn.x, nn.y};
+	ghost_state(P.gas, P.bc[M.bf_bc[f]], P.uinf, a, n, g);
+	st4(ubc, f, g);
+	cons2prim(P.gas, g, p);
+	st4(ug, f, p);
+}
+
+// ------------------------------------------------------------------------------------------------
+// gradients (agradientschemes.cpp). One thread per cell; the cell's faces are visited in ascending
+// reference face index, which is the reference's single-thread accumulation order.
+// ------------------------------------------------------------------------------------------------
+__global__ void __launch_bounds__(256) k_grad_wls(DevMesh M, const double* __restrict__ up,
+                                                  const double* __restrict__ ug, double* __restrict__ grad)
+{
+	const int c = blockIdx.x*blockDim.x + threadIdx.x;
+	if(c >= M.ncell) return;
+	const int N = M.ncell;
+	const int4 cs = M.cell_slots[c];
+	const int e[4] = {cs.x, cs.y, cs.z, cs.w};
+	double f[8] = {0,0,0,0,0,0,0,0};
+	#pragma unroll
+	for(int k = 0; k < 4; k++) {
+		if(e[k] < 0) break;
+		const int2 lr = M.slot_LR[e[k] >> 1];
+		double uL[4], uR[4];
+		const double2 rl = M.rc[lr.x];
+		double2 rr;
+		ld4(up, lr.x, uL);
+		if(lr.y >= N) { rr = M.bf_rcbp[lr.y - N]; ld4(ug, lr.y - N, uR); }
+		else          { rr = M.rc[lr.y];           ld4(up, lr.y, uR); }
+		double w2 = 0;
+		w2 += (rl.x-rr.x)*(rl.x-rr.x);
+		w2 += (rl.y-rr.y)*(rl.y-rr.y);
+		const double dr0 = rl.x-rr.x, dr1 = rl.y-rr.y;
+		w2 = 1.0/(w2);
+		#pragma unroll
+		for(int iv = 0; iv < 4; iv++) {
+			const double du = uL[iv] - uR[iv];
+			f[iv*2+0] += w2*dr0*du;
+			f[iv*2+1] += w2*dr1*du;
+		}
+	}
+	const double4 V = M.wls_V[c];
+	double g[8];
+	#pragma unroll
+	for(int iv = 0; iv < 4; iv++) {
+		g[iv*2+0] = V.x*f[iv*2+0] + V.y*f[iv*2+1];
+		g[iv*2+1] = V.z*f[iv*2+0] + V.w*f[iv*2+1];
+	}
+	st8(grad, c, g);
+}
+
+__global__ void __launch_bounds__(256) k_grad_gg(DevMesh M, const double* __restrict__ up,
+                                                 const double* __restrict__ ug, double* __restrict__ grad)
+{
+	const int c = blockIdx.x*blockDim.x + threadIdx.x;
+	if(c >= M.ncell) return;
+	const int N = M.ncell;
+	const int4 cs = M.cell_slots[c];
+	const int e[4] = {cs.x, cs.y, cs.z, cs.w};
+	double g[8] = {0,0,0,0,0,0,0,0};
+	const double ainv = 1.0/M.area[c];
+	#pragma unroll
+	for(int k = 0; k < 4; k++) {
+		if(e[k] < 0) break;
+		const int s = e[k] >> 1;
+		const int2 lr = M.slot_LR[s];
+		const double2 mid = M.slot_gr[s];
+		const double2 nn = M.slot_n[s];
+		const double len = M.slot_len[s];
+		double uL[4], uR[4];
+		const double2 rl = M.rc[lr.x];
+		double2 rr;
+		ld4(up, lr.x, uL);
+		if(lr.y >= N) { rr = M.bf_rcbp[lr.y - N]; ld4(ug, lr.y - N, uR); }
+		else          { rr = M.rc[lr.y];           ld4(up, lr.y, uR); }
+		double dL = 0, dR = 0;
+		dL += (mid.x-rl.x)*(mid.x-rl.x); dR += (mid.x-rr.x)*(mid.x-rr.x);
+		dL += (mid.y-rl.y)*(mid.y-rl.y); dR += (mid.y-rr.y)*(mid.y-rr.y);
+		dL = 1.0/sqrt(dL);
+		dR = 1.0/sqrt(dR);
+		const bool right = e[k] & 1;
+		#pragma unroll
+		for(int iv = 0; iv < 4; iv++) {
+			const double ut = (uL[iv]*dL + uR[iv]*dR)/(dL+dR) * len;
+			if(!right) { g[iv*2+0] += (ut*nn.x)*ainv; g[iv*2+1] += (ut*nn.y)*ainv; }
+			else       { g[iv*2+0] -= (ut*nn.x)*ainv; g[iv*2+1] -= (ut*nn.y)*ainv; }
+		}
+	}
+	st8(grad, c, g);
+}
+
+// ------------------------------------------------------------------------------------------------
+// limiters (limitedlinearreconstruction.cpp:107-268). Physical-boundary neighbours use the ghost
+// primitive state (documented deviation: the reference reads past the end of its array there).
+// ------------------------------------------------------------------------------------------------
+template <bool VENK>
+__global__ void __launch_bounds__(256) k_limiter(DevMesh M, const double* __restrict__ up, const double* __restrict__ ug,
+                                                 const double* __restrict__ grad, double* __restrict__ phi)
+{
+	const int c = blockIdx.x*blockDim.x + threadIdx.x;
+	if(c >= M.ncell) return;
+	const int N = M.ncell;
+	double uc[4], g[8];
+	ld4(up, c, uc);
+	ld8(grad, c, g);
+	const int4 nb4 = M.cell_nbr[c], fs4 = M.cell_face[c];
+	const int nbr[4] = {nb4.x, nb4.y, nb4.z, nb4.w}, fcs[4] = {fs4.x, fs4.y, fs4.z, fs4.w};
+	const double2 r = M.rc[c];
+	const double eps2 = VENK ? M.venk_eps2[c] : 0.0;
+	double un[4][4];
+	double2 gp[4];
+	#pragma unroll
+	for(int j = 0; j < 4; j++) {
+		if(nbr[j] < 0) continue;
+		if(nbr[j] >= N) ld4(ug, nbr[j]-N, un[j]); else ld4(up, nbr[j], un[j]);
+		gp[j] = M.slot_gr[fcs[j]];
+	}
+	double out[4];
+	#pragma unroll
+	for(int iv = 0; iv < 4; iv++) {
+		double dmin = 0, dmax = 0;
+		#pragma unroll
+		for(int j = 0; j < 4; j++) {
+			if(nbr[j] < 0) continue;
+			const double d = un[j][iv]-uc[iv];
+			if(d > dmax) dmax = d;
+			if(d < dmin) dmin = d;
+		}
+		double lim = 1.0;
+		#pragma unroll
+		for(int j = 0; j < 4; j++) {
+			if(nbr[j] < 0) continue;
+			double uf = uc[iv];
+			uf += 1.0*g[iv*2+0]*(gp[j].x - r.x);
+			uf += 1.0*g[iv*2+1]*(gp[j].y - r.y);
+			double ph;
+			if(VENK) {
+				const double dm = uf - uc[iv];
+				const double dp = dm < 0 ? dmin : dmax;
+				ph = (dp*dp + 2*dp*dm + eps2)/(dp*dp + dp*dm + 2*dm*dm + eps2);
+			} else {
+				const double diff = uf - uc[iv];
+				if(diff > 0) ph = 1 < dmax/diff ? 1 : dmax/diff;
+				else if(diff < 0) ph = 1 < dmin/diff ? 1 : dmin/diff;
+				else ph = 1;
+			}
+			if(ph < lim) lim = ph;
+		}
+		out[iv] = lim;
+	}
+	st4(phi, c, out);
+}
+
+// WENO-limited gradients (limitedlinearreconstruction.cpp:27-105)
+__global__ void __launch_bounds__(256) k_weno(DevMesh M, double lambda, const double* __restrict__ grad,
+                                              double* __restrict__ lgrad)
+{
+	const int c = blockIdx.x*blockDim.x + threadIdx.x;
+	if(c >= M.ncell) return;
+	const int N = M.ncell;
+	const double gamma = 4.0, epsilon = 1.0e-5;
+	double g0[8];
+	ld8(grad, c, g0);
+	const int4 nb4 = M.cell_nbr[c];
+	const int nbr[4] = {nb4.x, nb4.y, nb4.z, nb4.w};
+	double gn[4][8];
+	#pragma unroll
+	for(int j = 0; j < 4; j++) if(nbr[j] >= 0 && nbr[j] < N) ld8(grad, nbr[j], gn[j]);
+	double out[8];
+	#pragma unroll
+	for(int iv = 0; iv < 4; iv++) {
+		double wsum = 0, l0 = 0, l1 = 0;
+		{
+			double m2 = 0; m2 += g0[iv*2]*g0[iv*2]; m2 += g0[iv*2+1]*g0[iv*2+1];
+			const double w = lambda / pow(m2 + epsilon, gamma);
+			wsum += w; l0 += w*g0[iv*2]; l1 += w*g0[iv*2+1];
+		}
+		#pragma unroll
+		for(int j = 0; j < 4; j++) {
+			if(nbr[j] < 0 || nbr[j] >= N) continue;
+			double m2 = 0; m2 += gn[j][iv*2]*gn[j][iv*2]; m2 += gn[j][iv*2+1]*gn[j][iv*2+1];
+			const double w = 1.0 / pow(m2 + epsilon, gamma);
+			wsum += w; l0 += w*gn[j][iv*2]; l1 += w*gn[j][iv*2+1];
+		}
+		out[iv*2] = l0/wsum; out[iv*2+1] = l1/wsum;
+	}
+	st8(lgrad, c, out);
+}
+
+// ------------------------------------------------------------------------------------------------
+// THE SWEEP
+// ------------------------------------------------------------------------------------------------
+
+/// MUSCL / Van Albada pieces (musclreconstruction.cpp:33-59)
+__device__ __forceinline__ double muscl_phi(double d, double du) {
+	const double eps = 1e-8;
+	double ph = (2.0*d * du + eps) / (d*d + du*du + eps);
+	return ph < 0.0 ? 0.0 : ph;
+}
+__device__ __forceinline__ double muscl_left(double ui, double uj, double dm, double ph) {
+	const double k = 1.0/3.0;
+	return ui + ph/4.0*( (1.0-k*ph)*dm + (1.0+k*ph)*(uj - ui) );
+}
+__device__ __forceinline__ double muscl_right(double ui, double uj, double dp, double ph) {
+	const double k = 1.0/3.0;
+	return uj - ph/4.0*( (1.0-k*ph)*dp + (1.0+k*ph)*(uj - ui) );
+}
+
+template <int FLUX, int REC, int VISC, bool DT, bool PHI>
+__global__ void __launch_bounds__(SLOTS_MAX) k_sweep(const DevMesh M, const DevPhys P, const SweepBuffers B)
+{
+	__shared__ double sf[4][SLOTS_MAX];
+	__shared__ double ssr[DT ? 2 : 1][DT ? SLOTS_MAX : 1];
+
+	// XCD-aware mapping: consecutive patches (which share halo cells) land on the same XCD
+	const int np = M.npatch;
+	const int q = (np + 7) >> 3;
+	const int p = (blockIdx.x & 7) * q + (blockIdx.x >> 3);
+	if(p >= np) return;
+	const int s0 = M.patch_slot[p], s1 = M.patch_slot[p+1];
+	const int c0 = M.patch_cell[p], c1 = M.patch_cell[p+1];
+	const int N = M.ncell;
+	const Gas& G = P.gas;
+
+	const int s = s0 + static_cast<int>(threadIdx.x);
+	if(s < s1) {
+		const int2 lr = M.slot_LR[s];
+		const double2 nn = M.slot_n[s];
+		const double len = M.slot_len[s];
+		const double n[2] = {nn.x, nn.y};
+		const bool bnd = lr.y >= N;
+		const int bf = lr.y - N;
+		double ul[4], ur[4];
+
+		if(REC == SR_FIRST) {
+			ld4(B.u, lr.x, ul);
+			if(bnd) ghost_state(G, P.bc[M.bf_bc[bf]], P.uinf, ul, n, ur);
+			else    ld4(B.u, lr.y, ur);
+		}
+		else if(REC == SR_MUSCL) {
+			const double2 ri = M.rc[lr.x];
+			double ui[4], gi[8];
+			ld4(B.up, lr.x, ui);
+			ld8(B.rgrad, lr.x, gi);
+			if(!bnd) {
+				const double2 rj = M.rc[lr.y];
+				double uj[4], gj[8];
+				ld4(B.up, lr.y, uj);
+				ld8(B.rgrad, lr.y, gj);
+				const double dx = rj.x-ri.x, dy = rj.y-ri.y;
+				#pragma unroll
+				for(int i = 0; i < 4; i++) {
+					double dl = 0; dl += gi[i*2]*dx; dl += gi[i*2+1]*dy;
+					double dr = 0; dr += gj[i*2]*dx; dr += gj[i*2+1]*dy;
+					const double du = uj[i] - ui[i];
+					const double dm = 2.0*dl - du;
+					const double dp = 2.0*dr - du;
+					ul[i] = muscl_left(ui[i], uj[i], dm, muscl_phi(dm, du));
+					ur[i] = muscl_right(ui[i], uj[i], dp, muscl_phi(dp, du));
+				}
+				prim2cons(G, ul, ul);
+				prim2cons(G, ur, ur);
+			} else {
+				const double2 rj = M.bf_rcbp[bf];
+				double uj[4];
+				ld4(B.ug, bf, uj);
+				const double dx = rj.x-ri.x, dy = rj.y-ri.y;
+				#pragma unroll
+				for(int i = 0; i < 4; i++) {
+					double dl = 0; dl += gi[i*2]*dx; dl += gi[i*2+1]*dy;
+					const double du = uj[i] - ui[i];
+					const double dm = 2.0*dl - du;
+					ul[i] = muscl_left(ui[i], uj[i], dm, muscl_phi(dm, du));
+				}
+				prim2cons(G, ul, ul);
+				ghost_state(G, P.bc[M.bf_bc[bf]], P.uinf, ul, n, ur);
+			}
+		}
+		else {  // SR_LINEAR: unlimited, WENO-limited gradients or BJ/Venkatakrishnan limiter values
+			const double2 gp = M.slot_gr[s];
+			{
+				const double2 ri = M.rc[lr.x];
+				double ui[4], gi[8], ph[4] = {1.0, 1.0, 1.0, 1.0};
+				ld4(B.up, lr.x, ui);
+				ld8(B.rgrad, lr.x, gi);
+				if(PHI) ld4(B.phi, lr.x, ph);
+				#pragma unroll
+				for(int i = 0; i < 4; i++) {
+					double v = ui[i];
+					v += ph[i]*gi[i*2]*(gp.x - ri.x);
+					v += ph[i]*gi[i*2+1]*(gp.y - ri.y);
+					ul[i] = v;
+				}
+				prim2cons(G, ul, ul);
+			}
+			if(!bnd) {
+				const double2 rj = M.rc[lr.y];
+				double uj[4], gj[8], ph[4] = {1.0, 1.0, 1.0, 1.0};
+				ld4(B.up, lr.y, uj);
+				ld8(B.rgrad, lr.y, gj);
+				if(PHI) ld4(B.phi, lr.y, ph);
+				#pragma unroll
+				for(int i = 0; i < 4; i++) {
+					double v = uj[i];
+					v += ph[i]*gj[i*2]*(gp.x - rj.x);
+					v += ph[i]*gj[i*2+1]*(gp.y - rj.y);
+					ur[i] = v;
+				}
+				prim2cons(G, ur, ur);
+			} else {
+				ghost_state(G, P.bc[M.bf_bc[bf]], P.uinf, ul, n, ur);
+			}
+		}
+
+		double f[4];
+		inviscid_flux<FLUX>(G, ul, ur, n, f);
+		#pragma unroll
+		for(int k = 0; k < 4; k++) f[k] *= len;
+
+		if(VISC != SV_NONE) {
+			double ucl[4], ucr[4], gl[8], gr[8];
+			const double2 rl = M.rc[lr.x];
+			double2 rr;
+			ld4(B.u, lr.x, ucl);
+			if(bnd) {
+				rr = M.bf_rcbp[bf];
+				if(REC == SR_FIRST) { for(int k = 0; k < 4; k++) ucr[k] = ur[k]; }
+				else ld4(B.ubc, bf, ucr);
+			} else {
+				rr = M.rc[lr.y];
+				ld4(B.u, lr.y, ucr);
+			}
+			if(REC != SR_FIRST) {
+				ld8(B.grad, lr.x, gl);
+				ld8(B.grad, bnd ? lr.x : lr.y, gr);
+			}
+			const double rcl[2] = {rl.x, rl.y}, rcr[2] = {rr.x, rr.y};
+			double vf[4];
+			viscous_flux<REC != SR_FIRST, VISC == SV_CONST>(G, n, rcl, rcr, ucl, ucr, gl, gr, ul, ur, vf);
+			#pragma unroll
+			for(int k = 0; k < 4; k++) f[k] += vf[k]*len;
+		}
+
+		const int ls = s - s0;
+		sf[0][ls] = f[0]; sf[1][ls] = f[1]; sf[2][ls] = f[2]; sf[3][ls] = f[3];
+
+		if(DT) {
+			const double ci = sound_speed_cons(G, ul), cj = sound_speed_cons(G, ur);
+			const double vni = dot2(&ul[1],n)/ul[0];
+			const double vnj = dot2(&ur[1],n)/ur[0];
+			double sri = (fabs(vni)+ci)*len;
+			double srj = (fabs(vnj)+cj)*len;
+			if(VISC != SV_NONE) {
+				const double mui = VISC == SV_CONST ? 1.0/G.Reinf : sutherland(G, ul);
+				const double muj = VISC == SV_CONST ? 1.0/G.Reinf : sutherland(G, ur);
+				const double ai = 4.0/(3*ul[0]), bi = G.g/ul[0];
+				const double aj = 4.0/(3*ur[0]), bj = G.g/ur[0];
+				const double coi = (ai < bi) ? bi : ai;          // std::max
+				const double coj = (aj < bj) ? bj : aj;
+				sri += coi*mui/G.Pr * len*len/M.area[lr.x];
+				if(!bnd) srj += coj*muj/G.Pr * len*len/M.area[lr.y];
+			}
+			ssr[0][ls] = sri;
+			ssr[1][ls] = srj;
+		}
+	}
+	__syncthreads();
+
+	const int c = c0 + static_cast<int>(threadIdx.x);
+	if(c < c1) {
+		double r[4];
+		if(B.overwrite) { r[0] = r[1] = r[2] = r[3] = 0.0; }
+		else ld4(B.r, c, r);
+		double integ = 0.0;
+		const int4 cs = M.cell_slots[c];
+		const int e[4] = {cs.x, cs.y, cs.z, cs.w};
+		#pragma unroll
+		for(int k = 0; k < 4; k++) {
+			if(e[k] < 0) break;
+			const int ls = (e[k] >> 1) - s0;
+			if(e[k] & 1) {
+				r[0] += sf[0][ls]; r[1] += sf[1][ls]; r[2] += sf[2][ls]; r[3] += sf[3][ls];
+				if(DT) integ += ssr[1][ls];
+			} else {
+				r[0] -= sf[0][ls]; r[1] -= sf[1][ls]; r[2] -= sf[2][ls]; r[3] -= sf[3][ls];
+				if(DT) integ += ssr[0][ls];
+			}
+		}
+		st4(B.r, c, r);
+		if(DT) B.dtm[c] = M.area[c]/integ;
+	}
+}
+
+// ------------------------------------------------------------------------------------------------
+// misc
+// ------------------------------------------------------------------------------------------------
+__global__ void k_fill(double* p, double v, long long n)
+{
+	const long long i = static_cast<long long>(blockIdx.x)*blockDim.x + threadIdx.x;
+	if(i < n) p[i] = v;
+}
+
+__global__ void k_local_flux(int type, Gas G, int nf, const double* ul, const double* ur, const double* n, double* f)
+{
+	const int i = blockIdx.x*blockDim.x + threadIdx.x;
+	if(i >= nf) return;
+	double a[4], b[4], o[4];
+	ld4(ul, i, a); ld4(ur, i, b);
+	const double nn[2] = {n[2*i], n[2*i+1]};
+	inviscid_flux_rt(type, G, a, b, nn, o);
+	st4(f, i, o);
+}
+
+__global__ void k_gather(const int* perm, const double* src, double* dst, int n, int width)
+{
+	const long long i = static_cast<long long>(blockIdx.x)*blockDim.x + threadIdx.x;
+	if(i >= static_cast<long long>(n)*width) return;
+	const int c = static_cast<int>(i / width), w = static_cast<int>(i % width);
+	dst[i] = src[static_cast<size_t>(perm[c])*width + w];
+}
+
+// ------------------------------------------------------------------------------------------------
+// launchers
+// ------------------------------------------------------------------------------------------------
+static inline int nblk(long long n, int b) { return static_cast<int>((n + b - 1)/b); }
+
+void launch_prep(const DevMesh& M, const DevPhys& P, const double* u, double* up, double* ubc, double* ug,
+                 bool cells, hipStream_t s)
+{
+	if(cells && M.ncell > 0) k_prep_cells<<<nblk(M.ncell,256), 256, 0, s>>>(M.ncell, P.gas, u, up);
+	if(M.nbface > 0) k_prep_bfaces<<<nblk(M.nbface,256), 256, 0, s>>>(M, P, u, ubc, ug);
+}
+void launch_grad_wls(const DevMesh& M, const double* up, const double* ug, double* grad, hipStream_t s)
+{ if(M.ncell > 0) k_grad_wls<<<nblk(M.ncell,256), 256, 0, s>>>(M, up, ug, grad); }
+void launch_grad_gg(const DevMesh& M, const double* up, const double* ug, double* grad, hipStream_t s)
+{ if(M.ncell > 0) k_grad_gg<<<nblk(M.ncell,256), 256, 0, s>>>(M, up, ug, grad); }
+void launch_limiter(const DevMesh& M, const DevPhys& P, int venk, const double* up, const double* ug,
+                    const double* grad, double* phi, hipStream_t s)
+{
+	if(M.ncell <= 0) return;
+	if(venk) k_limiter<true><<<nblk(M.ncell,256), 256, 0, s>>>(M, up, ug, grad, phi);
+	else     k_limiter<false><<<nblk(M.ncell,256), 256, 0, s>>>(M, up, ug, grad, phi);
+}
+void launch_weno(const DevMesh& M, const DevPhys& P, const double* grad, double* lgrad, hipStream_t s)
+{ if(M.ncell > 0) k_weno<<<nblk(M.ncell,256), 256, 0, s>>>(M, P.limiter_param, grad, lgrad); }
+void launch_fill(double* p, double v, long long n, hipStream_t s)
+{ if(n > 0) k_fill<<<nblk(n,256), 256, 0, s>>>(p, v, n); }
+void launch_local_flux(int flux, const Gas& G, int nf, const double* ul, const double* ur,
+                       const double* n, double* f, hipStream_t s)
+{ if(nf > 0) k_local_flux<<<nblk(nf,256), 256, 0, s>>>(flux, G, nf, ul, ur, n, f); }
+void launch_gather_cells(const int* perm, const double* src, double* dst, int n, int width, hipStream_t s)
+{ if(n > 0) k_gather<<<nblk(static_cast<long long>(n)*width,256), 256, 0, s>>>(perm, src, dst, n, width); }
+
+// sweep dispatch over (flux, reconstruction, viscous, dt, phi)
+typedef void (*SweepFn)(const DevMesh, const DevPhys, const SweepBuffers);
+
+template <int FLUX, int REC, int VISC>
+static SweepFn pick4(bool dt, bool phi) {
+	if(REC == SR_LINEAR) {
+		if(dt) return phi ? k_sweep<FLUX,REC,VISC,true,true> : k_sweep<FLUX,REC,VISC,true,false>;
+		return phi ? k_sweep<FLUX,REC,VISC,false,true> : k_sweep<FLUX,REC,VISC,false,false>;
+	}
+	return dt ? k_sweep<FLUX,REC,VISC,true,false> : k_sweep<FLUX,REC,VISC,false,false>;
+}
+template <int FLUX, int REC>
+static SweepFn pick3(int visc, bool dt, bool phi) {
+	switch(visc) {
+		case SV_NONE: return pick4<FLUX,REC,SV_NONE>(dt, phi);
+		case SV_SUTHERLAND: return pick4<FLUX,REC,SV_SUTHERLAND>(dt, phi);
+		default: return pick4<FLUX,REC,SV_CONST>(dt, phi);
+	}
+}
+template <int FLUX>
+static SweepFn pick2(int rec, int visc, bool dt, bool phi) {
+	switch(rec) {
+		case SR_FIRST: return pick3<FLUX,SR_FIRST>(visc, dt, phi);
+		case SR_MUSCL: return pick3<FLUX,SR_MUSCL>(visc, dt, phi);
+		default: return pick3<FLUX,SR_LINEAR>(visc, dt, phi);
+	}
+}
+
+static const char* kSweepNames[7] = {"k_sweep<LLF>", "k_sweep<VANLEER>", "k_sweep<AUSM>", "k_sweep<AUSMPLUS>",
+                                     "k_sweep<ROE>", "k_sweep<HLL>", "k_sweep<HLLC>"};
+
+const char* launch_sweep(const DevMesh& M, const DevPhys& P, const SweepBuffers& B, int flux, int rec,
+                         int visc, bool dt, hipStream_t s)
+{
+	const bool phi = B.phi != nullptr;
+	SweepFn fn;
+	switch(flux) {
+		case 0: fn = pick2<0>(rec, visc, dt, phi); break;
+		case 1: fn = pick2<1>(rec, visc, dt, phi); break;
+		case 2: fn = pick2<2>(rec, visc, dt, phi); break;
+		case 3: fn = pick2<3>(rec, visc, dt, phi); break;
+		case 4: fn = pick2<4>(rec, visc, dt, phi); break;
+		case 5: fn = pick2<5>(rec, visc, dt, phi); break;
+		default: fn = pick2<6>(rec, visc, dt, phi); break;
+	}
+	const int q = (M.npatch + 7) / 8;
+	if(M.npatch > 0) hipLaunchKernelGGL(fn, dim3(8*q), dim3(SLOTS_MAX), 0, s, M, P, B);
+	return kSweepNames[flux < 0 || flux > 6 ? 6 : flux];
+}
+
+}

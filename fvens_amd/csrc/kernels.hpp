@@ -1,0 +1,81 @@
+/** \file kernels.hpp
+ * \brief Launch interface of the HIP kernels of the face sweep (kernels.hip).
+ */
+#ifndef FVHIP_KERNELS_HPP
+#define FVHIP_KERNELS_HPP
+
+#include <hip/hip_runtime.h>
+#include "gasdyn.hpp"
+
+namespace fvhip {
+
+constexpr int MAXBC = 16;
+
+/// Reconstruction kinds of the fused sweep
+enum SweepRec { SR_FIRST = 0, SR_MUSCL = 1, SR_LINEAR = 2 };
+/// Viscous kinds
+enum SweepVisc { SV_NONE = 0, SV_SUTHERLAND = 1, SV_CONST = 2 };
+
+struct DevMesh
+{
+	int ncell, nbface, npatch, nslot;
+	const int* patch_cell;     // [npatch+1]
+	const int* patch_slot;     // [npatch+1]
+	const int2* slot_LR;       // [S]
+	const double2* slot_n;     // [S]
+	const double* slot_len;    // [S]
+	const double2* slot_gr;    // [S]
+	const int4* cell_slots;    // [N] (slot<<1 | isRight), -1 padded, ascending reference face
+	const int4* cell_nbr;      // [N] esuel order neighbours (internal / ncell+bf)
+	const int4* cell_face;     // [N] esuel order slots
+	const double2* rc;         // [N]
+	const double* area;        // [N]
+	const double4* wls_V;      // [N] row-major 2x2
+	const double* venk_eps2;   // [N]
+	const int* bf_L;           // [nb]
+	const int* bf_bc;          // [nb]
+	const double2* bf_n;       // [nb]
+	const double2* bf_rcbp;    // [nb]
+};
+
+struct DevPhys
+{
+	gd::Gas gas;
+	double uinf[4];
+	gd::BCDev bc[MAXBC];
+	int nbc;
+	double limiter_param;
+};
+
+struct SweepBuffers
+{
+	const double* u;      // [N][4] conserved
+	const double* up;     // [N][4] primitive (order 2)
+	const double* grad;   // [N][8] primitive gradients (viscous term)
+	const double* rgrad;  // [N][8] gradients used for reconstruction (grad, or WENO-limited)
+	const double* phi;    // [N][4] limiter values (BJ/Venkatakrishnan) or null
+	const double* ubc;    // [nb][4] conserved ghost state of the cell value (order 2)
+	const double* ug;     // [nb][4] primitive ghost state of the cell value (order 2)
+	double* r;            // [N][4]
+	double* dtm;          // [N]
+	int overwrite;
+};
+
+// host launchers (all asynchronous on stream)
+void launch_prep(const DevMesh& M, const DevPhys& P, const double* u, double* up, double* ubc, double* ug,
+                 bool cells, hipStream_t s);
+void launch_grad_wls(const DevMesh& M, const double* up, const double* ug, double* grad, hipStream_t s);
+void launch_grad_gg(const DevMesh& M, const double* up, const double* ug, double* grad, hipStream_t s);
+void launch_limiter(const DevMesh& M, const DevPhys& P, int venk, const double* up, const double* ug,
+                    const double* grad, double* phi, hipStream_t s);
+void launch_weno(const DevMesh& M, const DevPhys& P, const double* grad, double* lgrad, hipStream_t s);
+/// returns kernel name for profiling
+const char* launch_sweep(const DevMesh& M, const DevPhys& P, const SweepBuffers& B, int flux, int rec,
+                         int visc, bool dt, hipStream_t s);
+void launch_fill(double* p, double v, long long n, hipStream_t s);
+void launch_local_flux(int flux, const gd::Gas& G, int nf, const double* ul, const double* ur,
+                       const double* n, double* f, hipStream_t s);
+void launch_gather_cells(const int* perm, const double* src, double* dst, int n, int width, hipStream_t s);
+
+}
+#endif

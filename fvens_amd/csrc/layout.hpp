@@ -1,0 +1,68 @@
+/** \file layout.hpp
+ * \brief Device data layout for the MI355X face sweep.
+ *
+ * Cells are renumbered internally along a Hilbert curve and cut into PATCHES: contiguous ranges
+ * of internal cells whose touching faces number at most SLOTS_MAX. A patch is processed by one
+ * workgroup: each face touching the patch gets a SLOT (faces shared by two patches are stored,
+ * and computed, once per patch), its flux goes to LDS, and every cell then sums its faces from
+ * LDS in ascending reference face index — the single-thread order of the reference's
+ * `omp atomic` scatter (flow_spatial.cpp:552-561) — so residuals are deterministic and
+ * reproduce the reference bit for bit. Exported indices are never changed.
+ */
+#ifndef FVHIP_LAYOUT_HPP
+#define FVHIP_LAYOUT_HPP
+
+#include <vector>
+#include <cstdint>
+#include "../../include/fvhip.h"
+
+namespace fvhip {
+
+constexpr int SLOTS_MAX = 512;   ///< faces per patch = threads per sweep workgroup
+constexpr int CELLS_MAX = 512;
+constexpr int MAXF = 4;          ///< max faces per cell (linear tri/quad)
+
+struct Layout
+{
+	int ncell = 0;               ///< owned cells
+	int nbface = 0, naface = 0, ninface = 0;
+	std::vector<int> perm;       ///< perm[internal] = reference cell
+	std::vector<int> iperm;      ///< iperm[reference] = internal
+	// patches
+	std::vector<int> patch_cell;   ///< [npatch+1] start of each patch's cells (internal ids)
+	std::vector<int> patch_slot;   ///< [npatch+1] start of each patch's slots
+	// slots (patch order; faces touching two patches appear twice)
+	std::vector<int> slot_L, slot_R;       ///< internal cell ids; R >= ncell: physical boundary R-ncell
+	std::vector<int> slot_face;            ///< reference face index
+	std::vector<double> slot_n;            ///< [S][2]
+	std::vector<double> slot_len;          ///< [S]
+	std::vector<double> slot_gr;           ///< [S][2]
+	// cells (internal order)
+	std::vector<int> cell_slots;           ///< [ncell][4]: (slot << 1 | cell-is-right) of the cell's
+	                                       ///<  faces in ascending reference face index, -1 padded;
+	                                       ///<  the slot is the copy in the cell's own patch
+	std::vector<int> cell_nbr_local;       ///< [ncell][4]: esuel neighbours (internal or boundary
+	                                       ///<  code ncell+bf) in local-face order (WENO, limiters)
+	std::vector<int> cell_face_local;      ///< [ncell][4]: slot of local face j (own patch)
+	std::vector<int> cell_nfael;
+	std::vector<double> rc;                ///< [ncell][2]
+	std::vector<double> area;              ///< [ncell]
+	std::vector<double> wls_V;             ///< [ncell][4] WLS inverse, row-major (if built)
+	std::vector<double> venk_eps2;         ///< [ncell] (K*clength)^3 (if built)
+	// boundary faces (reference order)
+	std::vector<int> bf_L;                 ///< internal id of the boundary cell
+	std::vector<int> bf_bc;                ///< index into the BC table
+	std::vector<double> bf_n;              ///< [nb][2]
+	std::vector<double> bf_rcbp;           ///< [nb][2]
+	// interior faces (reference order, for the Jacobian): internal L, R
+	std::vector<int> if_L, if_R;
+	std::vector<int> if_slot;              ///< one slot carrying the face's geometry
+	int max_slots = 0;
+};
+
+/// Builds the layout from the reference's mesh arrays. bc_of_tag maps a boundary marker to the
+/// index of its BC in the config. Throws std::runtime_error on unsupported meshes.
+Layout buildLayout(const fvhip_mesh& m, const fvhip_flow_config& cfg, bool renumber);
+
+}
+#endif

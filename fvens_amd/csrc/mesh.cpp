@@ -1,0 +1,600 @@
+/** \file mesh.cpp
+ * \brief Host mesh ingest, the reference face-indexing contract, geometry and generators.
+ * See mesh.hpp for the reference lines each routine reproduces.
+ */
+#include "mesh.hpp"
+
+#include <cmath>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <fstream>
+#include <sstream>
+#include <stdexcept>
+#include <algorithm>
+#include <numeric>
+
+namespace fvhip {
+
+// ------------------------------------------------------------------------------------------------
+// Gmsh 2.2 ASCII (meshreaders.cpp:66-265)
+// ------------------------------------------------------------------------------------------------
+
+namespace {
+
+/// Minimal fast tokenizer over a whole file; numbers parsed with strtol/strtod, which is what
+/// std::istream's num_get reduces to, so coordinates round identically to the reference reader.
+struct Tok
+{
+	std::vector<char> buf;
+	size_t pos = 0;
+	explicit Tok(const std::string& path) {
+		std::ifstream f(path, std::ios::binary);
+		if(!f) throw std::runtime_error("readGmsh2: cannot open " + path);
+		f.seekg(0, std::ios::end);
+		const size_t n = static_cast<size_t>(f.tellg());
+		f.seekg(0);
+		buf.resize(n+1);
+		f.read(buf.data(), static_cast<std::streamsize>(n));
+		buf[n] = '\0';
+	}
+	void skipLine() {
+		while(pos < buf.size() && buf[pos] != '\n') pos++;
+		if(pos < buf.size()) pos++;
+	}
+	void skipWs() { while(buf[pos] && isspace(static_cast<unsigned char>(buf[pos]))) pos++; }
+	long getInt() {
+		skipWs(); char* e; const long v = strtol(&buf[pos], &e, 10);
+		if(e == &buf[pos]) throw std::runtime_error("readGmsh2: expected integer");
+		pos = static_cast<size_t>(e - buf.data()); return v;
+	}
+	double getDouble() {
+		skipWs(); char* e; const double v = strtod(&buf[pos], &e);
+		if(e == &buf[pos]) throw std::runtime_error("readGmsh2: expected real");
+		pos = static_cast<size_t>(e - buf.data()); return v;
+	}
+	std::string getWord() {
+		skipWs(); const size_t s = pos;
+		while(buf[pos] && !isspace(static_cast<unsigned char>(buf[pos]))) pos++;
+		return std::string(&buf[s], pos-s);
+	}
+};
+
+}
+
+MeshData readGmsh2(const std::string& path)
+{
+	Tok t(path);
+	MeshData m;
+	for(int i = 0; i < 4; i++) t.skipLine();           // meshreaders.cpp:74-77
+
+	m.npoin = static_cast<int>(t.getInt());
+	m.coords.resize(static_cast<size_t>(m.npoin)*2);
+	for(int i = 0; i < m.npoin; i++) {
+		t.getInt();
+		m.coords[2*i] = t.getDouble();
+		m.coords[2*i+1] = t.getDouble();
+		t.getDouble();                                  // z dropped (NDIM < 3)
+	}
+	t.getWord(); t.getWord();                           // $EndNodes $Elements
+
+	const int nelm = static_cast<int>(t.getInt());
+	constexpr int width = 25;
+	std::vector<int> elms(static_cast<size_t>(nelm)*width, 0);
+	std::vector<int> nnodes(nelm, 0), nfaels(nelm, 0);
+	m.ndtag = 0; m.nbtag = 0; m.nbface = 0; m.nelem = 0;
+	for(int i = 0; i < nelm; i++)
+	{
+		int* e = &elms[static_cast<size_t>(i)*width];
+		t.getInt();
+		const int type = static_cast<int>(t.getInt());
+		int nn = 0, nfa = 0; bool isface = false;
+		switch(type) {
+			case 1: m.nnofa = 2; isface = true; break;
+			case 8: m.nnofa = 3; isface = true; break;
+			case 2: nn = 3; nfa = 3; m.nnofa = 2; break;
+			case 3: nn = 4; nfa = 4; m.nnofa = 2; break;
+			case 9: nn = 6; nfa = 3; m.nnofa = 3; break;
+			case 16: nn = 8; nfa = 4; m.nnofa = 3; break;
+			case 10: nn = 9; nfa = 4; m.nnofa = 3; break;
+			default: nn = 3; nfa = 3; m.nnofa = 2;       // meshreaders.cpp:197-209
+		}
+		const int ntags = static_cast<int>(t.getInt());
+		if(isface) {
+			if(ntags > m.nbtag) m.nbtag = ntags;
+			for(int j = 0; j < ntags; j++) e[j+m.nnofa] = static_cast<int>(t.getInt());
+			for(int j = 0; j < m.nnofa; j++) e[j] = static_cast<int>(t.getInt());
+			m.nbface++;
+		} else {
+			nnodes[i] = nn; nfaels[i] = nfa;
+			if(ntags > m.ndtag) m.ndtag = ntags;
+			for(int j = 0; j < ntags; j++) e[j+nn] = static_cast<int>(t.getInt());
+			for(int j = 0; j < nn; j++) e[j] = static_cast<int>(t.getInt());
+			m.nelem++;
+		}
+	}
+	if(m.nnofa != 2)
+		throw std::runtime_error("readGmsh2: only linear meshes are supported by the device path");
+
+	m.maxnnode = nnodes[m.nbface]; m.maxnfael = nfaels[m.nbface];   // meshreaders.cpp:218-226
+	for(int i = 0; i < nelm; i++) {
+		m.maxnnode = std::max(m.maxnnode, nnodes[i]);
+		m.maxnfael = std::max(m.maxnfael, nfaels[i]);
+	}
+
+	const int bw = m.nnofa + m.nbtag;
+	m.bface.assign(static_cast<size_t>(m.nbface)*bw, 0);
+	for(int i = 0; i < m.nbface; i++) {
+		const int* e = &elms[static_cast<size_t>(i)*width];
+		for(int j = 0; j < m.nnofa; j++) m.bface[i*bw+j] = e[j]-1;
+		for(int j = m.nnofa; j < bw; j++) m.bface[i*bw+j] = e[j];
+	}
+	m.inpoel.assign(static_cast<size_t>(m.nelem)*m.maxnnode, -1);
+	m.vol_regions.assign(static_cast<size_t>(m.nelem)*m.ndtag, 0);
+	m.nnode.resize(m.nelem); m.nfael.resize(m.nelem);
+	for(int i = 0; i < m.nelem; i++) {
+		const int k = i + m.nbface;
+		const int* e = &elms[static_cast<size_t>(k)*width];
+		for(int j = 0; j < nnodes[k]; j++) m.inpoel[static_cast<size_t>(i)*m.maxnnode+j] = e[j]-1;
+		for(int j = 0; j < m.ndtag; j++) m.vol_regions[static_cast<size_t>(i)*m.ndtag+j] = e[j+nnodes[k]];
+		m.nnode[i] = nnodes[k]; m.nfael[i] = nfaels[k];
+	}
+	return m;
+}
+
+void writeGmsh2(const MeshData& m, const std::string& path)
+{
+	FILE* f = fopen(path.c_str(), "w");
+	if(!f) throw std::runtime_error("writeGmsh2: cannot open " + path);
+	fprintf(f, "$MeshFormat\n2.2 0 8\n$EndMeshFormat\n$Nodes\n%d\n", m.npoin);
+	for(int i = 0; i < m.npoin; i++)
+		fprintf(f, "%d %.17g %.17g 0\n", i+1, m.coords[2*i], m.coords[2*i+1]);
+	fprintf(f, "$EndNodes\n$Elements\n%d\n", m.nbface + m.nelem);
+	const int bw = m.nnofa + m.nbtag;
+	int id = 1;
+	for(int i = 0; i < m.nbface; i++) {
+		fprintf(f, "%d 1 %d", id++, m.nbtag);
+		for(int j = 0; j < m.nbtag; j++) fprintf(f, " %d", m.bface[i*bw+m.nnofa+j]);
+		for(int j = 0; j < m.nnofa; j++) fprintf(f, " %d", m.bface[i*bw+j]+1);
+		fprintf(f, "\n");
+	}
+	for(int i = 0; i < m.nelem; i++) {
+		fprintf(f, "%d %d %d", id++, m.nnode[i] == 3 ? 2 : 3, m.ndtag);
+		for(int j = 0; j < m.ndtag; j++) fprintf(f, " %d", m.vol_regions[static_cast<size_t>(i)*m.ndtag+j]);
+		for(int j = 0; j < m.nnode[i]; j++) fprintf(f, " %d", m.inpoel[static_cast<size_t>(i)*m.maxnnode+j]+1);
+		fprintf(f, "\n");
+	}
+	fprintf(f, "$EndElements\n");
+	fclose(f);
+}
+
+// ------------------------------------------------------------------------------------------------
+// Topology
+// ------------------------------------------------------------------------------------------------
+
+namespace {
+
+/// CSR elements-surrounding-points (mesh.cpp:425-465); elements listed in increasing order.
+void buildEsup(const MeshData& m, std::vector<int>& esup_p, std::vector<int>& esup)
+{
+	esup_p.assign(m.npoin+1, 0);
+	for(int i = 0; i < m.nelem; i++)
+		for(int j = 0; j < m.nnode[i]; j++)
+			esup_p[m.inpoel[static_cast<size_t>(i)*m.maxnnode+j]+1]++;
+	for(int i = 1; i <= m.npoin; i++) esup_p[i] += esup_p[i-1];
+	esup.resize(esup_p[m.npoin]);
+	std::vector<int> fill(esup_p.begin(), esup_p.end()-1);
+	for(int i = 0; i < m.nelem; i++)
+		for(int j = 0; j < m.nnode[i]; j++)
+			esup[fill[m.inpoel[static_cast<size_t>(i)*m.maxnnode+j]]++] = i;
+}
+
+inline int nodeOf(const MeshData& m, int iel, int j) {
+	return m.inpoel[static_cast<size_t>(iel)*m.maxnnode + j];
+}
+
+/// Local face of element iel whose node set is {a,b}; -1 if none. (getFaceEIndex, mesh.cpp:560)
+inline int faceWithNodes(const MeshData& m, int iel, int a, int b)
+{
+	const int nn = m.nnode[iel];
+	for(int f = 0; f < m.nfael[iel]; f++) {
+		const int p = nodeOf(m, iel, f % nn), q = nodeOf(m, iel, (f+1) % nn);
+		if((p == a && q == b) || (p == b && q == a)) return f;
+	}
+	return -1;
+}
+
+/// Host element and local face of each boundary face (compute_phyBFaceNeighboringElements,
+/// mesh.cpp:608-657): the unique element containing both nodes.
+void bfaceHosts(const MeshData& m, const std::vector<int>& esup_p, const std::vector<int>& esup,
+                std::vector<int>& helem, std::vector<int>& hface)
+{
+	const int bw = m.nnofa + m.nbtag;
+	helem.assign(m.nbface, -1); hface.assign(m.nbface, -1);
+	for(int i = 0; i < m.nbface; i++) {
+		const int a = m.bface[i*bw], b = m.bface[i*bw+1];
+		int found = 0;
+		for(int k = esup_p[a]; k < esup_p[a+1]; k++) {
+			const int e = esup[k];
+			bool hasb = false;
+			for(int j = 0; j < m.nnode[e]; j++) if(nodeOf(m,e,j) == b) hasb = true;
+			if(hasb) {
+				if(found) throw std::logic_error("More than one neighboring element found for bface "
+				                                 + std::to_string(i));
+				helem[i] = e; found = 1;
+			}
+		}
+		if(!found) throw std::logic_error("No host element for bface " + std::to_string(i));
+		hface[i] = faceWithNodes(m, helem[i], a, b);
+		if(hface[i] < 0) throw std::logic_error("bface is not an element face");
+	}
+}
+
+/// Drops points not referenced by any cell, keeping the sorted order, exactly as the 1-rank
+/// restriction does (meshpartitioning.cpp:185-222, 36-66).
+void compactPoints(MeshData& m)
+{
+	std::vector<char> used(m.npoin, 0);
+	for(int i = 0; i < m.nelem; i++)
+		for(int j = 0; j < m.nnode[i]; j++) used[nodeOf(m,i,j)] = 1;
+	std::vector<int> g2l(m.npoin, -1);
+	int n = 0;
+	for(int p = 0; p < m.npoin; p++) if(used[p]) g2l[p] = n++;
+	if(n == m.npoin) return;
+	std::vector<double> c(static_cast<size_t>(n)*2);
+	for(int p = 0; p < m.npoin; p++)
+		if(used[p]) { c[2*g2l[p]] = m.coords[2*p]; c[2*g2l[p]+1] = m.coords[2*p+1]; }
+	m.coords.swap(c);
+	for(auto& v : m.inpoel) if(v >= 0) v = g2l[v];
+	const int bw = m.nnofa + m.nbtag;
+	for(int i = 0; i < m.nbface; i++)
+		for(int j = 0; j < m.nnofa; j++) m.bface[i*bw+j] = g2l[m.bface[i*bw+j]];
+	m.npoin = n;
+}
+
+}
+
+Mesh buildMesh(MeshData md)
+{
+	if(md.nnofa != 2) throw std::runtime_error("buildMesh: linear 2D meshes only");
+	Mesh M;
+	std::vector<int> esup_p, esup, helem, hface;
+
+	// correctBoundaryFaceOrientation (mesh.cpp:55-82)
+	buildEsup(md, esup_p, esup);
+	bfaceHosts(md, esup_p, esup, helem, hface);
+	const int bw = md.nnofa + md.nbtag;
+	for(int i = 0; i < md.nbface; i++) {
+		const int e = helem[i], f = hface[i], nn = md.nnode[e];
+		if(nodeOf(md,e,(f+0)%nn) != md.bface[i*bw] || nodeOf(md,e,(f+1)%nn) != md.bface[i*bw+1])
+			std::swap(md.bface[i*bw], md.bface[i*bw+1]);
+	}
+
+	// 1-rank restriction (drops unused points) then preprocessMesh's compute_topological
+	compactPoints(md);
+	buildEsup(md, esup_p, esup);
+
+	const int N = md.nelem, mf = md.maxnfael;
+	M.esuel.assign(static_cast<size_t>(N)*mf, -1);
+	// compute_elementsSurroundingElements (mesh.cpp:467-541): neighbour across each local face
+	for(int ie = 0; ie < N; ie++) {
+		const int nn = md.nnode[ie];
+		for(int f = 0; f < md.nfael[ie]; f++) {
+			const int a = nodeOf(md,ie,f%nn), b = nodeOf(md,ie,(f+1)%nn);
+			for(int k = esup_p[a]; k < esup_p[a+1]; k++) {
+				const int je = esup[k];
+				if(je == ie) continue;
+				const int jf = faceWithNodes(md, je, a, b);
+				if(jf >= 0) {
+					M.esuel[static_cast<size_t>(ie)*mf+f] = je;
+					M.esuel[static_cast<size_t>(je)*mf+jf] = ie;
+				}
+			}
+		}
+	}
+
+	// compute_faceConnectivity (mesh.cpp:659-762), nconnface = 0 on a single domain
+	M.nconnface = 0;
+	int ninface = 0;
+	for(int ie = 0; ie < N; ie++)
+		for(int in = 0; in < md.nfael[ie]; in++) {
+			const int je = M.esuel[static_cast<size_t>(ie)*mf+in];
+			if(je > ie && je < N) ninface++;
+		}
+	M.ninface = ninface;
+	M.naface = ninface + md.nbface + M.nconnface;
+	M.intfac.assign(static_cast<size_t>(M.naface)*4, -1);
+	M.elemface.assign(static_cast<size_t>(N)*mf, -1);
+	M.btags.assign(static_cast<size_t>(md.nbface)*md.nbtag, 0);
+
+	bfaceHosts(md, esup_p, esup, helem, hface);
+	for(int i = 0; i < md.nbface; i++) {
+		M.intfac[4*i+0] = helem[i];
+		M.intfac[4*i+1] = N + M.nconnface + i;
+		M.intfac[4*i+2] = md.bface[i*bw];
+		M.intfac[4*i+3] = md.bface[i*bw+1];
+		for(int j = 0; j < md.nbtag; j++) M.btags[i*md.nbtag+j] = md.bface[i*bw+md.nnofa+j];
+		M.esuel[static_cast<size_t>(helem[i])*mf+hface[i]] = N + M.nconnface + i;
+		M.elemface[static_cast<size_t>(helem[i])*mf+hface[i]] = i;
+	}
+	int fi = md.nbface;
+	for(int ie = 0; ie < N; ie++) {
+		const int nn = md.nnode[ie];
+		for(int in = 0; in < nn; in++) {
+			const int je = M.esuel[static_cast<size_t>(ie)*mf+in];
+			if(je > ie && je < N) {
+				const int in1 = (in+1) % nn;
+				M.intfac[4*fi+0] = ie; M.intfac[4*fi+1] = je;
+				M.intfac[4*fi+2] = nodeOf(md,ie,in); M.intfac[4*fi+3] = nodeOf(md,ie,in1);
+				M.elemface[static_cast<size_t>(ie)*mf+in] = fi;
+				for(int jn = 0; jn < md.nnode[je]; jn++)
+					if(nodeOf(md,ie,in1) == nodeOf(md,je,jn))
+						M.elemface[static_cast<size_t>(je)*mf+jn] = fi;
+				fi++;
+			}
+		}
+	}
+	if(fi != md.nbface + ninface) throw std::logic_error("buildMesh: face count mismatch");
+
+	// compute_areas (mesh.cpp:290-313)
+	auto X = [&](int p) { return md.coords[2*p]; };
+	auto Y = [&](int p) { return md.coords[2*p+1]; };
+	M.area.resize(N);
+	for(int i = 0; i < N; i++) {
+		const int p0 = nodeOf(md,i,0), p1 = nodeOf(md,i,1), p2 = nodeOf(md,i,2);
+		double a = 0.5*(X(p0)*(Y(p1) - Y(p2)) - Y(p0)*(X(p1) - X(p2)) + X(p1)*Y(p2) - X(p2)*Y(p1));
+		if(md.nnode[i] == 4) {
+			const int p3 = nodeOf(md,i,3);
+			a += 0.5*(X(p0)*(Y(p2) - Y(p3)) - Y(p0)*(X(p2) - X(p3)) + X(p2)*Y(p3) - X(p3)*Y(p2));
+		}
+		M.area[i] = a;
+	}
+
+	// compute_face_data (mesh.cpp:346-365): pow(x,2) in glibc is exactly x*x rounded
+	M.facemetric.resize(static_cast<size_t>(M.naface)*3);
+	for(int i = 0; i < M.naface; i++) {
+		const int a = M.intfac[4*i+2], b = M.intfac[4*i+3];
+		double nx = Y(b) - Y(a);
+		double ny = -1.0*(X(b) - X(a));
+		const double len = std::sqrt(nx*nx + ny*ny);
+		M.facemetric[3*i+0] = nx/len;
+		M.facemetric[3*i+1] = ny/len;
+		M.facemetric[3*i+2] = len;
+	}
+
+	// compute_cell_centres (mesh.cpp:316-328)
+	M.rc.resize(static_cast<size_t>(N + M.nconnface)*2);
+	for(int i = 0; i < N; i++)
+		for(int d = 0; d < 2; d++) {
+			double s = 0;
+			for(int j = 0; j < md.nnode[i]; j++) s += md.coords[2*nodeOf(md,i,j)+d];
+			M.rc[2*i+d] = s / static_cast<double>(md.nnode[i]);
+		}
+
+	// face centres (aspatial.cpp:50-61): gr starts at zero, nodes summed in order, /nnofa
+	M.gr.resize(static_cast<size_t>(M.naface)*2);
+	for(int i = 0; i < M.naface; i++)
+		for(int d = 0; d < 2; d++) {
+			double s = 0;
+			s += md.coords[2*M.intfac[4*i+2]+d];
+			s += md.coords[2*M.intfac[4*i+3]+d];
+			M.gr[2*i+d] = s / 2;
+		}
+
+	// ghost centres about face midpoints (aspatial.cpp:97-119)
+	M.rcbp.resize(static_cast<size_t>(md.nbface)*2);
+	for(int i = 0; i < md.nbface; i++) {
+		const int ie = M.intfac[4*i];
+		for(int d = 0; d < 2; d++) {
+			double mid = 0;
+			mid += md.coords[2*M.intfac[4*i+2]+d];
+			mid += md.coords[2*M.intfac[4*i+3]+d];
+			mid /= 2;
+			M.rcbp[2*i+d] = 2.0*mid - M.rc[2*ie+d];
+		}
+	}
+
+	M.md = std::move(md);
+	return M;
+}
+
+// ------------------------------------------------------------------------------------------------
+// Synthetic meshes
+// ------------------------------------------------------------------------------------------------
+
+namespace {
+
+/// NACA 0012 half-thickness with a closed trailing edge (coefficient -0.1036).
+inline double naca0012(double x) {
+	return 0.6*(0.2969*std::sqrt(x) - 0.1260*x - 0.3516*x*x + 0.2843*x*x*x - 0.1036*x*x*x*x);
+}
+
+/// Adds an O-grid of points (ntheta x (nlayers+1)), layer 0 = body, and returns the point index
+void addOgridCells(MeshData& m, int ntheta, int nquad, int ntri, int pt0)
+{
+	const int nl = nquad + ntri;
+	auto P = [&](int i, int j) { return pt0 + j*ntheta + (i % ntheta); };
+	for(int j = 0; j < nl; j++)
+		for(int i = 0; i < ntheta; i++) {
+			// i runs counter-clockwise round the body and j outwards, so (i,j) -> (i,j+1) ->
+			// (i+1,j+1) -> (i+1,j) is counter-clockwise
+			const int a = P(i,j), b = P(i,j+1), c = P(i+1,j+1), d = P(i+1,j);
+			if(j < nquad) {
+				m.inpoel.insert(m.inpoel.end(), {a, b, c, d});
+				m.nnode.push_back(4); m.nfael.push_back(4);
+			} else {
+				// alternate the diagonal by cell parity for a less biased triangulation
+				if((i + j) % 2 == 0) {
+					m.inpoel.insert(m.inpoel.end(), {a, b, c, -1, d, a, c, -1});
+				} else {
+					m.inpoel.insert(m.inpoel.end(), {a, b, d, -1, b, c, d, -1});
+				}
+				m.nnode.push_back(3); m.nfael.push_back(3);
+				m.nnode.push_back(3); m.nfael.push_back(3);
+			}
+		}
+}
+
+void finishOgrid(MeshData& m, int ntheta, int nl, int wallmarker, int farmarker)
+{
+	m.nnofa = 2; m.nbtag = 2; m.ndtag = 2;
+	m.nelem = static_cast<int>(m.nnode.size());
+	m.maxnnode = 0; m.maxnfael = 0;
+	for(int i = 0; i < m.nelem; i++) {
+		m.maxnnode = std::max(m.maxnnode, m.nnode[i]); m.maxnfael = std::max(m.maxnfael, m.nfael[i]);
+	}
+	// inpoel was pushed with stride 4; compact to maxnnode if all-triangle
+	if(m.maxnnode == 3) {
+		std::vector<int> c(static_cast<size_t>(m.nelem)*3);
+		for(int i = 0; i < m.nelem; i++) for(int j = 0; j < 3; j++) c[3*i+j] = m.inpoel[4*i+j];
+		m.inpoel.swap(c);
+	}
+	m.vol_regions.assign(static_cast<size_t>(m.nelem)*2, 0);
+	for(int i = 0; i < m.nelem; i++) { m.vol_regions[2*i] = 1; m.vol_regions[2*i+1] = 1; }
+	// boundary faces: wall (inner loop, traversed so that the outward normal points into the body)
+	// then farfield; orientation is fixed later by correctBoundaryFaceOrientation anyway.
+	m.nbface = 2*ntheta;
+	m.bface.resize(static_cast<size_t>(m.nbface)*4);
+	for(int i = 0; i < ntheta; i++) {
+		const int a = i, b = (i+1) % ntheta;
+		int* f = &m.bface[4*i];
+		f[0] = a; f[1] = b; f[2] = wallmarker; f[3] = 1;
+	}
+	for(int i = 0; i < ntheta; i++) {
+		const int a = nl*ntheta + i, b = nl*ntheta + (i+1) % ntheta;
+		int* f = &m.bface[4*(ntheta+i)];
+		f[0] = b; f[1] = a; f[2] = farmarker; f[3] = 1;
+	}
+}
+
+}
+
+MeshData generateNacaOgrid(int ntheta, int nquad, int ntri, double rfar, double wallspacing)
+{
+	if(ntheta < 8 || ntheta % 2) throw std::invalid_argument("ntheta must be even and >= 8");
+	MeshData m;
+	const int nl = nquad + ntri;
+	m.npoin = ntheta*(nl+1);
+	m.coords.resize(static_cast<size_t>(m.npoin)*2);
+	const double PI = 3.14159265358979323846;
+	// surface: i = 0 at the trailing edge, going over the lower surface to the LE and back over the
+	// upper surface (counter-clockwise), cosine clustering at LE and TE
+	std::vector<double> sx(ntheta), sy(ntheta), fx(ntheta), fy(ntheta);
+	const int half = ntheta/2;
+	for(int i = 0; i < ntheta; i++) {
+		double x, y;
+		if(i <= half) {
+			const double s = static_cast<double>(i)/half;             // 0 at TE, 1 at LE
+			x = 0.5*(1.0 + std::cos(PI*s));
+			y = -naca0012(x);
+		} else {
+			const double s = static_cast<double>(i-half)/half;        // 0 at LE, 1 at TE
+			x = 0.5*(1.0 - std::cos(PI*s));
+			y = naca0012(x);
+		}
+		sx[i] = x; sy[i] = y;
+		// matching far-field point: same direction from the mid-chord centre
+		double ang = std::atan2(y, x - 0.5);
+		if(i == 0) ang = 0.0;
+		if(i == half) ang = PI;
+		fx[i] = 0.5 + rfar*std::cos(ang); fy[i] = rfar*std::sin(ang);
+	}
+	// The surface runs clockwise when i increases (TE -> lower -> LE -> upper is clockwise seen
+	// from above? lower surface first with y<0 going from x=1 to x=0 is clockwise). Reverse i so
+	// that cells come out counter-clockwise.
+	std::reverse(sx.begin()+1, sx.end()); std::reverse(sy.begin()+1, sy.end());
+	std::reverse(fx.begin()+1, fx.end()); std::reverse(fy.begin()+1, fy.end());
+	// radial distribution: geometric growth from wallspacing, capped so the sum reaches 1
+	std::vector<double> eta(nl+1, 0.0);
+	{
+		// find growth ratio q such that wallspacing*(q^nl - 1)/(q - 1) = 1 (in normalised units of
+		// the body-to-farfield distance ~ rfar)
+		const double target = 1.0/ (wallspacing/rfar);
+		double lo = 1.0 + 1e-12, hi = 2.0;
+		for(int it = 0; it < 200; it++) {
+			const double q = 0.5*(lo+hi);
+			const double s = (std::pow(q, nl) - 1.0)/(q - 1.0);
+			if(s > target) hi = q; else lo = q;
+		}
+		const double q = 0.5*(lo+hi);
+		double acc = 0, d = 1.0;
+		for(int j = 1; j <= nl; j++) { acc += d; eta[j] = acc; d *= q; }
+		for(int j = 1; j <= nl; j++) eta[j] /= acc;
+	}
+	for(int j = 0; j <= nl; j++)
+		for(int i = 0; i < ntheta; i++) {
+			const size_t p = static_cast<size_t>(j)*ntheta + i;
+			m.coords[2*p] = sx[i] + eta[j]*(fx[i] - sx[i]);
+			m.coords[2*p+1] = sy[i] + eta[j]*(fy[i] - sy[i]);
+		}
+	addOgridCells(m, ntheta, nquad, ntri, 0);
+	finishOgrid(m, ntheta, nl, 2, 4);
+	return m;
+}
+
+MeshData generateCylinderOgrid(int ntheta, int nr, double r0, double r1)
+{
+	MeshData m;
+	m.npoin = ntheta*(nr+1);
+	m.coords.resize(static_cast<size_t>(m.npoin)*2);
+	const double PI = 3.14159265358979323846;
+	const double q = std::pow(r1/r0, 1.0/nr);          // geometric radial spacing
+	for(int j = 0; j <= nr; j++) {
+		const double r = r0*std::pow(q, j);
+		for(int i = 0; i < ntheta; i++) {
+			const double a = 2.0*PI*i/ntheta;
+			const size_t p = static_cast<size_t>(j)*ntheta + i;
+			m.coords[2*p] = r*std::cos(a); m.coords[2*p+1] = r*std::sin(a);
+		}
+	}
+	addOgridCells(m, ntheta, 0, nr, 0);
+	finishOgrid(m, ntheta, nr, 2, 4);
+	return m;
+}
+
+MeshData generateFlatPlate(int nx, int ny, double xlead, double h, double wallspacing)
+{
+	MeshData m;
+	m.npoin = (nx+1)*(ny+1);
+	m.coords.resize(static_cast<size_t>(m.npoin)*2);
+	// x: uniform-ish with clustering at the leading edge x=0
+	std::vector<double> xs(nx+1), ys(ny+1);
+	const int nlead = std::max(1, nx/8);
+	for(int i = 0; i <= nlead; i++) xs[i] = -xlead*(1.0 - static_cast<double>(i)/nlead);
+	for(int i = nlead; i <= nx; i++) {
+		const double s = static_cast<double>(i - nlead)/(nx - nlead);
+		xs[i] = s*s*(3.0 - 2.0*s)*0.0 + s;                 // uniform on the plate
+	}
+	double lo = 1.0 + 1e-12, hi = 2.0;
+	for(int it = 0; it < 200; it++) {
+		const double q = 0.5*(lo+hi);
+		const double s = wallspacing*(std::pow(q, ny) - 1.0)/(q - 1.0);
+		if(s > h) hi = q; else lo = q;
+	}
+	const double q = 0.5*(lo+hi);
+	ys[0] = 0; double d = wallspacing;
+	for(int j = 1; j <= ny; j++) { ys[j] = ys[j-1] + d; d *= q; }
+	for(int j = 0; j <= ny; j++) ys[j] *= h/ys[ny];
+	for(int j = 0; j <= ny; j++)
+		for(int i = 0; i <= nx; i++) {
+			const size_t p = static_cast<size_t>(j)*(nx+1) + i;
+			m.coords[2*p] = xs[i]; m.coords[2*p+1] = ys[j];
+		}
+	auto P = [&](int i, int j) { return j*(nx+1) + i; };
+	for(int j = 0; j < ny; j++)
+		for(int i = 0; i < nx; i++) {
+			m.inpoel.insert(m.inpoel.end(), {P(i,j), P(i+1,j), P(i+1,j+1), P(i,j+1)});
+			m.nnode.push_back(4); m.nfael.push_back(4);
+		}
+	m.nelem = nx*ny; m.maxnnode = 4; m.maxnfael = 4; m.nnofa = 2; m.nbtag = 2; m.ndtag = 2;
+	m.vol_regions.assign(static_cast<size_t>(m.nelem)*2, 1);
+	auto addb = [&](int a, int b, int tag) { m.bface.insert(m.bface.end(), {a, b, tag, 1}); };
+	for(int i = 0; i < nx; i++) addb(P(i,0), P(i+1,0), xs[i] < 0.0 ? 3 : 2);     // bottom
+	for(int j = 0; j < ny; j++) addb(P(nx,j), P(nx,j+1), 5);                   // right (outflow)
+	for(int i = nx; i > 0; i--) addb(P(i,ny), P(i-1,ny), 4);                   // top
+	for(int j = ny; j > 0; j--) addb(P(0,j), P(0,j-1), 5);                     // left (inflow)
+	m.nbface = static_cast<int>(m.bface.size()/4);
+	return m;
+}
+
+}

@@ -1,0 +1,82 @@
+/** \file mesh.hpp
+ * \brief Host-side mesh for the MI355X face sweep: Gmsh-2 ingest, the reference's face-indexing
+ *   contract, geometry, synthetic generators and the locality ordering used on the device.
+ *
+ * Everything exported (cell, face and boundary-face indices, normals, lengths, areas, centres)
+ * follows FVENS's UMesh contract bit for bit:
+ *  - readGmsh2               /root/reference/src/mesh/meshreaders.cpp:66-265
+ *  - correctBoundaryFaceOrientation  mesh.cpp:55-82
+ *  - compute_faceConnectivity        mesh.cpp:659-762 (face order, ghost index rule mesh.hpp:84-96)
+ *  - compute_face_data               mesh.cpp:346-365
+ *  - compute_areas / cell centres    mesh.cpp:290-328
+ *  - face centres, ghost centres     aspatial.cpp:50-61, 97-119
+ * The topology is found with a per-node incidence scan (O(N)), not the reference's nested loops,
+ * but the loop that NUMBERS faces is the reference's, so indices are identical.
+ */
+#ifndef FVHIP_MESH_HPP
+#define FVHIP_MESH_HPP
+
+#include <vector>
+#include <string>
+#include <cstdint>
+
+namespace fvhip {
+
+/// Raw mesh as read from a file or generated; mirrors fvens::MeshData (meshreaders.hpp)
+struct MeshData
+{
+	int npoin = 0, nelem = 0, nbface = 0;
+	int nnofa = 2;           ///< nodes per face (linear only)
+	int nbtag = 0, ndtag = 0;
+	int maxnnode = 0, maxnfael = 0;
+	std::vector<double> coords;    ///< [npoin][2]
+	std::vector<int> inpoel;       ///< [nelem][maxnnode], -1 padded
+	std::vector<int> nnode, nfael; ///< [nelem]
+	std::vector<int> bface;        ///< [nbface][nnofa+nbtag]: nodes then tags
+	std::vector<int> vol_regions;  ///< [nelem][ndtag]
+};
+
+/// A single-domain mesh with the reference's connectivity and geometry.
+struct Mesh
+{
+	MeshData md;
+	int naface = 0, ninface = 0, nconnface = 0;
+	std::vector<int> esuel;        ///< [nelem][maxnfael]
+	std::vector<int> elemface;     ///< [nelem][maxnfael]
+	std::vector<int> intfac;       ///< [naface][4] = {L, R, node0, node1}
+	std::vector<int> btags;        ///< [nbface][nbtag]
+	std::vector<double> facemetric;///< [naface][3] = {nx, ny, len}
+	std::vector<double> area;      ///< [nelem]
+	std::vector<double> rc;        ///< [nelem+nconnface][2] cell centres (vertex average)
+	std::vector<double> gr;        ///< [naface][2] face centres
+	std::vector<double> rcbp;      ///< [nbface][2] ghost cell centres about face midpoints
+};
+
+/// Reads a Gmsh 2.2 ASCII mesh exactly as readGmsh2 does (boundary edges must precede cells).
+MeshData readGmsh2(const std::string& path);
+
+/// Writes a MeshData in Gmsh 2.2 ASCII format (boundary edges first, as readGmsh2 expects).
+void writeGmsh2(const MeshData& m, const std::string& path);
+
+/// Full reference preprocessing for one rank: orientation fix, topology, areas, face data,
+/// centres. (constructMesh ameshutils.cpp:102-153 with a trivial 1-rank partition)
+Mesh buildMesh(MeshData md);
+
+/// Synthetic hybrid O-grid around a NACA 0012 aerofoil (chord 1, LE at origin).
+/// ntheta points around the surface, nquad quad layers at the wall, ntri triangle-split layers
+/// outside them, outer circle radius rfar about (0.5,0). Wall marker 2, farfield marker 4.
+/// Cells: ntheta*(nquad + 2*ntri).
+MeshData generateNacaOgrid(int ntheta, int nquad, int ntri, double rfar, double wallspacing);
+
+/// Synthetic O-grid annulus about a cylinder of radius r0 out to r1, all quads split into
+/// triangles (2dcylinder-like). Inner marker 2, outer marker 4. Cells 2*ntheta*nr.
+MeshData generateCylinderOgrid(int ntheta, int nr, double r0, double r1);
+
+/// Structured flat-plate channel of nx*ny quads on [-xlead, 1]x[0, h] with wall clustering.
+/// Markers: 3 = symmetry (slipwall, y=0 x<0), 2 = plate (adiabatic wall, y=0 x>=0),
+/// 4 = top farfield, 5 = inflow/outflow (left and right).
+MeshData generateFlatPlate(int nx, int ny, double xlead, double h, double wallspacing);
+
+}
+
+#endif

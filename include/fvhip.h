@@ -1,0 +1,178 @@
+/** \file fvhip.h
+ * \brief C-ABI of the MI355X face-sweep library (libfvhip.so).
+ *
+ * This is the drop-in boundary for FVENS's spatial-discretisation hot path. Each entry point
+ * replaces one method of the reference's operator classes (paths under /root/reference/src):
+ *
+ *   fvhip_create             FlowFV<scalar,order2,constVisc>::FlowFV      spatial/flow_spatial.cpp:312-337
+ *                            (+ FlowFV_base ctor :34-59, Spatial ctor spatial/aspatial.cpp:36-76,
+ *                             factory create_const_flowSpatialDiscretization utilities/afactory.cpp:251-267)
+ *   fvhip_destroy            FlowFV::~FlowFV                               spatial/flow_spatial.cpp:339-346
+ *   fvhip_compute_residual   FlowFV::compute_residual                      spatial/flow_spatial.cpp:636-816
+ *                            (virtual Spatial::compute_residual            spatial/aspatial.hpp:62-63)
+ *   fvhip_get_gradients      FlowFV_base::getGradients                     spatial/flow_spatial.cpp:95-112
+ *   fvhip_assemble_jacobian  Spatial::assemble_jacobian                    spatial/aspatial.cpp:242-340
+ *   fvhip_matfree_set_state  MatrixFreeSpatialJacobian::set_state          linalg/alinalg.cpp:131-140
+ *   fvhip_matfree_apply      MatrixFreeSpatialJacobian::apply              linalg/alinalg.cpp:142-233
+ *   fvhip_local_flux         InviscidFlux::get_flux                        spatial/anumericalflux.hpp:32-34
+ *   fvhip_local_flux_jacobian InviscidFlux::get_jacobian                   spatial/anumericalflux.hpp:43-45
+ *
+ * Conventions (identical to the reference, spatial/flow_spatial.hpp:73-85, aspatial.hpp:49-66):
+ *  - u is the ghosted conserved state (rho, rho*vx, rho*vy, rho*E), row-major [nelem+nconnface][4]
+ *    in the reference's cell numbering; r is [nelem][4]; dtm is [nelem].
+ *  - compute_residual ADDS -r(u) into r; dtm[i] = area_i / sum_faces(spectral radius * length).
+ *  - Jacobian blocks are row-major 4x4 and are ADDED (ADD_VALUES) into the caller's arrays.
+ *  - Every function returns 0 on success, nonzero on failure; fvhip_last_error() describes it.
+ *    No C++ exception crosses this boundary. Calls on one handle are not thread-safe
+ *    (like the reference, flow_spatial.hpp:196-197); each handle owns one HIP stream.
+ *  - *_device variants take device pointers in the library's internal cell order (see
+ *    fvhip_to_internal / fvhip_from_internal) and are asynchronous on the handle's stream.
+ */
+#ifndef FVHIP_H
+#define FVHIP_H
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define FVHIP_NVARS 4
+#define FVHIP_NDIM 2
+
+/* Numerical inviscid fluxes, afactory.cpp:38-81 ("VANLEER","ROE","HLL","HLLC","LLF","AUSM","AUSMPLUS") */
+enum fvhip_flux_type {
+	FVHIP_FLUX_LLF = 0, FVHIP_FLUX_VANLEER = 1, FVHIP_FLUX_AUSM = 2, FVHIP_FLUX_AUSMPLUS = 3,
+	FVHIP_FLUX_ROE = 4, FVHIP_FLUX_HLL = 5, FVHIP_FLUX_HLLC = 6
+};
+/* Gradient schemes, afactory.cpp:111-127 ("LEASTSQUARES","GREENGAUSS", anything else -> zero) */
+enum fvhip_gradient_type { FVHIP_GRAD_ZERO = 0, FVHIP_GRAD_GREENGAUSS = 1, FVHIP_GRAD_LEASTSQUARES = 2 };
+/* Reconstructions, afactory.cpp:178-211 ("NONE","WENO","VANALBADA","BARTHJESPERSEN","VENKATAKRISHNAN") */
+enum fvhip_recon_type {
+	FVHIP_REC_NONE = 0, FVHIP_REC_WENO = 1, FVHIP_REC_VANALBADA = 2, FVHIP_REC_BARTHJESPERSEN = 3,
+	FVHIP_REC_VENKATAKRISHNAN = 4
+};
+/* Boundary condition types in the reference's enum order, spatial/abctypes.hpp:12-21 */
+enum fvhip_bc_type {
+	FVHIP_BC_SLIPWALL = 0, FVHIP_BC_FARFIELD = 1, FVHIP_BC_INFLOW_OUTFLOW = 2,
+	FVHIP_BC_SUBSONIC_INFLOW = 3, FVHIP_BC_EXTRAPOLATION = 4, FVHIP_BC_PERIODIC = 5,
+	FVHIP_BC_ISOTHERMAL_WALL = 6, FVHIP_BC_ADIABATIC_WALL = 7
+};
+
+/** FlowPhysicsConfig (flow_spatial.hpp:33-44) + FlowNumericsConfig (:47-55) + FlowBCConfig list */
+typedef struct fvhip_flow_config {
+	double gamma, Minf, Tinf, Reinf, Pr, aoa;   /* aoa in radians */
+	int viscous_sim, const_visc;
+	int conv_numflux;         /* enum fvhip_flux_type */
+	int conv_numflux_jac;     /* enum fvhip_flux_type, used by the Jacobian */
+	int gradientscheme;       /* enum fvhip_gradient_type */
+	int reconstruction;       /* enum fvhip_recon_type */
+	double limiter_param;     /* Venkatakrishnan K / WENO lambda (must be given explicitly) */
+	int order2;               /* second-order (gradients + reconstruction) if nonzero */
+	int nbc;                  /* number of boundary conditions */
+	const int* bc_type;       /* [nbc] enum fvhip_bc_type */
+	const int* bc_tag;        /* [nbc] boundary marker (gbtags(face,0)) */
+	const double* bc_vals;    /* [nbc][2] boundary_values (wall velocity, temperature, ...) */
+} fvhip_flow_config;
+
+/** The UMesh data the sweep needs, exactly as the reference's accessors return it
+ *  (mesh/mesh.hpp: gcoords, ginpoel, gnnode, gintfac, gbtags, gfacemetric, garea, gesuel,
+ *  gelemface; cell centres rc from Spatial::rcvec, ghost centres rcbp, face centres gr). */
+typedef struct fvhip_mesh {
+	int nelem, npoin, nbface, naface, nconnface, maxnnode, maxnfael, nbtag;
+	const double* coords;     /* [npoin][2] */
+	const int* inpoel;        /* [nelem][maxnnode] */
+	const int* nnode;         /* [nelem] (== nfael for linear 2D cells) */
+	const int* esuel;         /* [nelem][maxnfael] */
+	const int* elemface;      /* [nelem][maxnfael] */
+	const int* intfac;        /* [naface][4] = {L, R, node0, node1} */
+	const int* btags;         /* [nbface][nbtag] */
+	const double* facemetric; /* [naface][3] = {nx, ny, length} */
+	const double* area;       /* [nelem] */
+	const double* rc;         /* [nelem+nconnface][2] */
+	const double* rcbp;       /* [nbface][2] */
+	const double* gr;         /* [naface][2] */
+} fvhip_mesh;
+
+typedef struct fvhip_ctx* fvhip_handle;
+
+/** Text of the last error on this thread */
+const char* fvhip_last_error(void);
+/** Library version string */
+const char* fvhip_version(void);
+/** Number of visible HIP devices (0 if none; never fails) */
+int fvhip_device_count(void);
+
+/** Builds the device-resident discretisation for a mesh on a device */
+int fvhip_create(const fvhip_mesh* mesh, const fvhip_flow_config* cfg, int device, fvhip_handle* out);
+int fvhip_destroy(fvhip_handle h);
+
+/** FlowFV::compute_residual on host arrays (copies through PCIe) */
+int fvhip_compute_residual(fvhip_handle h, const double* u, double* r, int gettimesteps, double* dtm);
+/** Device-resident sweep; u/r/dtm in internal order. flags: FVHIP_RES_OVERWRITE = r is known
+ *  to be zero on entry (as every reference caller guarantees), so it is written, not read. */
+#define FVHIP_RES_OVERWRITE 1
+int fvhip_compute_residual_device(fvhip_handle h, const double* d_u, double* d_r, int gettimesteps,
+                                  double* d_dtm, int flags);
+/** FlowFV_base::getGradients: conserved-variable gradients, GradBlock layout [nelem][4 vars][2 dims] */
+int fvhip_get_gradients(fvhip_handle h, const double* u, double* grads);
+
+/** Spatial::assemble_jacobian into block-sparse storage: diag [nelem][16] (diagonal blocks),
+ *  lower/upper [ninface][16] for interior faces in face order (A[R][L] += L, A[L][R] += U). */
+int fvhip_assemble_jacobian(fvhip_handle h, const double* u, double* diag, double* lower, double* upper);
+
+/** MatrixFreeSpatialJacobian: set_state(u, r = -r(u), mdt = area/(CFL*dt)) then y = J x */
+int fvhip_matfree_set_state(fvhip_handle h, const double* u, const double* r, const double* mdt);
+int fvhip_matfree_apply(fvhip_handle h, const double* x, double* y);
+/** -matrix_free_difference_step (default 1e-7, alinalg.cpp:124-129) */
+int fvhip_matfree_set_eps(fvhip_handle h, double eps);
+
+/** Permute a cell array [nelem][width] between reference order (host) and internal order (device) */
+int fvhip_to_internal(fvhip_handle h, const double* host_ref, double* d_internal, int width);
+int fvhip_from_internal(fvhip_handle h, const double* d_internal, double* host_ref, int width);
+/** Internal order of cells: perm[internal] = reference cell index */
+int fvhip_get_permutation(fvhip_handle h, int* perm);
+
+/** Device scratch allocation helpers (hipMalloc on the handle's device) */
+int fvhip_device_alloc(fvhip_handle h, unsigned long long bytes, void** ptr);
+int fvhip_device_free(fvhip_handle h, void* ptr);
+int fvhip_synchronize(fvhip_handle h);
+/** The handle's HIP stream (hipStream_t as void*) */
+void* fvhip_stream(fvhip_handle h);
+
+/** Kernel timing with HIP events on the handle's stream. enable=1 starts recording every
+ *  kernel launch; fvhip_kernel_times returns, per kernel id, (total ms, launches). */
+int fvhip_profile(fvhip_handle h, int enable);
+int fvhip_kernel_times(fvhip_handle h, int maxk, char* names, int namelen, double* ms, int* counts);
+
+/** Layout statistics: [0]=cells [1]=faces [2]=face slots incl. duplicated cut faces
+ *  [3]=patches [4]=max slots per patch [5]=boundary faces */
+int fvhip_layout_stats(fvhip_handle h, long long* stats);
+
+/** Point-wise numerical flux on the device (get_flux) for nf faces: ul, ur [nf][4], n [nf][2] */
+int fvhip_local_flux(int flux_type, const double* gas5, int nf, const double* ul, const double* ur,
+                     const double* n, double* flux);
+/** Point-wise flux Jacobians (get_jacobian) on the device: dfdl, dfdr [nf][16] */
+int fvhip_local_flux_jacobian(int flux_type, const double* gas5, int nf, const double* ul,
+                              const double* ur, const double* n, double* dfdl, double* dfdr);
+
+/* ---------------------------------------------------------------------------------------------
+ * Mesh builder (host). Produces the reference's UMesh arrays from a Gmsh-2 file or a synthetic
+ * generator, index-for-index as readGmsh2 + constructMesh + preprocessMesh would on one rank.
+ * ------------------------------------------------------------------------------------------- */
+typedef struct fvmesh_s* fvmesh_handle;
+int fvmesh_read_gmsh(const char* path, fvmesh_handle* out);
+/** kind: 0 = NACA0012 hybrid O-grid (a=ntheta, b=nquad, c=ntri, x=rfar, y=wall spacing)
+ *        1 = cylinder triangle O-grid (a=ntheta, b=nr, x=r0, y=r1)
+ *        2 = flat plate quads (a=nx, b=ny, x=lead length, y=height, z=wall spacing) */
+int fvmesh_generate(int kind, int a, int b, int c, double x, double y, double z, fvmesh_handle* out);
+int fvmesh_write_gmsh(fvmesh_handle m, const char* path);
+int fvmesh_destroy(fvmesh_handle m);
+/** Fills a fvhip_mesh view whose pointers stay valid until fvmesh_destroy */
+int fvmesh_view(fvmesh_handle m, fvhip_mesh* view);
+/** Raw (pre-topology) arrays: npoin, nelem, maxnnode, nbface, nbtag */
+int fvmesh_raw_info(fvmesh_handle m, int* info5);
+int fvmesh_raw_arrays(fvmesh_handle m, double* coords, int* inpoel, int* nnode, int* bface);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,35 @@
+import os
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+
+
+def pytest_configure(config):
+    config.addinivalue_line("markers", "gpu: needs an MI355X (run with -m gpu on the GPU box)")
+
+
+def _ensure_built():
+    lib = os.path.join(ROOT, "fvens_amd", "libfvhip.so")
+    orc = os.path.join(ROOT, "oracle", "liboracle.so")
+    if not (os.path.exists(lib) and os.path.exists(orc)):
+        import __graft_entry__
+        __graft_entry__.build()
+
+
+_ensure_built()
+
+
+@pytest.fixture(scope="session")
+def gpu_available():
+    import fvens_amd._ffi as ffi
+    return ffi.lib().fvhip_device_count() > 0
+
+
+def pytest_collection_modifyitems(config, items):
+    # GPU tests fail loudly (not skip) when selected on a machine without a GPU: the product has no
+    # CPU fallback. Without -m gpu they are deselected by the driver's -m "not gpu".
+    pass
