@@ -1,0 +1,97 @@
+"""The native mesh builder reproduces the reference's face-indexing contract bit for bit
+(mesh.cpp:55-82, 290-365, 425-762; aspatial.cpp:50-119): checked against the oracle's literal
+restatement on the reference's own test meshes and on every synthetic generator."""
+import numpy as np
+import pytest
+
+import fvens_amd as fa
+import _oracle as orc
+import cases
+
+FIXTURES = ["testperiodic", "2dcylinderhybrid", "testhybrid", "squareunsquad0", "2dcylinder0",
+            "2dcylinder1", "2dcylinder2", "naca0012luo"]
+ARRAYS = ["intfac", "btags", "facemetric", "area", "rc", "gr", "rcbp"]
+
+
+def compare(m, om):
+    assert (m.nelem, m.naface, m.nbface) == (om.nelem, om.naface, om.nbface)
+    for name in ARRAYS:
+        a = getattr(m, name)
+        if name == "rc":
+            a = a[:m.nelem]
+        b = om.get(name)
+        assert a.shape == b.shape, name
+        assert np.array_equal(a, b), name
+    # esuel/elemface entries beyond a cell's face count are unspecified in the reference
+    mask = np.arange(m.maxnfael)[None, :] < m.nnode[:, None]
+    assert np.array_equal(m.esuel[mask], om.get("esuel")[mask])
+    assert np.array_equal(m.elemface[mask], om.get("elemface")[mask])
+
+
+@pytest.mark.parametrize("name", FIXTURES)
+def test_gmsh_fixture_indexing(name):
+    p = cases.fixture_mesh(name)
+    compare(fa.UMesh.read_gmsh(p), orc.OracleMesh.read(p))
+
+
+@pytest.mark.parametrize("gen", [
+    lambda: fa.UMesh.naca_ogrid(64, 4, 12),
+    lambda: fa.UMesh.naca_ogrid(200, 10, 30, 15.0, 1e-3),
+    lambda: fa.UMesh.cylinder_ogrid(48, 12),
+    lambda: fa.UMesh.flat_plate(40, 24),
+])
+def test_generated_mesh_indexing(gen):
+    m = gen()
+    compare(m, orc.OracleMesh.from_raw(m.raw()))
+    assert (m.area > 0).all()
+
+
+def test_face_structure_contract():
+    """Face order: physical boundary [0,nb) with R = N+i; interior faces with L<R; normals point L->R
+    (mesh.cpp:680-733, 354-359); each face appears in elemface of both neighbours."""
+    m = fa.UMesh.read_gmsh(cases.fixture_mesh("2dcylinderhybrid"))
+    N, nb = m.nelem, m.nbface
+    assert np.array_equal(m.intfac[:nb, 1], N + np.arange(nb))
+    assert (m.intfac[nb:, 0] < m.intfac[nb:, 1]).all()
+    # unit normals, positive lengths
+    assert np.allclose(np.hypot(m.facemetric[:, 0], m.facemetric[:, 1]), 1.0)
+    assert (m.facemetric[:, 2] > 0).all()
+    # normal points from L centre towards R centre (or outwards at the boundary)
+    d = m.rc[m.intfac[nb:, 1]] - m.rc[m.intfac[nb:, 0]]
+    assert ((d * m.facemetric[nb:, :2]).sum(1) > 0).all()
+    dout = m.gr[:nb] - m.rc[m.intfac[:nb, 0]]
+    assert ((dout * m.facemetric[:nb, :2]).sum(1) > 0).all()
+    # closed cells: sum of n*len over faces of each cell = 0
+    acc = np.zeros((N, 2))
+    nl = m.facemetric[:, :2] * m.facemetric[:, 2:3]
+    np.add.at(acc, m.intfac[:, 0], nl)
+    np.add.at(acc, m.intfac[nb:, 1], -nl[nb:])
+    assert np.abs(acc).max() < 1e-12
+
+
+def test_testhybrid_counts():
+    """tests/common-input/testhybrid.msh: 12 tris + 6 quads; the partition golden files list the
+    same 18 global cells (testhybrid-distb.dat)"""
+    m = fa.UMesh.read_gmsh(cases.fixture_mesh("testhybrid"))
+    assert m.nelem == 18 and (m.nnode == 3).sum() == 12 and (m.nnode == 4).sum() == 6
+
+
+def test_c1_cylinder_size():
+    """C1 of SURVEY.md 8(d): Ntheta=64 x Nr=40 triangle-split O-grid, 5120 cells, 7744 faces"""
+    m = fa.UMesh.cylinder_ogrid(64, 40)
+    assert (m.nelem, m.naface) == (5120, 7744)
+
+
+def test_c2_naca_size():
+    """C2: NACA0012 O-grid Ntheta=512, 64 quad + 192 triangle layers: 229,376 cells, 360,960 faces"""
+    m = fa.UMesh.naca_ogrid(512, 64, 192)
+    assert (m.nelem, m.naface) == (229376, 360960)
+
+
+def test_gmsh_roundtrip(tmp_path):
+    m = fa.UMesh.naca_ogrid(64, 4, 12)
+    p = tmp_path / "o.msh"
+    m.write_gmsh(p)
+    m2 = fa.UMesh.read_gmsh(p)
+    assert np.array_equal(m.intfac, m2.intfac)
+    assert np.array_equal(m.facemetric, m2.facemetric)
