@@ -39,6 +39,25 @@ def sweep_algorithmic_bytes(N, F, Fb):
     return 32 * F + 144 * N + 48 * Fb + 16 * N
 
 
+def pmc_traffic(kernel_symbol, workload_cells):
+    """HBM bytes per launch of `kernel_symbol` from the newest committed rocprofv3 PMC summary
+    (profiles/r*/pmc_traffic.json: FETCH_SIZE x2 + WRITE_SIZE, calibrated as MI355X_MICROARCH.md
+    prescribes), if it was measured on the same workload; else None."""
+    import glob
+    best = None
+    for f in sorted(glob.glob(os.path.join(ROOT, "profiles", "r*", "pmc_traffic.json"))):
+        try:
+            d = json.load(open(f))
+        except Exception:
+            continue
+        if str(workload_cells) not in d.get("workload", "").replace(",", ""):
+            continue
+        for k, v in d.get("kernels", {}).items():
+            if k.endswith(kernel_symbol):
+                best = (v["hbm_bytes_corrected"], os.path.relpath(f, ROOT))
+    return best
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -134,6 +153,8 @@ def main():
 
     if rank == 0:
         stats = sp.layout_stats()
+        # template of the timed sweep: k_sweep<FLUX=ROE(4), REC=MUSCL(1), VISC=none(0), DT, no PHI>
+        tr = pmc_traffic("k_sweep<4, 1, 0, true, false>", N)
         out = {
             "metric": "Mfaces/s (flux+residual sweep) + achieved HBM GB/s, 1/2/4/8 MI355X",
             "value": round(value, 3),
@@ -153,7 +174,9 @@ def main():
                        "parallelism": f"replicas x{world}" if world > 1 else "single GPU",
                        "layout": stats, "setup_s": round(t_setup, 2)},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
+                         "frac": round(achieved / HBM_PEAK_GBS, 4),
+                         "traffic": int(tr[0]) if tr else None,
+                         "traffic_source": tr[1] if tr else None,
                          "kernel": sweep_name[0] if sweep_name else None,
                          "kernel_ms": round(sweep_ms, 5), "algorithmic_bytes": ab},
             "kernels_ms": {k: round(v, 5) for k, v in kernels_ms.items()},

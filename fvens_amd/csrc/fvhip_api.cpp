@@ -203,6 +203,7 @@ int fvhip_create(const fvhip_mesh* mesh, const fvhip_flow_config* cfg, int devic
 		M.cell_slots = reinterpret_cast<const int4*>(upload(L.cell_slots, o));
 		M.cell_nbr = reinterpret_cast<const int4*>(upload(L.cell_nbr_local, o));
 		M.cell_face = reinterpret_cast<const int4*>(upload(L.cell_face_local, o));
+		M.cell_nbr_fo = reinterpret_cast<const int4*>(upload(L.cell_nbr_fo, o));
 		M.rc = reinterpret_cast<const double2*>(upload(L.rc, o));
 		M.area = upload(L.area, o);
 		M.wls_V = reinterpret_cast<const double4*>(upload(L.wls_V, o));

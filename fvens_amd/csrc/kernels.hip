@@ -70,38 +70,46 @@ __global__ void __launch_bounds__(256) k_prep_bfaces(DevMesh M, DevPhys P, const
 // gradients (agradientschemes.cpp). One thread per cell; the cell's faces are visited in ascending
 // reference face index, which is the reference's single-thread accumulation order.
 // ------------------------------------------------------------------------------------------------
+// WLS (agradientschemes.cpp:322-440). Each face contributes w2*dr*du with dr = rc(L)-rc(R),
+// du = u(L)-u(R); computing both differences from this cell's side negates both factors exactly,
+// so the product is bitwise the same and no face orientation is needed.
 __global__ void __launch_bounds__(256) k_grad_wls(DevMesh M, const double* __restrict__ up,
                                                   const double* __restrict__ ug, double* __restrict__ grad)
 {
 	const int c = blockIdx.x*blockDim.x + threadIdx.x;
 	if(c >= M.ncell) return;
 	const int N = M.ncell;
-	const int4 cs = M.cell_slots[c];
-	const int e[4] = {cs.x, cs.y, cs.z, cs.w};
+	const int4 nb4 = M.cell_nbr_fo[c];
+	const int nb[4] = {nb4.x, nb4.y, nb4.z, nb4.w};
+	const double2 rcc = M.rc[c];
+	double uc[4];
+	ld4(up, c, uc);
+	// issue all neighbour loads before the arithmetic
+	double un[4][4];
+	double2 rn[4];
+	#pragma unroll
+	for(int k = 0; k < 4; k++) {
+		if(nb[k] < 0) continue;
+		if(nb[k] >= N) { rn[k] = M.bf_rcbp[nb[k] - N]; ld4(ug, nb[k] - N, un[k]); }
+		else           { rn[k] = M.rc[nb[k]];           ld4(up, nb[k], un[k]); }
+	}
+	const double4 V = M.wls_V[c];
 	double f[8] = {0,0,0,0,0,0,0,0};
 	#pragma unroll
 	for(int k = 0; k < 4; k++) {
-		if(e[k] < 0) break;
-		const int2 lr = M.slot_LR[e[k] >> 1];
-		double uL[4], uR[4];
-		const double2 rl = M.rc[lr.x];
-		double2 rr;
-		ld4(up, lr.x, uL);
-		if(lr.y >= N) { rr = M.bf_rcbp[lr.y - N]; ld4(ug, lr.y - N, uR); }
-		else          { rr = M.rc[lr.y];           ld4(up, lr.y, uR); }
+		if(nb[k] < 0) break;
 		double w2 = 0;
-		w2 += (rl.x-rr.x)*(rl.x-rr.x);
-		w2 += (rl.y-rr.y)*(rl.y-rr.y);
-		const double dr0 = rl.x-rr.x, dr1 = rl.y-rr.y;
+		w2 += (rcc.x-rn[k].x)*(rcc.x-rn[k].x);
+		w2 += (rcc.y-rn[k].y)*(rcc.y-rn[k].y);
+		const double dr0 = rcc.x-rn[k].x, dr1 = rcc.y-rn[k].y;
 		w2 = 1.0/(w2);
 		#pragma unroll
 		for(int iv = 0; iv < 4; iv++) {
-			const double du = uL[iv] - uR[iv];
+			const double du = uc[iv] - un[k][iv];
 			f[iv*2+0] += w2*dr0*du;
 			f[iv*2+1] += w2*dr1*du;
 		}
 	}
-	const double4 V = M.wls_V[c];
 	double g[8];
 	#pragma unroll
 	for(int iv = 0; iv < 4; iv++) {

@@ -28,6 +28,7 @@ struct DevMesh
 	const int4* cell_slots;    // [N] (slot<<1 | isRight), -1 padded, ascending reference face
 	const int4* cell_nbr;      // [N] esuel order neighbours (internal / ncell+bf)
 	const int4* cell_face;     // [N] esuel order slots
+	const int4* cell_nbr_fo;   // [N] neighbours in ascending reference face order
 	const double2* rc;         // [N]
 	const double* area;        // [N]
 	const double4* wls_V;      // [N] row-major 2x2

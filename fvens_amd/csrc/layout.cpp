@@ -99,6 +99,7 @@ Layout buildLayout(const fvhip_mesh& m, const fvhip_flow_config& cfg, bool renum
 	Lo.cell_slots.assign(static_cast<size_t>(N)*MAXF, -1);
 	Lo.cell_face_local.assign(static_cast<size_t>(N)*MAXF, -1);
 	Lo.cell_nbr_local.assign(static_cast<size_t>(N)*MAXF, -1);
+	Lo.cell_nbr_fo.assign(static_cast<size_t>(N)*MAXF, -1);
 	Lo.cell_nfael.assign(N, 0);
 	Lo.patch_slot.push_back(0);
 	std::vector<int> inner, cut, bnd;
@@ -148,8 +149,11 @@ Layout buildLayout(const fvhip_mesh& m, const fvhip_flow_config& cfg, bool renum
 				Lo.cell_nbr_local[static_cast<size_t>(c)*MAXF+j] = toInt(esu(ref,j));
 			}
 			std::sort(fs, fs+k);
-			for(int j = 0; j < k; j++)
+			for(int j = 0; j < k; j++) {
 				Lo.cell_slots[static_cast<size_t>(c)*MAXF+j] = (face_slot[fs[j]] << 1) | (Lref(fs[j]) != ref ? 1 : 0);
+				const int other = Lref(fs[j]) != ref ? Lref(fs[j]) : Rref(fs[j]);
+				Lo.cell_nbr_fo[static_cast<size_t>(c)*MAXF+j] = toInt(other);
+			}
 		}
 	}
 

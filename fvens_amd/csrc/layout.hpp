@@ -44,6 +44,8 @@ struct Layout
 	std::vector<int> cell_nbr_local;       ///< [ncell][4]: esuel neighbours (internal or boundary
 	                                       ///<  code ncell+bf) in local-face order (WENO, limiters)
 	std::vector<int> cell_face_local;      ///< [ncell][4]: slot of local face j (own patch)
+	std::vector<int> cell_nbr_fo;          ///< [ncell][4]: neighbour across each face in ascending
+	                                       ///<  reference face index (internal / ncell+bf), -1 pad
 	std::vector<int> cell_nfael;
 	std::vector<double> rc;                ///< [ncell][2]
 	std::vector<double> area;              ///< [ncell]

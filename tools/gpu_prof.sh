@@ -1,0 +1,22 @@
+#!/bin/bash
+# GPU-box profiling: rocprofv3 kernel trace + stats, then separate PMC passes (never combined with
+# trace domains). Every step under its own time limit; stop at the first failure.
+set -u
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+export TMPDIR=/tmp
+OUT=gpurun_out/prof
+mkdir -p $OUT
+ARGS="--steps 10 --warmup 2 --no-cpu-baseline"
+run() {  # name timeout cmd...
+  local name=$1 to=$2; shift 2
+  echo "== $name"; date
+  timeout -k 10 "$to" "$@" > "$OUT/$name.log" 2>&1
+  local rc=$?
+  echo "rc=$rc"; tail -3 "$OUT/$name.log"
+  [ $rc -eq 0 ] || { echo "stopping after $name"; exit $rc; }
+}
+run trace 600 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/trace -o run -- python3 bench.py $ARGS
+run pmc_fetch 600 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $OUT/fetch -o run -- python3 bench.py $ARGS
+run pmc_write 600 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $OUT/write -o run -- python3 bench.py $ARGS
+run pmc_sq 600 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_BUSY_CYCLES --output-format csv -d $OUT/sq -o run -- python3 bench.py $ARGS
+echo done
