@@ -192,7 +192,62 @@ class FlowFV:
         check(_ffi.lib().fvhip_get_gradients(self._h, dptr(u), dptr(g)))
         return g
 
+    def assemble_jacobian(self, u, diag=None, lower=None, upper=None):
+        """Spatial::assemble_jacobian (aspatial.cpp:242-340): blocks are ADDED into diag [nelem][4][4],
+        lower/upper [ninface][4][4] (A[R][L] += lower, A[L][R] += upper); zeros if not given."""
+        N, Fi = self.mesh.nelem, self.mesh.naface - self.mesh.nbface
+        diag = np.zeros((N, 4, 4)) if diag is None else diag
+        lower = np.zeros((Fi, 4, 4)) if lower is None else lower
+        upper = np.zeros((Fi, 4, 4)) if upper is None else upper
+        check(_ffi.lib().fvhip_assemble_jacobian(self._h, dptr(u), dptr(diag), dptr(lower), dptr(upper)))
+        return diag, lower, upper
+
+    def jacobian_pattern(self):
+        """Block-CSR pattern of the Jacobian (setJacobianPreallocation, alinalg.cpp:42-85)"""
+        N, Fi = self.mesh.nelem, self.mesh.naface - self.mesh.nbface
+        rowptr = np.zeros(N + 1, np.int32)
+        colind = np.zeros(N + 2 * Fi, np.int32)
+        check(_ffi.lib().fvhip_jacobian_pattern(self._h, iptr(rowptr), iptr(colind)))
+        return rowptr, colind
+
+    def assemble_jacobian_bsr(self, u, rowptr, colind):
+        vals = np.zeros((int(rowptr[-1]), 4, 4))
+        check(_ffi.lib().fvhip_assemble_jacobian_bsr(self._h, dptr(u), iptr(rowptr), iptr(colind), dptr(vals)))
+        return vals
+
+    def matfree_set_state(self, u, r, mdt):
+        """MatrixFreeSpatialJacobian::set_state (alinalg.cpp:131-140); r = -r(u), mdt = area/(CFL dt)"""
+        self._mf = (np.ascontiguousarray(u), np.ascontiguousarray(r), np.ascontiguousarray(mdt))
+        check(_ffi.lib().fvhip_matfree_set_state(self._h, *[dptr(a) for a in self._mf]))
+
+    def matfree_apply(self, x):
+        """MatrixFreeSpatialJacobian::apply (alinalg.cpp:142-233)"""
+        y = np.zeros((self.mesh.nelem, 4))
+        check(_ffi.lib().fvhip_matfree_apply(self._h, dptr(np.ascontiguousarray(x)), dptr(y)))
+        return y
+
+    def matfree_set_eps(self, eps):
+        check(_ffi.lib().fvhip_matfree_set_eps(self._h, float(eps)))
+
     # --- device-resident interface (internal cell order) -----------------------------------------
+    def assemble_jacobian_device(self, d_u, d_diag, d_lower, d_upper):
+        check(_ffi.lib().fvhip_assemble_jacobian_device(self._h, *[ctypes.c_void_p(p) for p in
+                                                                   (d_u, d_diag, d_lower, d_upper)]))
+
+    def add_pseudo_time_term_device(self, cfl, d_dtm, d_diag):
+        check(_ffi.lib().fvhip_add_pseudo_time_term_device(self._h, float(cfl), ctypes.c_void_p(d_dtm),
+                                                           ctypes.c_void_p(d_diag)))
+
+    def block_apply_device(self, d_diag, d_lower, d_upper, d_x, d_y):
+        check(_ffi.lib().fvhip_block_apply_device(self._h, *[ctypes.c_void_p(p) for p in
+                                                             (d_diag, d_lower, d_upper, d_x, d_y)]))
+
+    def matfree_set_state_device(self, d_u, d_r, d_mdt):
+        check(_ffi.lib().fvhip_matfree_set_state_device(self._h, *[ctypes.c_void_p(p) for p in (d_u, d_r, d_mdt)]))
+
+    def matfree_apply_device(self, d_x, d_y):
+        check(_ffi.lib().fvhip_matfree_apply_device(self._h, ctypes.c_void_p(d_x), ctypes.c_void_p(d_y)))
+
     def compute_residual_device(self, d_u, d_r, d_dtm=None, gettimesteps=False, overwrite=True):
         check(_ffi.lib().fvhip_compute_residual_device(self._h, ctypes.c_void_p(d_u), ctypes.c_void_p(d_r),
                                                        int(gettimesteps), ctypes.c_void_p(d_dtm or 0),
@@ -259,3 +314,17 @@ def local_flux(flux, gas, ul, ur, n):
     check(_ffi.lib().fvhip_local_flux(FLUXES[flux.upper()] if isinstance(flux, str) else flux, dptr(g),
                                       ul.shape[0], dptr(ul), dptr(ur), dptr(n), dptr(out)))
     return out
+
+
+def local_flux_jacobian(flux, gas, ul, ur, n):
+    """InviscidFlux::get_jacobian on the device: (dfdl, dfdr) [nf][4][4] with dfdl = -dF/dul"""
+    ul = np.ascontiguousarray(ul, np.float64)
+    ur = np.ascontiguousarray(ur, np.float64)
+    n = np.ascontiguousarray(n, np.float64)
+    nf = ul.shape[0]
+    dl = np.zeros((nf, 4, 4))
+    dr = np.zeros((nf, 4, 4))
+    g = np.array(gas, np.float64)
+    check(_ffi.lib().fvhip_local_flux_jacobian(FLUXES[flux.upper()] if isinstance(flux, str) else flux, dptr(g),
+                                               nf, dptr(ul), dptr(ur), dptr(n), dptr(dl), dptr(dr)))
+    return dl, dr

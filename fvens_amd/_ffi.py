@@ -46,8 +46,16 @@ _SIGS = {
                                                      ctypes.c_int, ctypes.c_void_p, ctypes.c_int]),
     "fvhip_get_gradients": (ctypes.c_int, [ctypes.c_void_p, c_dbl_p, c_dbl_p]),
     "fvhip_assemble_jacobian": (ctypes.c_int, [ctypes.c_void_p, c_dbl_p, c_dbl_p, c_dbl_p, c_dbl_p]),
+    "fvhip_assemble_jacobian_device": (ctypes.c_int, [ctypes.c_void_p] + [ctypes.c_void_p] * 4),
+    "fvhip_add_pseudo_time_term_device": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_double, ctypes.c_void_p,
+                                                         ctypes.c_void_p]),
+    "fvhip_block_apply_device": (ctypes.c_int, [ctypes.c_void_p] + [ctypes.c_void_p] * 5),
+    "fvhip_jacobian_pattern": (ctypes.c_int, [ctypes.c_void_p, c_int_p, c_int_p]),
+    "fvhip_assemble_jacobian_bsr": (ctypes.c_int, [ctypes.c_void_p, c_dbl_p, c_int_p, c_int_p, c_dbl_p]),
     "fvhip_matfree_set_state": (ctypes.c_int, [ctypes.c_void_p, c_dbl_p, c_dbl_p, c_dbl_p]),
     "fvhip_matfree_apply": (ctypes.c_int, [ctypes.c_void_p, c_dbl_p, c_dbl_p]),
+    "fvhip_matfree_set_state_device": (ctypes.c_int, [ctypes.c_void_p] + [ctypes.c_void_p] * 3),
+    "fvhip_matfree_apply_device": (ctypes.c_int, [ctypes.c_void_p] + [ctypes.c_void_p] * 2),
     "fvhip_matfree_set_eps": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_double]),
     "fvhip_to_internal": (ctypes.c_int, [ctypes.c_void_p, c_dbl_p, ctypes.c_void_p, ctypes.c_int]),
     "fvhip_from_internal": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, c_dbl_p, ctypes.c_int]),

@@ -6,10 +6,12 @@
 #include "../../include/fvhip.h"
 #include "layout.hpp"
 #include "kernels.hpp"
+#include "jacobian.hpp"
 #include "mesh.hpp"
 
 #include <hip/hip_runtime.h>
 #include <cstring>
+#include <algorithm>
 #include <cmath>
 #include <string>
 #include <vector>
@@ -82,6 +84,12 @@ struct fvhip_ctx
 	// mat-free state
 	double *d_mf_u = nullptr, *d_mf_r = nullptr, *d_mf_mdt = nullptr, *d_mf_aux = nullptr, *d_mf_y = nullptr;
 	double mf_eps = 1e-7;
+	const double *mf_u = nullptr, *mf_r = nullptr, *mf_mdt = nullptr;   // device state of the operator
+	double *d_part = nullptr, *d_pm = nullptr;
+	// Jacobian
+	JacMesh J{};
+	bool jac_ready = false;
+	double *d_jb = nullptr, *d_jlo = nullptr, *d_jup = nullptr, *d_jdiag = nullptr;
 	std::vector<double> h_stage;
 	// profiling
 	bool prof = false;
@@ -153,6 +161,50 @@ struct fvhip_ctx
 		// name is only known after launch; record under a generic label then rename
 		timed("k_sweep", [&]{ nm = launch_sweep(M, P, B, cfg.conv_numflux, rk, viscKind(), dt, stream); });
 		if(prof && !recs.empty() && recs.back().name == "k_sweep" && nm) recs.back().name = nm;
+		HC(hipGetLastError());
+	}
+
+	/// face-ordered mesh view and block buffers for the Jacobian, built on first use
+	void ensureJacobian() {
+		const int jf = cfg.conv_numflux_jac;
+		if(jf == FVHIP_FLUX_VANLEER) throw std::runtime_error(" ! VanLeerFlux: Not implemented!");   // anumericalflux.cpp:253-257
+		if(jf == FVHIP_FLUX_AUSMPLUS) throw std::runtime_error(" ! AUSMPlusFlux: Not implemented!"); // :556-560
+		if(jf < 0 || jf > 6) throw std::invalid_argument("unknown Jacobian flux");
+		for(int i = 0; i < cfg.nbc; i++)
+			if(bc_type[i] == FVHIP_BC_SUBSONIC_INFLOW)   // InFlow::computeGhostStateAndJacobian, abc.cpp:178-185
+				throw std::runtime_error("subsonic inflow BC has no Jacobian (Not implemented!)");
+		if(jac_ready) return;
+		auto& o = owned;
+		J.ncell = L.ncell; J.nbface = L.nbface; J.ninface = L.ninface;
+		J.if_LR = reinterpret_cast<const int2*>(upload(pack2(L.if_L, L.if_R), o));
+		J.if_n = reinterpret_cast<const double2*>(upload(L.if_n, o));
+		J.if_len = upload(L.if_len, o);
+		J.bf_L = M.bf_L; J.bf_bc = M.bf_bc; J.bf_n = M.bf_n; J.bf_rcbp = M.bf_rcbp; J.rc = M.rc;
+		J.bf_len = upload(L.bf_len, o);
+		J.cell_rfaces = reinterpret_cast<const int4*>(upload(L.cell_rfaces, o));
+		J.cell_nbr_fo = M.cell_nbr_fo;
+		d_jb = dalloc(16*static_cast<size_t>(std::max(L.nbface,1)), o);
+		jac_ready = true;
+	}
+
+	/// Spatial::assemble_jacobian into (diag internal order, lower/upper reference face order)
+	void assemble(const double* u, double* diag, double* lower, double* upper) {
+		ensureJacobian();
+		timed("k_jac_faces", [&]{ launch_jac_faces(J, P, cfg.conv_numflux_jac, viscKind(), u, d_jb, lower, upper, stream); });
+		timed("k_jac_diag", [&]{ launch_jac_diag(J, d_jb, lower, upper, diag, stream); });
+		HC(hipGetLastError());
+	}
+
+	/// MatrixFreeSpatialJacobian::apply on device vectors (internal order)
+	void matfree(const double* x, double* y) {
+		if(!mf_u || !mf_r || !mf_mdt) throw std::runtime_error("matrix-free operator: state not set");
+		const size_t N = static_cast<size_t>(L.ncell);
+		if(!d_part) { d_part = dalloc(mf_partials(), owned); d_pm = dalloc(2, owned); }
+		if(!d_mf_aux) { d_mf_aux = dalloc(4*N, owned); d_mf_y = dalloc(4*N, owned); }
+		timed("k_mf_norm", [&]{ launch_mf_norm(4LL*L.ncell, x, mf_eps, d_part, d_pm, stream); });
+		timed("k_mf_perturb", [&]{ launch_mf_perturb(4LL*L.ncell, mf_u, x, d_pm, d_mf_aux, stream); });
+		residual(d_mf_aux, d_mf_y, false, nullptr, true);
+		timed("k_mf_combine", [&]{ launch_mf_combine(L.ncell, mf_mdt, x, d_mf_y, mf_r, d_pm, y, stream); });
 		HC(hipGetLastError());
 	}
 };
@@ -308,16 +360,149 @@ int fvhip_get_gradients(fvhip_handle h, const double* u, double* grads)
 
 int fvhip_assemble_jacobian(fvhip_handle h, const double* u, double* diag, double* lower, double* upper)
 {
-	return guard([&] { throw std::runtime_error("fvhip_assemble_jacobian: not built yet"); });
+	return guard([&] {
+		HC(hipSetDevice(h->device));
+		const size_t N = static_cast<size_t>(h->L.ncell), Fi = static_cast<size_t>(h->L.ninface);
+		std::vector<double>& st = h->h_stage;
+		toInternal(h, u, st.data(), 4);
+		HC(hipMemcpyAsync(h->d_u, st.data(), 4*N*sizeof(double), hipMemcpyHostToDevice, h->stream));
+		HC(hipStreamSynchronize(h->stream));
+		if(!h->d_jdiag) {
+			h->d_jdiag = dalloc(16*N, h->owned);
+			h->d_jlo = dalloc(16*std::max<size_t>(Fi,1), h->owned);
+			h->d_jup = dalloc(16*std::max<size_t>(Fi,1), h->owned);
+		}
+		h->assemble(h->d_u, h->d_jdiag, h->d_jlo, h->d_jup);
+		// ADD_VALUES into the caller's blocks (the reference's caller zeroes them, aodesolver.cpp:456)
+		std::vector<double> dg(16*N), tmp(16*N), lo(16*Fi), up(16*Fi);
+		HC(hipMemcpyAsync(dg.data(), h->d_jdiag, 16*N*sizeof(double), hipMemcpyDeviceToHost, h->stream));
+		if(Fi) {
+			HC(hipMemcpyAsync(lo.data(), h->d_jlo, 16*Fi*sizeof(double), hipMemcpyDeviceToHost, h->stream));
+			HC(hipMemcpyAsync(up.data(), h->d_jup, 16*Fi*sizeof(double), hipMemcpyDeviceToHost, h->stream));
+		}
+		HC(hipStreamSynchronize(h->stream));
+		fromInternal(h, dg.data(), tmp.data(), 16);
+		for(size_t k = 0; k < 16*N; k++) diag[k] += tmp[k];
+		for(size_t k = 0; k < 16*Fi; k++) { lower[k] += lo[k]; upper[k] += up[k]; }
+	});
 }
+
+int fvhip_assemble_jacobian_device(fvhip_handle h, const double* d_u, double* d_diag, double* d_lower, double* d_upper)
+{
+	return guard([&] {
+		HC(hipSetDevice(h->device));
+		h->assemble(d_u, d_diag, d_lower, d_upper);
+	});
+}
+
+int fvhip_add_pseudo_time_term_device(fvhip_handle h, double cfl, double* d_dtm, double* d_diag)
+{
+	return guard([&] {
+		HC(hipSetDevice(h->device));
+		h->ensureJacobian();
+		h->timed("k_pseudo_time", [&]{ launch_pseudo_time(h->L.ncell, h->M.area, cfl, d_dtm, d_diag, h->stream); });
+		HC(hipGetLastError());
+	});
+}
+
+int fvhip_block_apply_device(fvhip_handle h, const double* d_diag, const double* d_lower, const double* d_upper,
+                             const double* d_x, double* d_y)
+{
+	return guard([&] {
+		HC(hipSetDevice(h->device));
+		h->ensureJacobian();
+		h->timed("k_block_apply", [&]{ launch_block_apply(h->J, d_diag, d_lower, d_upper, d_x, d_y, h->stream); });
+		HC(hipGetLastError());
+	});
+}
+
+int fvhip_jacobian_pattern(fvhip_handle h, int* rowptr, int* colind)
+{
+	return guard([&] {
+		const int N = h->L.ncell, nb = h->L.nbface, Fi = h->L.ninface;
+		// reference cell numbering: diagonal plus one block per interior face on each side
+		std::vector<int> cnt(N, 1);
+		for(int fi = 0; fi < Fi; fi++) { cnt[h->L.perm[h->L.if_L[fi]]]++; cnt[h->L.perm[h->L.if_R[fi]]]++; }
+		rowptr[0] = 0;
+		for(int c = 0; c < N; c++) rowptr[c+1] = rowptr[c] + cnt[c];
+		std::vector<int> pos(rowptr, rowptr + N);
+		for(int c = 0; c < N; c++) colind[pos[c]++] = c;
+		for(int fi = 0; fi < Fi; fi++) {
+			const int l = h->L.perm[h->L.if_L[fi]], r = h->L.perm[h->L.if_R[fi]];
+			colind[pos[l]++] = r; colind[pos[r]++] = l;
+		}
+		for(int c = 0; c < N; c++) std::sort(colind + rowptr[c], colind + rowptr[c+1]);
+		(void)nb;
+	});
+}
+
+int fvhip_assemble_jacobian_bsr(fvhip_handle h, const double* u, const int* rowptr, const int* colind, double* vals)
+{
+	return guard([&] {
+		const int N = h->L.ncell, Fi = h->L.ninface;
+		std::vector<double> diag(16*static_cast<size_t>(N)), lo(16*static_cast<size_t>(std::max(Fi,1))),
+			up(16*static_cast<size_t>(std::max(Fi,1)));
+		if(fvhip_assemble_jacobian(h, u, diag.data(), lo.data(), up.data())) throw std::runtime_error(g_err);
+		auto find = [&](int row, int col) -> size_t {
+			const int* b = colind + rowptr[row]; const int* e = colind + rowptr[row+1];
+			const int* it = std::lower_bound(b, e, col);
+			if(it == e || *it != col) throw std::runtime_error("Jacobian pattern does not match the mesh");
+			return static_cast<size_t>(it - colind);
+		};
+		std::fill(vals, vals + 16*static_cast<size_t>(rowptr[N]), 0.0);
+		for(int c = 0; c < N; c++) std::memcpy(vals + 16*find(c,c), &diag[16*static_cast<size_t>(c)], 16*sizeof(double));
+		for(int fi = 0; fi < Fi; fi++) {
+			const int l = h->L.perm[h->L.if_L[fi]], r = h->L.perm[h->L.if_R[fi]];
+			std::memcpy(vals + 16*find(r,l), &lo[16*static_cast<size_t>(fi)], 16*sizeof(double));
+			std::memcpy(vals + 16*find(l,r), &up[16*static_cast<size_t>(fi)], 16*sizeof(double));
+		}
+	});
+}
+
 int fvhip_matfree_set_state(fvhip_handle h, const double* u, const double* r, const double* mdt)
 {
-	return guard([&] { throw std::runtime_error("fvhip_matfree_set_state: not built yet"); });
+	return guard([&] {
+		HC(hipSetDevice(h->device));
+		const size_t N = static_cast<size_t>(h->L.ncell);
+		if(!h->d_mf_u) { h->d_mf_u = dalloc(4*N, h->owned); h->d_mf_r = dalloc(4*N, h->owned); h->d_mf_mdt = dalloc(N, h->owned); }
+		std::vector<double> st(4*N);
+		toInternal(h, u, st.data(), 4);
+		HC(hipMemcpy(h->d_mf_u, st.data(), 4*N*sizeof(double), hipMemcpyHostToDevice));
+		toInternal(h, r, st.data(), 4);
+		HC(hipMemcpy(h->d_mf_r, st.data(), 4*N*sizeof(double), hipMemcpyHostToDevice));
+		toInternal(h, mdt, st.data(), 1);
+		HC(hipMemcpy(h->d_mf_mdt, st.data(), N*sizeof(double), hipMemcpyHostToDevice));
+		h->mf_u = h->d_mf_u; h->mf_r = h->d_mf_r; h->mf_mdt = h->d_mf_mdt;
+	});
 }
+
 int fvhip_matfree_apply(fvhip_handle h, const double* x, double* y)
 {
-	return guard([&] { throw std::runtime_error("fvhip_matfree_apply: not built yet"); });
+	return guard([&] {
+		HC(hipSetDevice(h->device));
+		const size_t N = static_cast<size_t>(h->L.ncell);
+		if(!h->d_mf_u) throw std::runtime_error("matrix-free operator: state not set");
+		std::vector<double> st(4*N);
+		toInternal(h, x, st.data(), 4);
+		double *dx = h->d_u, *dy = h->d_r;   // scratch: the operator's state lives in d_mf_*
+		HC(hipMemcpyAsync(dx, st.data(), 4*N*sizeof(double), hipMemcpyHostToDevice, h->stream));
+		h->matfree(dx, dy);
+		HC(hipMemcpyAsync(st.data(), dy, 4*N*sizeof(double), hipMemcpyDeviceToHost, h->stream));
+		HC(hipStreamSynchronize(h->stream));
+		fromInternal(h, st.data(), y, 4);
+	});
 }
+
+int fvhip_matfree_set_state_device(fvhip_handle h, const double* d_u, const double* d_r, const double* d_mdt)
+{
+	return guard([&] { h->mf_u = d_u; h->mf_r = d_r; h->mf_mdt = d_mdt; });
+}
+
+int fvhip_matfree_apply_device(fvhip_handle h, const double* d_x, double* d_y)
+{
+	return guard([&] { HC(hipSetDevice(h->device)); h->matfree(d_x, d_y); });
+}
+
 int fvhip_matfree_set_eps(fvhip_handle h, double eps) { return guard([&] { h->mf_eps = eps; }); }
 
 int fvhip_to_internal(fvhip_handle h, const double* host_ref, double* d_internal, int width)
@@ -411,7 +596,24 @@ int fvhip_local_flux(int flux_type, const double* gas5, int nf, const double* ul
 int fvhip_local_flux_jacobian(int flux_type, const double* gas5, int nf, const double* ul,
                               const double* ur, const double* n, double* dfdl, double* dfdr)
 {
-	return guard([&] { throw std::runtime_error("fvhip_local_flux_jacobian: not built yet"); });
+	return guard([&] {
+		if(flux_type == FVHIP_FLUX_VANLEER) throw std::runtime_error(" ! VanLeerFlux: Not implemented!");
+		if(flux_type == FVHIP_FLUX_AUSMPLUS) throw std::runtime_error(" ! AUSMPlusFlux: Not implemented!");
+		if(flux_type < 0 || flux_type > 6) throw std::invalid_argument("unknown flux");
+		gd::Gas G{gas5[0], gas5[1], gas5[2], gas5[3], gas5[4], 110.5};
+		double *a, *b, *c, *d, *e;
+		HC(hipMalloc(&a, 4*sizeof(double)*nf + 8)); HC(hipMalloc(&b, 4*sizeof(double)*nf + 8));
+		HC(hipMalloc(&c, 2*sizeof(double)*nf + 8)); HC(hipMalloc(&d, 16*sizeof(double)*nf + 8));
+		HC(hipMalloc(&e, 16*sizeof(double)*nf + 8));
+		HC(hipMemcpy(a, ul, 4*sizeof(double)*nf, hipMemcpyHostToDevice));
+		HC(hipMemcpy(b, ur, 4*sizeof(double)*nf, hipMemcpyHostToDevice));
+		HC(hipMemcpy(c, n, 2*sizeof(double)*nf, hipMemcpyHostToDevice));
+		launch_local_jac(flux_type, G, nf, a, b, c, d, e, nullptr);
+		HC(hipGetLastError());
+		HC(hipMemcpy(dfdl, d, 16*sizeof(double)*nf, hipMemcpyDeviceToHost));
+		HC(hipMemcpy(dfdr, e, 16*sizeof(double)*nf, hipMemcpyDeviceToHost));
+		(void)hipFree(a); (void)hipFree(b); (void)hipFree(c); (void)hipFree(d); (void)hipFree(e);
+	});
 }
 
 // ------------------------------------------------------------------------------------------------

@@ -1,0 +1,375 @@
+/** \file jacobian.hip
+ * \brief Analytic first-order Jacobian assembly, pseudo-time diagonal, block operator apply and the
+ *   matrix-free finite-difference operator on MI355X.
+ *
+ * Replaces Spatial::assemble_jacobian (aspatial.cpp:242-340) with
+ * FlowFV::compute_local_jacobian_interior/_boundary (flow_spatial.cpp:818-875),
+ * SteadyBackwardEulerSolver::addPseudoTimeTerm (aodesolver.cpp:300-329) and
+ * MatrixFreeSpatialJacobian::apply (alinalg.cpp:142-233).
+ *
+ * Storage is face-based, which is what the reference's assembly produces block by block:
+ *   lower[fi], upper[fi] (interior face fi = f - nbface, reference order): A[R][L] += L, A[L][R] += U;
+ *   diag[c] (internal cell order): 0 + sum over the cell's faces in ascending reference face index
+ *   of -left (boundary), -L (cell is left), -U (cell is right) — the order of the reference's
+ *   ADD_VALUES calls in a single-thread run, so diagonal blocks are bitwise reproducible.
+ * One thread per face computes its blocks column by column (gasjac.hpp), so no atomics are used.
+ */
+#include "jacobian.hpp"
+#include "gasjac.hpp"
+
+namespace fvhip {
+
+using namespace gd;
+
+// -------------------------------------------------------------------------------------------------
+// interior faces
+// -------------------------------------------------------------------------------------------------
+template <int FLUX, int VISC>
+__global__ __launch_bounds__(256)
+void k_jac_interior(JacMesh J, gd::Gas G, const double* __restrict__ u,
+                    double* __restrict__ lower, double* __restrict__ upper)
+{
+	const int fi = blockIdx.x*blockDim.x + threadIdx.x;
+	if(fi >= J.ninface) return;
+	const int2 lr = J.if_LR[fi];
+	const double2 nn = J.if_n[fi];
+	const double n[2] = {nn.x, nn.y};
+	const double len = J.if_len[fi];
+	double ul[4], ur[4];
+	{
+		const double4* u4 = reinterpret_cast<const double4*>(u);
+		const double4 a = u4[lr.x], b = u4[lr.y];
+		ul[0] = a.x; ul[1] = a.y; ul[2] = a.z; ul[3] = a.w;
+		ur[0] = b.x; ur[1] = b.y; ur[2] = b.z; ur[3] = b.w;
+	}
+	typename JacOf<FLUX>::T F;
+	jac_prepare<FLUX>(G, ul, ur, n, F);
+	ViscJ V;
+	if(VISC) {
+		const double2 a = J.rc[lr.x], b = J.rc[lr.y];
+		const double cl[2] = {a.x, a.y}, cr[2] = {b.x, b.y};
+		visc_jac_prepare(G, VISC == 2, ul, ur, cl, cr, V);
+	}
+	double* Lo = lower + 16*static_cast<size_t>(fi);
+	double* Up = upper + 16*static_cast<size_t>(fi);
+#pragma unroll
+	for(int k = 0; k < 4; k++) {
+		double dl[4], dr[4];
+		jac_col<FLUX>(G, F, n, k, dl, dr);
+		if(VISC) visc_jac_col(G, V, ul, ur, n, k, dl, dr);
+		for(int i = 0; i < 4; i++) {
+			Lo[i*4+k] = dl[i]*len;
+			Up[i*4+k] = dr[i]*len;
+		}
+	}
+}
+
+// -------------------------------------------------------------------------------------------------
+// physical boundary faces: left = len*(dfdl - dfdr * d(ghost)/d(u_L))
+// -------------------------------------------------------------------------------------------------
+template <int FLUX, int VISC>
+__global__ __launch_bounds__(64)
+void k_jac_boundary(JacMesh J, DevPhys P, const double* __restrict__ u, double* __restrict__ bblk)
+{
+	const int f = blockIdx.x*blockDim.x + threadIdx.x;
+	if(f >= J.nbface) return;
+	const int c = J.bf_L[f];
+	const double2 nn = J.bf_n[f];
+	const double n[2] = {nn.x, nn.y};
+	const double len = J.bf_len[f];
+	double ul[4];
+	for(int i = 0; i < 4; i++) ul[i] = u[4*static_cast<size_t>(c)+i];
+	double gs[4], dgs[16];
+	ghost_jacobian(P.gas, P.bc[J.bf_bc[f]], P.uinf, ul, n, gs, dgs);
+	typename JacOf<FLUX>::T F;
+	jac_prepare<FLUX>(P.gas, ul, gs, n, F);
+	ViscJ V;
+	if(VISC) {
+		const double2 a = J.rc[c], b = J.bf_rcbp[f];
+		const double cl[2] = {a.x, a.y}, cr[2] = {b.x, b.y};
+		visc_jac_prepare(P.gas, VISC == 2, ul, gs, cl, cr, V);
+	}
+	double left[16], right[16];
+#pragma unroll
+	for(int k = 0; k < 4; k++) {
+		double dl[4], dr[4];
+		jac_col<FLUX>(P.gas, F, n, k, dl, dr);
+		if(VISC) visc_jac_col(P.gas, V, ul, gs, n, k, dl, dr);
+		for(int i = 0; i < 4; i++) { left[i*4+k] = dl[i]; right[i*4+k] = dr[i]; }
+	}
+	double* out = bblk + 16*static_cast<size_t>(f);
+#pragma unroll
+	for(int i = 0; i < 4; i++)
+#pragma unroll
+		for(int j = 0; j < 4; j++) {
+			double s = right[i*4+0]*dgs[0*4+j];
+			for(int k = 1; k < 4; k++) s += right[i*4+k]*dgs[k*4+j];
+			out[i*4+j] = len*(left[i*4+j] - s);
+		}
+}
+
+// -------------------------------------------------------------------------------------------------
+// diagonal blocks: per cell, ascending reference face order
+// -------------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256)
+void k_jac_diag(JacMesh J, const double* __restrict__ bblk, const double* __restrict__ lower,
+                const double* __restrict__ upper, double* __restrict__ diag)
+{
+	const int c = blockIdx.x*blockDim.x + threadIdx.x;
+	if(c >= J.ncell) return;
+	const int4 fc = J.cell_rfaces[c];
+	const int codes[4] = {fc.x, fc.y, fc.z, fc.w};
+	double d[16];
+#pragma unroll
+	for(int k = 0; k < 16; k++) d[k] = 0;
+#pragma unroll
+	for(int j = 0; j < 4; j++) {
+		const int code = codes[j];
+		if(code < 0) continue;
+		const int f = code >> 1;
+		const double* blk;
+		if(f < J.nbface) blk = bblk + 16*static_cast<size_t>(f);
+		else blk = ((code & 1) ? upper : lower) + 16*static_cast<size_t>(f - J.nbface);
+		const double4* b4 = reinterpret_cast<const double4*>(blk);
+#pragma unroll
+		for(int q = 0; q < 4; q++) {
+			const double4 v = b4[q];
+			d[4*q+0] += -1.0*v.x; d[4*q+1] += -1.0*v.y; d[4*q+2] += -1.0*v.z; d[4*q+3] += -1.0*v.w;
+		}
+	}
+	double4* o = reinterpret_cast<double4*>(diag + 16*static_cast<size_t>(c));
+#pragma unroll
+	for(int q = 0; q < 4; q++) o[q] = make_double4(d[4*q], d[4*q+1], d[4*q+2], d[4*q+3]);
+}
+
+// -------------------------------------------------------------------------------------------------
+// pseudo-time term: dtm <- area/(cfl*dtm); diag += dtm*I (all 16 entries, as MatSetValuesBlocked)
+// -------------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256)
+void k_pseudo_time(int ncell, const double* __restrict__ area, double cfl, double* __restrict__ dtm,
+                   double* __restrict__ diag)
+{
+	const int c = blockIdx.x*blockDim.x + threadIdx.x;
+	if(c >= ncell) return;
+	const double m = area[c] / (cfl*dtm[c]);
+	dtm[c] = m;
+	double* d = diag + 16*static_cast<size_t>(c);
+#pragma unroll
+	for(int i = 0; i < 4; i++)
+#pragma unroll
+		for(int j = 0; j < 4; j++) d[i*4+j] += m*(i == j ? 1.0 : 0.0);
+}
+
+// -------------------------------------------------------------------------------------------------
+// y = A x with the face-based blocks; per cell: diag first, then faces in ascending reference order
+// -------------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256)
+void k_block_apply(JacMesh J, const double* __restrict__ diag, const double* __restrict__ lower,
+                   const double* __restrict__ upper, const double* __restrict__ x, double* __restrict__ y)
+{
+	const int c = blockIdx.x*blockDim.x + threadIdx.x;
+	if(c >= J.ncell) return;
+	const double4* x4 = reinterpret_cast<const double4*>(x);
+	double acc[4];
+	{
+		const double4 xc = x4[c];
+		const double xv[4] = {xc.x, xc.y, xc.z, xc.w};
+		const double* D = diag + 16*static_cast<size_t>(c);
+		for(int i = 0; i < 4; i++) {
+			double s = D[i*4]*xv[0];
+			for(int k = 1; k < 4; k++) s += D[i*4+k]*xv[k];
+			acc[i] = s;
+		}
+	}
+	const int4 fc = J.cell_rfaces[c];
+	const int4 nb = J.cell_nbr_fo[c];
+	const int codes[4] = {fc.x, fc.y, fc.z, fc.w};
+	const int nbrs[4] = {nb.x, nb.y, nb.z, nb.w};
+#pragma unroll
+	for(int j = 0; j < 4; j++) {
+		const int code = codes[j];
+		if(code < 0) continue;
+		const int f = code >> 1;
+		if(f < J.nbface) continue;
+		const double* B = ((code & 1) ? lower : upper) + 16*static_cast<size_t>(f - J.nbface);
+		const double4 xo = x4[nbrs[j]];
+		const double xv[4] = {xo.x, xo.y, xo.z, xo.w};
+		for(int i = 0; i < 4; i++) {
+			double s = B[i*4]*xv[0];
+			for(int k = 1; k < 4; k++) s += B[i*4+k]*xv[k];
+			acc[i] += s;
+		}
+	}
+	reinterpret_cast<double4*>(y)[c] = make_double4(acc[0], acc[1], acc[2], acc[3]);
+}
+
+// -------------------------------------------------------------------------------------------------
+// matrix-free pieces
+// -------------------------------------------------------------------------------------------------
+constexpr int RED_BLOCKS = 1024;
+
+/// deterministic two-stage sum of squares: fixed partition, fixed tree
+__global__ __launch_bounds__(256)
+void k_sumsq_partial(long long n, const double* __restrict__ x, double* __restrict__ part)
+{
+	__shared__ double s[256];
+	double acc = 0;
+	for(long long i = blockIdx.x*256LL + threadIdx.x; i < n; i += 256LL*gridDim.x) acc += x[i]*x[i];
+	s[threadIdx.x] = acc;
+	__syncthreads();
+	for(int w = 128; w > 0; w >>= 1) {
+		if(threadIdx.x < w) s[threadIdx.x] += s[threadIdx.x + w];
+		__syncthreads();
+	}
+	if(threadIdx.x == 0) part[blockIdx.x] = s[0];
+}
+
+/// pertmag = eps / sqrt(sum(part))
+__global__ __launch_bounds__(256)
+void k_pertmag(int np, const double* __restrict__ part, double eps, double* __restrict__ out)
+{
+	__shared__ double s[256];
+	double acc = 0;
+	for(int i = threadIdx.x; i < np; i += 256) acc += part[i];
+	s[threadIdx.x] = acc;
+	__syncthreads();
+	for(int w = 128; w > 0; w >>= 1) {
+		if(threadIdx.x < w) s[threadIdx.x] += s[threadIdx.x + w];
+		__syncthreads();
+	}
+	if(threadIdx.x == 0) { out[0] = sqrt(s[0]); out[1] = eps/out[0]; }
+}
+
+__global__ __launch_bounds__(256)
+void k_mf_perturb(long long n, const double* __restrict__ u, const double* __restrict__ x,
+                  const double* __restrict__ pm, double* __restrict__ aux)
+{
+	const long long i = blockIdx.x*256LL + threadIdx.x;
+	if(i >= n) return;
+	aux[i] = u[i] + pm[1]*x[i];
+}
+
+__global__ __launch_bounds__(256)
+void k_mf_combine(int ncell, const double* __restrict__ mdt, const double* __restrict__ x,
+                  const double* __restrict__ yg, const double* __restrict__ res,
+                  const double* __restrict__ pm, double* __restrict__ y)
+{
+	const int c = blockIdx.x*256 + threadIdx.x;
+	if(c >= ncell) return;
+	const double pert = pm[1];
+	for(int i = 0; i < 4; i++) {
+		const size_t k = 4*static_cast<size_t>(c) + i;
+		y[k] = mdt[c]*x[k] + (-yg[k] + res[k])/pert;
+	}
+}
+
+// pointwise flux Jacobians (InviscidFlux::get_jacobian)
+template <int FLUX>
+__global__ __launch_bounds__(256)
+void k_local_jac(gd::Gas G, int nf, const double* __restrict__ ul, const double* __restrict__ ur,
+                 const double* __restrict__ nrm, double* __restrict__ dfdl, double* __restrict__ dfdr)
+{
+	const int f = blockIdx.x*blockDim.x + threadIdx.x;
+	if(f >= nf) return;
+	double a[4], b[4], n[2] = {nrm[2*f], nrm[2*f+1]};
+	for(int i = 0; i < 4; i++) { a[i] = ul[4*f+i]; b[i] = ur[4*f+i]; }
+	typename JacOf<FLUX>::T F;
+	jac_prepare<FLUX>(G, a, b, n, F);
+#pragma unroll
+	for(int k = 0; k < 4; k++) {
+		double dl[4], dr[4];
+		jac_col<FLUX>(G, F, n, k, dl, dr);
+		for(int i = 0; i < 4; i++) { dfdl[16*f+i*4+k] = dl[i]; dfdr[16*f+i*4+k] = dr[i]; }
+	}
+}
+
+// -------------------------------------------------------------------------------------------------
+// launchers
+// -------------------------------------------------------------------------------------------------
+static inline int nblk(long long n, int b) { return static_cast<int>((n + b - 1)/b); }
+
+template <int FLUX, int VISC>
+static void jac_launch(const JacMesh& J, const DevPhys& P, const double* u, double* bblk, double* lower,
+                       double* upper, hipStream_t s)
+{
+	if(J.ninface > 0)
+		hipLaunchKernelGGL((k_jac_interior<FLUX,VISC>), dim3(nblk(J.ninface,256)), dim3(256), 0, s, J, P.gas, u, lower, upper);
+	if(J.nbface > 0)
+		hipLaunchKernelGGL((k_jac_boundary<FLUX,VISC>), dim3(nblk(J.nbface,64)), dim3(64), 0, s, J, P, u, bblk);
+}
+
+template <int FLUX>
+static void jac_launch_v(const JacMesh& J, const DevPhys& P, int visc, const double* u, double* bblk,
+                         double* lower, double* upper, hipStream_t s)
+{
+	switch(visc) {
+		case 0: jac_launch<FLUX,0>(J, P, u, bblk, lower, upper, s); break;
+		case 1: jac_launch<FLUX,1>(J, P, u, bblk, lower, upper, s); break;
+		default: jac_launch<FLUX,2>(J, P, u, bblk, lower, upper, s);
+	}
+}
+
+void launch_jac_faces(const JacMesh& J, const DevPhys& P, int jflux, int visc, const double* u, double* bblk,
+                      double* lower, double* upper, hipStream_t s)
+{
+	switch(jflux) {
+		case 0: jac_launch_v<0>(J, P, visc, u, bblk, lower, upper, s); break;
+		case 2: jac_launch_v<2>(J, P, visc, u, bblk, lower, upper, s); break;
+		case 4: jac_launch_v<4>(J, P, visc, u, bblk, lower, upper, s); break;
+		case 5: jac_launch_v<5>(J, P, visc, u, bblk, lower, upper, s); break;
+		case 6: jac_launch_v<6>(J, P, visc, u, bblk, lower, upper, s); break;
+		default: break;
+	}
+}
+
+void launch_jac_diag(const JacMesh& J, const double* bblk, const double* lower, const double* upper,
+                     double* diag, hipStream_t s)
+{
+	hipLaunchKernelGGL(k_jac_diag, dim3(nblk(J.ncell,256)), dim3(256), 0, s, J, bblk, lower, upper, diag);
+}
+
+void launch_pseudo_time(int ncell, const double* area, double cfl, double* dtm, double* diag, hipStream_t s)
+{
+	hipLaunchKernelGGL(k_pseudo_time, dim3(nblk(ncell,256)), dim3(256), 0, s, ncell, area, cfl, dtm, diag);
+}
+
+void launch_block_apply(const JacMesh& J, const double* diag, const double* lower, const double* upper,
+                        const double* x, double* y, hipStream_t s)
+{
+	hipLaunchKernelGGL(k_block_apply, dim3(nblk(J.ncell,256)), dim3(256), 0, s, J, diag, lower, upper, x, y);
+}
+
+void launch_mf_norm(long long n, const double* x, double eps, double* part, double* pm, hipStream_t s)
+{
+	hipLaunchKernelGGL(k_sumsq_partial, dim3(RED_BLOCKS), dim3(256), 0, s, n, x, part);
+	hipLaunchKernelGGL(k_pertmag, dim3(1), dim3(256), 0, s, RED_BLOCKS, part, eps, pm);
+}
+
+void launch_mf_perturb(long long n, const double* u, const double* x, const double* pm, double* aux, hipStream_t s)
+{
+	hipLaunchKernelGGL(k_mf_perturb, dim3(nblk(n,256)), dim3(256), 0, s, n, u, x, pm, aux);
+}
+
+void launch_mf_combine(int ncell, const double* mdt, const double* x, const double* yg, const double* res,
+                       const double* pm, double* y, hipStream_t s)
+{
+	hipLaunchKernelGGL(k_mf_combine, dim3(nblk(ncell,256)), dim3(256), 0, s, ncell, mdt, x, yg, res, pm, y);
+}
+
+int mf_partials() { return RED_BLOCKS; }
+
+void launch_local_jac(int flux, const gd::Gas& G, int nf, const double* ul, const double* ur, const double* n,
+                      double* dfdl, double* dfdr, hipStream_t s)
+{
+	const dim3 g(nblk(nf,256)), b(256);
+	switch(flux) {
+		case 0: hipLaunchKernelGGL(k_local_jac<0>, g, b, 0, s, G, nf, ul, ur, n, dfdl, dfdr); break;
+		case 2: hipLaunchKernelGGL(k_local_jac<2>, g, b, 0, s, G, nf, ul, ur, n, dfdl, dfdr); break;
+		case 4: hipLaunchKernelGGL(k_local_jac<4>, g, b, 0, s, G, nf, ul, ur, n, dfdl, dfdr); break;
+		case 5: hipLaunchKernelGGL(k_local_jac<5>, g, b, 0, s, G, nf, ul, ur, n, dfdl, dfdr); break;
+		case 6: hipLaunchKernelGGL(k_local_jac<6>, g, b, 0, s, G, nf, ul, ur, n, dfdl, dfdr); break;
+		default: break;
+	}
+}
+
+}

@@ -178,9 +178,22 @@ Layout buildLayout(const fvhip_mesh& m, const fvhip_flow_config& cfg, bool renum
 	}
 	// --- interior faces (reference order) ---
 	Lo.if_L.resize(F-nb); Lo.if_R.resize(F-nb); Lo.if_slot.assign(F-nb, -1);
-	for(int f = nb; f < F; f++) { Lo.if_L[f-nb] = Lo.iperm[Lref(f)]; Lo.if_R[f-nb] = Lo.iperm[Rref(f)]; }
+	Lo.if_n.resize(2*static_cast<size_t>(F-nb)); Lo.if_len.resize(F-nb); Lo.bf_len.resize(nb);
+	for(int f = nb; f < F; f++) {
+		Lo.if_L[f-nb] = Lo.iperm[Lref(f)]; Lo.if_R[f-nb] = Lo.iperm[Rref(f)];
+		Lo.if_n[2*static_cast<size_t>(f-nb)] = m.facemetric[3*static_cast<size_t>(f)];
+		Lo.if_n[2*static_cast<size_t>(f-nb)+1] = m.facemetric[3*static_cast<size_t>(f)+1];
+		Lo.if_len[f-nb] = m.facemetric[3*static_cast<size_t>(f)+2];
+	}
+	for(int f = 0; f < nb; f++) Lo.bf_len[f] = m.facemetric[3*static_cast<size_t>(f)+2];
 	for(size_t s = 0; s < Lo.slot_face.size(); s++)
 		if(Lo.slot_face[s] >= nb) Lo.if_slot[Lo.slot_face[s]-nb] = static_cast<int>(s);
+	// each cell's faces as reference face codes, same order as cell_slots
+	Lo.cell_rfaces.assign(4*static_cast<size_t>(N), -1);
+	for(size_t k = 0; k < Lo.cell_slots.size(); k++) {
+		const int code = Lo.cell_slots[k];
+		if(code >= 0) Lo.cell_rfaces[k] = (Lo.slot_face[code >> 1] << 1) | (code & 1);
+	}
 
 	// --- WLS normal matrices (agradientschemes.cpp:218-317), reference face order ---
 	if(cfg.gradientscheme == FVHIP_GRAD_LEASTSQUARES) {

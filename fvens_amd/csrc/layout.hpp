@@ -59,6 +59,10 @@ struct Layout
 	// interior faces (reference order, for the Jacobian): internal L, R
 	std::vector<int> if_L, if_R;
 	std::vector<int> if_slot;              ///< one slot carrying the face's geometry
+	std::vector<double> if_n, if_len;      ///< [Fi][2], [Fi]
+	std::vector<double> bf_len;            ///< [nb]
+	std::vector<int> cell_rfaces;          ///< [ncell][4]: (reference face << 1 | cell-is-right),
+	                                       ///<  same order as cell_slots
 	int max_slots = 0;
 };
 

@@ -118,10 +118,29 @@ int fvhip_get_gradients(fvhip_handle h, const double* u, double* grads);
 /** Spatial::assemble_jacobian into block-sparse storage: diag [nelem][16] (diagonal blocks),
  *  lower/upper [ninface][16] for interior faces in face order (A[R][L] += L, A[L][R] += U). */
 int fvhip_assemble_jacobian(fvhip_handle h, const double* u, double* diag, double* lower, double* upper);
+/** Same on device arrays: d_u, d_diag in internal cell order; d_lower/d_upper [ninface][16] in
+ *  reference interior-face order. The Jacobian flux is cfg.conv_numflux_jac (LLF/AUSM/Roe/HLL/HLLC). */
+int fvhip_assemble_jacobian_device(fvhip_handle h, const double* d_u, double* d_diag, double* d_lower,
+                                   double* d_upper);
+/** SteadyBackwardEulerSolver::addPseudoTimeTerm (aodesolver.cpp:300-329) on device arrays:
+ *  d_dtm <- area/(cfl*d_dtm); d_diag += d_dtm * I */
+int fvhip_add_pseudo_time_term_device(fvhip_handle h, double cfl, double* d_dtm, double* d_diag);
+/** y = A x with the face-based blocks (the product PETSc's MatMult forms, alinalg.cpp:90-119) */
+int fvhip_block_apply_device(fvhip_handle h, const double* d_diag, const double* d_lower,
+                             const double* d_upper, const double* d_x, double* d_y);
+/** setJacobianPreallocation (alinalg.cpp:42-85) as block CSR in reference cell numbering:
+ *  rowptr [nelem+1], colind [nelem + 2*ninface] sorted per row */
+int fvhip_jacobian_pattern(fvhip_handle h, int* rowptr, int* colind);
+/** assemble_jacobian into row-major 4x4 blocks vals [nnzb][16] of that pattern (BAIJ, bs = 4) */
+int fvhip_assemble_jacobian_bsr(fvhip_handle h, const double* u, const int* rowptr, const int* colind,
+                                double* vals);
 
 /** MatrixFreeSpatialJacobian: set_state(u, r = -r(u), mdt = area/(CFL*dt)) then y = J x */
 int fvhip_matfree_set_state(fvhip_handle h, const double* u, const double* r, const double* mdt);
 int fvhip_matfree_apply(fvhip_handle h, const double* x, double* y);
+/** Device variants (internal order). set_state keeps the pointers, as the reference keeps the Vecs. */
+int fvhip_matfree_set_state_device(fvhip_handle h, const double* d_u, const double* d_r, const double* d_mdt);
+int fvhip_matfree_apply_device(fvhip_handle h, const double* d_x, double* d_y);
 /** -matrix_free_difference_step (default 1e-7, alinalg.cpp:124-129) */
 int fvhip_matfree_set_eps(fvhip_handle h, double eps);
 
