@@ -60,6 +60,9 @@ class FlowNumericsConfig:
     reconstruction: str = "VANALBADA"
     limiter_param: float = 20.0
     order2: bool = True
+    # Not a reference option: contracted FMAs + approximate division/sqrt in the residual sweep
+    # (results within a stated tolerance instead of bitwise; include/fvhip.h)
+    fast_math: bool = False
 
 
 class UMesh:
@@ -153,6 +156,7 @@ def _config_struct(pconf: FlowPhysicsConfig, nconf: FlowNumericsConfig):
                                                      pconf.Pr, pconf.aoa)
     c.viscous_sim, c.const_visc = int(pconf.viscous_sim), int(pconf.const_visc)
     c.conv_numflux = FLUXES[nconf.conv_numflux.upper()]
+    c.fast_math = int(getattr(nconf, "fast_math", False))
     c.conv_numflux_jac = FLUXES[nconf.conv_numflux_jac.upper()]
     grad = nconf.gradientscheme.upper()
     c.gradientscheme = GRADIENTS.get(grad, 0)

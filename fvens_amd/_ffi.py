@@ -30,7 +30,7 @@ class FvFlowConfig(ctypes.Structure):
                 ("conv_numflux", ctypes.c_int), ("conv_numflux_jac", ctypes.c_int),
                 ("gradientscheme", ctypes.c_int), ("reconstruction", ctypes.c_int),
                 ("limiter_param", ctypes.c_double), ("order2", ctypes.c_int), ("nbc", ctypes.c_int),
-                ("bc_type", c_int_p), ("bc_tag", c_int_p), ("bc_vals", c_dbl_p)]
+                ("bc_type", c_int_p), ("bc_tag", c_int_p), ("bc_vals", c_dbl_p), ("fast_math", ctypes.c_int)]
 
 
 # name -> (restype, argtypes); kept in sync with include/fvhip.h (tests check every symbol)

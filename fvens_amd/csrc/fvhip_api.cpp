@@ -125,6 +125,8 @@ struct fvhip_ctx
 		recs.clear();
 	}
 
+	/// kernels of the selected numerics mode (exact: bitwise parity; fast: stated tolerance)
+#define KOPS(fn) (cfg.fast_math ? fast::fn : exact::fn)
 	int recKind() const {
 		if(!cfg.order2) return SR_FIRST;
 		return cfg.reconstruction == FVHIP_REC_VANALBADA ? SR_MUSCL : SR_LINEAR;
@@ -140,26 +142,28 @@ struct fvhip_ctx
 		SweepBuffers B{};
 		B.u = u; B.r = r; B.dtm = dtm; B.overwrite = overwrite ? 1 : 0;
 		if(rk != SR_FIRST) {
-			timed("k_prep", [&]{ launch_prep(M, P, u, d_up, d_ubc, d_ug, true, stream); });
-			switch(cfg.gradientscheme) {
-				case FVHIP_GRAD_LEASTSQUARES: timed("k_grad_wls", [&]{ launch_grad_wls(M, d_up, d_ug, d_grad, stream); }); break;
-				case FVHIP_GRAD_GREENGAUSS: timed("k_grad_gg", [&]{ launch_grad_gg(M, d_up, d_ug, d_grad, stream); }); break;
-				default: launch_fill(d_grad, 0.0, 8LL*L.ncell, stream);
+			if(cfg.gradientscheme == FVHIP_GRAD_LEASTSQUARES) {
+				timed("k_prep_grad_wls", [&]{ KOPS(launch_prep_grad_wls)(M, P, u, d_up, d_ubc, d_ug, d_grad, stream); });
+			} else {
+				timed("k_prep", [&]{ KOPS(launch_prep)(M, P, u, d_up, d_ubc, d_ug, true, stream); });
+				if(cfg.gradientscheme == FVHIP_GRAD_GREENGAUSS)
+					timed("k_grad_gg", [&]{ KOPS(launch_grad_gg)(M, d_up, d_ug, d_grad, stream); });
+				else KOPS(launch_fill)(d_grad, 0.0, 8LL*L.ncell, stream);
 			}
 			B.up = d_up; B.grad = d_grad; B.rgrad = d_grad; B.ubc = d_ubc; B.ug = d_ug;
 			if(cfg.reconstruction == FVHIP_REC_BARTHJESPERSEN || cfg.reconstruction == FVHIP_REC_VENKATAKRISHNAN) {
 				const int venk = cfg.reconstruction == FVHIP_REC_VENKATAKRISHNAN;
-				timed("k_limiter", [&]{ launch_limiter(M, P, venk, d_up, d_ug, d_grad, d_phi, stream); });
+				timed("k_limiter", [&]{ KOPS(launch_limiter)(M, P, venk, d_up, d_ug, d_grad, d_phi, stream); });
 				B.phi = d_phi;
 			}
 			if(cfg.reconstruction == FVHIP_REC_WENO) {
-				timed("k_weno", [&]{ launch_weno(M, P, d_grad, d_lgrad, stream); });
+				timed("k_weno", [&]{ KOPS(launch_weno)(M, P, d_grad, d_lgrad, stream); });
 				B.rgrad = d_lgrad;
 			}
 		}
 		const char* nm = nullptr;
 		// name is only known after launch; record under a generic label then rename
-		timed("k_sweep", [&]{ nm = launch_sweep(M, P, B, cfg.conv_numflux, rk, viscKind(), dt, stream); });
+		timed("k_sweep", [&]{ nm = KOPS(launch_sweep)(M, P, B, cfg.conv_numflux, rk, viscKind(), dt, stream); });
 		if(prof && !recs.empty() && recs.back().name == "k_sweep" && nm) recs.back().name = nm;
 		HC(hipGetLastError());
 	}
@@ -345,11 +349,11 @@ int fvhip_get_gradients(fvhip_handle h, const double* u, double* grads)
 		toInternal(h, u, st.data(), 4);
 		HC(hipMemcpyAsync(h->d_u, st.data(), 4*N*sizeof(double), hipMemcpyHostToDevice, h->stream));
 		// ghost states from cell values, then the gradient scheme on CONSERVED variables
-		launch_prep(h->M, h->P, h->d_u, h->d_up, h->d_ubc, h->d_ug, false, h->stream);
+		exact::launch_prep(h->M, h->P, h->d_u, h->d_up, h->d_ubc, h->d_ug, false, h->stream);
 		switch(h->cfg.gradientscheme) {
-			case FVHIP_GRAD_LEASTSQUARES: launch_grad_wls(h->M, h->d_u, h->d_ubc, h->d_grad, h->stream); break;
-			case FVHIP_GRAD_GREENGAUSS: launch_grad_gg(h->M, h->d_u, h->d_ubc, h->d_grad, h->stream); break;
-			default: launch_fill(h->d_grad, 0.0, 8LL*h->L.ncell, h->stream);
+			case FVHIP_GRAD_LEASTSQUARES: exact::launch_grad_wls(h->M, h->d_u, h->d_ubc, h->d_grad, h->stream); break;
+			case FVHIP_GRAD_GREENGAUSS: exact::launch_grad_gg(h->M, h->d_u, h->d_ubc, h->d_grad, h->stream); break;
+			default: exact::launch_fill(h->d_grad, 0.0, 8LL*h->L.ncell, h->stream);
 		}
 		HC(hipGetLastError());
 		HC(hipMemcpyAsync(st.data(), h->d_grad, 8*N*sizeof(double), hipMemcpyDeviceToHost, h->stream));
@@ -586,7 +590,7 @@ int fvhip_local_flux(int flux_type, const double* gas5, int nf, const double* ul
 		HC(hipMemcpy(a, ul, 4*sizeof(double)*nf, hipMemcpyHostToDevice));
 		HC(hipMemcpy(b, ur, 4*sizeof(double)*nf, hipMemcpyHostToDevice));
 		HC(hipMemcpy(c, n, 2*sizeof(double)*nf, hipMemcpyHostToDevice));
-		launch_local_flux(flux_type, G, nf, a, b, c, d, nullptr);
+		exact::launch_local_flux(flux_type, G, nf, a, b, c, d, nullptr);
 		HC(hipGetLastError());
 		HC(hipMemcpy(flux, d, 4*sizeof(double)*nf, hipMemcpyDeviceToHost));
 		(void)hipFree(a); (void)hipFree(b); (void)hipFree(c); (void)hipFree(d);

@@ -17,9 +17,23 @@
 #include "kernels.hpp"
 #include "layout.hpp"
 
+#ifndef FVHIP_NS
+#define FVHIP_NS exact
+#endif
+
 namespace fvhip {
+namespace FVHIP_NS {
 
 using namespace gd;
+
+/// XCD-aware block -> chunk mapping: the hardware deals consecutive blocks round-robin over the 8
+/// XCDs; chunk p = (b%8)*q + b/8 keeps consecutive (Hilbert-adjacent) chunks on one XCD's L2.
+/// Launch 8*q blocks; blocks with p >= nchunk return.
+__device__ __forceinline__ int xcd_chunk(int nchunk) {
+	const int q = (nchunk + 7) >> 3;
+	return (static_cast<int>(blockIdx.x) & 7) * q + (static_cast<int>(blockIdx.x) >> 3);
+}
+static inline int xcd_blocks(long long nchunk) { return static_cast<int>(8*((nchunk + 7)/8)); }
 
 __device__ __forceinline__ void ld4(const double* p, int i, double* o) {
 	const double4 v = reinterpret_cast<const double4*>(p)[i];
@@ -92,6 +106,78 @@ __global__ void __launch_bounds__(256) k_grad_wls(DevMesh M, const double* __res
 		if(nb[k] < 0) continue;
 		if(nb[k] >= N) { rn[k] = M.bf_rcbp[nb[k] - N]; ld4(ug, nb[k] - N, un[k]); }
 		else           { rn[k] = M.rc[nb[k]];           ld4(up, nb[k], un[k]); }
+	}
+	const double4 V = M.wls_V[c];
+	double f[8] = {0,0,0,0,0,0,0,0};
+	#pragma unroll
+	for(int k = 0; k < 4; k++) {
+		if(nb[k] < 0) break;
+		double w2 = 0;
+		w2 += (rcc.x-rn[k].x)*(rcc.x-rn[k].x);
+		w2 += (rcc.y-rn[k].y)*(rcc.y-rn[k].y);
+		const double dr0 = rcc.x-rn[k].x, dr1 = rcc.y-rn[k].y;
+		w2 = 1.0/(w2);
+		#pragma unroll
+		for(int iv = 0; iv < 4; iv++) {
+			const double du = uc[iv] - un[k][iv];
+			f[iv*2+0] += w2*dr0*du;
+			f[iv*2+1] += w2*dr1*du;
+		}
+	}
+	double g[8];
+	#pragma unroll
+	for(int iv = 0; iv < 4; iv++) {
+		g[iv*2+0] = V.x*f[iv*2+0] + V.y*f[iv*2+1];
+		g[iv*2+1] = V.z*f[iv*2+0] + V.w*f[iv*2+1];
+	}
+	st8(grad, c, g);
+}
+
+/// Fused preparation + WLS gradient for the residual path: converts this cell's conserved state
+/// (written as up[c]) and its neighbours' (k_prep_cells' cons2prim, bit for bit), builds the ghost
+/// states of this cell's boundary faces (k_prep_bfaces; each boundary face has exactly one cell),
+/// then the same WLS arithmetic as k_grad_wls. Replaces three launches and one round trip of up.
+__global__ void __launch_bounds__(256) k_prep_grad_wls(DevMesh M, DevPhys P, const double* __restrict__ u,
+                                                       double* __restrict__ up, double* __restrict__ ubc,
+                                                       double* __restrict__ ug, double* __restrict__ grad)
+{
+	const int c = xcd_chunk(static_cast<int>((M.ncell + 255) >> 8))*256 + static_cast<int>(threadIdx.x);
+	if(c >= M.ncell) return;
+	const int N = M.ncell;
+	const Gas& G = P.gas;
+	const int4 nb4 = M.cell_nbr_fo[c];
+	const int nb[4] = {nb4.x, nb4.y, nb4.z, nb4.w};
+	const double2 rcc = M.rc[c];
+	double ucons[4], uc[4];
+	ld4(u, c, ucons);
+	double un[4][4];
+	double2 rn[4];
+	#pragma unroll
+	for(int k = 0; k < 4; k++) {
+		if(nb[k] < 0 || nb[k] >= N) continue;
+		rn[k] = M.rc[nb[k]];
+		ld4(u, nb[k], un[k]);
+	}
+	cons2prim(G, ucons, uc);
+	st4(up, c, uc);
+	#pragma unroll
+	for(int k = 0; k < 4; k++) {
+		if(nb[k] < 0) continue;
+		if(nb[k] >= N) {
+			const int bf = nb[k] - N;
+			const double2 nn = M.bf_n[bf];
+			const double n[2] = {nn.x, nn.y};
+			double gs[4];
+			ghost_state(G, P.bc[M.bf_bc[bf]], P.uinf, ucons, n, gs);
+			st4(ubc, bf, gs);
+			cons2prim(G, gs, un[k]);
+			st4(ug, bf, un[k]);
+			rn[k] = M.bf_rcbp[bf];
+		} else {
+			double t[4];
+			cons2prim(G, un[k], t);
+			un[k][0] = t[0]; un[k][1] = t[1]; un[k][2] = t[2]; un[k][3] = t[3];
+		}
 	}
 	const double4 V = M.wls_V[c];
 	double f[8] = {0,0,0,0,0,0,0,0};
@@ -502,6 +588,9 @@ void launch_prep(const DevMesh& M, const DevPhys& P, const double* u, double* up
 }
 void launch_grad_wls(const DevMesh& M, const double* up, const double* ug, double* grad, hipStream_t s)
 { if(M.ncell > 0) k_grad_wls<<<nblk(M.ncell,256), 256, 0, s>>>(M, up, ug, grad); }
+void launch_prep_grad_wls(const DevMesh& M, const DevPhys& P, const double* u, double* up, double* ubc,
+                          double* ug, double* grad, hipStream_t s)
+{ if(M.ncell > 0) k_prep_grad_wls<<<xcd_blocks((M.ncell + 255)/256), 256, 0, s>>>(M, P, u, up, ubc, ug, grad); }
 void launch_grad_gg(const DevMesh& M, const double* up, const double* ug, double* grad, hipStream_t s)
 { if(M.ncell > 0) k_grad_gg<<<nblk(M.ncell,256), 256, 0, s>>>(M, up, ug, grad); }
 void launch_limiter(const DevMesh& M, const DevPhys& P, int venk, const double* up, const double* ug,
@@ -549,8 +638,14 @@ static SweepFn pick2(int rec, int visc, bool dt, bool phi) {
 	}
 }
 
+#ifdef FVHIP_FAST
+static const char* kSweepNames[7] = {"k_sweep_fast<LLF>", "k_sweep_fast<VANLEER>", "k_sweep_fast<AUSM>",
+                                     "k_sweep_fast<AUSMPLUS>", "k_sweep_fast<ROE>", "k_sweep_fast<HLL>",
+                                     "k_sweep_fast<HLLC>"};
+#else
 static const char* kSweepNames[7] = {"k_sweep<LLF>", "k_sweep<VANLEER>", "k_sweep<AUSM>", "k_sweep<AUSMPLUS>",
                                      "k_sweep<ROE>", "k_sweep<HLL>", "k_sweep<HLLC>"};
+#endif
 
 const char* launch_sweep(const DevMesh& M, const DevPhys& P, const SweepBuffers& B, int flux, int rec,
                          int visc, bool dt, hipStream_t s)
@@ -571,4 +666,5 @@ const char* launch_sweep(const DevMesh& M, const DevPhys& P, const SweepBuffers&
 	return kSweepNames[flux < 0 || flux > 6 ? 6 : flux];
 }
 
+}
 }

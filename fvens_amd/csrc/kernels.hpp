@@ -62,21 +62,29 @@ struct SweepBuffers
 	int overwrite;
 };
 
-// host launchers (all asynchronous on stream)
-void launch_prep(const DevMesh& M, const DevPhys& P, const double* u, double* up, double* ubc, double* ug,
-                 bool cells, hipStream_t s);
-void launch_grad_wls(const DevMesh& M, const double* up, const double* ug, double* grad, hipStream_t s);
-void launch_grad_gg(const DevMesh& M, const double* up, const double* ug, double* grad, hipStream_t s);
-void launch_limiter(const DevMesh& M, const DevPhys& P, int venk, const double* up, const double* ug,
-                    const double* grad, double* phi, hipStream_t s);
-void launch_weno(const DevMesh& M, const DevPhys& P, const double* grad, double* lgrad, hipStream_t s);
-/// returns kernel name for profiling
-const char* launch_sweep(const DevMesh& M, const DevPhys& P, const SweepBuffers& B, int flux, int rec,
-                         int visc, bool dt, hipStream_t s);
-void launch_fill(double* p, double v, long long n, hipStream_t s);
-void launch_local_flux(int flux, const gd::Gas& G, int nf, const double* ul, const double* ur,
-                       const double* n, double* f, hipStream_t s);
+// Host launchers (all asynchronous on stream). kernels.hip is compiled twice: namespace `exact`
+// (-ffp-contract=off, IEEE division/sqrt: bitwise parity with the reference) and namespace `fast`
+// (contracted FMAs and approximate division/sqrt: the reference's results to a stated tolerance).
+#define FVHIP_SWEEP_LAUNCHERS \
+void launch_prep(const DevMesh& M, const DevPhys& P, const double* u, double* up, double* ubc, double* ug, \
+                 bool cells, hipStream_t s); \
+void launch_grad_wls(const DevMesh& M, const double* up, const double* ug, double* grad, hipStream_t s); \
+void launch_prep_grad_wls(const DevMesh& M, const DevPhys& P, const double* u, double* up, double* ubc, \
+                          double* ug, double* grad, hipStream_t s); \
+void launch_grad_gg(const DevMesh& M, const double* up, const double* ug, double* grad, hipStream_t s); \
+void launch_limiter(const DevMesh& M, const DevPhys& P, int venk, const double* up, const double* ug, \
+                    const double* grad, double* phi, hipStream_t s); \
+void launch_weno(const DevMesh& M, const DevPhys& P, const double* grad, double* lgrad, hipStream_t s); \
+/* returns the kernel name for profiling */ \
+const char* launch_sweep(const DevMesh& M, const DevPhys& P, const SweepBuffers& B, int flux, int rec, \
+                         int visc, bool dt, hipStream_t s); \
+void launch_fill(double* p, double v, long long n, hipStream_t s); \
+void launch_local_flux(int flux, const gd::Gas& G, int nf, const double* ul, const double* ur, \
+                       const double* n, double* f, hipStream_t s); \
 void launch_gather_cells(const int* perm, const double* src, double* dst, int n, int width, hipStream_t s);
+
+namespace exact { FVHIP_SWEEP_LAUNCHERS }
+namespace fast { FVHIP_SWEEP_LAUNCHERS }
 
 }
 #endif

@@ -71,6 +71,10 @@ typedef struct fvhip_flow_config {
 	const int* bc_type;       /* [nbc] enum fvhip_bc_type */
 	const int* bc_tag;        /* [nbc] boundary marker (gbtags(face,0)) */
 	const double* bc_vals;    /* [nbc][2] boundary_values (wall velocity, temperature, ...) */
+	int fast_math;            /* 0: parity mode, residuals bitwise equal to the reference's
+	                             single-thread arithmetic; 1: contracted FMAs and approximate
+	                             division/sqrt in the residual sweep (relative differences ~1e-15,
+	                             tested at 1e-11 of max|r|). Not a reference option. */
 } fvhip_flow_config;
 
 /** The UMesh data the sweep needs, exactly as the reference's accessors return it

@@ -223,3 +223,26 @@ def test_local_flux_bitwise(flux):
     f = fa.local_flux(flux, gas, ul, ur, nn)
     f0 = np.array([orc.flux(flux, gas, ul[i], ur[i], nn[i]) for i in range(nf)])
     np.testing.assert_array_equal(f, f0)
+
+
+# ------------------------------------------------------------------------------------------------
+# fast-math mode (not a reference option): contracted FMAs and approximate division/sqrt in the
+# sweep. Bar: |dr| <= 1e-11 * max|r| per variable and |d dt| <= 1e-12 |dt| against the oracle.
+# ------------------------------------------------------------------------------------------------
+FAST_CASES = [("naca_small", "naca", "ROE", "LEASTSQUARES", "VANALBADA"),
+              ("naca_c2", "naca", "ROE", "LEASTSQUARES", "VANALBADA"),
+              ("2dcylinderhybrid.msh", "cyl", "HLLC", "GREENGAUSS", "VANALBADA"),
+              ("naca_small", "naca", "HLLC", "LEASTSQUARES", "VENKATAKRISHNAN"),
+              ("naca_small", "viscconst", "ROE", "LEASTSQUARES", "NONE"),
+              ("plate_small", "plate", "HLLC", "LEASTSQUARES", "VANALBADA"),
+              ("naca_small", "naca", "LLF", "NONE", "NONE")]
+
+
+@pytest.mark.parametrize("meshkey,kind,flux,grad,rec", FAST_CASES)
+def test_fast_math_within_tolerance(meshkey, kind, flux, grad, rec):
+    p = cases.physics(kind)
+    n = cases.numerics(flux, grad, rec, order2=grad != "NONE")
+    n.fast_math = True
+    r, dt, r0, dt0 = run_both(meshkey, p, n)
+    assert_close(r, r0, None, None, rtol=1e-11)
+    np.testing.assert_allclose(dt, dt0, rtol=1e-12, atol=0)
