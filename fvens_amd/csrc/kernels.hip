@@ -136,34 +136,46 @@ __global__ void __launch_bounds__(256) k_grad_wls(DevMesh M, const double* __res
 /// Fused preparation + WLS gradient for the residual path: converts this cell's conserved state
 /// (written as up[c]) and its neighbours' (k_prep_cells' cons2prim, bit for bit), builds the ghost
 /// states of this cell's boundary faces (k_prep_bfaces; each boundary face has exactly one cell),
-/// then the same WLS arithmetic as k_grad_wls. Replaces three launches and one round trip of up.
+/// then the same WLS arithmetic as k_grad_wls. A block owns 256 consecutive (Hilbert-ordered)
+/// cells; their primitive states and centres are staged in LDS, so only neighbours outside the
+/// block are gathered from global memory.
 __global__ void __launch_bounds__(256) k_prep_grad_wls(DevMesh M, DevPhys P, const double* __restrict__ u,
                                                        double* __restrict__ up, double* __restrict__ ubc,
                                                        double* __restrict__ ug, double* __restrict__ grad)
 {
-	const int c = xcd_chunk(static_cast<int>((M.ncell + 255) >> 8))*256 + static_cast<int>(threadIdx.x);
-	if(c >= M.ncell) return;
+	__shared__ __attribute__((aligned(16))) double s_up[256][4];
+	__shared__ __attribute__((aligned(16))) double2 s_rc[256];
 	const int N = M.ncell;
+	const int cb = xcd_chunk(static_cast<int>((N + 255) >> 8))*256;
+	if(cb >= N) return;
+	const int t = static_cast<int>(threadIdx.x);
+	const int c = cb + t;
+	const int ncb = (N - cb) < 256 ? (N - cb) : 256;
 	const Gas& G = P.gas;
+	double ucons[4], uc[4];
+	double2 rcc = make_double2(0, 0);
+	if(c < N) {
+		ld4(u, c, ucons);
+		cons2prim(G, ucons, uc);
+		st4(up, c, uc);
+		rcc = M.rc[c];
+		st4(&s_up[t][0], 0, uc);
+		s_rc[t] = rcc;
+	}
+	__syncthreads();
+	if(c >= N) return;
 	const int4 nb4 = M.cell_nbr_fo[c];
 	const int nb[4] = {nb4.x, nb4.y, nb4.z, nb4.w};
-	const double2 rcc = M.rc[c];
-	double ucons[4], uc[4];
-	ld4(u, c, ucons);
 	double un[4][4];
 	double2 rn[4];
 	#pragma unroll
 	for(int k = 0; k < 4; k++) {
-		if(nb[k] < 0 || nb[k] >= N) continue;
-		rn[k] = M.rc[nb[k]];
-		ld4(u, nb[k], un[k]);
-	}
-	cons2prim(G, ucons, uc);
-	st4(up, c, uc);
-	#pragma unroll
-	for(int k = 0; k < 4; k++) {
 		if(nb[k] < 0) continue;
-		if(nb[k] >= N) {
+		const int j = nb[k] - cb;
+		if(static_cast<unsigned>(j) < static_cast<unsigned>(ncb)) {
+			ld4(&s_up[j][0], 0, un[k]);
+			rn[k] = s_rc[j];
+		} else if(nb[k] >= N) {
 			const int bf = nb[k] - N;
 			const double2 nn = M.bf_n[bf];
 			const double n[2] = {nn.x, nn.y};
@@ -174,9 +186,10 @@ __global__ void __launch_bounds__(256) k_prep_grad_wls(DevMesh M, DevPhys P, con
 			st4(ug, bf, un[k]);
 			rn[k] = M.bf_rcbp[bf];
 		} else {
-			double t[4];
-			cons2prim(G, un[k], t);
-			un[k][0] = t[0]; un[k][1] = t[1]; un[k][2] = t[2]; un[k][3] = t[3];
+			double t4[4];
+			ld4(u, nb[k], t4);
+			rn[k] = M.rc[nb[k]];
+			cons2prim(G, t4, un[k]);
 		}
 	}
 	const double4 V = M.wls_V[c];
@@ -362,11 +375,27 @@ __device__ __forceinline__ double muscl_right(double ui, double uj, double dp, d
 	return uj - ph/4.0*( (1.0-k*ph)*dp + (1.0+k*ph)*(uj - ui) );
 }
 
+/// Per-cell words (doubles) staged in LDS for a sweep variant, one 16-byte-aligned row per cell:
+///   order 2: [up 4][reconstruction gradient 8][rc 2] (+[u 4] if viscous) (+[phi 4] if limiter)
+///   order 1: [u 4] (+[rc 2] if viscous)
+template <int REC, int VISC, bool PHI> struct Stage {
+	static constexpr bool O2 = REC != SR_FIRST;
+	static constexpr bool V = VISC != SV_NONE;
+	static constexpr int UP = 0, RG = 4;
+	static constexpr int RC = O2 ? 12 : 4;
+	static constexpr int UC = O2 ? 14 : 0;
+	static constexpr int PH = V ? 18 : 14;
+	static constexpr int W0 = O2 ? (14 + (V ? 4 : 0) + (PHI ? 4 : 0)) : (V ? 6 : 4);
+	static constexpr int W = (W0 + 1) & ~1;
+	static constexpr int BUF = (W > 6 ? W : 6) * SLOTS_MAX;   // flux staging reuses the buffer
+};
+
 template <int FLUX, int REC, int VISC, bool DT, bool PHI>
 __global__ void __launch_bounds__(SLOTS_MAX) k_sweep(const DevMesh M, const DevPhys P, const SweepBuffers B)
 {
-	__shared__ double sf[4][SLOTS_MAX];
-	__shared__ double ssr[DT ? 2 : 1][DT ? SLOTS_MAX : 1];
+	typedef Stage<REC, VISC, PHI> S;
+	constexpr int W = S::W;
+	__shared__ __attribute__((aligned(16))) double sbuf[S::BUF];
 
 	// XCD-aware mapping: consecutive patches (which share halo cells) land on the same XCD
 	const int np = M.npatch;
@@ -375,10 +404,45 @@ __global__ void __launch_bounds__(SLOTS_MAX) k_sweep(const DevMesh M, const DevP
 	if(p >= np) return;
 	const int s0 = M.patch_slot[p], s1 = M.patch_slot[p+1];
 	const int c0 = M.patch_cell[p], c1 = M.patch_cell[p+1];
+	const int nc = c1 - c0;
 	const int N = M.ncell;
 	const Gas& G = P.gas;
+	const int t = static_cast<int>(threadIdx.x);
 
-	const int s = s0 + static_cast<int>(threadIdx.x);
+	// phase 0: stage the patch's own cells (contiguous range) with coalesced loads
+	if(t < nc) {
+		const int c = c0 + t;
+		double* row = &sbuf[t*W];
+		double a[8];
+		if(S::O2) {
+			ld4(B.up, c, a); st4(row + S::UP, 0, a);
+			ld8(B.rgrad, c, a); st8(row + S::RG, 0, a);
+			const double2 r = M.rc[c]; *reinterpret_cast<double2*>(row + S::RC) = r;
+			if(S::V) { ld4(B.u, c, a); st4(row + S::UC, 0, a); }
+			if(PHI) { ld4(B.phi, c, a); st4(row + S::PH, 0, a); }
+		} else {
+			ld4(B.u, c, a); st4(row + S::UC, 0, a);
+			if(S::V) { const double2 r = M.rc[c]; *reinterpret_cast<double2*>(row + S::RC) = r; }
+		}
+	}
+	__syncthreads();
+
+	// cell data from LDS when the cell is in this patch, else from global memory (halo)
+	auto inp = [&](int cell) { return static_cast<unsigned>(cell - c0) < static_cast<unsigned>(nc); };
+	auto get4 = [&](int cell, int off, const double* g, double* o) {
+		if(inp(cell)) ld4(&sbuf[(cell - c0)*W + off], 0, o); else ld4(g, cell, o);
+	};
+	auto get8 = [&](int cell, int off, const double* g, double* o) {
+		if(inp(cell)) ld8(&sbuf[(cell - c0)*W + off], 0, o); else ld8(g, cell, o);
+	};
+	auto getrc = [&](int cell) -> double2 {
+		if(inp(cell)) return *reinterpret_cast<const double2*>(&sbuf[(cell - c0)*W + S::RC]);
+		return M.rc[cell];
+	};
+
+	const int s = s0 + t;
+	double f[4] = {0, 0, 0, 0};
+	double sri = 0, srj = 0;
 	if(s < s1) {
 		const int2 lr = M.slot_LR[s];
 		const double2 nn = M.slot_n[s];
@@ -389,20 +453,20 @@ __global__ void __launch_bounds__(SLOTS_MAX) k_sweep(const DevMesh M, const DevP
 		double ul[4], ur[4];
 
 		if(REC == SR_FIRST) {
-			ld4(B.u, lr.x, ul);
+			get4(lr.x, S::UC, B.u, ul);
 			if(bnd) ghost_state(G, P.bc[M.bf_bc[bf]], P.uinf, ul, n, ur);
-			else    ld4(B.u, lr.y, ur);
+			else    get4(lr.y, S::UC, B.u, ur);
 		}
 		else if(REC == SR_MUSCL) {
-			const double2 ri = M.rc[lr.x];
+			const double2 ri = getrc(lr.x);
 			double ui[4], gi[8];
-			ld4(B.up, lr.x, ui);
-			ld8(B.rgrad, lr.x, gi);
+			get4(lr.x, S::UP, B.up, ui);
+			get8(lr.x, S::RG, B.rgrad, gi);
 			if(!bnd) {
-				const double2 rj = M.rc[lr.y];
+				const double2 rj = getrc(lr.y);
 				double uj[4], gj[8];
-				ld4(B.up, lr.y, uj);
-				ld8(B.rgrad, lr.y, gj);
+				get4(lr.y, S::UP, B.up, uj);
+				get8(lr.y, S::RG, B.rgrad, gj);
 				const double dx = rj.x-ri.x, dy = rj.y-ri.y;
 				#pragma unroll
 				for(int i = 0; i < 4; i++) {
@@ -435,11 +499,11 @@ __global__ void __launch_bounds__(SLOTS_MAX) k_sweep(const DevMesh M, const DevP
 		else {  // SR_LINEAR: unlimited, WENO-limited gradients or BJ/Venkatakrishnan limiter values
 			const double2 gp = M.slot_gr[s];
 			{
-				const double2 ri = M.rc[lr.x];
+				const double2 ri = getrc(lr.x);
 				double ui[4], gi[8], ph[4] = {1.0, 1.0, 1.0, 1.0};
-				ld4(B.up, lr.x, ui);
-				ld8(B.rgrad, lr.x, gi);
-				if(PHI) ld4(B.phi, lr.x, ph);
+				get4(lr.x, S::UP, B.up, ui);
+				get8(lr.x, S::RG, B.rgrad, gi);
+				if(PHI) get4(lr.x, S::PH, B.phi, ph);
 				#pragma unroll
 				for(int i = 0; i < 4; i++) {
 					double v = ui[i];
@@ -450,11 +514,11 @@ __global__ void __launch_bounds__(SLOTS_MAX) k_sweep(const DevMesh M, const DevP
 				prim2cons(G, ul, ul);
 			}
 			if(!bnd) {
-				const double2 rj = M.rc[lr.y];
+				const double2 rj = getrc(lr.y);
 				double uj[4], gj[8], ph[4] = {1.0, 1.0, 1.0, 1.0};
-				ld4(B.up, lr.y, uj);
-				ld8(B.rgrad, lr.y, gj);
-				if(PHI) ld4(B.phi, lr.y, ph);
+				get4(lr.y, S::UP, B.up, uj);
+				get8(lr.y, S::RG, B.rgrad, gj);
+				if(PHI) get4(lr.y, S::PH, B.phi, ph);
 				#pragma unroll
 				for(int i = 0; i < 4; i++) {
 					double v = uj[i];
@@ -468,27 +532,27 @@ __global__ void __launch_bounds__(SLOTS_MAX) k_sweep(const DevMesh M, const DevP
 			}
 		}
 
-		double f[4];
 		inviscid_flux<FLUX>(G, ul, ur, n, f);
 		#pragma unroll
 		for(int k = 0; k < 4; k++) f[k] *= len;
 
 		if(VISC != SV_NONE) {
 			double ucl[4], ucr[4], gl[8], gr[8];
-			const double2 rl = M.rc[lr.x];
+			const double2 rl = getrc(lr.x);
 			double2 rr;
-			ld4(B.u, lr.x, ucl);
+			get4(lr.x, S::UC, B.u, ucl);
 			if(bnd) {
 				rr = M.bf_rcbp[bf];
 				if(REC == SR_FIRST) { for(int k = 0; k < 4; k++) ucr[k] = ur[k]; }
 				else ld4(B.ubc, bf, ucr);
 			} else {
-				rr = M.rc[lr.y];
-				ld4(B.u, lr.y, ucr);
+				rr = getrc(lr.y);
+				get4(lr.y, S::UC, B.u, ucr);
 			}
 			if(REC != SR_FIRST) {
-				ld8(B.grad, lr.x, gl);
-				ld8(B.grad, bnd ? lr.x : lr.y, gr);
+				const int cr = bnd ? lr.x : lr.y;
+				if(B.grad == B.rgrad) { get8(lr.x, S::RG, B.grad, gl); get8(cr, S::RG, B.grad, gr); }
+				else { ld8(B.grad, lr.x, gl); ld8(B.grad, cr, gr); }
 			}
 			const double rcl[2] = {rl.x, rl.y}, rcr[2] = {rr.x, rr.y};
 			double vf[4];
@@ -497,15 +561,12 @@ __global__ void __launch_bounds__(SLOTS_MAX) k_sweep(const DevMesh M, const DevP
 			for(int k = 0; k < 4; k++) f[k] += vf[k]*len;
 		}
 
-		const int ls = s - s0;
-		sf[0][ls] = f[0]; sf[1][ls] = f[1]; sf[2][ls] = f[2]; sf[3][ls] = f[3];
-
 		if(DT) {
 			const double ci = sound_speed_cons(G, ul), cj = sound_speed_cons(G, ur);
 			const double vni = dot2(&ul[1],n)/ul[0];
 			const double vnj = dot2(&ur[1],n)/ur[0];
-			double sri = (fabs(vni)+ci)*len;
-			double srj = (fabs(vnj)+cj)*len;
+			sri = (fabs(vni)+ci)*len;
+			srj = (fabs(vnj)+cj)*len;
 			if(VISC != SV_NONE) {
 				const double mui = VISC == SV_CONST ? 1.0/G.Reinf : sutherland(G, ul);
 				const double muj = VISC == SV_CONST ? 1.0/G.Reinf : sutherland(G, ur);
@@ -516,13 +577,19 @@ __global__ void __launch_bounds__(SLOTS_MAX) k_sweep(const DevMesh M, const DevP
 				sri += coi*mui/G.Pr * len*len/M.area[lr.x];
 				if(!bnd) srj += coj*muj/G.Pr * len*len/M.area[lr.y];
 			}
-			ssr[0][ls] = sri;
-			ssr[1][ls] = srj;
 		}
+	}
+	__syncthreads();   // every slot has read the staged cells: reuse the buffer for the fluxes
+	double* sf = sbuf;                  // [4][SLOTS_MAX]
+	double* ssr = sbuf + 4*SLOTS_MAX;   // [2][SLOTS_MAX]
+	if(s < s1) {
+		sf[0*SLOTS_MAX + t] = f[0]; sf[1*SLOTS_MAX + t] = f[1];
+		sf[2*SLOTS_MAX + t] = f[2]; sf[3*SLOTS_MAX + t] = f[3];
+		if(DT) { ssr[t] = sri; ssr[SLOTS_MAX + t] = srj; }
 	}
 	__syncthreads();
 
-	const int c = c0 + static_cast<int>(threadIdx.x);
+	const int c = c0 + t;
 	if(c < c1) {
 		double r[4];
 		if(B.overwrite) { r[0] = r[1] = r[2] = r[3] = 0.0; }
@@ -535,11 +602,13 @@ __global__ void __launch_bounds__(SLOTS_MAX) k_sweep(const DevMesh M, const DevP
 			if(e[k] < 0) break;
 			const int ls = (e[k] >> 1) - s0;
 			if(e[k] & 1) {
-				r[0] += sf[0][ls]; r[1] += sf[1][ls]; r[2] += sf[2][ls]; r[3] += sf[3][ls];
-				if(DT) integ += ssr[1][ls];
+				r[0] += sf[0*SLOTS_MAX + ls]; r[1] += sf[1*SLOTS_MAX + ls];
+				r[2] += sf[2*SLOTS_MAX + ls]; r[3] += sf[3*SLOTS_MAX + ls];
+				if(DT) integ += ssr[SLOTS_MAX + ls];
 			} else {
-				r[0] -= sf[0][ls]; r[1] -= sf[1][ls]; r[2] -= sf[2][ls]; r[3] -= sf[3][ls];
-				if(DT) integ += ssr[0][ls];
+				r[0] -= sf[0*SLOTS_MAX + ls]; r[1] -= sf[1*SLOTS_MAX + ls];
+				r[2] -= sf[2*SLOTS_MAX + ls]; r[3] -= sf[3*SLOTS_MAX + ls];
+				if(DT) integ += ssr[ls];
 			}
 		}
 		st4(B.r, c, r);
