@@ -142,7 +142,9 @@ def main():
         fsweep = [k for k in fk if k.startswith("k_sweep")]
         fsms = fk[fsweep[0]] if fsweep else float("nan")
         fab = sweep_algorithmic_bytes(N, F, Fb) / (fsms * 1e-3) / 1e9
+        ftr = pmc_traffic("fast::k_sweep<4, 1, 0, true, false>", N)
         fast = {"value": round(world * F / (fms * 1e-3) / 1e6, 3), "ms_per_step": round(fms, 5),
+                "traffic": int(ftr[0]) if ftr else None,
                 "kernels_ms": {k: round(v, 5) for k, v in fk.items()},
                 "roofline_frac": round(fab / HBM_PEAK_GBS, 4), "achieved_GBs": round(fab, 1),
                 "tolerance": "|dr| <= 1e-11 max|r| per variable, |d dt| <= 1e-12 |dt| "
@@ -168,7 +170,7 @@ def main():
 
     if rank == 0:
         # template of the timed sweep: k_sweep<FLUX=ROE(4), REC=MUSCL(1), VISC=none(0), DT, no PHI>
-        tr = pmc_traffic("k_sweep<4, 1, 0, true, false>", N)
+        tr = pmc_traffic("exact::k_sweep<4, 1, 0, true, false>", N)
         out = {
             "metric": "Mfaces/s (flux+residual sweep) + achieved HBM GB/s, 1/2/4/8 MI355X",
             "value": round(value, 3),
