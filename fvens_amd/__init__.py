@@ -172,18 +172,37 @@ def _config_struct(pconf: FlowPhysicsConfig, nconf: FlowNumericsConfig):
 class FlowFV:
     """Device-resident FlowFV<freal,order2,constVisc> (spatial/flow_spatial.hpp:174-320)."""
 
-    def __init__(self, mesh: UMesh, pconf: FlowPhysicsConfig, nconf: FlowNumericsConfig, device: int = 0):
+    def __init__(self, mesh: UMesh, pconf: FlowPhysicsConfig, nconf: FlowNumericsConfig, device: int = 0,
+                 partition=None, rank: int = 0):
+        """partition: per-cell part array (e.g. UMesh.partition_rcb) -> this handle is rank `rank`'s
+        piece with one ghost layer (multi-GPU); None -> the whole mesh."""
         self.mesh, self.pconf, self.nconf = mesh, pconf, nconf
         cfg, self._keep = _config_struct(pconf, nconf)
         h = ctypes.c_void_p()
-        check(_ffi.lib().fvhip_create(ctypes.byref(mesh.view), ctypes.byref(cfg), device, ctypes.byref(h)))
+        self.rank, self.nparts = rank, 1
+        if partition is None:
+            check(_ffi.lib().fvhip_create(ctypes.byref(mesh.view), ctypes.byref(cfg), device, ctypes.byref(h)))
+            self.nown, self.nghost = mesh.nelem, 0
+        else:
+            part = np.ascontiguousarray(partition, np.int32)
+            self.nparts = int(part.max()) + 1
+            check(_ffi.lib().fvhip_create_partitioned(ctypes.byref(mesh.view), ctypes.byref(cfg), iptr(part),
+                                                      self.nparts, rank, device, ctypes.byref(h)))
         self._h = h
+        if partition is not None:
+            st = self.layout_stats()
+            self.nown, self.nghost = st["cells"], st["ghosts"]
+
+    def comm_init(self, nranks, rank, uid):
+        """RCCL communicator of the partition (uid: 128 bytes from comm_unique_id on rank 0)"""
+        buf = ctypes.create_string_buffer(bytes(uid), 128)
+        check(_ffi.lib().fvhip_comm_init(self._h, nranks, rank, buf))
 
     # --- reference-ordered host interface -----------------------------------------------------
     def compute_residual(self, u, r, gettimesteps=False, dtm=None):
         """Adds -r(u) into r (flow_spatial.hpp:73-87); fills dtm if gettimesteps."""
-        N = self.mesh.nelem
-        assert u.shape == (N + self.mesh.nconnface, 4) and r.shape == (N, 4)
+        N = self.nown
+        assert u.shape[1] == 4 and u.shape[0] >= N and r.shape == (N, 4)
         if gettimesteps:
             assert dtm is not None and dtm.shape == (N,)
         check(_ffi.lib().fvhip_compute_residual(self._h, dptr(u), dptr(r), int(gettimesteps),
@@ -258,7 +277,7 @@ class FlowFV:
                                                        1 if overwrite else 0))
 
     def permutation(self):
-        p = np.zeros(self.mesh.nelem, np.int32)
+        p = np.zeros(self.nown, np.int32)
         check(_ffi.lib().fvhip_get_permutation(self._h, iptr(p)))
         return p
 
@@ -286,9 +305,9 @@ class FlowFV:
         return out
 
     def layout_stats(self):
-        s = (ctypes.c_longlong * 6)()
+        s = (ctypes.c_longlong * 9)()
         check(_ffi.lib().fvhip_layout_stats(self._h, s))
-        keys = ("cells", "faces", "slots", "patches", "max_slots", "bfaces")
+        keys = ("cells", "faces", "slots", "patches", "max_slots", "bfaces", "ghosts", "neighbours", "send_rows")
         return dict(zip(keys, [int(x) for x in s]))
 
     def close(self):
@@ -332,3 +351,66 @@ def local_flux_jacobian(flux, gas, ul, ur, n):
     check(_ffi.lib().fvhip_local_flux_jacobian(FLUXES[flux.upper()] if isinstance(flux, str) else flux, dptr(g),
                                                nf, dptr(ul), dptr(ur), dptr(n), dptr(dl), dptr(dr)))
     return dl, dr
+
+
+def comm_unique_id():
+    """128-byte RCCL unique id (create on rank 0, broadcast, pass to FlowFV.comm_init)"""
+    buf = ctypes.create_string_buffer(128)
+    check(_ffi.lib().fvhip_comm_unique_id(buf))
+    return bytes(buf.raw)
+
+
+def partition_rcb(mesh, nparts):
+    """Recursive coordinate bisection of the cell centres (Scotch is not available here)"""
+    part = np.zeros(mesh.nelem, np.int32)
+    check(_ffi.lib().fvhip_partition_rcb(ctypes.byref(mesh.view), int(nparts), iptr(part)))
+    return part
+
+
+def partition_info(mesh, part, rank):
+    """Host-side halo description of `rank` (fvhip_partition_info)"""
+    part = np.ascontiguousarray(part, np.int32)
+    counts = np.zeros(6, np.int32)
+    null = ctypes.POINTER(ctypes.c_int)()
+    check(_ffi.lib().fvhip_partition_info(ctypes.byref(mesh.view), iptr(part), rank, iptr(counts),
+                                          null, null, null, null, null))
+    nown, ngh, nb, nf, nnbr, nsend = [int(x) for x in counts]
+    cg = np.zeros(nown + ngh, np.int32)
+    nbr = np.zeros(max(nnbr, 1), np.int32)
+    gs = np.zeros(nnbr + 1, np.int32)
+    ss = np.zeros(nnbr + 1, np.int32)
+    sg = np.zeros(max(nsend, 1), np.int32)
+    check(_ffi.lib().fvhip_partition_info(ctypes.byref(mesh.view), iptr(part), rank, iptr(counts), iptr(cg),
+                                          iptr(nbr), iptr(gs), iptr(ss), iptr(sg)))
+    return dict(owned=nown, ghosts=ngh, bfaces=nb, faces=nf, cell_global=cg, nbr_rank=nbr[:nnbr],
+                ghost_start=gs, send_start=ss, send_global=sg[:nsend])
+
+
+class FlowFVGroup:
+    """All ranks of one partition driven from one process (device copies instead of RCCL)."""
+
+    def __init__(self, spatials):
+        self.sps = list(spatials)
+        arr = (ctypes.c_void_p * len(self.sps))(*[s._h.value for s in self.sps])
+        g = ctypes.c_void_p()
+        check(_ffi.lib().fvhip_group_create(arr, len(self.sps), ctypes.byref(g)))
+        self._g = g
+
+    def compute_residual_device(self, d_us, d_rs, d_dts=None, gettimesteps=False, overwrite=True):
+        n = len(self.sps)
+        P = ctypes.c_void_p * n
+        u, r = P(*d_us), P(*d_rs)
+        d = P(*(d_dts if d_dts else [0] * n))
+        check(_ffi.lib().fvhip_group_compute_residual_device(self._g, u, r, int(gettimesteps), d,
+                                                             1 if overwrite else 0))
+
+    def close(self):
+        if getattr(self, "_g", None):
+            _ffi.lib().fvhip_group_destroy(self._g)
+            self._g = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass

@@ -41,6 +41,20 @@ _SIGS = {
     "fvhip_create": (ctypes.c_int, [ctypes.POINTER(FvMeshView), ctypes.POINTER(FvFlowConfig), ctypes.c_int,
                                     ctypes.POINTER(ctypes.c_void_p)]),
     "fvhip_destroy": (ctypes.c_int, [ctypes.c_void_p]),
+    "fvhip_partition_rcb": (ctypes.c_int, [ctypes.POINTER(FvMeshView), ctypes.c_int, c_int_p]),
+    "fvhip_partition_info": (ctypes.c_int, [ctypes.POINTER(FvMeshView), c_int_p, ctypes.c_int, c_int_p, c_int_p,
+                                            c_int_p, c_int_p, c_int_p, c_int_p]),
+    "fvhip_create_partitioned": (ctypes.c_int, [ctypes.POINTER(FvMeshView), ctypes.POINTER(FvFlowConfig), c_int_p,
+                                                ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                                ctypes.POINTER(ctypes.c_void_p)]),
+    "fvhip_comm_unique_id": (ctypes.c_int, [ctypes.c_void_p]),
+    "fvhip_comm_init": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_void_p]),
+    "fvhip_group_create": (ctypes.c_int, [ctypes.POINTER(ctypes.c_void_p), ctypes.c_int,
+                                          ctypes.POINTER(ctypes.c_void_p)]),
+    "fvhip_group_destroy": (ctypes.c_int, [ctypes.c_void_p]),
+    "fvhip_group_compute_residual_device": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(ctypes.c_void_p),
+                                                           ctypes.POINTER(ctypes.c_void_p), ctypes.c_int,
+                                                           ctypes.POINTER(ctypes.c_void_p), ctypes.c_int]),
     "fvhip_compute_residual": (ctypes.c_int, [ctypes.c_void_p, c_dbl_p, c_dbl_p, ctypes.c_int, c_dbl_p]),
     "fvhip_compute_residual_device": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
                                                      ctypes.c_int, ctypes.c_void_p, ctypes.c_int]),

@@ -8,6 +8,9 @@
 #include "kernels.hpp"
 #include "jacobian.hpp"
 #include "mesh.hpp"
+#include "partition.hpp"
+#include "halo.hpp"
+#include <rccl/rccl.h>
 
 #include <hip/hip_runtime.h>
 #include <cstring>
@@ -18,6 +21,7 @@
 #include <map>
 #include <stdexcept>
 #include <memory>
+#include <functional>
 
 using namespace fvhip;
 
@@ -31,6 +35,11 @@ inline void hipCheck(hipError_t e, const char* what) {
 	if(e != hipSuccess) throw HipError(std::string(what) + ": " + hipGetErrorString(e));
 }
 #define HC(x) hipCheck((x), #x)
+
+inline void ncclCheck(ncclResult_t e, const char* what) {
+	if(e != ncclSuccess) throw std::runtime_error(std::string(what) + ": " + ncclGetErrorString(e));
+}
+#define NC(x) ncclCheck((x), #x)
 
 template <typename F>
 int guard(F&& f) {
@@ -91,6 +100,13 @@ struct fvhip_ctx
 	bool jac_ready = false;
 	double *d_jb = nullptr, *d_jlo = nullptr, *d_jup = nullptr, *d_jdiag = nullptr;
 	std::vector<double> h_stage;
+	// partitioned meshes: halo exchange with the neighbour ranks (RCCL, or in-process for a group)
+	int rank = 0, nparts = 1;
+	ncclComm_t comm = nullptr;
+	bool in_group = false;
+	int* d_send = nullptr;
+	double* d_sendbuf = nullptr;
+	int nsend = 0;
 	// profiling
 	bool prof = false;
 	struct Rec { std::string name; hipEvent_t a, b; };
@@ -99,6 +115,7 @@ struct fvhip_ctx
 
 	~fvhip_ctx() {
 		(void)hipSetDevice(device);
+		if(comm) (void)ncclCommDestroy(comm);
 		for(auto& r : recs) { (void)hipEventDestroy(r.a); (void)hipEventDestroy(r.b); }
 		for(void* p : owned) (void)hipFree(p);
 		if(stream) (void)hipStreamDestroy(stream);
@@ -136,30 +153,39 @@ struct fvhip_ctx
 		return cfg.const_visc ? SV_CONST : SV_SUTHERLAND;
 	}
 
-	/// the device sweep: -r(u) added (or written) into r, time steps into dtm
-	void residual(const double* u, double* r, bool dt, double* dtm, bool overwrite) {
+	bool halo() const { return !L.nbr_rank.empty(); }
+	int ntotal() const { return L.ncell + L.nghost; }
+
+	// --- residual stages (FlowFV::compute_residual, flow_spatial.cpp:636-816); between them the
+	// ghost rows of u, of the gradients and of limiter data are exchanged on partitioned meshes ---
+	void stage_gradients(const double* u) {
+		if(L.nghost > 0)
+			timed("k_ghost_prim", [&]{ launch_cons2prim_rows(P.gas, u, d_up, L.ncell, L.nghost, stream); });
+		if(cfg.gradientscheme == FVHIP_GRAD_LEASTSQUARES) {
+			timed("k_prep_grad_wls", [&]{ KOPS(launch_prep_grad_wls)(M, P, u, d_up, d_ubc, d_ug, d_grad, stream); });
+		} else {
+			timed("k_prep", [&]{ KOPS(launch_prep)(M, P, u, d_up, d_ubc, d_ug, true, stream); });
+			if(cfg.gradientscheme == FVHIP_GRAD_GREENGAUSS)
+				timed("k_grad_gg", [&]{ KOPS(launch_grad_gg)(M, d_up, d_ug, d_grad, stream); });
+			else KOPS(launch_fill)(d_grad, 0.0, 8LL*ntotal(), stream);
+		}
+	}
+	bool limited() const {
+		return cfg.reconstruction == FVHIP_REC_BARTHJESPERSEN || cfg.reconstruction == FVHIP_REC_VENKATAKRISHNAN;
+	}
+	void stage_limiter() {
+		const int venk = cfg.reconstruction == FVHIP_REC_VENKATAKRISHNAN;
+		timed("k_limiter", [&]{ KOPS(launch_limiter)(M, P, venk, d_up, d_ug, d_grad, d_phi, stream); });
+	}
+	void stage_weno() { timed("k_weno", [&]{ KOPS(launch_weno)(M, P, d_grad, d_lgrad, stream); }); }
+	void stage_sweep(const double* u, double* r, bool dt, double* dtm, bool overwrite) {
 		const int rk = recKind();
 		SweepBuffers B{};
 		B.u = u; B.r = r; B.dtm = dtm; B.overwrite = overwrite ? 1 : 0;
 		if(rk != SR_FIRST) {
-			if(cfg.gradientscheme == FVHIP_GRAD_LEASTSQUARES) {
-				timed("k_prep_grad_wls", [&]{ KOPS(launch_prep_grad_wls)(M, P, u, d_up, d_ubc, d_ug, d_grad, stream); });
-			} else {
-				timed("k_prep", [&]{ KOPS(launch_prep)(M, P, u, d_up, d_ubc, d_ug, true, stream); });
-				if(cfg.gradientscheme == FVHIP_GRAD_GREENGAUSS)
-					timed("k_grad_gg", [&]{ KOPS(launch_grad_gg)(M, d_up, d_ug, d_grad, stream); });
-				else KOPS(launch_fill)(d_grad, 0.0, 8LL*L.ncell, stream);
-			}
 			B.up = d_up; B.grad = d_grad; B.rgrad = d_grad; B.ubc = d_ubc; B.ug = d_ug;
-			if(cfg.reconstruction == FVHIP_REC_BARTHJESPERSEN || cfg.reconstruction == FVHIP_REC_VENKATAKRISHNAN) {
-				const int venk = cfg.reconstruction == FVHIP_REC_VENKATAKRISHNAN;
-				timed("k_limiter", [&]{ KOPS(launch_limiter)(M, P, venk, d_up, d_ug, d_grad, d_phi, stream); });
-				B.phi = d_phi;
-			}
-			if(cfg.reconstruction == FVHIP_REC_WENO) {
-				timed("k_weno", [&]{ KOPS(launch_weno)(M, P, d_grad, d_lgrad, stream); });
-				B.rgrad = d_lgrad;
-			}
+			if(limited()) B.phi = d_phi;
+			if(cfg.reconstruction == FVHIP_REC_WENO) B.rgrad = d_lgrad;
 		}
 		const char* nm = nullptr;
 		// name is only known after launch; record under a generic label then rename
@@ -168,8 +194,65 @@ struct fvhip_ctx
 		HC(hipGetLastError());
 	}
 
+	/// pack the rows of `arr` (width doubles per cell) that the neighbours hold as ghosts
+	void pack(const double* arr, int width) {
+		timed("k_pack", [&]{ launch_pack_rows(d_send, nsend, arr, width, d_sendbuf, stream); });
+	}
+	/// RCCL point-to-point exchange with every neighbour rank, on this handle's stream
+	void exchange_rccl(double* arr, int width) {
+		if(!halo()) return;
+		if(!comm) throw std::runtime_error("partitioned handle: call fvhip_comm_init (or use a group) first");
+		pack(arr, width);
+		NC(ncclGroupStart());
+		for(size_t k = 0; k < L.nbr_rank.size(); k++) {
+			const int q = L.nbr_rank[k];
+			const size_t ns = static_cast<size_t>(L.send_start[k+1] - L.send_start[k]);
+			const size_t ng = static_cast<size_t>(L.ghost_start[k+1] - L.ghost_start[k]);
+			NC(ncclSend(d_sendbuf + static_cast<size_t>(width)*L.send_start[k], width*ns, ncclDouble, q, comm, stream));
+			NC(ncclRecv(arr + static_cast<size_t>(width)*(L.ncell + L.ghost_start[k]), width*ng, ncclDouble, q, comm, stream));
+		}
+		NC(ncclGroupEnd());
+	}
+
+	/// the device sweep: -r(u) added (or written) into r, time steps into dtm. On a partitioned
+	/// mesh u must have room for the ghost rows (ncell+nghost rows), which this fills.
+	void residual(const double* u, double* r, bool dt, double* dtm, bool overwrite) {
+		std::vector<fvhip_ctx*> one{this};
+		residual_seq(one, {u}, {r}, dt, {dtm}, overwrite, GroupExchange());
+	}
+
+	typedef std::function<double*(size_t)> ArrayOf;
+	typedef std::function<void(const ArrayOf&, int)> GroupExchange;
+
+	/// The residual as a sequence of stages over one or several handles (several: the ranks of a
+	/// partition held by one process, exchanging through device copies, see fvhip_group_*)
+	static void residual_seq(std::vector<fvhip_ctx*>& hs, const std::vector<const double*>& us,
+	                         const std::vector<double*>& rs, bool dt, const std::vector<double*>& dts,
+	                         bool overwrite, const GroupExchange& exg) {
+		auto exchange = [&](const ArrayOf& arr_of, int width) {
+			if(exg) { exg(arr_of, width); return; }
+			for(size_t i = 0; i < hs.size(); i++) hs[i]->exchange_rccl(arr_of(i), width);
+		};
+		fvhip_ctx* h0 = hs[0];
+		exchange([&](size_t i) { return const_cast<double*>(us[i]); }, 4);
+		if(h0->recKind() != SR_FIRST) {
+			for(size_t i = 0; i < hs.size(); i++) hs[i]->stage_gradients(us[i]);
+			exchange([&](size_t i) { return hs[i]->d_grad; }, 8);
+			if(h0->limited()) {
+				for(fvhip_ctx* h : hs) h->stage_limiter();
+				exchange([&](size_t i) { return hs[i]->d_phi; }, 4);
+			}
+			if(h0->cfg.reconstruction == FVHIP_REC_WENO) {
+				for(fvhip_ctx* h : hs) h->stage_weno();
+				exchange([&](size_t i) { return hs[i]->d_lgrad; }, 8);
+			}
+		}
+		for(size_t i = 0; i < hs.size(); i++) hs[i]->stage_sweep(us[i], rs[i], dt, dts[i], overwrite);
+	}
+
 	/// face-ordered mesh view and block buffers for the Jacobian, built on first use
 	void ensureJacobian() {
+		if(nparts > 1) throw std::runtime_error("Jacobian assembly on partitioned meshes is not built yet");
 		const int jf = cfg.conv_numflux_jac;
 		if(jf == FVHIP_FLUX_VANLEER) throw std::runtime_error(" ! VanLeerFlux: Not implemented!");   // anumericalflux.cpp:253-257
 		if(jf == FVHIP_FLUX_AUSMPLUS) throw std::runtime_error(" ! AUSMPlusFlux: Not implemented!"); // :556-560
@@ -201,6 +284,7 @@ struct fvhip_ctx
 
 	/// MatrixFreeSpatialJacobian::apply on device vectors (internal order)
 	void matfree(const double* x, double* y) {
+		if(nparts > 1) throw std::runtime_error("matrix-free operator on partitioned meshes is not built yet");
 		if(!mf_u || !mf_r || !mf_mdt) throw std::runtime_error("matrix-free operator: state not set");
 		const size_t N = static_cast<size_t>(L.ncell);
 		if(!d_part) { d_part = dalloc(mf_partials(), owned); d_pm = dalloc(2, owned); }
@@ -223,75 +307,207 @@ int fvhip_device_count(void) {
 	return n;
 }
 
+static void checkConfig(const fvhip_flow_config* cfg)
+{
+	if(cfg->nbc > MAXBC) throw std::invalid_argument("too many boundary conditions");
+	if(cfg->conv_numflux < 0 || cfg->conv_numflux > 6) throw std::invalid_argument("unknown flux"); // afactory.cpp:78-80
+	for(int i = 0; i < cfg->nbc; i++) {
+		const int t = cfg->bc_type[i];
+		if(t == FVHIP_BC_PERIODIC || t < 0 || t > 7) throw std::invalid_argument("BC type not implemented yet!"); // abc.cpp:493-494
+	}
+}
+
+/// device-resident discretisation of a (possibly partitioned) topology
+static fvhip_ctx* createCtx(const MeshTopo& T, const fvhip_flow_config* cfg, int device)
+{
+	checkConfig(cfg);
+	std::unique_ptr<fvhip_ctx> h(new fvhip_ctx());
+	h->device = device;
+	HC(hipSetDevice(device));
+	HC(hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking));
+	h->cfg = *cfg;
+	h->bc_type.assign(cfg->bc_type, cfg->bc_type + cfg->nbc);
+	h->bc_tag.assign(cfg->bc_tag, cfg->bc_tag + cfg->nbc);
+	h->bc_vals.assign(cfg->bc_vals, cfg->bc_vals + 2*cfg->nbc);
+	h->cfg.bc_type = h->bc_type.data(); h->cfg.bc_tag = h->bc_tag.data(); h->cfg.bc_vals = h->bc_vals.data();
+
+	h->L = buildLayout(T, h->cfg, true);
+	Layout& L = h->L;
+	auto& o = h->owned;
+	DevMesh& M = h->M;
+	M.ncell = L.ncell + L.nghost; M.nown = L.ncell; M.nbface = L.nbface;
+	M.npatch = static_cast<int>(L.patch_cell.size()) - 1;
+	M.nslot = static_cast<int>(L.slot_L.size());
+	M.patch_cell = upload(L.patch_cell, o);
+	M.patch_slot = upload(L.patch_slot, o);
+	M.slot_LR = reinterpret_cast<const int2*>(upload(pack2(L.slot_L, L.slot_R), o));
+	M.slot_n = reinterpret_cast<const double2*>(upload(L.slot_n, o));
+	M.slot_len = upload(L.slot_len, o);
+	M.slot_gr = reinterpret_cast<const double2*>(upload(L.slot_gr, o));
+	M.cell_slots = reinterpret_cast<const int4*>(upload(L.cell_slots, o));
+	M.cell_nbr = reinterpret_cast<const int4*>(upload(L.cell_nbr_local, o));
+	M.cell_face = reinterpret_cast<const int4*>(upload(L.cell_face_local, o));
+	M.cell_nbr_fo = reinterpret_cast<const int4*>(upload(L.cell_nbr_fo, o));
+	M.rc = reinterpret_cast<const double2*>(upload(L.rc, o));
+	M.area = upload(L.area, o);
+	M.wls_V = reinterpret_cast<const double4*>(upload(L.wls_V, o));
+	M.venk_eps2 = upload(L.venk_eps2, o);
+	M.bf_L = upload(L.bf_L, o);
+	M.bf_bc = upload(L.bf_bc, o);
+	M.bf_n = reinterpret_cast<const double2*>(upload(L.bf_n, o));
+	M.bf_rcbp = reinterpret_cast<const double2*>(upload(L.bf_rcbp, o));
+	h->d_perm = upload(L.perm, o);
+	h->nsend = static_cast<int>(L.send_cells.size());
+	if(h->nsend > 0) {
+		h->d_send = upload(L.send_cells, o);
+		h->d_sendbuf = dalloc(8*static_cast<size_t>(h->nsend), o);
+	}
+
+	DevPhys& P = h->P;
+	P.gas = gd::Gas{cfg->gamma, cfg->Minf, cfg->Tinf, cfg->Reinf, cfg->Pr, 110.5};
+	// free stream, aphysics.cpp:43-58 (sideslip 0)
+	const double beta = 0;
+	P.uinf[0] = 1.0;
+	P.uinf[1] = std::cos(cfg->aoa)*std::cos(beta);
+	P.uinf[2] = std::sin(cfg->aoa)*std::cos(beta);
+	const double pinf = (1.0/(cfg->gamma*cfg->Minf*cfg->Minf));
+	P.uinf[3] = pinf/(cfg->gamma-1.0) + 0.5*1.0*1.0;
+	P.nbc = cfg->nbc;
+	for(int i = 0; i < cfg->nbc; i++) P.bc[i] = gd::BCDev{cfg->bc_type[i], cfg->bc_vals[2*i], cfg->bc_vals[2*i+1]};
+	P.limiter_param = cfg->limiter_param;
+
+	const size_t N = static_cast<size_t>(L.ncell), NT = N + static_cast<size_t>(L.nghost);
+	const size_t nb = static_cast<size_t>(L.nbface);
+	h->d_u = dalloc(4*NT, o); h->d_r = dalloc(4*N, o); h->d_dtm = dalloc(N, o);
+	h->d_up = dalloc(4*NT, o); h->d_grad = dalloc(8*NT, o);
+	h->d_ubc = dalloc(4*nb, o); h->d_ug = dalloc(4*nb, o);
+	if(cfg->reconstruction == FVHIP_REC_WENO) h->d_lgrad = dalloc(8*NT, o);
+	if(cfg->reconstruction == FVHIP_REC_BARTHJESPERSEN || cfg->reconstruction == FVHIP_REC_VENKATAKRISHNAN)
+		h->d_phi = dalloc(4*NT, o);
+	h->h_stage.resize(16*N);
+	return h.release();
+}
+
 int fvhip_create(const fvhip_mesh* mesh, const fvhip_flow_config* cfg, int device, fvhip_handle* out)
 {
 	return guard([&] {
 		if(!mesh || !cfg || !out) throw std::invalid_argument("null argument");
-		if(cfg->nbc > MAXBC) throw std::invalid_argument("too many boundary conditions");
-		if(cfg->conv_numflux < 0 || cfg->conv_numflux > 6) throw std::invalid_argument("unknown flux"); // afactory.cpp:78-80
-		for(int i = 0; i < cfg->nbc; i++) {
-			const int t = cfg->bc_type[i];
-			if(t == FVHIP_BC_PERIODIC || t < 0 || t > 7) throw std::invalid_argument("BC type not implemented yet!"); // abc.cpp:493-494
+		*out = createCtx(topoFromMesh(*mesh), cfg, device);
+	});
+}
+
+int fvhip_create_partitioned(const fvhip_mesh* mesh, const fvhip_flow_config* cfg, const int* part, int nparts,
+                             int rank, int device, fvhip_handle* out)
+{
+	return guard([&] {
+		if(!mesh || !cfg || !part || !out) throw std::invalid_argument("null argument");
+		if(rank < 0 || rank >= nparts) throw std::invalid_argument("rank out of range");
+		for(int e = 0; e < mesh->nelem; e++)
+			if(part[e] < 0 || part[e] >= nparts) throw std::invalid_argument("partition entry out of range");
+		fvhip_ctx* h = createCtx(extractPartition(*mesh, part, rank), cfg, device);
+		h->rank = rank; h->nparts = nparts;
+		*out = h;
+	});
+}
+
+int fvhip_partition_rcb(const fvhip_mesh* mesh, int nparts, int* part)
+{
+	return guard([&] {
+		const std::vector<int> p = partitionRCB(mesh->rc, mesh->nelem, nparts);
+		std::memcpy(part, p.data(), p.size()*sizeof(int));
+	});
+}
+
+int fvhip_partition_info(const fvhip_mesh* mesh, const int* part, int rank, int* counts, int* cell_global,
+                         int* nbr_rank, int* ghost_start, int* send_start, int* send_global)
+{
+	return guard([&] {
+		const MeshTopo T = extractPartition(*mesh, part, rank);
+		const int nnbr = static_cast<int>(T.nbr_rank.size());
+		counts[0] = T.nown; counts[1] = T.nghost; counts[2] = T.nbface; counts[3] = T.naface;
+		counts[4] = nnbr; counts[5] = static_cast<int>(T.send_cells.size());
+		if(cell_global) std::memcpy(cell_global, T.cell_global.data(), T.cell_global.size()*sizeof(int));
+		if(nbr_rank) for(int k = 0; k < nnbr; k++) nbr_rank[k] = T.nbr_rank[k];
+		if(ghost_start) for(int k = 0; k <= nnbr; k++) ghost_start[k] = nnbr ? T.ghost_start[k] : 0;
+		if(send_start) for(int k = 0; k <= nnbr; k++) send_start[k] = T.send_start[k];
+		if(send_global) for(size_t i = 0; i < T.send_cells.size(); i++) send_global[i] = T.cell_global[T.send_cells[i]];
+	});
+}
+
+int fvhip_comm_unique_id(void* id128)
+{
+	return guard([&] {
+		ncclUniqueId id;
+		NC(ncclGetUniqueId(&id));
+		std::memcpy(id128, &id, sizeof(id));
+	});
+}
+
+int fvhip_comm_init(fvhip_handle h, int nranks, int rank, const void* id128)
+{
+	return guard([&] {
+		if(nranks != h->nparts || rank != h->rank)
+			throw std::invalid_argument("communicator does not match the handle's partition");
+		HC(hipSetDevice(h->device));
+		ncclUniqueId id;
+		std::memcpy(&id, id128, sizeof(id));
+		NC(ncclCommInitRank(&h->comm, nranks, id, rank));
+	});
+}
+
+struct fvhip_group_s { std::vector<fvhip_ctx*> hs; };
+
+int fvhip_group_create(fvhip_handle* hs, int n, fvhip_group* out)
+{
+	return guard([&] {
+		std::unique_ptr<fvhip_group_s> g(new fvhip_group_s());
+		std::vector<int> seen(n, 0);
+		for(int i = 0; i < n; i++) {
+			if(!hs[i] || hs[i]->nparts != n || hs[i]->rank < 0 || hs[i]->rank >= n || seen[hs[i]->rank]++)
+				throw std::invalid_argument("a group needs one handle per rank of one partition");
+			g->hs.push_back(hs[i]);
 		}
-		std::unique_ptr<fvhip_ctx> h(new fvhip_ctx());
-		h->device = device;
-		HC(hipSetDevice(device));
-		HC(hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking));
-		h->cfg = *cfg;
-		h->bc_type.assign(cfg->bc_type, cfg->bc_type + cfg->nbc);
-		h->bc_tag.assign(cfg->bc_tag, cfg->bc_tag + cfg->nbc);
-		h->bc_vals.assign(cfg->bc_vals, cfg->bc_vals + 2*cfg->nbc);
-		h->cfg.bc_type = h->bc_type.data(); h->cfg.bc_tag = h->bc_tag.data(); h->cfg.bc_vals = h->bc_vals.data();
+		for(fvhip_ctx* h : g->hs) h->in_group = true;
+		*out = g.release();
+	});
+}
 
-		h->L = buildLayout(*mesh, h->cfg, true);
-		Layout& L = h->L;
-		auto& o = h->owned;
-		DevMesh& M = h->M;
-		M.ncell = L.ncell; M.nbface = L.nbface;
-		M.npatch = static_cast<int>(L.patch_cell.size()) - 1;
-		M.nslot = static_cast<int>(L.slot_L.size());
-		M.patch_cell = upload(L.patch_cell, o);
-		M.patch_slot = upload(L.patch_slot, o);
-		M.slot_LR = reinterpret_cast<const int2*>(upload(pack2(L.slot_L, L.slot_R), o));
-		M.slot_n = reinterpret_cast<const double2*>(upload(L.slot_n, o));
-		M.slot_len = upload(L.slot_len, o);
-		M.slot_gr = reinterpret_cast<const double2*>(upload(L.slot_gr, o));
-		M.cell_slots = reinterpret_cast<const int4*>(upload(L.cell_slots, o));
-		M.cell_nbr = reinterpret_cast<const int4*>(upload(L.cell_nbr_local, o));
-		M.cell_face = reinterpret_cast<const int4*>(upload(L.cell_face_local, o));
-		M.cell_nbr_fo = reinterpret_cast<const int4*>(upload(L.cell_nbr_fo, o));
-		M.rc = reinterpret_cast<const double2*>(upload(L.rc, o));
-		M.area = upload(L.area, o);
-		M.wls_V = reinterpret_cast<const double4*>(upload(L.wls_V, o));
-		M.venk_eps2 = upload(L.venk_eps2, o);
-		M.bf_L = upload(L.bf_L, o);
-		M.bf_bc = upload(L.bf_bc, o);
-		M.bf_n = reinterpret_cast<const double2*>(upload(L.bf_n, o));
-		M.bf_rcbp = reinterpret_cast<const double2*>(upload(L.bf_rcbp, o));
-		h->d_perm = upload(L.perm, o);
+int fvhip_group_destroy(fvhip_group g) { return guard([&] { for(fvhip_ctx* h : g->hs) h->in_group = false; delete g; }); }
 
-		DevPhys& P = h->P;
-		P.gas = gd::Gas{cfg->gamma, cfg->Minf, cfg->Tinf, cfg->Reinf, cfg->Pr, 110.5};
-		// free stream, aphysics.cpp:43-58 (sideslip 0)
-		const double beta = 0;
-		P.uinf[0] = 1.0;
-		P.uinf[1] = std::cos(cfg->aoa)*std::cos(beta);
-		P.uinf[2] = std::sin(cfg->aoa)*std::cos(beta);
-		const double pinf = (1.0/(cfg->gamma*cfg->Minf*cfg->Minf));
-		P.uinf[3] = pinf/(cfg->gamma-1.0) + 0.5*1.0*1.0;
-		P.nbc = cfg->nbc;
-		for(int i = 0; i < cfg->nbc; i++) P.bc[i] = gd::BCDev{cfg->bc_type[i], cfg->bc_vals[2*i], cfg->bc_vals[2*i+1]};
-		P.limiter_param = cfg->limiter_param;
-
-		const size_t N = static_cast<size_t>(L.ncell), nb = static_cast<size_t>(L.nbface);
-		h->d_u = dalloc(4*N, o); h->d_r = dalloc(4*N, o); h->d_dtm = dalloc(N, o);
-		h->d_up = dalloc(4*N, o); h->d_grad = dalloc(8*N, o);
-		h->d_ubc = dalloc(4*nb, o); h->d_ug = dalloc(4*nb, o);
-		if(cfg->reconstruction == FVHIP_REC_WENO) h->d_lgrad = dalloc(8*N, o);
-		if(cfg->reconstruction == FVHIP_REC_BARTHJESPERSEN || cfg->reconstruction == FVHIP_REC_VENKATAKRISHNAN)
-			h->d_phi = dalloc(4*N, o);
-		h->h_stage.resize(8*N);
-		*out = h.release();
+int fvhip_group_compute_residual_device(fvhip_group g, const double* const* d_u, double* const* d_r,
+                                        int gettimesteps, double* const* d_dtm, int flags)
+{
+	return guard([&] {
+		const size_t n = g->hs.size();
+		std::vector<fvhip_ctx*> byrank(n);
+		for(fvhip_ctx* h : g->hs) byrank[h->rank] = h;
+		// in-process exchange: pack everywhere, then copy each neighbour's packed rows into the ghost block
+		auto exg = [&](const fvhip_ctx::ArrayOf& arr_of, int width) {
+			for(size_t i = 0; i < n; i++) if(g->hs[i]->halo()) { HC(hipSetDevice(g->hs[i]->device)); g->hs[i]->pack(arr_of(i), width); }
+			for(size_t i = 0; i < n; i++) HC(hipStreamSynchronize(g->hs[i]->stream));
+			for(size_t i = 0; i < n; i++) {
+				fvhip_ctx* h = g->hs[i];
+				const Layout& L = h->L;
+				for(size_t k = 0; k < L.nbr_rank.size(); k++) {
+					fvhip_ctx* q = byrank[L.nbr_rank[k]];
+					const Layout& Q = q->L;
+					size_t kk = 0;
+					while(kk < Q.nbr_rank.size() && Q.nbr_rank[kk] != h->rank) kk++;
+					if(kk == Q.nbr_rank.size()) throw std::logic_error("halo lists are not symmetric");
+					const int cnt = L.ghost_start[k+1] - L.ghost_start[k];
+					if(cnt != Q.send_start[kk+1] - Q.send_start[kk]) throw std::logic_error("halo sizes differ");
+					HC(hipMemcpyAsync(arr_of(i) + static_cast<size_t>(width)*(L.ncell + L.ghost_start[k]),
+					                  q->d_sendbuf + static_cast<size_t>(width)*Q.send_start[kk],
+					                  sizeof(double)*width*static_cast<size_t>(cnt), hipMemcpyDeviceToDevice, h->stream));
+				}
+			}
+			for(size_t i = 0; i < n; i++) HC(hipStreamSynchronize(g->hs[i]->stream));
+		};
+		std::vector<const double*> us(d_u, d_u + n);
+		std::vector<double*> rs(d_r, d_r + n), dts(n, nullptr);
+		if(gettimesteps) dts.assign(d_dtm, d_dtm + n);
+		fvhip_ctx::residual_seq(g->hs, us, rs, gettimesteps != 0, dts, (flags & FVHIP_RES_OVERWRITE) != 0, exg);
+		for(size_t i = 0; i < n; i++) HC(hipStreamSynchronize(g->hs[i]->stream));
 	});
 }
 
@@ -576,6 +792,7 @@ int fvhip_layout_stats(fvhip_handle h, long long* s)
 	return guard([&] {
 		s[0] = h->L.ncell; s[1] = h->L.naface; s[2] = static_cast<long long>(h->L.slot_L.size());
 		s[3] = static_cast<long long>(h->L.patch_cell.size()) - 1; s[4] = h->L.max_slots; s[5] = h->L.nbface;
+		s[6] = h->L.nghost; s[7] = static_cast<long long>(h->L.nbr_rank.size()); s[8] = h->nsend;
 	});
 }
 

@@ -91,8 +91,8 @@ __global__ void __launch_bounds__(256) k_grad_wls(DevMesh M, const double* __res
                                                   const double* __restrict__ ug, double* __restrict__ grad)
 {
 	const int c = blockIdx.x*blockDim.x + threadIdx.x;
-	if(c >= M.ncell) return;
-	const int N = M.ncell;
+	if(c >= M.nown) return;
+	const int N = M.ncell;     // cells incl. ghosts: codes >= N are boundary faces
 	const int4 nb4 = M.cell_nbr_fo[c];
 	const int nb[4] = {nb4.x, nb4.y, nb4.z, nb4.w};
 	const double2 rcc = M.rc[c];
@@ -145,16 +145,17 @@ __global__ void __launch_bounds__(256) k_prep_grad_wls(DevMesh M, DevPhys P, con
 {
 	__shared__ __attribute__((aligned(16))) double s_up[256][4];
 	__shared__ __attribute__((aligned(16))) double2 s_rc[256];
-	const int N = M.ncell;
-	const int cb = xcd_chunk(static_cast<int>((N + 255) >> 8))*256;
-	if(cb >= N) return;
+	const int N = M.ncell;        // owned + ghost: neighbour codes >= N are boundary faces
+	const int NO = M.nown;
+	const int cb = xcd_chunk(static_cast<int>((NO + 255) >> 8))*256;
+	if(cb >= NO) return;
 	const int t = static_cast<int>(threadIdx.x);
 	const int c = cb + t;
-	const int ncb = (N - cb) < 256 ? (N - cb) : 256;
+	const int ncb = (NO - cb) < 256 ? (NO - cb) : 256;
 	const Gas& G = P.gas;
 	double ucons[4], uc[4];
 	double2 rcc = make_double2(0, 0);
-	if(c < N) {
+	if(c < NO) {
 		ld4(u, c, ucons);
 		cons2prim(G, ucons, uc);
 		st4(up, c, uc);
@@ -163,7 +164,7 @@ __global__ void __launch_bounds__(256) k_prep_grad_wls(DevMesh M, DevPhys P, con
 		s_rc[t] = rcc;
 	}
 	__syncthreads();
-	if(c >= N) return;
+	if(c >= NO) return;
 	const int4 nb4 = M.cell_nbr_fo[c];
 	const int nb[4] = {nb4.x, nb4.y, nb4.z, nb4.w};
 	double un[4][4];
@@ -222,8 +223,8 @@ __global__ void __launch_bounds__(256) k_grad_gg(DevMesh M, const double* __rest
                                                  const double* __restrict__ ug, double* __restrict__ grad)
 {
 	const int c = blockIdx.x*blockDim.x + threadIdx.x;
-	if(c >= M.ncell) return;
-	const int N = M.ncell;
+	if(c >= M.nown) return;
+	const int N = M.ncell;     // cells incl. ghosts: codes >= N are boundary faces
 	const int4 cs = M.cell_slots[c];
 	const int e[4] = {cs.x, cs.y, cs.z, cs.w};
 	double g[8] = {0,0,0,0,0,0,0,0};
@@ -267,8 +268,8 @@ __global__ void __launch_bounds__(256) k_limiter(DevMesh M, const double* __rest
                                                  const double* __restrict__ grad, double* __restrict__ phi)
 {
 	const int c = blockIdx.x*blockDim.x + threadIdx.x;
-	if(c >= M.ncell) return;
-	const int N = M.ncell;
+	if(c >= M.nown) return;
+	const int N = M.ncell;     // cells incl. ghosts: codes >= N are boundary faces
 	double uc[4], g[8];
 	ld4(up, c, uc);
 	ld8(grad, c, g);
@@ -325,8 +326,8 @@ __global__ void __launch_bounds__(256) k_weno(DevMesh M, double lambda, const do
                                               double* __restrict__ lgrad)
 {
 	const int c = blockIdx.x*blockDim.x + threadIdx.x;
-	if(c >= M.ncell) return;
-	const int N = M.ncell;
+	if(c >= M.nown) return;
+	const int N = M.ncell;     // cells incl. ghosts: codes >= N are boundary faces
 	const double gamma = 4.0, epsilon = 1.0e-5;
 	double g0[8];
 	ld8(grad, c, g0);
@@ -652,25 +653,25 @@ static inline int nblk(long long n, int b) { return static_cast<int>((n + b - 1)
 void launch_prep(const DevMesh& M, const DevPhys& P, const double* u, double* up, double* ubc, double* ug,
                  bool cells, hipStream_t s)
 {
-	if(cells && M.ncell > 0) k_prep_cells<<<nblk(M.ncell,256), 256, 0, s>>>(M.ncell, P.gas, u, up);
+	if(cells && M.nown > 0) k_prep_cells<<<nblk(M.nown,256), 256, 0, s>>>(M.nown, P.gas, u, up);
 	if(M.nbface > 0) k_prep_bfaces<<<nblk(M.nbface,256), 256, 0, s>>>(M, P, u, ubc, ug);
 }
 void launch_grad_wls(const DevMesh& M, const double* up, const double* ug, double* grad, hipStream_t s)
-{ if(M.ncell > 0) k_grad_wls<<<nblk(M.ncell,256), 256, 0, s>>>(M, up, ug, grad); }
+{ if(M.nown > 0) k_grad_wls<<<nblk(M.nown,256), 256, 0, s>>>(M, up, ug, grad); }
 void launch_prep_grad_wls(const DevMesh& M, const DevPhys& P, const double* u, double* up, double* ubc,
                           double* ug, double* grad, hipStream_t s)
-{ if(M.ncell > 0) k_prep_grad_wls<<<xcd_blocks((M.ncell + 255)/256), 256, 0, s>>>(M, P, u, up, ubc, ug, grad); }
+{ if(M.nown > 0) k_prep_grad_wls<<<xcd_blocks((M.nown + 255)/256), 256, 0, s>>>(M, P, u, up, ubc, ug, grad); }
 void launch_grad_gg(const DevMesh& M, const double* up, const double* ug, double* grad, hipStream_t s)
-{ if(M.ncell > 0) k_grad_gg<<<nblk(M.ncell,256), 256, 0, s>>>(M, up, ug, grad); }
+{ if(M.nown > 0) k_grad_gg<<<nblk(M.nown,256), 256, 0, s>>>(M, up, ug, grad); }
 void launch_limiter(const DevMesh& M, const DevPhys& P, int venk, const double* up, const double* ug,
                     const double* grad, double* phi, hipStream_t s)
 {
-	if(M.ncell <= 0) return;
-	if(venk) k_limiter<true><<<nblk(M.ncell,256), 256, 0, s>>>(M, up, ug, grad, phi);
-	else     k_limiter<false><<<nblk(M.ncell,256), 256, 0, s>>>(M, up, ug, grad, phi);
+	if(M.nown <= 0) return;
+	if(venk) k_limiter<true><<<nblk(M.nown,256), 256, 0, s>>>(M, up, ug, grad, phi);
+	else     k_limiter<false><<<nblk(M.nown,256), 256, 0, s>>>(M, up, ug, grad, phi);
 }
 void launch_weno(const DevMesh& M, const DevPhys& P, const double* grad, double* lgrad, hipStream_t s)
-{ if(M.ncell > 0) k_weno<<<nblk(M.ncell,256), 256, 0, s>>>(M, P.limiter_param, grad, lgrad); }
+{ if(M.nown > 0) k_weno<<<nblk(M.nown,256), 256, 0, s>>>(M, P.limiter_param, grad, lgrad); }
 void launch_fill(double* p, double v, long long n, hipStream_t s)
 { if(n > 0) k_fill<<<nblk(n,256), 256, 0, s>>>(p, v, n); }
 void launch_local_flux(int flux, const Gas& G, int nf, const double* ul, const double* ur,

@@ -18,7 +18,9 @@ enum SweepVisc { SV_NONE = 0, SV_SUTHERLAND = 1, SV_CONST = 2 };
 
 struct DevMesh
 {
-	int ncell, nbface, npatch, nslot;
+	int ncell;                 // owned + ghost cells: a neighbour code >= ncell is a boundary face
+	int nown;                  // owned cells (internal ids 0 .. nown-1)
+	int nbface, npatch, nslot;
 	const int* patch_cell;     // [npatch+1]
 	const int* patch_slot;     // [npatch+1]
 	const int2* slot_LR;       // [S]

@@ -5,6 +5,7 @@
  *   - Venkatakrishnan eps^2 = (K*clength)^3, limitedlinearreconstruction.cpp:178-205, 222
  */
 #include "layout.hpp"
+#include "partition.hpp"
 #include <algorithm>
 #include <numeric>
 #include <stdexcept>
@@ -55,24 +56,27 @@ std::vector<int> hilbertOrder(const double* rc, int N)
 
 Layout buildLayout(const fvhip_mesh& m, const fvhip_flow_config& cfg, bool renumber)
 {
-	if(m.nconnface != 0)
-		throw std::runtime_error("buildLayout: connectivity faces need the partitioned path");
-	if(m.maxnfael > MAXF) throw std::runtime_error("buildLayout: cells with more than 4 faces");
-	Layout Lo;
-	const int N = m.nelem, nb = m.nbface, F = m.naface;
-	Lo.ncell = N; Lo.nbface = nb; Lo.naface = F; Lo.ninface = F - nb;
+	return buildLayout(topoFromMesh(m), cfg, renumber);
+}
 
-	Lo.perm = renumber ? hilbertOrder(m.rc, N) : std::vector<int>(N);
+Layout buildLayout(const MeshTopo& T, const fvhip_flow_config& cfg, bool renumber)
+{
+	Layout Lo;
+	const int N = T.nown, NT = T.ncell(), nb = T.nbface, F = T.naface;
+	Lo.ncell = N; Lo.nghost = T.nghost; Lo.nbface = nb; Lo.naface = F; Lo.ninface = F - nb;
+
+	Lo.perm = renumber ? hilbertOrder(T.rc.data(), N) : std::vector<int>(N);
 	if(!renumber) std::iota(Lo.perm.begin(), Lo.perm.end(), 0);
 	Lo.iperm.assign(N, -1);
 	for(int i = 0; i < N; i++) Lo.iperm[Lo.perm[i]] = i;
 
-	auto nf = [&](int ref) { return m.nnode[ref]; };
-	auto efc = [&](int ref, int j) { return m.elemface[static_cast<size_t>(ref)*m.maxnfael+j]; };
-	auto esu = [&](int ref, int j) { return m.esuel[static_cast<size_t>(ref)*m.maxnfael+j]; };
-	auto Lref = [&](int f) { return m.intfac[4*static_cast<size_t>(f)]; };
-	auto Rref = [&](int f) { return m.intfac[4*static_cast<size_t>(f)+1]; };
-	auto toInt = [&](int refcell) { return refcell < N ? Lo.iperm[refcell] : N + (refcell - N - m.nconnface); };
+	auto nf = [&](int ref) { return T.nfael[ref]; };
+	auto efc = [&](int ref, int j) { return T.cell_faces[4*static_cast<size_t>(ref)+j]; };
+	auto esu = [&](int ref, int j) { return T.cell_esuel[4*static_cast<size_t>(ref)+j]; };
+	auto Lref = [&](int f) { return T.L[f]; };
+	auto Rref = [&](int f) { return T.R[f]; };
+	// owned cells are renumbered; ghosts (>= N) and boundary codes (>= NT) keep their value
+	auto toInt = [&](int refcell) { return refcell < N ? Lo.iperm[refcell] : refcell; };
 
 	// --- patches (greedy over internal cells, bounded slots and cells) ---
 	std::vector<int> mark(F, -1);
@@ -113,7 +117,7 @@ Layout buildLayout(const fvhip_mesh& m, const fvhip_flow_config& cfg, bool renum
 				if(face_slot[f] == -2 - p) continue;     // already collected for this patch
 				face_slot[f] = -2 - p;
 				if(f < nb) { bnd.push_back(f); continue; }
-				const int l = Lo.iperm[Lref(f)], r = Lo.iperm[Rref(f)];
+				const int l = toInt(Lref(f)), r = toInt(Rref(f));
 				if(l >= c0 && l < c1 && r >= c0 && r < c1) inner.push_back(f);
 				else cut.push_back(f);
 			}
@@ -124,11 +128,11 @@ Layout buildLayout(const fvhip_mesh& m, const fvhip_flow_config& cfg, bool renum
 			Lo.slot_L.push_back(toInt(Lref(f)));
 			Lo.slot_R.push_back(toInt(Rref(f)));
 			Lo.slot_face.push_back(f);
-			Lo.slot_n.push_back(m.facemetric[3*static_cast<size_t>(f)]);
-			Lo.slot_n.push_back(m.facemetric[3*static_cast<size_t>(f)+1]);
-			Lo.slot_len.push_back(m.facemetric[3*static_cast<size_t>(f)+2]);
-			Lo.slot_gr.push_back(m.gr[2*static_cast<size_t>(f)]);
-			Lo.slot_gr.push_back(m.gr[2*static_cast<size_t>(f)+1]);
+			Lo.slot_n.push_back(T.facemetric[3*static_cast<size_t>(f)]);
+			Lo.slot_n.push_back(T.facemetric[3*static_cast<size_t>(f)+1]);
+			Lo.slot_len.push_back(T.facemetric[3*static_cast<size_t>(f)+2]);
+			Lo.slot_gr.push_back(T.gr[2*static_cast<size_t>(f)]);
+			Lo.slot_gr.push_back(T.gr[2*static_cast<size_t>(f)+1]);
 		};
 		for(int f : inner) addSlot(f);
 		for(int f : cut) addSlot(f);
@@ -148,7 +152,7 @@ Layout buildLayout(const fvhip_mesh& m, const fvhip_flow_config& cfg, bool renum
 				Lo.cell_face_local[static_cast<size_t>(c)*MAXF+j] = face_slot[fs[j]];
 				Lo.cell_nbr_local[static_cast<size_t>(c)*MAXF+j] = toInt(esu(ref,j));
 			}
-			std::sort(fs, fs+k);
+			std::sort(fs, fs+k);     // local faces are in ascending global order
 			for(int j = 0; j < k; j++) {
 				Lo.cell_slots[static_cast<size_t>(c)*MAXF+j] = (face_slot[fs[j]] << 1) | (Lref(fs[j]) != ref ? 1 : 0);
 				const int other = Lref(fs[j]) != ref ? Lref(fs[j]) : Rref(fs[j]);
@@ -157,35 +161,46 @@ Layout buildLayout(const fvhip_mesh& m, const fvhip_flow_config& cfg, bool renum
 		}
 	}
 
-	// --- cell geometry (internal order) ---
-	Lo.rc.resize(2*static_cast<size_t>(N)); Lo.area.resize(N);
+	// --- cell geometry (internal order; ghosts after the owned cells) ---
+	Lo.rc.resize(2*static_cast<size_t>(NT)); Lo.area.resize(N);
 	for(int c = 0; c < N; c++) {
 		const int ref = Lo.perm[c];
-		Lo.rc[2*c] = m.rc[2*ref]; Lo.rc[2*c+1] = m.rc[2*ref+1]; Lo.area[c] = m.area[ref];
+		Lo.rc[2*c] = T.rc[2*ref]; Lo.rc[2*c+1] = T.rc[2*ref+1]; Lo.area[c] = T.area[ref];
 	}
+	for(int c = N; c < NT; c++) { Lo.rc[2*c] = T.rc[2*c]; Lo.rc[2*c+1] = T.rc[2*c+1]; }
+
+	// --- halo (internal ids) ---
+	Lo.nbr_rank = T.nbr_rank;
+	Lo.ghost_start = T.ghost_start;
+	Lo.send_start = T.send_start;
+	Lo.send_cells.resize(T.send_cells.size());
+	for(size_t i = 0; i < T.send_cells.size(); i++) Lo.send_cells[i] = Lo.iperm[T.send_cells[i]];
+	Lo.cell_global.resize(NT);
+	for(int c = 0; c < N; c++) Lo.cell_global[c] = T.cell_global[Lo.perm[c]];
+	for(int c = N; c < NT; c++) Lo.cell_global[c] = T.cell_global[c];
 
 	// --- boundary faces ---
 	Lo.bf_L.resize(nb); Lo.bf_bc.resize(nb); Lo.bf_n.resize(2*static_cast<size_t>(nb)); Lo.bf_rcbp.resize(2*static_cast<size_t>(nb));
 	for(int f = 0; f < nb; f++) {
 		Lo.bf_L[f] = Lo.iperm[Lref(f)];
-		const int tag = m.btags[static_cast<size_t>(f)*m.nbtag];
+		const int tag = T.btag[f];
 		int bi = -1;
 		for(int i = 0; i < cfg.nbc; i++) if(cfg.bc_tag[i] == tag) bi = i;
 		if(bi < 0) throw std::runtime_error("no boundary condition for marker " + std::to_string(tag)); // bcs.at()
 		Lo.bf_bc[f] = bi;
-		Lo.bf_n[2*f] = m.facemetric[3*static_cast<size_t>(f)]; Lo.bf_n[2*f+1] = m.facemetric[3*static_cast<size_t>(f)+1];
-		Lo.bf_rcbp[2*f] = m.rcbp[2*f]; Lo.bf_rcbp[2*f+1] = m.rcbp[2*f+1];
+		Lo.bf_n[2*f] = T.facemetric[3*static_cast<size_t>(f)]; Lo.bf_n[2*f+1] = T.facemetric[3*static_cast<size_t>(f)+1];
+		Lo.bf_rcbp[2*f] = T.rcbp[2*f]; Lo.bf_rcbp[2*f+1] = T.rcbp[2*f+1];
 	}
 	// --- interior faces (reference order) ---
 	Lo.if_L.resize(F-nb); Lo.if_R.resize(F-nb); Lo.if_slot.assign(F-nb, -1);
 	Lo.if_n.resize(2*static_cast<size_t>(F-nb)); Lo.if_len.resize(F-nb); Lo.bf_len.resize(nb);
 	for(int f = nb; f < F; f++) {
-		Lo.if_L[f-nb] = Lo.iperm[Lref(f)]; Lo.if_R[f-nb] = Lo.iperm[Rref(f)];
-		Lo.if_n[2*static_cast<size_t>(f-nb)] = m.facemetric[3*static_cast<size_t>(f)];
-		Lo.if_n[2*static_cast<size_t>(f-nb)+1] = m.facemetric[3*static_cast<size_t>(f)+1];
-		Lo.if_len[f-nb] = m.facemetric[3*static_cast<size_t>(f)+2];
+		Lo.if_L[f-nb] = toInt(Lref(f)); Lo.if_R[f-nb] = toInt(Rref(f));
+		Lo.if_n[2*static_cast<size_t>(f-nb)] = T.facemetric[3*static_cast<size_t>(f)];
+		Lo.if_n[2*static_cast<size_t>(f-nb)+1] = T.facemetric[3*static_cast<size_t>(f)+1];
+		Lo.if_len[f-nb] = T.facemetric[3*static_cast<size_t>(f)+2];
 	}
-	for(int f = 0; f < nb; f++) Lo.bf_len[f] = m.facemetric[3*static_cast<size_t>(f)+2];
+	for(int f = 0; f < nb; f++) Lo.bf_len[f] = T.facemetric[3*static_cast<size_t>(f)+2];
 	for(size_t s = 0; s < Lo.slot_face.size(); s++)
 		if(Lo.slot_face[s] >= nb) Lo.if_slot[Lo.slot_face[s]-nb] = static_cast<int>(s);
 	// each cell's faces as reference face codes, same order as cell_slots
@@ -197,8 +212,8 @@ Layout buildLayout(const fvhip_mesh& m, const fvhip_flow_config& cfg, bool renum
 
 	// --- WLS normal matrices (agradientschemes.cpp:218-317), reference face order ---
 	if(cfg.gradientscheme == FVHIP_GRAD_LEASTSQUARES) {
-		std::vector<double> V(4*static_cast<size_t>(N), 0.0);
-		const double* rc = m.rc; const double* rcbp = m.rcbp;
+		std::vector<double> V(4*static_cast<size_t>(NT), 0.0);
+		const double* rc = T.rc.data(); const double* rcbp = T.rcbp.data();
 		for(int f = 0; f < nb; f++) {
 			const int ie = Lref(f);
 			double w2 = 0, dr[2];
@@ -234,19 +249,7 @@ Layout buildLayout(const fvhip_mesh& m, const fvhip_flow_config& cfg, bool renum
 	// --- Venkatakrishnan eps^2 ---
 	if(cfg.reconstruction == FVHIP_REC_VENKATAKRISHNAN) {
 		Lo.venk_eps2.resize(N);
-		for(int c = 0; c < N; c++) {
-			const int ref = Lo.perm[c];
-			double cl = 0;
-			for(int ifa = 0; ifa < m.nnode[ref]; ifa++) {
-				const int a = m.inpoel[static_cast<size_t>(ref)*m.maxnnode+ifa];
-				const int b = m.inpoel[static_cast<size_t>(ref)*m.maxnnode+(ifa+1)%m.nnode[ref]];
-				double llen = 0;
-				for(int d = 0; d < 2; d++) llen += std::pow(m.coords[2*a+d] - m.coords[2*b+d], 2);
-				if(cl < llen) cl = llen;
-			}
-			cl = std::sqrt(cl);
-			Lo.venk_eps2[c] = std::pow(cfg.limiter_param*cl, 3);
-		}
+		for(int c = 0; c < N; c++) Lo.venk_eps2[c] = std::pow(cfg.limiter_param*T.clength[Lo.perm[c]], 3);
 	}
 	return Lo;
 }

@@ -25,6 +25,7 @@ constexpr int MAXF = 4;          ///< max faces per cell (linear tri/quad)
 struct Layout
 {
 	int ncell = 0;               ///< owned cells
+	int nghost = 0;              ///< ghost cells (internal ids ncell .. ncell+nghost-1)
 	int nbface = 0, naface = 0, ninface = 0;
 	std::vector<int> perm;       ///< perm[internal] = reference cell
 	std::vector<int> iperm;      ///< iperm[reference] = internal
@@ -47,7 +48,7 @@ struct Layout
 	std::vector<int> cell_nbr_fo;          ///< [ncell][4]: neighbour across each face in ascending
 	                                       ///<  reference face index (internal / ncell+bf), -1 pad
 	std::vector<int> cell_nfael;
-	std::vector<double> rc;                ///< [ncell][2]
+	std::vector<double> rc;                ///< [ncell+nghost][2]
 	std::vector<double> area;              ///< [ncell]
 	std::vector<double> wls_V;             ///< [ncell][4] WLS inverse, row-major (if built)
 	std::vector<double> venk_eps2;         ///< [ncell] (K*clength)^3 (if built)
@@ -64,11 +65,19 @@ struct Layout
 	std::vector<int> cell_rfaces;          ///< [ncell][4]: (reference face << 1 | cell-is-right),
 	                                       ///<  same order as cell_slots
 	int max_slots = 0;
+	// halo (partitioned meshes): ghosts from nbr_rank[k] are internal cells
+	// ncell+ghost_start[k] .. ncell+ghost_start[k+1]-1; send_cells[send_start[k]..] go to nbr_rank[k]
+	std::vector<int> nbr_rank, ghost_start, send_start, send_cells;
+	std::vector<int> cell_global;          ///< [ncell+nghost] global cell of each internal cell
 };
 
 /// Builds the layout from the reference's mesh arrays. bc_of_tag maps a boundary marker to the
 /// index of its BC in the config. Throws std::runtime_error on unsupported meshes.
 Layout buildLayout(const fvhip_mesh& m, const fvhip_flow_config& cfg, bool renumber);
+struct MeshTopo;
+/// Same from a (possibly partitioned) topology: owned cells are renumbered and patched, ghost
+/// cells keep internal ids after them and are only read (partition.hpp)
+Layout buildLayout(const MeshTopo& T, const fvhip_flow_config& cfg, bool renumber);
 
 }
 #endif

@@ -1,0 +1,196 @@
+/** \file partition.cpp
+ * \brief RCB partitioning and per-rank local topologies (see partition.hpp).
+ */
+#include "partition.hpp"
+#include <algorithm>
+#include <cmath>
+#include <numeric>
+#include <stdexcept>
+
+namespace fvhip {
+
+namespace {
+
+/// longest edge of a cell (limitedlinearreconstruction.cpp:186-205)
+double cellLength(const fvhip_mesh& m, int ref)
+{
+	double cl = 0;
+	for(int ifa = 0; ifa < m.nnode[ref]; ifa++) {
+		const int a = m.inpoel[static_cast<size_t>(ref)*m.maxnnode+ifa];
+		const int b = m.inpoel[static_cast<size_t>(ref)*m.maxnnode+(ifa+1)%m.nnode[ref]];
+		double llen = 0;
+		for(int d = 0; d < 2; d++) llen += std::pow(m.coords[2*a+d] - m.coords[2*b+d], 2);
+		if(cl < llen) cl = llen;
+	}
+	return std::sqrt(cl);
+}
+
+void rcbRecurse(const double* rc, int* idx, int n, int p0, int np, int* part)
+{
+	if(np == 1) { for(int i = 0; i < n; i++) part[idx[i]] = p0; return; }
+	double lo[2] = {INFINITY, INFINITY}, hi[2] = {-INFINITY, -INFINITY};
+	for(int i = 0; i < n; i++)
+		for(int d = 0; d < 2; d++) {
+			lo[d] = std::min(lo[d], rc[2*idx[i]+d]);
+			hi[d] = std::max(hi[d], rc[2*idx[i]+d]);
+		}
+	const int ax = (hi[1]-lo[1] > hi[0]-lo[0]) ? 1 : 0;
+	const int npl = np/2;
+	const int nl = static_cast<int>((static_cast<long long>(n)*npl)/np);
+	std::nth_element(idx, idx + nl, idx + n, [&](int a, int b) {
+		return rc[2*a+ax] < rc[2*b+ax] || (rc[2*a+ax] == rc[2*b+ax] && a < b); });
+	rcbRecurse(rc, idx, nl, p0, npl, part);
+	rcbRecurse(rc, idx + nl, n - nl, p0 + npl, np - npl, part);
+}
+
+}
+
+std::vector<int> partitionRCB(const double* rc, int ncell, int nparts)
+{
+	if(nparts < 1) throw std::invalid_argument("partitionRCB: nparts < 1");
+	std::vector<int> part(ncell, 0), idx(ncell);
+	std::iota(idx.begin(), idx.end(), 0);
+	if(ncell > 0) rcbRecurse(rc, idx.data(), ncell, 0, nparts, part.data());
+	return part;
+}
+
+MeshTopo topoFromMesh(const fvhip_mesh& m)
+{
+	if(m.nconnface != 0)
+		throw std::runtime_error("mesh with connectivity faces: pass the global mesh and a partition instead");
+	if(m.maxnfael > 4) throw std::runtime_error("cells with more than 4 faces are not supported");
+	MeshTopo T;
+	const int N = m.nelem, nb = m.nbface, F = m.naface;
+	T.nown = N; T.nghost = 0; T.nbface = nb; T.naface = F;
+	T.cell_global.resize(N); std::iota(T.cell_global.begin(), T.cell_global.end(), 0);
+	T.nfael.resize(N);
+	T.cell_faces.assign(4*static_cast<size_t>(N), -1);
+	T.cell_esuel.assign(4*static_cast<size_t>(N), -1);
+	T.clength.resize(N);
+	for(int e = 0; e < N; e++) {
+		T.nfael[e] = m.nnode[e];
+		for(int j = 0; j < m.nnode[e]; j++) {
+			T.cell_faces[4*static_cast<size_t>(e)+j] = m.elemface[static_cast<size_t>(e)*m.maxnfael+j];
+			T.cell_esuel[4*static_cast<size_t>(e)+j] = m.esuel[static_cast<size_t>(e)*m.maxnfael+j];
+		}
+		T.clength[e] = cellLength(m, e);
+	}
+	T.rc.assign(m.rc, m.rc + 2*static_cast<size_t>(N));
+	T.area.assign(m.area, m.area + N);
+	T.face_global.resize(F); std::iota(T.face_global.begin(), T.face_global.end(), 0);
+	T.L.resize(F); T.R.resize(F);
+	for(int f = 0; f < F; f++) { T.L[f] = m.intfac[4*static_cast<size_t>(f)]; T.R[f] = m.intfac[4*static_cast<size_t>(f)+1]; }
+	T.facemetric.assign(m.facemetric, m.facemetric + 3*static_cast<size_t>(F));
+	T.gr.assign(m.gr, m.gr + 2*static_cast<size_t>(F));
+	T.btag.resize(nb);
+	for(int f = 0; f < nb; f++) T.btag[f] = m.btags[static_cast<size_t>(f)*m.nbtag];
+	T.rcbp.assign(m.rcbp, m.rcbp + 2*static_cast<size_t>(nb));
+	T.ghost_start.assign(1, 0);
+	T.send_start.assign(1, 0);
+	return T;
+}
+
+MeshTopo extractPartition(const fvhip_mesh& m, const int* part, int rank)
+{
+	if(m.nconnface != 0) throw std::runtime_error("extractPartition: expects the single-domain mesh");
+	if(m.maxnfael > 4) throw std::runtime_error("cells with more than 4 faces are not supported");
+	const int N = m.nelem, nb = m.nbface, F = m.naface;
+	auto Lg = [&](int f) { return m.intfac[4*static_cast<size_t>(f)]; };
+	auto Rg = [&](int f) { return m.intfac[4*static_cast<size_t>(f)+1]; };
+	MeshTopo T;
+	std::vector<int> loc(N, -1);
+	for(int e = 0; e < N; e++) if(part[e] == rank) { loc[e] = T.nown++; T.cell_global.push_back(e); }
+	if(T.nown == 0) throw std::runtime_error("extractPartition: rank owns no cells");
+
+	// faces touching owned cells, ascending global index; ghosts across interior faces
+	std::vector<int> ghosts;
+	for(int f = 0; f < F; f++) {
+		const int l = Lg(f), r = Rg(f);
+		const bool lo = part[l] == rank;
+		if(f < nb) { if(lo) { T.face_global.push_back(f); T.nbface++; } continue; }
+		const bool ro = part[r] == rank;
+		if(!lo && !ro) continue;
+		T.face_global.push_back(f);
+		if(!lo) ghosts.push_back(l);
+		if(!ro) ghosts.push_back(r);
+	}
+	T.naface = static_cast<int>(T.face_global.size());
+	std::sort(ghosts.begin(), ghosts.end(), [&](int a, int b) { return part[a] < part[b] || (part[a] == part[b] && a < b); });
+	ghosts.erase(std::unique(ghosts.begin(), ghosts.end()), ghosts.end());
+	T.nghost = static_cast<int>(ghosts.size());
+	T.ghost_start.push_back(0);
+	for(int i = 0; i < T.nghost; i++) {
+		const int g = ghosts[i];
+		loc[g] = T.nown + i;
+		T.cell_global.push_back(g);
+		if(T.nbr_rank.empty() || T.nbr_rank.back() != part[g]) {
+			if(!T.nbr_rank.empty()) T.ghost_start.push_back(i);
+			T.nbr_rank.push_back(part[g]);
+		}
+	}
+	if(!T.nbr_rank.empty()) T.ghost_start.push_back(T.nghost);
+	const int NT = T.ncell();
+
+	// faces
+	std::vector<int> floc(F, -1);
+	T.L.resize(T.naface); T.R.resize(T.naface);
+	T.facemetric.resize(3*static_cast<size_t>(T.naface)); T.gr.resize(2*static_cast<size_t>(T.naface));
+	for(int i = 0; i < T.naface; i++) {
+		const int f = T.face_global[i];
+		floc[f] = i;
+		T.L[i] = loc[Lg(f)];
+		T.R[i] = f < nb ? NT + i : loc[Rg(f)];
+		for(int k = 0; k < 3; k++) T.facemetric[3*static_cast<size_t>(i)+k] = m.facemetric[3*static_cast<size_t>(f)+k];
+		for(int k = 0; k < 2; k++) T.gr[2*static_cast<size_t>(i)+k] = m.gr[2*static_cast<size_t>(f)+k];
+	}
+	T.btag.resize(T.nbface); T.rcbp.resize(2*static_cast<size_t>(T.nbface));
+	for(int i = 0; i < T.nbface; i++) {
+		const int f = T.face_global[i];
+		T.btag[i] = m.btags[static_cast<size_t>(f)*m.nbtag];
+		T.rcbp[2*i] = m.rcbp[2*f]; T.rcbp[2*i+1] = m.rcbp[2*f+1];
+	}
+
+	// cells
+	T.nfael.resize(T.nown);
+	T.cell_faces.assign(4*static_cast<size_t>(T.nown), -1);
+	T.cell_esuel.assign(4*static_cast<size_t>(T.nown), -1);
+	T.area.resize(T.nown); T.clength.resize(T.nown);
+	T.rc.resize(2*static_cast<size_t>(NT));
+	for(int c = 0; c < NT; c++) {
+		const int e = T.cell_global[c];
+		T.rc[2*c] = m.rc[2*e]; T.rc[2*c+1] = m.rc[2*e+1];
+	}
+	for(int c = 0; c < T.nown; c++) {
+		const int e = T.cell_global[c];
+		T.area[c] = m.area[e];
+		T.clength[c] = cellLength(m, e);
+		T.nfael[c] = m.nnode[e];
+		for(int j = 0; j < m.nnode[e]; j++) {
+			const int f = m.elemface[static_cast<size_t>(e)*m.maxnfael+j];
+			T.cell_faces[4*static_cast<size_t>(c)+j] = floc[f];
+			const int nbr = m.esuel[static_cast<size_t>(e)*m.maxnfael+j];
+			T.cell_esuel[4*static_cast<size_t>(c)+j] = nbr >= N ? NT + floc[f] : loc[nbr];
+		}
+	}
+
+	// send lists: owned cells adjacent to a cell of each neighbour rank, ascending global id
+	T.send_start.push_back(0);
+	for(size_t k = 0; k < T.nbr_rank.size(); k++) {
+		const int q = T.nbr_rank[k];
+		std::vector<int> s;
+		for(int i = 0; i < T.naface; i++) {
+			const int f = T.face_global[i];
+			if(f < nb) continue;
+			const int l = Lg(f), r = Rg(f);
+			if(part[l] == rank && part[r] == q) s.push_back(l);
+			if(part[r] == rank && part[l] == q) s.push_back(r);
+		}
+		std::sort(s.begin(), s.end());
+		s.erase(std::unique(s.begin(), s.end()), s.end());
+		for(int g : s) T.send_cells.push_back(loc[g]);
+		T.send_start.push_back(static_cast<int>(T.send_cells.size()));
+	}
+	return T;
+}
+
+}

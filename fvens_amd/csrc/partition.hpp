@@ -1,0 +1,61 @@
+/** \file partition.hpp
+ * \brief Cell partitioning and per-rank local meshes with one ghost-cell layer.
+ *
+ * Replaces, for the hot path, the reference's partitioned-mesh construction
+ * (mesh/meshpartitioning.cpp:24-159, Scotch graph partition :376-458) with:
+ *  - recursive coordinate bisection of cell centres (Scotch is not available in this image; the
+ *    reference's own default is a trivial block partition, ameshutils.cpp:122-123);
+ *  - a local topology per rank: owned cells, one layer of ghost cells (grouped by owner rank,
+ *    ascending global id), and every global face touching an owned cell in ascending GLOBAL face
+ *    index with its GLOBAL orientation. Unlike the reference's connectivity faces (local outward
+ *    normal, faces appended last), this makes each owned cell's residual the same sequence of
+ *    floating-point operations as on one GPU, so the N-GPU residual is bitwise the 1-GPU one.
+ */
+#ifndef FVHIP_PARTITION_HPP
+#define FVHIP_PARTITION_HPP
+
+#include <vector>
+#include "../../include/fvhip.h"
+
+namespace fvhip {
+
+/// Mesh topology in the form the layout builder consumes. Cells [0,nown) are owned, [nown,ncell)
+/// ghosts; a face's R >= ncell denotes physical boundary face R - ncell. Faces are sorted by global
+/// index, physical boundary faces first.
+struct MeshTopo
+{
+	int nown = 0, nghost = 0, nbface = 0, naface = 0;
+	int ncell() const { return nown + nghost; }
+	std::vector<int> cell_global;      ///< [ncell]
+	std::vector<int> nfael;            ///< [nown]
+	std::vector<int> cell_faces;       ///< [nown][4] local faces in the cell's own (elemface) order
+	std::vector<int> cell_esuel;       ///< [nown][4] neighbour across each: local cell or ncell+bface
+	std::vector<double> rc;            ///< [ncell][2]
+	std::vector<double> area;          ///< [nown]
+	std::vector<double> clength;       ///< [nown] longest edge (Venkatakrishnan), as the reference computes it
+	std::vector<int> face_global;      ///< [naface]
+	std::vector<int> L, R;             ///< [naface]
+	std::vector<double> facemetric;    ///< [naface][3]
+	std::vector<double> gr;            ///< [naface][2]
+	std::vector<int> btag;             ///< [nbface]
+	std::vector<double> rcbp;          ///< [nbface][2]
+	// halo
+	std::vector<int> nbr_rank;         ///< neighbour ranks, ascending
+	std::vector<int> ghost_start;      ///< [nnbr+1] ghosts owned by nbr_rank[k] are local cells
+	                                   ///<  nown+ghost_start[k] .. nown+ghost_start[k+1]-1
+	std::vector<int> send_start;       ///< [nnbr+1] ranges into send_cells
+	std::vector<int> send_cells;       ///< local owned cells each neighbour holds as ghosts (ascending global id)
+};
+
+/// Whole mesh as one rank (no ghosts)
+MeshTopo topoFromMesh(const fvhip_mesh& m);
+
+/// Rank `rank`'s piece of a single-domain mesh partitioned by `part` (part[cell] in [0,nparts))
+MeshTopo extractPartition(const fvhip_mesh& m, const int* part, int rank);
+
+/// Recursive coordinate bisection of cell centres into nparts parts with sizes differing by at
+/// most one cell per bisection level; deterministic (ties broken by cell index)
+std::vector<int> partitionRCB(const double* rc, int ncell, int nparts);
+
+}
+#endif

@@ -109,6 +109,35 @@ int fvhip_device_count(void);
 int fvhip_create(const fvhip_mesh* mesh, const fvhip_flow_config* cfg, int device, fvhip_handle* out);
 int fvhip_destroy(fvhip_handle h);
 
+/* ---------------------------------------------------------------------------------------------
+ * Multi-GPU (one rank per GPU). Replaces the reference's partitioned mesh (meshpartitioning.cpp:
+ * 24-159, Scotch :376-458) and ghost scatters (alinalg.cpp:17-29, tracevector.cpp:213-340).
+ * Every rank passes the single-domain mesh and the same partition vector; the handle holds the
+ * rank's owned cells plus one ghost layer, faces in global order with global orientation, so the
+ * residual of every owned cell is bitwise the single-GPU one. Ghost rows of u, gradients and
+ * limiter data are exchanged with RCCL ncclSend/ncclRecv on the handle's stream.
+ * -------------------------------------------------------------------------------------------- */
+typedef struct fvhip_group_s* fvhip_group;
+/** Recursive coordinate bisection of the cell centres into nparts (part [nelem]) */
+int fvhip_partition_rcb(const fvhip_mesh* mesh, int nparts, int* part);
+/** Halo description of one rank (host only). counts[6] = {owned, ghosts, boundary faces, faces,
+ *  neighbour ranks, send rows}; arrays may be NULL: cell_global [owned+ghosts] (owned ascending,
+ *  then ghosts by owner rank), nbr_rank [nnbr], ghost_start/send_start [nnbr+1], send_global [nsend] */
+int fvhip_partition_info(const fvhip_mesh* mesh, const int* part, int rank, int* counts, int* cell_global,
+                         int* nbr_rank, int* ghost_start, int* send_start, int* send_global);
+/** The rank's handle; host u/r/dtm then hold the owned cells in ascending global order, device
+ *  u has owned+ghost rows (fvhip_layout_stats[6] = ghosts) and the ghost rows are filled by it */
+int fvhip_create_partitioned(const fvhip_mesh* mesh, const fvhip_flow_config* cfg, const int* part, int nparts,
+                             int rank, int device, fvhip_handle* out);
+/** RCCL communicator of the partition: rank 0 creates the 128-byte id, all ranks pass it */
+int fvhip_comm_unique_id(void* id128);
+int fvhip_comm_init(fvhip_handle h, int nranks, int rank, const void* id128);
+/** All ranks of a partition in ONE process (e.g. on one device): exchange by device copies */
+int fvhip_group_create(fvhip_handle* handles, int n, fvhip_group* out);
+int fvhip_group_destroy(fvhip_group g);
+int fvhip_group_compute_residual_device(fvhip_group g, const double* const* d_u, double* const* d_r,
+                                        int gettimesteps, double* const* d_dtm, int flags);
+
 /** FlowFV::compute_residual on host arrays (copies through PCIe) */
 int fvhip_compute_residual(fvhip_handle h, const double* u, double* r, int gettimesteps, double* dtm);
 /** Device-resident sweep; u/r/dtm in internal order. flags: FVHIP_RES_OVERWRITE = r is known
@@ -167,7 +196,8 @@ int fvhip_profile(fvhip_handle h, int enable);
 int fvhip_kernel_times(fvhip_handle h, int maxk, char* names, int namelen, double* ms, int* counts);
 
 /** Layout statistics: [0]=cells [1]=faces [2]=face slots incl. duplicated cut faces
- *  [3]=patches [4]=max slots per patch [5]=boundary faces */
+ *  [3]=patches [4]=max slots per patch [5]=boundary faces [6]=ghost cells [7]=neighbour ranks
+ *  [8]=rows sent per exchange */
 int fvhip_layout_stats(fvhip_handle h, long long* stats);
 
 /** Point-wise numerical flux on the device (get_flux) for nf faces: ul, ur [nf][4], n [nf][2] */

@@ -1,0 +1,88 @@
+"""Multi-GPU path on one device: all ranks of a partition held by one process (FlowFVGroup, the
+halo exchanged by device copies instead of RCCL). Bar: every rank's owned-cell residual and time
+step are BITWISE equal to the single-GPU residual of the whole mesh (faces keep global order and
+orientation on every rank), with ghost rows starting as NaN so a missed exchange cannot pass."""
+import numpy as np
+import pytest
+
+import fvens_amd as fa
+import cases
+from test_gpu_residual import get_mesh
+
+pytestmark = pytest.mark.gpu
+
+CONFIGS = [("naca_small", "naca", "ROE", "LEASTSQUARES", "VANALBADA", True),
+           ("naca_small", "naca", "LLF", "NONE", "NONE", False),
+           ("2dcylinderhybrid.msh", "cyl", "HLLC", "GREENGAUSS", "VENKATAKRISHNAN", True),
+           ("naca_small", "naca", "ROE", "LEASTSQUARES", "BARTHJESPERSEN", True),
+           ("naca_small", "naca", "AUSM", "GREENGAUSS", "WENO", True),
+           ("naca_small", "viscconst", "ROE", "LEASTSQUARES", "VANALBADA", True),
+           ("plate_small", "plate", "HLLC", "LEASTSQUARES", "NONE", True),
+           ("naca_c2", "naca", "ROE", "LEASTSQUARES", "VANALBADA", True)]
+
+
+def run_partitioned(meshkey, kind, flux, grad, rec, order2, nparts, fast=False):
+    import torch
+    m, _ = get_mesh(meshkey)
+    p = cases.physics(kind)
+    n = cases.numerics(flux, grad, rec, order2=order2)
+    n.fast_math = fast
+    u = cases.state(m, p, seed=3)
+    # single GPU reference
+    one = fa.FlowFV(m, p, n)
+    r1 = np.zeros((m.nelem, 4))
+    dt1 = np.zeros(m.nelem)
+    one.compute_residual(u, r1, True, dt1)
+    one.close()
+    part = fa.partition_rcb(m, nparts)
+    sps = [fa.FlowFV(m, p, n, partition=part, rank=k) for k in range(nparts)]
+    glob = []
+    dus, drs, dts = [], [], []
+    for k, sp in enumerate(sps):
+        owned = np.nonzero(part == k)[0]                 # local reference order = ascending global id
+        g_int = owned[sp.permutation()]                  # global id of each internal owned row
+        glob.append(g_int)
+        du = torch.full((sp.nown + sp.nghost, 4), float("nan"), dtype=torch.float64, device="cuda")
+        du[:sp.nown] = torch.tensor(u[g_int], device="cuda")
+        dus.append(du)
+        drs.append(torch.full((sp.nown, 4), float("nan"), dtype=torch.float64, device="cuda"))
+        dts.append(torch.full((sp.nown,), float("nan"), dtype=torch.float64, device="cuda"))
+    grp = fa.FlowFVGroup(sps)
+    grp.compute_residual_device([d.data_ptr() for d in dus], [d.data_ptr() for d in drs],
+                                [d.data_ptr() for d in dts], True, True)
+    torch.cuda.synchronize()
+    r = np.full((m.nelem, 4), np.nan)
+    dt = np.full(m.nelem, np.nan)
+    for k in range(nparts):
+        r[glob[k]] = drs[k].cpu().numpy()
+        dt[glob[k]] = dts[k].cpu().numpy()
+    stats = [sp.layout_stats() for sp in sps]
+    grp.close()
+    for sp in sps:
+        sp.close()
+    return r, dt, r1, dt1, stats
+
+
+@pytest.mark.parametrize("nparts", [2, 3, 8])
+@pytest.mark.parametrize("cfg", CONFIGS[:7], ids=lambda c: f"{c[0]}-{c[2]}-{c[3]}-{c[4]}")
+def test_partitioned_residual_bitwise(cfg, nparts):
+    r, dt, r1, dt1, stats = run_partitioned(*cfg, nparts)
+    assert sum(s["ghosts"] for s in stats) > 0
+    if cfg[1] in ("plate",) or cfg[4] == "WENO":
+        # pow() paths: the same device code on both sides, so still bitwise
+        pass
+    np.testing.assert_array_equal(r, r1)
+    np.testing.assert_array_equal(dt, dt1)
+
+
+def test_partitioned_c2_eight_ranks():
+    r, dt, r1, dt1, stats = run_partitioned(*CONFIGS[7], 8)
+    np.testing.assert_array_equal(r, r1)
+    np.testing.assert_array_equal(dt, dt1)
+
+
+def test_partitioned_fast_math_bitwise_to_fast_single():
+    # the fast kernels are also deterministic: partitioned == single GPU in fast mode too
+    r, dt, r1, dt1, _ = run_partitioned(*CONFIGS[0], 4, fast=True)
+    np.testing.assert_array_equal(r, r1)
+    np.testing.assert_array_equal(dt, dt1)

@@ -1,0 +1,104 @@
+"""Host-side multi-GPU plumbing (no GPU): RCB partition, per-rank halo description, and the halo
+exchange protocol run over a real collective transport (torch.distributed gloo, world size 2),
+mirroring what the library does with RCCL ncclSend/ncclRecv between GPUs."""
+import os
+
+import numpy as np
+import pytest
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+import fvens_amd as fa
+import cases
+
+
+def small_mesh():
+    return fa.UMesh.naca_ogrid(96, 6, 18)
+
+
+@pytest.mark.parametrize("nparts", [2, 3, 4, 8])
+def test_rcb_balanced_and_complete(nparts):
+    m = small_mesh()
+    part = fa.partition_rcb(m, nparts)
+    counts = np.bincount(part, minlength=nparts)
+    assert counts.min() > 0 and len(counts) == nparts
+    assert counts.max() - counts.min() <= nparts      # one cell per bisection level at most
+    # deterministic
+    np.testing.assert_array_equal(part, fa.partition_rcb(m, nparts))
+
+
+@pytest.mark.parametrize("nparts", [2, 3, 5, 8])
+def test_halo_lists_consistent(nparts):
+    m = small_mesh()
+    part = fa.partition_rcb(m, nparts)
+    L, R = m.intfac[:, 0], m.intfac[:, 1]
+    nb = m.nbface
+    infos = [fa.partition_info(m, part, r) for r in range(nparts)]
+    owned_all = np.concatenate([inf["cell_global"][:inf["owned"]] for inf in infos])
+    assert np.array_equal(np.sort(owned_all), np.arange(m.nelem))
+    faces_total = 0
+    for r, inf in enumerate(infos):
+        own = inf["cell_global"][:inf["owned"]]
+        assert np.all(part[own] == r) and np.all(np.diff(own) > 0)
+        ghosts = inf["cell_global"][inf["owned"]:]
+        # ghosts are exactly the off-rank cells across interior faces of owned cells
+        Li, Ri = L[nb:], R[nb:]
+        exp = set(Ri[(part[Li] == r) & (part[Ri] != r)]) | set(Li[(part[Ri] == r) & (part[Li] != r)])
+        assert set(ghosts.tolist()) == exp and len(ghosts) == len(exp)
+        # every face touching an owned cell, boundary faces = those of owned cells
+        touching = np.count_nonzero((part[Li] == r) | (part[Ri] == r))
+        bnd = np.count_nonzero(part[L[:nb]] == r)
+        assert inf["bfaces"] == bnd and inf["faces"] == bnd + touching
+        faces_total += inf["faces"]
+        # symmetric send/receive lists
+        for k, q in enumerate(inf["nbr_rank"]):
+            mine = ghosts[inf["ghost_start"][k]:inf["ghost_start"][k + 1]]
+            other = infos[q]
+            kk = list(other["nbr_rank"]).index(r)
+            sent = other["send_global"][other["send_start"][kk]:other["send_start"][kk + 1]]
+            np.testing.assert_array_equal(mine, sent)
+    cut = np.count_nonzero(part[L[nb:]] != part[R[nb:]])
+    assert faces_total == m.naface + cut
+
+
+def _exchange_worker(rank, world, port, nparts_check):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    import torch
+    m = small_mesh()
+    part = fa.partition_rcb(m, world)
+    inf = fa.partition_info(m, part, rank)
+    p = cases.physics("naca")
+    ug = cases.state(m, p, seed=11)                      # the global state every rank agrees on
+    cg = inf["cell_global"]
+    nown = inf["owned"]
+    u = np.full((len(cg), 4), np.nan)
+    u[:nown] = ug[cg[:nown]]                             # each rank knows only its owned rows
+    # the library's protocol: pack send rows per neighbour, point-to-point, receive into the
+    # contiguous ghost block of that neighbour
+    row = {g: i for i, g in enumerate(cg)}
+    reqs, recvbufs = [], []
+    for k, q in enumerate(inf["nbr_rank"]):
+        send = np.stack([u[row[g]] for g in inf["send_global"][inf["send_start"][k]:inf["send_start"][k + 1]]])
+        reqs.append(dist.isend(torch.from_numpy(np.ascontiguousarray(send)), int(q)))
+        n = inf["ghost_start"][k + 1] - inf["ghost_start"][k]
+        buf = torch.empty((n, 4), dtype=torch.float64)
+        reqs.append(dist.irecv(buf, int(q)))
+        recvbufs.append((k, buf))
+    for rq in reqs:
+        rq.wait()
+    for k, buf in recvbufs:
+        a = nown + inf["ghost_start"][k]
+        u[a:a + buf.shape[0]] = buf.numpy()
+    ok = np.array_equal(u, ug[cg])
+    t = torch.tensor([1 if ok else 0])
+    dist.all_reduce(t, op=dist.ReduceOp.MIN)
+    dist.destroy_process_group()
+    if int(t.item()) != 1:
+        raise SystemExit(3)
+
+
+def test_halo_exchange_gloo_two_ranks():
+    port = 29500 + (os.getpid() % 500)
+    mp.spawn(_exchange_worker, args=(2, port, 2), nprocs=2, join=True)
