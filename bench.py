@@ -7,8 +7,11 @@ Ntheta = 2048, 256 quad + 864 triangle-split layers = 4,063,232 cells, 6,359,040
 Roe flux + weighted-least-squares gradients + MUSCL/Van Albada reconstruction, M 0.8, 1.25 deg.
 One step = one full residual evaluation (primitive conversion, BC ghosts, WLS gradients, fused
 reconstruction/flux/scatter/time-step sweep) with the state resident in HBM.
-Multi-GPU: one process per GPU; each rank sweeps its own C4-size mesh (weak scaling, no data-path
-collective yet: the partitioned halo-exchange path is not built in this round — DESIGN.md).
+Multi-GPU (torchrun, one process per GPU): the mesh is partitioned by recursive coordinate bisection,
+each rank holds its cells plus one ghost layer, and the ghost rows of u and of the gradients are
+exchanged every residual with RCCL ncclSend/ncclRecv over xGMI (the library's own communicator).
+--scaling weak (default): the O-grid has N x 2048 cells around, so every GPU owns a C4-size part;
+--scaling strong: the C4 mesh itself is split N ways (BASELINE.json config 4).
 """
 import argparse
 import json
@@ -25,8 +28,8 @@ sys.path.insert(0, os.path.join(ROOT, "tests"))
 HBM_PEAK_GBS = 8000.0   # MI355X HBM3E spec (MI355X_MICROARCH.md)
 
 
-def c4_mesh(fa, scale):
-    nt = 2048 // scale
+def c4_mesh(fa, scale, mult=1):
+    nt = 2048 * mult // scale
     nq = 256 // scale
     ntri = 864 // scale
     return fa.UMesh.naca_ogrid(nt, nq, ntri, 20.0, 1e-5), dict(ntheta=nt, nquad=nq, ntri=ntri)
@@ -67,6 +70,7 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-sweeps", type=int, default=3)
     ap.add_argument("--no-fast", action="store_true", help="skip the fast-math mode measurement")
+    ap.add_argument("--scaling", choices=["weak", "strong"], default="weak")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -85,11 +89,18 @@ def main():
     import cases
 
     t0 = time.time()
-    mesh, dims = c4_mesh(fa, args.scale)
+    mult = world if (world > 1 and args.scaling == "weak") else 1
+    mesh, dims = c4_mesh(fa, args.scale, mult)
     p = cases.physics("naca")
     n = cases.numerics("ROE", "LEASTSQUARES", "VANALBADA")
     u = cases.state(mesh, p, seed=42)
     N, F, Fb = mesh.nelem, mesh.naface, mesh.nbface
+    part, uid = None, None
+    if world > 1:
+        part = fa.partition_rcb(mesh, world)
+        obj = [fa.comm_unique_id() if rank == 0 else None]
+        dist.broadcast_object_list(obj, src=0)
+        uid = obj[0]
 
     def barrier(sp):
         if dist is not None:
@@ -100,11 +111,18 @@ def main():
     def measure(fast):
         """ms per step (timed region bracketed by barrier + sync, max over ranks) and per-kernel ms"""
         n.fast_math = fast
-        sp = fa.FlowFV(mesh, p, n, device=torch.cuda.current_device())
-        perm = sp.permutation()
-        du = torch.tensor(u[perm], device="cuda")
-        dr = torch.empty((N, 4), dtype=torch.float64, device="cuda")
-        ddt = torch.empty(N, dtype=torch.float64, device="cuda")
+        if world > 1:
+            sp = fa.FlowFV(mesh, p, n, device=torch.cuda.current_device(), partition=part, rank=rank)
+            sp.comm_init(world, rank, uid)
+            owned = np.nonzero(part == rank)[0]
+        else:
+            sp = fa.FlowFV(mesh, p, n, device=torch.cuda.current_device())
+            owned = np.arange(N)
+        gint = owned[sp.permutation()]
+        du = torch.zeros((sp.nown + sp.nghost, 4), dtype=torch.float64, device="cuda")
+        du[:sp.nown] = torch.tensor(u[gint], device="cuda")
+        dr = torch.empty((sp.nown, 4), dtype=torch.float64, device="cuda")
+        ddt = torch.empty(sp.nown, dtype=torch.float64, device="cuda")
         torch.cuda.synchronize()
 
         def step():
@@ -131,18 +149,22 @@ def main():
         kt = sp.kernel_times()
         sp.profile(False)
         stats = sp.layout_stats()
+        if dist is not None:
+            dist.barrier()
         sp.close()
         return 1e3 * elapsed / args.steps, {k: v[0] / v[1] for k, v in kt.items()}, stats
 
     t_setup = time.time() - t0
     ms_per_step, kernels_ms, stats = measure(False)
+    # this rank's algorithmic bytes (its owned cells, its faces incl. both copies of cut faces)
+    local_bytes = sweep_algorithmic_bytes(stats["cells"], stats["faces"], stats["bfaces"])
     fast = None
     if not args.no_fast:
         fms, fk, _ = measure(True)
         fsweep = [k for k in fk if k.startswith("k_sweep")]
         fsms = fk[fsweep[0]] if fsweep else float("nan")
         fab = sweep_algorithmic_bytes(N, F, Fb) / (fsms * 1e-3) / 1e9
-        ftr = pmc_traffic("fast::k_sweep<4, 1, 0, true, false>", N)
+        ftr = pmc_traffic("fast::k_sweep<4, 1, 0, true, false>", N) if world == 1 else None
         fast = {"value": round(world * F / (fms * 1e-3) / 1e6, 3), "ms_per_step": round(fms, 5),
                 "traffic": int(ftr[0]) if ftr else None,
                 "kernels_ms": {k: round(v, 5) for k, v in fk.items()},
@@ -152,9 +174,9 @@ def main():
     sweep_name = [k for k in kernels_ms if k.startswith("k_sweep")]
     sweep_ms = kernels_ms[sweep_name[0]] if sweep_name else float("nan")
 
-    ab = sweep_algorithmic_bytes(N, F, Fb)
+    ab = local_bytes
     achieved = ab / (sweep_ms * 1e-3) / 1e9
-    value = world * F / (ms_per_step * 1e-3) / 1e6
+    value = F / (ms_per_step * 1e-3) / 1e6       # every face of the (global) mesh once per step
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
@@ -170,7 +192,7 @@ def main():
 
     if rank == 0:
         # template of the timed sweep: k_sweep<FLUX=ROE(4), REC=MUSCL(1), VISC=none(0), DT, no PHI>
-        tr = pmc_traffic("exact::k_sweep<4, 1, 0, true, false>", N)
+        tr = pmc_traffic("exact::k_sweep<4, 1, 0, true, false>", N) if world == 1 else None
         out = {
             "metric": "Mfaces/s (flux+residual sweep) + achieved HBM GB/s, 1/2/4/8 MI355X",
             "value": round(value, 3),
@@ -180,14 +202,15 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": round(ms_per_step, 5),
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": args.scaling if world > 1 else "weak",
             "vs_baseline": None,
             "dtype": "f64",
             "data": "synthetic (generated C4 NACA0012 hybrid O-grid; seeded perturbed free stream)",
             "config": {"workload": "C4 mesh, Roe + WLS gradients + MUSCL/Van Albada, 2nd-order residual "
                                    "sweep with local time steps (explicit pseudo-time step)",
                        "cells": N, "faces": F, "boundary_faces": Fb, **dims,
-                       "parallelism": f"replicas x{world}" if world > 1 else "single GPU",
+                       "parallelism": (f"RCB {world}-way partition, RCCL p2p halo (u + gradients)"
+                                       if world > 1 else "single GPU"),
                        "layout": stats, "setup_s": round(t_setup, 2)},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 4),
