@@ -271,10 +271,11 @@ class FlowFV:
     def matfree_apply_device(self, d_x, d_y):
         check(_ffi.lib().fvhip_matfree_apply_device(self._h, ctypes.c_void_p(d_x), ctypes.c_void_p(d_y)))
 
-    def compute_residual_device(self, d_u, d_r, d_dtm=None, gettimesteps=False, overwrite=True):
+    def compute_residual_device(self, d_u, d_r, d_dtm=None, gettimesteps=False, overwrite=True, staged=False):
+        """staged=True forces the gradient + sweep kernels where the fused one-launch residual applies"""
         check(_ffi.lib().fvhip_compute_residual_device(self._h, ctypes.c_void_p(d_u), ctypes.c_void_p(d_r),
                                                        int(gettimesteps), ctypes.c_void_p(d_dtm or 0),
-                                                       1 if overwrite else 0))
+                                                       (1 if overwrite else 0) | (2 if staged else 0)))
 
     def permutation(self):
         p = np.zeros(self.nown, np.int32)

@@ -102,6 +102,7 @@ struct fvhip_ctx
 	std::vector<double> h_stage;
 	// partitioned meshes: halo exchange with the neighbour ranks (RCCL, or in-process for a group)
 	int rank = 0, nparts = 1;
+	bool use_staged = false;      ///< force the staged (gradient + sweep) path even if fused applies
 	ncclComm_t comm = nullptr;
 	bool in_group = false;
 	int* d_send = nullptr;
@@ -194,6 +195,17 @@ struct fvhip_ctx
 		HC(hipGetLastError());
 	}
 
+	/// one-launch residual (WLS + MUSCL / unlimited linear, inviscid, single domain)
+	bool fused() const { return !L.fz_ext_start.empty() && !use_staged; }
+	void stage_fused(const double* u, double* r, bool dt, double* dtm, bool overwrite) {
+		SweepBuffers B{};
+		B.u = u; B.r = r; B.dtm = dtm; B.overwrite = overwrite ? 1 : 0;
+		const char* nm = nullptr;
+		timed("k_residual_wls", [&]{ nm = KOPS(launch_residual_wls)(M, P, B, cfg.conv_numflux, recKind(), dt, stream); });
+		if(prof && !recs.empty() && recs.back().name == "k_residual_wls" && nm) recs.back().name = nm;
+		HC(hipGetLastError());
+	}
+
 	/// pack the rows of `arr` (width doubles per cell) that the neighbours hold as ghosts
 	void pack(const double* arr, int width) {
 		timed("k_pack", [&]{ launch_pack_rows(d_send, nsend, arr, width, d_sendbuf, stream); });
@@ -234,6 +246,10 @@ struct fvhip_ctx
 			for(size_t i = 0; i < hs.size(); i++) hs[i]->exchange_rccl(arr_of(i), width);
 		};
 		fvhip_ctx* h0 = hs[0];
+		if(h0->fused()) {
+			for(size_t i = 0; i < hs.size(); i++) hs[i]->stage_fused(us[i], rs[i], dt, dts[i], overwrite);
+			return;
+		}
 		exchange([&](size_t i) { return const_cast<double*>(us[i]); }, 4);
 		if(h0->recKind() != SR_FIRST) {
 			for(size_t i = 0; i < hs.size(); i++) hs[i]->stage_gradients(us[i]);
@@ -356,6 +372,13 @@ static fvhip_ctx* createCtx(const MeshTopo& T, const fvhip_flow_config* cfg, int
 	M.bf_bc = upload(L.bf_bc, o);
 	M.bf_n = reinterpret_cast<const double2*>(upload(L.bf_n, o));
 	M.bf_rcbp = reinterpret_cast<const double2*>(upload(L.bf_rcbp, o));
+	if(!L.fz_ext_start.empty()) {
+		M.fz_ext_start = upload(L.fz_ext_start, o);
+		M.fz_ext = upload(L.fz_ext, o);
+		M.fz_gnbr = reinterpret_cast<const int4*>(upload(L.fz_gnbr, o));
+		M.fz_slot_lr = reinterpret_cast<const int2*>(upload(L.fz_slot_lr, o));
+		M.fz_max_cells = L.fz_max_cells;
+	}
 	h->d_perm = upload(L.perm, o);
 	h->nsend = static_cast<int>(L.send_cells.size());
 	if(h->nsend > 0) {
@@ -518,7 +541,9 @@ int fvhip_compute_residual_device(fvhip_handle h, const double* d_u, double* d_r
 {
 	return guard([&] {
 		HC(hipSetDevice(h->device));
+		h->use_staged = (flags & FVHIP_RES_STAGED) != 0;
 		h->residual(d_u, d_r, gettimesteps != 0, d_dtm, (flags & FVHIP_RES_OVERWRITE) != 0);
+		h->use_staged = false;
 	});
 }
 

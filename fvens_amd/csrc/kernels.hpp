@@ -39,6 +39,12 @@ struct DevMesh
 	const int* bf_bc;          // [nb]
 	const double2* bf_n;       // [nb]
 	const double2* bf_rcbp;    // [nb]
+	// fused residual (layout.hpp fz_*)
+	const int* fz_ext_start;   // [npatch+1]
+	const int* fz_ext;         // ring-1 cells
+	const int4* fz_gnbr;       // neighbour codes of staged cells
+	const int2* fz_slot_lr;    // [S] patch-local L, R
+	int fz_max_cells;
 };
 
 struct DevPhys
@@ -80,6 +86,8 @@ void launch_weno(const DevMesh& M, const DevPhys& P, const double* grad, double*
 /* returns the kernel name for profiling */ \
 const char* launch_sweep(const DevMesh& M, const DevPhys& P, const SweepBuffers& B, int flux, int rec, \
                          int visc, bool dt, hipStream_t s); \
+const char* launch_residual_wls(const DevMesh& M, const DevPhys& P, const SweepBuffers& B, int flux, int rec, \
+                                bool dt, hipStream_t s); \
 void launch_fill(double* p, double v, long long n, hipStream_t s); \
 void launch_local_flux(int flux, const gd::Gas& G, int nf, const double* ul, const double* ur, \
                        const double* n, double* f, hipStream_t s); \

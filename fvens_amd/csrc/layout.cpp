@@ -96,6 +96,42 @@ Layout buildLayout(const MeshTopo& T, const fvhip_flow_config& cfg, bool renumbe
 		}
 		Lo.patch_cell.push_back(N);
 	}
+	// fused residual path: also cap the patch cells + ring-1 cells the patch stages in LDS
+	const bool fused = fusedEligible(cfg) && T.nghost == 0;
+	if(fused) {
+		std::vector<int> ranges, mark2(N, -1);
+		int stamp = 0;
+		auto ring1 = [&](int c0, int c1) {
+			stamp++;
+			int n1 = 0;
+			for(int c = c0; c < c1; c++) {
+				const int ref = Lo.perm[c];
+				for(int j = 0; j < nf(ref); j++) {
+					const int nb = esu(ref, j);
+					if(nb < 0 || nb >= N) continue;
+					const int ci = Lo.iperm[nb];
+					if(ci >= c0 && ci < c1) continue;
+					if(mark2[ci] != stamp) { mark2[ci] = stamp; n1++; }
+				}
+			}
+			return n1;
+		};
+		std::vector<std::pair<int,int>> stack;
+		for(size_t k = 0; k + 1 < Lo.patch_cell.size(); k++) {
+			stack.assign(1, {Lo.patch_cell[k], Lo.patch_cell[k+1]});
+			std::vector<std::pair<int,int>> done;
+			while(!stack.empty()) {
+				const auto r = stack.back(); stack.pop_back();
+				if(r.second - r.first > 1 && (r.second - r.first) + ring1(r.first, r.second) > FUSED_LDS_CELLS) {
+					const int mid = (r.first + r.second)/2;
+					stack.push_back({mid, r.second}); stack.push_back({r.first, mid});
+				} else done.push_back(r);
+			}
+			for(const auto& r : done) ranges.push_back(r.first);
+		}
+		ranges.push_back(N);
+		Lo.patch_cell = ranges;
+	}
 	const int npatch = static_cast<int>(Lo.patch_cell.size()) - 1;
 
 	// --- slots per patch ---
@@ -251,7 +287,58 @@ Layout buildLayout(const MeshTopo& T, const fvhip_flow_config& cfg, bool renumbe
 		Lo.venk_eps2.resize(N);
 		for(int c = 0; c < N; c++) Lo.venk_eps2[c] = std::pow(cfg.limiter_param*T.clength[Lo.perm[c]], 3);
 	}
+	if(fused) buildFused(Lo);
 	return Lo;
+}
+
+bool fusedEligible(const fvhip_flow_config& cfg)
+{
+	return cfg.order2 && cfg.gradientscheme == FVHIP_GRAD_LEASTSQUARES && !cfg.viscous_sim &&
+	       (cfg.reconstruction == FVHIP_REC_VANALBADA || cfg.reconstruction == FVHIP_REC_NONE);
+}
+
+void buildFused(Layout& Lo)
+{
+	if(Lo.nghost != 0) throw std::runtime_error("fused residual: partitioned meshes use the staged path");
+	const int N = Lo.ncell;
+	const int npatch = static_cast<int>(Lo.patch_cell.size()) - 1;
+	Lo.fz_ext_start.assign(1, 0); Lo.fz_ext.clear(); Lo.fz_n1.assign(npatch, 0);
+	Lo.fz_gnbr.clear();
+	Lo.fz_slot_lr.assign(2*Lo.slot_L.size(), -1);
+	Lo.fz_max_cells = 0;
+	std::vector<int> lidx(N, -1);          // patch-local index of a cell while its patch is built
+	for(int p = 0; p < npatch; p++) {
+		const int c0 = Lo.patch_cell[p], c1 = Lo.patch_cell[p+1], nc = c1 - c0;
+		const size_t e0 = Lo.fz_ext.size();
+		for(int c = c0; c < c1; c++) lidx[c] = c - c0;
+		int nl = nc;
+		// ring 1: the other side of the patch's cut faces
+		auto add = [&](int c) {
+			if(c < 0 || c >= N || lidx[c] >= 0) return;
+			lidx[c] = nl++; Lo.fz_ext.push_back(c);
+		};
+		for(int s = Lo.patch_slot[p]; s < Lo.patch_slot[p+1]; s++) { add(Lo.slot_L[s]); add(Lo.slot_R[s]); }
+		if(nl > FUSED_LDS_CELLS) throw std::logic_error("fused residual: patch exceeds its LDS budget");
+		Lo.fz_n1[p] = nl - nc;
+		Lo.fz_ext_start.push_back(static_cast<int>(Lo.fz_ext.size()));
+		// neighbours of every staged cell, in the cell's ascending reference face order
+		auto code = [&](int nb) {
+			if(nb < 0) return -1;
+			if(nb >= N) return -2 - (nb - N);
+			return lidx[nb] >= 0 ? lidx[nb] : FUSED_GLOBAL + nb;
+		};
+		for(int i = 0; i < nl; i++) {
+			const int c = i < nc ? c0 + i : Lo.fz_ext[e0 + (i - nc)];
+			for(int j = 0; j < MAXF; j++) Lo.fz_gnbr.push_back(code(Lo.cell_nbr_fo[static_cast<size_t>(c)*MAXF+j]));
+		}
+		for(int s = Lo.patch_slot[p]; s < Lo.patch_slot[p+1]; s++) {
+			Lo.fz_slot_lr[2*static_cast<size_t>(s)] = code(Lo.slot_L[s]);
+			Lo.fz_slot_lr[2*static_cast<size_t>(s)+1] = code(Lo.slot_R[s]);
+		}
+		Lo.fz_max_cells = std::max(Lo.fz_max_cells, nl);
+		for(int c = c0; c < c1; c++) lidx[c] = -1;
+		for(size_t k = e0; k < Lo.fz_ext.size(); k++) lidx[Lo.fz_ext[k]] = -1;
+	}
 }
 
 }

@@ -69,7 +69,26 @@ struct Layout
 	// ncell+ghost_start[k] .. ncell+ghost_start[k+1]-1; send_cells[send_start[k]..] go to nbr_rank[k]
 	std::vector<int> nbr_rank, ghost_start, send_start, send_cells;
 	std::vector<int> cell_global;          ///< [ncell+nghost] global cell of each internal cell
+	// fused residual (k_residual_wls): per patch, the ring-1 cells (far side of its cut faces) whose
+	// primitive states and gradients it recomputes; patch-local index = [patch cells | ring 1]
+	std::vector<int> fz_ext_start;         ///< [npatch+1]
+	std::vector<int> fz_ext;               ///< ring-1 cells (internal ids)
+	std::vector<int> fz_n1;                ///< [npatch] ring-1 count
+	std::vector<int> fz_gnbr;              ///< per patch [patch cells + ring 1][4]: neighbours in
+	                                       ///<  ascending reference face order: local index (< FUSED_GLOBAL),
+	                                       ///<  FUSED_GLOBAL + internal id (read from global memory),
+	                                       ///<  -2-bf (boundary face), -1 (none); row offset = 4*(c0 + ext_start)
+	std::vector<int> fz_slot_lr;           ///< [S][2] local L, R (R boundary: -2-bf)
+	int fz_max_cells = 0;
 };
+
+constexpr int FUSED_LDS_CELLS = 704;     ///< staged cells per patch: 704 x 112 B = 77 KB (2 blocks/CU)
+constexpr int FUSED_GLOBAL = 1 << 20;    ///< neighbour codes >= this are global internal ids + FUSED_GLOBAL
+
+/// whether cfg takes the fused residual kernel (WLS + MUSCL/unlimited linear, inviscid)
+bool fusedEligible(const fvhip_flow_config& cfg);
+/// builds the fz_* arrays (owned-only meshes)
+void buildFused(Layout& Lo);
 
 /// Builds the layout from the reference's mesh arrays. bc_of_tag maps a boundary marker to the
 /// index of its BC in the config. Throws std::runtime_error on unsupported meshes.

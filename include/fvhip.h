@@ -143,6 +143,9 @@ int fvhip_compute_residual(fvhip_handle h, const double* u, double* r, int getti
 /** Device-resident sweep; u/r/dtm in internal order. flags: FVHIP_RES_OVERWRITE = r is known
  *  to be zero on entry (as every reference caller guarantees), so it is written, not read. */
 #define FVHIP_RES_OVERWRITE 1
+/** flags: FVHIP_RES_STAGED = use the gradient kernel + sweep kernel even where the one-launch
+ *  fused residual applies (WLS + MUSCL/unlimited linear, inviscid, single domain); same results */
+#define FVHIP_RES_STAGED 2
 int fvhip_compute_residual_device(fvhip_handle h, const double* d_u, double* d_r, int gettimesteps,
                                   double* d_dtm, int flags);
 /** FlowFV_base::getGradients: conserved-variable gradients, GradBlock layout [nelem][4 vars][2 dims] */

@@ -246,3 +246,32 @@ def test_fast_math_within_tolerance(meshkey, kind, flux, grad, rec):
     r, dt, r0, dt0 = run_both(meshkey, p, n)
     assert_close(r, r0, None, None, rtol=1e-11)
     np.testing.assert_allclose(dt, dt0, rtol=1e-12, atol=0)
+
+
+# ------------------------------------------------------------------------------------------------
+# one-launch fused residual (WLS + MUSCL / unlimited linear, inviscid) vs the staged kernels
+# ------------------------------------------------------------------------------------------------
+@pytest.mark.parametrize("flux", ["ROE", "HLLC", "LLF", "AUSMPLUS"])
+@pytest.mark.parametrize("rec", ["VANALBADA", "NONE"])
+@pytest.mark.parametrize("meshkey,kind", [("naca_small", "naca"), ("2dcylinderhybrid.msh", "cyl"),
+                                          ("plate_small", "plate_inviscid"), ("naca_c2", "naca")])
+def test_fused_equals_staged_bitwise(flux, rec, meshkey, kind):
+    import torch
+    m, _ = get_mesh(meshkey)
+    p = cases.physics(kind)
+    n = cases.numerics(flux, "LEASTSQUARES", rec)
+    u = cases.state(m, p, 5)
+    dev = fa.FlowFV(m, p, n)
+    perm = dev.permutation()
+    du = torch.tensor(u[perm], device="cuda")
+    out = []
+    for staged in (False, True):
+        dr = torch.full((m.nelem, 4), float("nan"), dtype=torch.float64, device="cuda")
+        dt = torch.full((m.nelem,), float("nan"), dtype=torch.float64, device="cuda")
+        dev.compute_residual_device(du.data_ptr(), dr.data_ptr(), dt.data_ptr(), True, True, staged=staged)
+        dev.synchronize()
+        out.append((dr.cpu().numpy(), dt.cpu().numpy()))
+    np.testing.assert_array_equal(out[0][0], out[1][0])
+    np.testing.assert_array_equal(out[0][1], out[1][1])
+    kt = dev.kernel_times() if False else None
+    dev.close()
