@@ -265,6 +265,16 @@ class FlowFV:
         check(_ffi.lib().fvhip_block_apply_device(self._h, *[ctypes.c_void_p(p) for p in
                                                              (d_diag, d_lower, d_upper, d_x, d_y)]))
 
+    def steady_forward_euler_device(self, d_u, cfl, tol, maxiter):
+        """SteadyForwardEulerSolver::solve on the device (aodesolver.cpp:170-240); returns
+        (steps, final residual ratio, residual-norm history)"""
+        steps = np.zeros(1, np.int32)
+        ratio = np.zeros(1)
+        hist = np.zeros(max(int(maxiter), 1))
+        check(_ffi.lib().fvhip_steady_forward_euler_device(self._h, ctypes.c_void_p(d_u), float(cfl), float(tol),
+                                                           int(maxiter), iptr(steps), dptr(ratio), dptr(hist)))
+        return int(steps[0]), float(ratio[0]), hist[:int(steps[0])]
+
     def matfree_set_state_device(self, d_u, d_r, d_mdt):
         check(_ffi.lib().fvhip_matfree_set_state_device(self._h, *[ctypes.c_void_p(p) for p in (d_u, d_r, d_mdt)]))
 

@@ -66,6 +66,8 @@ _SIGS = {
     "fvhip_block_apply_device": (ctypes.c_int, [ctypes.c_void_p] + [ctypes.c_void_p] * 5),
     "fvhip_jacobian_pattern": (ctypes.c_int, [ctypes.c_void_p, c_int_p, c_int_p]),
     "fvhip_assemble_jacobian_bsr": (ctypes.c_int, [ctypes.c_void_p, c_dbl_p, c_int_p, c_int_p, c_dbl_p]),
+    "fvhip_steady_forward_euler_device": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_double,
+                                                         ctypes.c_double, ctypes.c_int, c_int_p, c_dbl_p, c_dbl_p]),
     "fvhip_matfree_set_state": (ctypes.c_int, [ctypes.c_void_p, c_dbl_p, c_dbl_p, c_dbl_p]),
     "fvhip_matfree_apply": (ctypes.c_int, [ctypes.c_void_p, c_dbl_p, c_dbl_p]),
     "fvhip_matfree_set_state_device": (ctypes.c_int, [ctypes.c_void_p] + [ctypes.c_void_p] * 3),

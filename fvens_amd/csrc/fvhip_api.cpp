@@ -10,6 +10,7 @@
 #include "mesh.hpp"
 #include "partition.hpp"
 #include "halo.hpp"
+#include "ode.hpp"
 #include <rccl/rccl.h>
 
 #include <hip/hip_runtime.h>
@@ -95,6 +96,7 @@ struct fvhip_ctx
 	double mf_eps = 1e-7;
 	const double *mf_u = nullptr, *mf_r = nullptr, *mf_mdt = nullptr;   // device state of the operator
 	double *d_part = nullptr, *d_pm = nullptr;
+	double *d_rn_part = nullptr, *d_rn = nullptr;   // residual-norm reduction of the explicit driver
 	// Jacobian
 	JacMesh J{};
 	bool jac_ready = false;
@@ -701,6 +703,35 @@ int fvhip_assemble_jacobian_bsr(fvhip_handle h, const double* u, const int* rowp
 			std::memcpy(vals + 16*find(r,l), &lo[16*static_cast<size_t>(fi)], 16*sizeof(double));
 			std::memcpy(vals + 16*find(l,r), &up[16*static_cast<size_t>(fi)], 16*sizeof(double));
 		}
+	});
+}
+
+int fvhip_steady_forward_euler_device(fvhip_handle h, double* d_u, double cfl, double tol, int maxiter,
+                                      int* steps, double* resratio, double* reshistory)
+{
+	return guard([&] {
+		HC(hipSetDevice(h->device));
+		if(h->nparts > 1) throw std::runtime_error("forward Euler driver: single-domain handles only");
+		const int N = h->L.ncell;
+		if(!h->d_rn) { h->d_rn_part = dalloc(resnorm_partials(), h->owned); h->d_rn = dalloc(1, h->owned); }
+		double* part = h->d_rn_part;
+		double* dn = h->d_rn;
+		double resi = 1.0, initres = 1.0;
+		int step = 0;
+		while(resi/initres > tol && step < maxiter) {
+			h->residual(d_u, h->d_r, true, h->d_dtm, true);       // r = 0 + (-r(u)), aodesolver.cpp:180-189
+			launch_fe_update(N, h->d_r, h->d_dtm, h->M.area, cfl, d_u, h->stream);
+			launch_resnorm(N, h->d_r, h->M.area, part, dn, h->stream);
+			HC(hipGetLastError());
+			HC(hipMemcpyAsync(&resi, dn, sizeof(double), hipMemcpyDeviceToHost, h->stream));
+			HC(hipStreamSynchronize(h->stream));
+			if(step == 0) initres = resi;
+			if(reshistory) reshistory[step] = resi;
+			step++;
+			if(!std::isfinite(resi)) throw std::runtime_error("forward Euler diverged");   // Numerical_error
+		}
+		if(steps) *steps = step;
+		if(resratio) *resratio = resi/initres;
 	});
 }
 

@@ -171,6 +171,12 @@ int fvhip_jacobian_pattern(fvhip_handle h, int* rowptr, int* colind);
 int fvhip_assemble_jacobian_bsr(fvhip_handle h, const double* u, const int* rowptr, const int* colind,
                                 double* vals);
 
+/** SteadyForwardEulerSolver::solve (aodesolver.cpp:170-240) on the device: explicit local-time-step
+ *  iterations on d_u (internal order) until ||r||/||r0|| <= tol or maxiter steps; reshistory [maxiter]
+ *  (may be NULL) receives the residual norms sqrt(sum r_energy^2 area) */
+int fvhip_steady_forward_euler_device(fvhip_handle h, double* d_u, double cfl, double tol, int maxiter,
+                                      int* steps, double* resratio, double* reshistory);
+
 /** MatrixFreeSpatialJacobian: set_state(u, r = -r(u), mdt = area/(CFL*dt)) then y = J x */
 int fvhip_matfree_set_state(fvhip_handle h, const double* u, const double* r, const double* mdt);
 int fvhip_matfree_apply(fvhip_handle h, const double* x, double* y);

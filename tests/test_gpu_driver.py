@@ -59,3 +59,31 @@ def test_explicit_pseudo_time_matches_oracle(tmp_path, fast):
     else:
         np.testing.assert_array_equal(u_dev, u)
         assert hist[-1] / hist[0] == ratio
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("meshkey,kind,flux,grad,rec,order2", [
+    ("2dcylinderhybrid.msh", "cyl", "LLF", "NONE", "NONE", False),        # BASELINE config 1 (C1-like)
+    ("naca_small", "naca", "ROE", "LEASTSQUARES", "VANALBADA", True)])
+def test_device_forward_euler_matches_oracle(meshkey, kind, flux, grad, rec, order2):
+    """Device-resident explicit pseudo-time loop: state after 30 steps bitwise equal to the oracle's
+    forward Euler (the norm reduction order differs, so only the state is compared bitwise)."""
+    import torch
+    from test_gpu_residual import get_mesh
+    m, om = get_mesh(meshkey)
+    p = cases.physics(kind)
+    n = cases.numerics(flux, grad, rec, order2=order2)
+    u0 = np.tile(cases.freestream(p), (m.nelem, 1))
+    u0 = u0 + 0.0 * cases.state(m, p, 1)
+    dev = fa.FlowFV(m, p, n)
+    perm = dev.permutation()
+    du = torch.tensor(u0[perm], device="cuda")
+    steps, ratio, hist = dev.steady_forward_euler_device(du.data_ptr(), 0.5, 0.0, 30)
+    u_dev = np.empty_like(u0)
+    u_dev[perm] = du.cpu().numpy()
+    u_ref = u0.copy()
+    s2, r2 = orc.OracleSpatial(om, p, n).forward_euler(u_ref, 0.5, 0.0, 30)
+    assert steps == s2 == 30
+    np.testing.assert_array_equal(u_dev, u_ref)
+    assert abs(ratio - r2) <= 1e-12 * abs(r2)
+    dev.close()
