@@ -74,7 +74,6 @@ def test_device_forward_euler_matches_oracle(meshkey, kind, flux, grad, rec, ord
     p = cases.physics(kind)
     n = cases.numerics(flux, grad, rec, order2=order2)
     u0 = np.tile(cases.freestream(p), (m.nelem, 1))
-    u0 = u0 + 0.0 * cases.state(m, p, 1)
     dev = fa.FlowFV(m, p, n)
     perm = dev.permutation()
     du = torch.tensor(u0[perm], device="cuda")
