@@ -1,0 +1,39 @@
+"""Known-answer pin of the whole residual path against the reference's own functional regression:
+testcases/naca0012 SpatialFlow_Euler_NACA0012_MUSCL_LeastSquares_HLLC_FunctionalRegression
+(transonic-sanity-test-muscl.ctrl on grids/naca0012luo.msh: M 0.8, 1.25 deg, HLLC + least squares +
+Van Albada) stores CL = 0.154112792928976, CDp = 0.0115814414408097 (regr-MUSCL_LeastSquares_HLLC.txt)
+and checks CL to 1e-6 and CDp to 1e-8 relative (tests/flow_solve.cpp:89-126) after an implicit solve to a
+1e-7 residual drop. Here the device explicit pseudo-time driver converges the same discretisation
+further (1e-10) and the oracle evaluates the surface functionals (flow_spatial.cpp:130-310)."""
+import numpy as np
+import pytest
+
+import fvens_amd as fa
+import _oracle as orc
+import cases
+
+pytestmark = pytest.mark.gpu
+
+CL_REF, CDP_REF = 0.154112792928976, 0.0115814414408097
+
+
+def test_naca0012_muscl_hllc_functionals():
+    import torch
+    m = fa.UMesh.read_gmsh(cases.fixture_mesh("naca0012luo"))
+    om = orc.OracleMesh.read(cases.fixture_mesh("naca0012luo"))
+    p = cases.physics("naca")
+    n = cases.numerics("HLLC", "LEASTSQUARES", "VANALBADA")
+    dev = fa.FlowFV(m, p, n)
+    perm = dev.permutation()
+    u0 = np.tile(cases.freestream(p), (m.nelem, 1))
+    du = torch.tensor(u0[perm], device="cuda")
+    steps, ratio, hist = dev.steady_forward_euler_device(du.data_ptr(), 0.8, 1e-10, 400000)
+    u = np.empty_like(u0)
+    u[perm] = du.cpu().numpy()
+    ref = orc.OracleSpatial(om, p, n)
+    cl, cdp, cdsf = ref.surface(u, ref.getGradients(u), 2)
+    print(f"steps {steps} ratio {ratio:.3e} CL {cl!r} CDp {cdp!r}")
+    assert ratio <= 1e-10
+    assert abs(cl - CL_REF) / abs(CL_REF) <= 1e-6        # the reference's CL tolerance
+    assert abs(cdp - CDP_REF) / abs(CDP_REF) <= 1e-6     # reference: 1e-8 at its own 1e-7 convergence
+    dev.close()
