@@ -138,6 +138,10 @@ int orc_bc_ghost(int type, const double* gas, double aoa, const double* vals, co
 	        if(dgs) b.ghostJac(p, ins, n, gs, dgs); else b.ghost(p, ins, n, gs))
 }
 
+/// OpenMP threads of the restatement (1 by default: the reference's single-thread order)
+static struct OmpOne { OmpOne() { omp_set_num_threads(1); } } g_omp_one;
+int orc_set_threads(int n) { omp_set_num_threads(n < 1 ? 1 : n); return omp_get_max_threads(); }
+
 /// CPU baseline timing: nrep sweeps of compute_residual; returns seconds per sweep (median-free
 /// mean over nrep after one warm-up). Single-threaded restatement.
 double orc_time_residual(void* h, const double* u, int nrep, int gettimesteps)

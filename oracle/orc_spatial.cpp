@@ -106,6 +106,7 @@ void Spatial::compute_gradients(const double* u, const double* ug, double* grads
 			}
 			for(int d = 0; d < 2; d++) md[d] /= 2;
 		};
+#pragma omp parallel for default(shared)
 		for(int f = 0; f < m.nbface; f++) {
 			const int ie = m.L(f);
 			double md[2]; mid(f, md);
@@ -118,9 +119,13 @@ void Spatial::compute_gradients(const double* u, const double* ug, double* grads
 			const double ai = 1.0/m.area[ie];
 			for(int iv = 0; iv < 4; iv++) {
 				const double ut = (u[4*ie+iv]*dL + ug[4*f+iv]*dR)/(dL+dR) * m.len(f);
-				for(int d = 0; d < 2; d++) GR(ie,d,iv) += (ut * m.facemetric[3*f+d])*ai;
+				for(int d = 0; d < 2; d++) {
+#pragma omp atomic update
+					GR(ie,d,iv) += (ut * m.facemetric[3*f+d])*ai;
+				}
 			}
 		}
+#pragma omp parallel for default(shared)
 		for(int f = m.nbface; f < m.nbface+m.ninface; f++) {
 			const int ie = m.L(f), je = m.Rt(f);
 			double md[2]; mid(f, md);
@@ -134,7 +139,9 @@ void Spatial::compute_gradients(const double* u, const double* ug, double* grads
 			for(int iv = 0; iv < 4; iv++) {
 				const double ut = (u[4*ie+iv]*dL + u[4*je+iv]*dR)/(dL+dR) * m.len(f);
 				for(int d = 0; d < 2; d++) {
+#pragma omp atomic update
 					GR(ie,d,iv) += (ut * m.facemetric[3*f+d])*a1;
+#pragma omp atomic update
 					GR(je,d,iv) -= (ut * m.facemetric[3*f+d])*a2;
 				}
 			}
@@ -142,6 +149,7 @@ void Spatial::compute_gradients(const double* u, const double* ug, double* grads
 	}
 	else if(cfg.grad == GRAD_LEASTSQUARES) {                       // :322-440
 		std::vector<double> fr(8*static_cast<size_t>(N), 0.0);   // f(jdim,ivar) at ivar*2+jdim
+#pragma omp parallel for default(shared)
 		for(int f = 0; f < m.nbface; f++) {
 			const int ie = m.L(f);
 			double w2 = 0, dr[2], du[4];
@@ -151,8 +159,12 @@ void Spatial::compute_gradients(const double* u, const double* ug, double* grads
 			}
 			w2 = 1.0/(w2);
 			for(int iv = 0; iv < 4; iv++) du[iv] = u[4*ie+iv] - ug[4*f+iv];
-			for(int iv = 0; iv < 4; iv++) for(int d = 0; d < 2; d++) fr[8*ie+iv*2+d] += w2*dr[d]*du[iv];
+			for(int iv = 0; iv < 4; iv++) for(int d = 0; d < 2; d++) {
+#pragma omp atomic update
+				fr[8*ie+iv*2+d] += w2*dr[d]*du[iv];
+			}
 		}
+#pragma omp parallel for default(shared)
 		for(int f = m.nbface; f < m.nbface+m.ninface; f++) {
 			const int ie = m.L(f), je = m.Rt(f);
 			double w2 = 0, dr[2], du[4];
@@ -163,11 +175,14 @@ void Spatial::compute_gradients(const double* u, const double* ug, double* grads
 			w2 = 1.0/(w2);
 			for(int iv = 0; iv < 4; iv++) du[iv] = u[4*ie+iv] - u[4*je+iv];
 			for(int iv = 0; iv < 4; iv++) for(int d = 0; d < 2; d++) {
+#pragma omp atomic update
 				fr[8*ie+iv*2+d] += w2*dr[d]*du[iv];
+#pragma omp atomic update
 				fr[8*je+iv*2+d] += w2*dr[d]*du[iv];
 			}
 		}
 		// d = V*f (Eigen lazy 2x2 * 2x4 product: d(i,j) = V(i,0) f(0,j) + V(i,1) f(1,j))
+#pragma omp parallel for default(shared)
 		for(int e = 0; e < N; e++) {
 			const double* v = &V[4*e];
 			for(int iv = 0; iv < 4; iv++)
@@ -195,6 +210,7 @@ void Spatial::compute_face_values(const double* up, const double* ug, const doub
 	};
 	switch(cfg.recon) {
 	case REC_NONE: {                                               // areconstruction.cpp:51-103
+#pragma omp parallel for default(shared)
 		for(int f = nb; f < nb+m.ninface; f++) {
 			const int ie = m.L(f), je = m.Rt(f);
 			for(int i = 0; i < 4; i++) {
@@ -229,6 +245,7 @@ void Spatial::compute_face_values(const double* up, const double* ug, const doub
 				ufl[4*f+i] = recL(up[4*ie+i], ug[4*f+i], dm, phi);
 			}
 		}
+#pragma omp parallel for default(shared)
 		for(int f = nb; f < F; f++) {
 			const int ie = m.L(f), je = m.Rt(f);
 			for(int i = 0; i < 4; i++) {
@@ -248,6 +265,7 @@ void Spatial::compute_face_values(const double* up, const double* ug, const doub
 	case REC_BARTHJESPERSEN:                                       // limitedlinearreconstruction.cpp:118-176
 	case REC_VENKATAKRISHNAN: {                                    // :207-268
 		const bool venk = cfg.recon == REC_VENKATAKRISHNAN;
+#pragma omp parallel for default(shared)
 		for(int e = 0; e < N; e++) {
 			const double eps2 = venk ? std::pow(cfg.limiter_param*clength[e], 3) : 0.0;
 			for(int iv = 0; iv < 4; iv++) {
@@ -288,6 +306,7 @@ void Spatial::compute_face_values(const double* up, const double* ug, const doub
 	case REC_WENO: {                                               // :27-105
 		const double gamma = 4.0, lambda = cfg.limiter_param, epsilon = 1.0e-5;
 		auto gm2 = [&](const double* g, int iv) { double r = 0; for(int j = 0; j < 2; j++) r += gat(g,j,iv)*gat(g,j,iv); return r; };
+#pragma omp parallel for default(shared)
 		for(int e = 0; e < N; e++) {
 			for(int iv = 0; iv < 4; iv++) {
 				double wsum = 0, lg[2] = {0,0};
@@ -387,6 +406,7 @@ void Spatial::compute_fluxes(const double* u, const double* grads, const double*
 {
 	const int N = m.nelem;
 	static const double zg[8] = {0,0,0,0,0,0,0,0};
+#pragma omp parallel for default(shared)
 	for(int f = 0; f < m.naface; f++) {
 		const double n[2] = {m.nx(f), m.ny(f)};
 		const double len = m.len(f);
@@ -404,8 +424,14 @@ void Spatial::compute_fluxes(const double* u, const double* grads, const double*
 			viscous_flux(n, &m.rc[2*le], rcr, &u[4*le], ucr, gl, grr, &ul[4*f], &ur[4*f], vf);
 			for(int iv = 0; iv < 4; iv++) fl[iv] += vf[iv]*len;
 		}
-		for(int iv = 0; iv < 4; iv++) res[4*le+iv] -= fl[iv];
-		if(re < N) for(int iv = 0; iv < 4; iv++) res[4*re+iv] += fl[iv];
+		for(int iv = 0; iv < 4; iv++) {
+#pragma omp atomic update
+			res[4*le+iv] -= fl[iv];
+		}
+		if(re < N) for(int iv = 0; iv < 4; iv++) {
+#pragma omp atomic update
+			res[4*re+iv] += fl[iv];
+		}
 	}
 }
 
@@ -414,6 +440,7 @@ void Spatial::compute_max_timestep(const double* ul, const double* ur, double* d
 {
 	const int N = m.nelem;
 	std::vector<double> integ(N, 0.0);
+#pragma omp parallel for default(shared)
 	for(int f = 0; f < m.naface; f++) {
 		const double n[2] = {m.nx(f), m.ny(f)};
 		const double len = m.len(f);
@@ -433,9 +460,14 @@ void Spatial::compute_max_timestep(const double* ul, const double* ur, double* d
 			sri += coi*mui/phy.Pr * len*len/m.area[le];
 			if(re < N) srj += coj*muj/phy.Pr * len*len/m.area[re];
 		}
+#pragma omp atomic update
 		integ[le] += sri;
-		if(re < N) integ[re] += srj;
+		if(re < N) {
+#pragma omp atomic update
+			integ[re] += srj;
+		}
 	}
+#pragma omp parallel for default(shared)
 	for(int e = 0; e < N; e++) dtm[e] = m.area[e]/integ[e];
 }
 
@@ -454,6 +486,7 @@ void Spatial::compute_residual(const double* u, double* res, bool gettimesteps, 
 			for(int j = 0; j < 4; j++) ubcell[4*f+j] = ur[4*f+j];
 			phy.primFromCons(&ur[4*f], &ur[4*f]);
 		}
+#pragma omp parallel for default(shared)
 		for(int e = 0; e < N; e++) phy.primFromCons(&u[4*e], &up[4*e]);
 		const double* ug = ur.data();
 		grads.assign(8*static_cast<size_t>(N), 0.0);
@@ -462,6 +495,7 @@ void Spatial::compute_residual(const double* u, double* res, bool gettimesteps, 
 		// exactly like the reference (ug aliases uright of the boundary faces)
 		std::vector<double> ugcopy(ur.begin(), ur.begin()+4*nb);
 		compute_face_values(up.data(), ugcopy.data(), grads.data(), ul.data(), ur.data());
+#pragma omp parallel for default(shared)
 		for(int f = nb; f < F; f++) {
 			phy.consFromPrim(&ul[4*f], &ul[4*f]);
 			phy.consFromPrim(&ur[4*f], &ur[4*f]);

@@ -37,6 +37,7 @@ _SIGS = {
     "orc_flux_jacobian": (ctypes.c_int, [ctypes.c_int, _dp, _dp, _dp, _dp, _dp, _dp]),
     "orc_bc_ghost": (ctypes.c_int, [ctypes.c_int, _dp, ctypes.c_double, _dp, _dp, _dp, _dp, _dp]),
     "orc_time_residual": (ctypes.c_double, [_vp, _dp, ctypes.c_int, ctypes.c_int]),
+    "orc_set_threads": (ctypes.c_int, [ctypes.c_int]),
 }
 
 _lib = None
@@ -185,8 +186,13 @@ class OracleSpatial:
         _chk(lib().orc_surface(self._h, _d(u), _d(grads), marker, _d(out)))
         return out
 
-    def time_residual(self, u, nrep, gettimesteps=True):
-        return lib().orc_time_residual(self._h, _d(u), nrep, int(gettimesteps))
+    def time_residual(self, u, nrep, gettimesteps=True, threads=1):
+        """seconds per sweep with `threads` OpenMP threads (the reference's omp structure)"""
+        lib().orc_set_threads(int(threads))
+        try:
+            return lib().orc_time_residual(self._h, _d(u), nrep, int(gettimesteps))
+        finally:
+            lib().orc_set_threads(1)
 
     def __del__(self):
         try:
