@@ -108,6 +108,8 @@ struct fvhip_ctx
 	ncclComm_t comm = nullptr;
 	bool in_group = false;
 	int* d_send = nullptr;
+	int* d_border = nullptr;
+	int nborder = 0;
 	double* d_sendbuf = nullptr;
 	int nsend = 0;
 	// profiling
@@ -197,7 +199,11 @@ struct fvhip_ctx
 		HC(hipGetLastError());
 	}
 
-	/// one-launch residual (WLS + MUSCL / unlimited linear, inviscid, single domain)
+	void stage_border_gradients(const double* u) {
+		timed("k_grad_wls_list", [&]{ KOPS(launch_grad_wls_list)(M, P, u, d_border, nborder, d_grad, stream); });
+	}
+
+	/// one-launch residual (WLS + MUSCL / unlimited linear, inviscid)
 	bool fused() const { return !L.fz_ext_start.empty() && !use_staged; }
 	void stage_fused(const double* u, double* r, bool dt, double* dtm, bool overwrite) {
 		SweepBuffers B{};
@@ -249,6 +255,12 @@ struct fvhip_ctx
 		};
 		fvhip_ctx* h0 = hs[0];
 		if(h0->fused()) {
+			if(h0->halo()) {
+				// ghost rows of u, then the gradients of the cells other ranks hold as ghosts
+				exchange([&](size_t i) { return const_cast<double*>(us[i]); }, 4);
+				for(size_t i = 0; i < hs.size(); i++) hs[i]->stage_border_gradients(us[i]);
+				exchange([&](size_t i) { return hs[i]->d_grad; }, 8);
+			}
 			for(size_t i = 0; i < hs.size(); i++) hs[i]->stage_fused(us[i], rs[i], dt, dts[i], overwrite);
 			return;
 		}
@@ -383,6 +395,8 @@ static fvhip_ctx* createCtx(const MeshTopo& T, const fvhip_flow_config* cfg, int
 	}
 	h->d_perm = upload(L.perm, o);
 	h->nsend = static_cast<int>(L.send_cells.size());
+	h->nborder = static_cast<int>(L.border_cells.size());
+	if(h->nborder > 0) h->d_border = upload(L.border_cells, o);
 	if(h->nsend > 0) {
 		h->d_send = upload(L.send_cells, o);
 		h->d_sendbuf = dalloc(8*static_cast<size_t>(h->nsend), o);

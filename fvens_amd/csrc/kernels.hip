@@ -220,6 +220,64 @@ __global__ void __launch_bounds__(256) k_prep_grad_wls(DevMesh M, DevPhys P, con
 	st8(grad, c, g);
 }
 
+/// WLS gradients of a list of owned cells (the cells other ranks hold as ghosts), all inputs from
+/// global memory: same arithmetic as k_prep_grad_wls, written to grad for the halo exchange
+__global__ void __launch_bounds__(256) k_grad_wls_list(DevMesh M, DevPhys P, const double* __restrict__ u,
+                                                       const int* __restrict__ list, int n, double* __restrict__ grad)
+{
+	const int i = blockIdx.x*blockDim.x + threadIdx.x;
+	if(i >= n) return;
+	const int c = list[i];
+	const int N = M.ncell;
+	const Gas& G = P.gas;
+	const int4 nb4 = M.cell_nbr_fo[c];
+	const int nb[4] = {nb4.x, nb4.y, nb4.z, nb4.w};
+	double ucons[4], uc[4];
+	ld4(u, c, ucons);
+	cons2prim(G, ucons, uc);
+	const double2 rcc = M.rc[c];
+	double f[8] = {0,0,0,0,0,0,0,0};
+	#pragma unroll
+	for(int k = 0; k < 4; k++) {
+		if(nb[k] < 0) break;
+		double un[4];
+		double2 rn;
+		if(nb[k] >= N) {
+			const int bf = nb[k] - N;
+			const double2 nn = M.bf_n[bf];
+			const double n[2] = {nn.x, nn.y};
+			double gs[4];
+			ghost_state(G, P.bc[M.bf_bc[bf]], P.uinf, ucons, n, gs);
+			cons2prim(G, gs, un);
+			rn = M.bf_rcbp[bf];
+		} else {
+			double t4[4];
+			ld4(u, nb[k], t4);
+			cons2prim(G, t4, un);
+			rn = M.rc[nb[k]];
+		}
+		double w2 = 0;
+		w2 += (rcc.x-rn.x)*(rcc.x-rn.x);
+		w2 += (rcc.y-rn.y)*(rcc.y-rn.y);
+		const double dr0 = rcc.x-rn.x, dr1 = rcc.y-rn.y;
+		w2 = 1.0/(w2);
+		#pragma unroll
+		for(int iv = 0; iv < 4; iv++) {
+			const double du = uc[iv] - un[iv];
+			f[iv*2+0] += w2*dr0*du;
+			f[iv*2+1] += w2*dr1*du;
+		}
+	}
+	const double4 V = M.wls_V[c];
+	double g[8];
+	#pragma unroll
+	for(int iv = 0; iv < 4; iv++) {
+		g[iv*2+0] = V.x*f[iv*2+0] + V.y*f[iv*2+1];
+		g[iv*2+1] = V.z*f[iv*2+0] + V.w*f[iv*2+1];
+	}
+	st8(grad, c, g);
+}
+
 __global__ void __launch_bounds__(256) k_grad_gg(DevMesh M, const double* __restrict__ up,
                                                  const double* __restrict__ ug, double* __restrict__ grad)
 {
@@ -677,6 +735,12 @@ __global__ void __launch_bounds__(SLOTS_MAX, 4) k_residual_wls(const DevMesh M, 
 	for(int i = t; i < nl; i += SLOTS_MAX) {
 		const int c = cellOf(i);
 		double* row = &fz[i*FZW];
+		if(c >= M.nown) {                       // ghost cell: gradient received from its owner
+			double g[8];
+			ld8(B.grad, c, g);
+			st8(row + 4, 0, g);
+			continue;
+		}
 		double uc[4];
 		ld4(row, 0, uc);
 		const double2 rcc = *reinterpret_cast<const double2*>(row + 12);
@@ -900,6 +964,9 @@ void launch_grad_wls(const DevMesh& M, const double* up, const double* ug, doubl
 void launch_prep_grad_wls(const DevMesh& M, const DevPhys& P, const double* u, double* up, double* ubc,
                           double* ug, double* grad, hipStream_t s)
 { if(M.nown > 0) k_prep_grad_wls<<<xcd_blocks((M.nown + 255)/256), 256, 0, s>>>(M, P, u, up, ubc, ug, grad); }
+void launch_grad_wls_list(const DevMesh& M, const DevPhys& P, const double* u, const int* list, int n,
+                          double* grad, hipStream_t s)
+{ if(n > 0) k_grad_wls_list<<<nblk(n,256), 256, 0, s>>>(M, P, u, list, n, grad); }
 void launch_grad_gg(const DevMesh& M, const double* up, const double* ug, double* grad, hipStream_t s)
 { if(M.nown > 0) k_grad_gg<<<nblk(M.nown,256), 256, 0, s>>>(M, up, ug, grad); }
 void launch_limiter(const DevMesh& M, const DevPhys& P, int venk, const double* up, const double* ug,

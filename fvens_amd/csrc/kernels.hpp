@@ -79,6 +79,8 @@ void launch_prep(const DevMesh& M, const DevPhys& P, const double* u, double* up
 void launch_grad_wls(const DevMesh& M, const double* up, const double* ug, double* grad, hipStream_t s); \
 void launch_prep_grad_wls(const DevMesh& M, const DevPhys& P, const double* u, double* up, double* ubc, \
                           double* ug, double* grad, hipStream_t s); \
+void launch_grad_wls_list(const DevMesh& M, const DevPhys& P, const double* u, const int* list, int n, \
+                          double* grad, hipStream_t s); \
 void launch_grad_gg(const DevMesh& M, const double* up, const double* ug, double* grad, hipStream_t s); \
 void launch_limiter(const DevMesh& M, const DevPhys& P, int venk, const double* up, const double* ug, \
                     const double* grad, double* phi, hipStream_t s); \

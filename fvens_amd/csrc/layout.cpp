@@ -97,9 +97,9 @@ Layout buildLayout(const MeshTopo& T, const fvhip_flow_config& cfg, bool renumbe
 		Lo.patch_cell.push_back(N);
 	}
 	// fused residual path: also cap the patch cells + ring-1 cells the patch stages in LDS
-	const bool fused = fusedEligible(cfg) && T.nghost == 0;
+	const bool fused = fusedEligible(cfg);
 	if(fused) {
-		std::vector<int> ranges, mark2(N, -1);
+		std::vector<int> ranges, mark2(NT, -1);
 		int stamp = 0;
 		auto ring1 = [&](int c0, int c1) {
 			stamp++;
@@ -108,8 +108,8 @@ Layout buildLayout(const MeshTopo& T, const fvhip_flow_config& cfg, bool renumbe
 				const int ref = Lo.perm[c];
 				for(int j = 0; j < nf(ref); j++) {
 					const int nb = esu(ref, j);
-					if(nb < 0 || nb >= N) continue;
-					const int ci = Lo.iperm[nb];
+					if(nb < 0 || nb >= NT) continue;          // boundary face
+					const int ci = toInt(nb);
 					if(ci >= c0 && ci < c1) continue;
 					if(mark2[ci] != stamp) { mark2[ci] = stamp; n1++; }
 				}
@@ -211,6 +211,9 @@ Layout buildLayout(const MeshTopo& T, const fvhip_flow_config& cfg, bool renumbe
 	Lo.send_start = T.send_start;
 	Lo.send_cells.resize(T.send_cells.size());
 	for(size_t i = 0; i < T.send_cells.size(); i++) Lo.send_cells[i] = Lo.iperm[T.send_cells[i]];
+	Lo.border_cells = Lo.send_cells;
+	std::sort(Lo.border_cells.begin(), Lo.border_cells.end());
+	Lo.border_cells.erase(std::unique(Lo.border_cells.begin(), Lo.border_cells.end()), Lo.border_cells.end());
 	Lo.cell_global.resize(NT);
 	for(int c = 0; c < N; c++) Lo.cell_global[c] = T.cell_global[Lo.perm[c]];
 	for(int c = N; c < NT; c++) Lo.cell_global[c] = T.cell_global[c];
@@ -299,8 +302,7 @@ bool fusedEligible(const fvhip_flow_config& cfg)
 
 void buildFused(Layout& Lo)
 {
-	if(Lo.nghost != 0) throw std::runtime_error("fused residual: partitioned meshes use the staged path");
-	const int N = Lo.ncell;
+	const int N = Lo.ncell + Lo.nghost;      // ghost cells may be ring-1 cells (their gradients are received)
 	const int npatch = static_cast<int>(Lo.patch_cell.size()) - 1;
 	Lo.fz_ext_start.assign(1, 0); Lo.fz_ext.clear(); Lo.fz_n1.assign(npatch, 0);
 	Lo.fz_gnbr.clear();
@@ -329,7 +331,8 @@ void buildFused(Layout& Lo)
 		};
 		for(int i = 0; i < nl; i++) {
 			const int c = i < nc ? c0 + i : Lo.fz_ext[e0 + (i - nc)];
-			for(int j = 0; j < MAXF; j++) Lo.fz_gnbr.push_back(code(Lo.cell_nbr_fo[static_cast<size_t>(c)*MAXF+j]));
+			for(int j = 0; j < MAXF; j++)     // ghost cells: gradient received, no neighbour list
+				Lo.fz_gnbr.push_back(c < Lo.ncell ? code(Lo.cell_nbr_fo[static_cast<size_t>(c)*MAXF+j]) : -1);
 		}
 		for(int s = Lo.patch_slot[p]; s < Lo.patch_slot[p+1]; s++) {
 			Lo.fz_slot_lr[2*static_cast<size_t>(s)] = code(Lo.slot_L[s]);

@@ -68,6 +68,7 @@ struct Layout
 	// halo (partitioned meshes): ghosts from nbr_rank[k] are internal cells
 	// ncell+ghost_start[k] .. ncell+ghost_start[k+1]-1; send_cells[send_start[k]..] go to nbr_rank[k]
 	std::vector<int> nbr_rank, ghost_start, send_start, send_cells;
+	std::vector<int> border_cells;         ///< unique send cells (their gradients are computed first)
 	std::vector<int> cell_global;          ///< [ncell+nghost] global cell of each internal cell
 	// fused residual (k_residual_wls): per patch, the ring-1 cells (far side of its cut faces) whose
 	// primitive states and gradients it recomputes; patch-local index = [patch cells | ring 1]
@@ -85,7 +86,8 @@ struct Layout
 constexpr int FUSED_LDS_CELLS = 704;     ///< staged cells per patch: 704 x 112 B = 77 KB (2 blocks/CU)
 constexpr int FUSED_GLOBAL = 1 << 20;    ///< neighbour codes >= this are global internal ids + FUSED_GLOBAL
 
-/// whether cfg takes the fused residual kernel (WLS + MUSCL/unlimited linear, inviscid)
+/// whether cfg takes the fused residual kernel (WLS + MUSCL/unlimited linear, inviscid). On a
+/// partitioned mesh, ghost cells in a patch's ring 1 take their received gradients.
 bool fusedEligible(const fvhip_flow_config& cfg);
 /// builds the fz_* arrays (owned-only meshes)
 void buildFused(Layout& Lo);
