@@ -208,6 +208,7 @@ struct fvhip_ctx
 	void stage_fused(const double* u, double* r, bool dt, double* dtm, bool overwrite) {
 		SweepBuffers B{};
 		B.u = u; B.r = r; B.dtm = dtm; B.overwrite = overwrite ? 1 : 0;
+		B.grad = d_grad;     // received gradients of ghost cells (partitioned meshes)
 		const char* nm = nullptr;
 		timed("k_residual_wls", [&]{ nm = KOPS(launch_residual_wls)(M, P, B, cfg.conv_numflux, recKind(), dt, stream); });
 		if(prof && !recs.empty() && recs.back().name == "k_residual_wls" && nm) recs.back().name = nm;
