@@ -42,6 +42,21 @@ def sweep_algorithmic_bytes(N, F, Fb):
     return 32 * F + 144 * N + 48 * Fb + 16 * N
 
 
+def residual_algorithmic_bytes(N, F, Fb):
+    """Compulsory bytes of the one-launch residual k_residual_wls (gradients computed in LDS, never
+    stored): 32 B/face (L,R 8 + nx,ny,len 24) + 128 B/cell (conserved state 32 + centre 16 + WLS
+    inverse 32 + area 8 read; residual 32 + time step 8 written) + 16 B/boundary face (ghost centre;
+    the ghost state is computed in registers)."""
+    return 32 * F + 128 * N + 16 * Fb
+
+
+def kernel_bytes(label, N, F, Fb):
+    """algorithmic bytes of one launch of the kernel `label` (profiling name)"""
+    if label.startswith("k_residual_wls"):
+        return residual_algorithmic_bytes(N, F, Fb)
+    return sweep_algorithmic_bytes(N, F, Fb)
+
+
 def kernel_symbol(label):
     """profiling label -> rocprofv3 kernel symbol suffix of the Roe/MUSCL/dt instantiation"""
     if label.startswith("k_residual_wls"):
@@ -164,7 +179,7 @@ def main():
     t_setup = time.time() - t0
     ms_per_step, kernels_ms, stats = measure(False)
     # this rank's algorithmic bytes (its owned cells, its faces incl. both copies of cut faces)
-    local_bytes = sweep_algorithmic_bytes(stats["cells"], stats["faces"], stats["bfaces"])
+    cnt = (stats["cells"], stats["faces"], stats["bfaces"])
 
     def dominant(km):
         k = max(km, key=km.get)
@@ -174,7 +189,7 @@ def main():
     if not args.no_fast:
         fms, fk, _ = measure(True)
         fname, fsms = dominant(fk)
-        fab = local_bytes / (fsms * 1e-3) / 1e9
+        fab = kernel_bytes(fname, *cnt) / (fsms * 1e-3) / 1e9
         ftr = pmc_traffic("fast::" + kernel_symbol(fname), N) if world == 1 else None
         fast = {"value": round(F / (fms * 1e-3) / 1e6, 3), "ms_per_step": round(fms, 5),
                 "traffic": int(ftr[0]) if ftr else None,
@@ -187,11 +202,12 @@ def main():
     sname, ssweep = [(k, v) for k, v in sk.items() if k.startswith("k_sweep")][0]
     staged = {"ms_per_step": round(sms, 5), "value": round(F / (sms * 1e-3) / 1e6, 3),
               "kernels_ms": {k: round(v, 5) for k, v in sk.items()},
-              "sweep_roofline_frac": round(local_bytes / (ssweep * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)}
+              "sweep_roofline_frac": round(sweep_algorithmic_bytes(*cnt) / (ssweep * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+              "sweep_algorithmic_bytes": sweep_algorithmic_bytes(*cnt)}
     sweep_name, sweep_ms = dominant(kernels_ms)
     sweep_name = [sweep_name]
 
-    ab = local_bytes
+    ab = kernel_bytes(sweep_name[0], *cnt)
     achieved = ab / (sweep_ms * 1e-3) / 1e9
     value = F / (ms_per_step * 1e-3) / 1e6       # every face of the (global) mesh once per step
 
