@@ -65,6 +65,38 @@ class FlowNumericsConfig:
     fast_math: bool = False
 
 
+@dataclass
+class ImplicitConfig:
+    """One pseudo-time solve (SteadySolverConfig, ode/aodesolver.hpp; control-file keys
+    pseudotime.{main,initialization}.*, controlparser.cpp:150-206) plus the linear-solver options of
+    the reference's .solverc files (include/fvhip.h fvhip_implicit_config)."""
+    cflinit: float = 50.0
+    cflfin: float = 3000.0
+    tol: float = 1e-8
+    maxiter: int = 100
+    matrix_free: bool = False       # -matrix_free_jacobian
+    mf_eps: float = 1e-7            # -matrix_free_difference_step
+    lin_rtol: float = 1e-2          # -ksp_rtol
+    lin_maxit: int = 30             # -ksp_max_it
+    restart: int = 30               # -ksp_gmres_restart
+    prec_sweeps: int = 1            # block-Jacobi sweeps per preconditioner application
+    min_relax: float = 1.0          # nonlinear_update_scheme: >= 1 "full", else "robust_flow" factor
+
+    def _struct(self):
+        c = _ffi.FvImplicitConfig()
+        c.cflinit, c.cflfin, c.tol, c.maxiter = float(self.cflinit), float(self.cflfin), float(self.tol), int(self.maxiter)
+        c.matrix_free, c.mf_eps = int(self.matrix_free), float(self.mf_eps)
+        c.lin_rtol, c.lin_maxit, c.restart = float(self.lin_rtol), int(self.lin_maxit), int(self.restart)
+        c.prec_sweeps, c.min_relax = int(self.prec_sweeps), float(self.min_relax)
+        return c
+
+
+def _solve_stats(st, hist):
+    n = int(st.steps)
+    return dict(steps=n, converged=bool(st.converged), lin_iters=int(st.lin_iters), resratio=float(st.resratio),
+                cfl=float(st.cfl)), hist[:n]
+
+
 class UMesh:
     """Reference-indexed mesh built natively (mesh/mesh.hpp accessors as numpy arrays)."""
 
@@ -275,6 +307,25 @@ class FlowFV:
                                                            int(maxiter), iptr(steps), dptr(ratio), dptr(hist)))
         return int(steps[0]), float(ratio[0]), hist[:int(steps[0])]
 
+    def steady_backward_euler_device(self, d_u, cfg: ImplicitConfig):
+        """SteadyBackwardEulerSolver::solve on the device (aodesolver.cpp:363-638), linear systems by
+        device GMRES; returns (stats dict, residual-norm history)"""
+        st = _ffi.FvSolveStats()
+        hist = np.zeros(max(int(cfg.maxiter), 1))
+        c = cfg._struct()
+        check(_ffi.lib().fvhip_steady_backward_euler_device(self._h, ctypes.c_void_p(d_u), ctypes.byref(c),
+                                                            ctypes.byref(st), dptr(hist)))
+        return _solve_stats(st, hist)
+
+    def gmres_blocks_device(self, d_diag, d_lower, d_upper, d_b, d_x, rtol, maxit, restart=30, sweeps=1):
+        """x = A^-1 b by device GMRES + block-Jacobi sweeps on face blocks; returns (iterations, |b - A x|)"""
+        it = np.zeros(1, np.int32)
+        rn = np.zeros(1)
+        check(_ffi.lib().fvhip_gmres_blocks_device(self._h, *[ctypes.c_void_p(p) for p in
+                                                              (d_diag, d_lower, d_upper, d_b, d_x)],
+                                                   float(rtol), int(maxit), int(restart), int(sweeps), iptr(it), dptr(rn)))
+        return int(it[0]), float(rn[0])
+
     def matfree_set_state_device(self, d_u, d_r, d_mdt):
         check(_ffi.lib().fvhip_matfree_set_state_device(self._h, *[ctypes.c_void_p(p) for p in (d_u, d_r, d_mdt)]))
 
@@ -414,6 +465,32 @@ class FlowFVGroup:
         d = P(*(d_dts if d_dts else [0] * n))
         check(_ffi.lib().fvhip_group_compute_residual_device(self._g, u, r, int(gettimesteps), d,
                                                              1 if overwrite else 0))
+
+    def _ptrs(self, ps):
+        return (ctypes.c_void_p * len(self.sps))(*ps)
+
+    def steady_forward_euler_device(self, d_us, cfl, tol, maxiter):
+        steps = np.zeros(1, np.int32)
+        ratio = np.zeros(1)
+        hist = np.zeros(max(int(maxiter), 1))
+        check(_ffi.lib().fvhip_group_steady_forward_euler_device(self._g, self._ptrs(d_us), float(cfl), float(tol),
+                                                                 int(maxiter), iptr(steps), dptr(ratio), dptr(hist)))
+        return int(steps[0]), float(ratio[0]), hist[:int(steps[0])]
+
+    def steady_backward_euler_device(self, d_us, cfg: ImplicitConfig):
+        st = _ffi.FvSolveStats()
+        hist = np.zeros(max(int(cfg.maxiter), 1))
+        c = cfg._struct()
+        check(_ffi.lib().fvhip_group_steady_backward_euler_device(self._g, self._ptrs(d_us), ctypes.byref(c),
+                                                                  ctypes.byref(st), dptr(hist)))
+        return _solve_stats(st, hist)
+
+    def matfree_set_state_device(self, d_us, d_rs, d_mdts):
+        check(_ffi.lib().fvhip_group_matfree_set_state_device(self._g, self._ptrs(d_us), self._ptrs(d_rs),
+                                                              self._ptrs(d_mdts)))
+
+    def matfree_apply_device(self, d_xs, d_ys):
+        check(_ffi.lib().fvhip_group_matfree_apply_device(self._g, self._ptrs(d_xs), self._ptrs(d_ys)))
 
     def close(self):
         if getattr(self, "_g", None):

@@ -33,6 +33,20 @@ class FvFlowConfig(ctypes.Structure):
                 ("bc_type", c_int_p), ("bc_tag", c_int_p), ("bc_vals", c_dbl_p), ("fast_math", ctypes.c_int)]
 
 
+class FvImplicitConfig(ctypes.Structure):
+    _fields_ = [("cflinit", ctypes.c_double), ("cflfin", ctypes.c_double), ("tol", ctypes.c_double),
+                ("maxiter", ctypes.c_int), ("matrix_free", ctypes.c_int), ("mf_eps", ctypes.c_double),
+                ("lin_rtol", ctypes.c_double), ("lin_maxit", ctypes.c_int), ("restart", ctypes.c_int),
+                ("prec_sweeps", ctypes.c_int), ("min_relax", ctypes.c_double)]
+
+
+class FvSolveStats(ctypes.Structure):
+    _fields_ = [("steps", ctypes.c_int), ("converged", ctypes.c_int), ("lin_iters", ctypes.c_int),
+                ("resratio", ctypes.c_double), ("cfl", ctypes.c_double)]
+
+
+_vpp = ctypes.POINTER(ctypes.c_void_p)
+
 # name -> (restype, argtypes); kept in sync with include/fvhip.h (tests check every symbol)
 _SIGS = {
     "fvhip_last_error": (ctypes.c_char_p, []),
@@ -68,6 +82,19 @@ _SIGS = {
     "fvhip_assemble_jacobian_bsr": (ctypes.c_int, [ctypes.c_void_p, c_dbl_p, c_int_p, c_int_p, c_dbl_p]),
     "fvhip_steady_forward_euler_device": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_double,
                                                          ctypes.c_double, ctypes.c_int, c_int_p, c_dbl_p, c_dbl_p]),
+    "fvhip_group_steady_forward_euler_device": (ctypes.c_int, [ctypes.c_void_p, _vpp, ctypes.c_double,
+                                                               ctypes.c_double, ctypes.c_int, c_int_p, c_dbl_p,
+                                                               c_dbl_p]),
+    "fvhip_steady_backward_euler_device": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p,
+                                                          ctypes.POINTER(FvImplicitConfig),
+                                                          ctypes.POINTER(FvSolveStats), c_dbl_p]),
+    "fvhip_group_steady_backward_euler_device": (ctypes.c_int, [ctypes.c_void_p, _vpp,
+                                                                ctypes.POINTER(FvImplicitConfig),
+                                                                ctypes.POINTER(FvSolveStats), c_dbl_p]),
+    "fvhip_gmres_blocks_device": (ctypes.c_int, [ctypes.c_void_p] + [ctypes.c_void_p] * 5 +
+                                  [ctypes.c_double, ctypes.c_int, ctypes.c_int, ctypes.c_int, c_int_p, c_dbl_p]),
+    "fvhip_group_matfree_set_state_device": (ctypes.c_int, [ctypes.c_void_p, _vpp, _vpp, _vpp]),
+    "fvhip_group_matfree_apply_device": (ctypes.c_int, [ctypes.c_void_p, _vpp, _vpp]),
     "fvhip_matfree_set_state": (ctypes.c_int, [ctypes.c_void_p, c_dbl_p, c_dbl_p, c_dbl_p]),
     "fvhip_matfree_apply": (ctypes.c_int, [ctypes.c_void_p, c_dbl_p, c_dbl_p]),
     "fvhip_matfree_set_state_device": (ctypes.c_int, [ctypes.c_void_p] + [ctypes.c_void_p] * 3),

@@ -1,0 +1,401 @@
+/** \file ctx.hpp
+ * \brief The library handle (struct fvhip_ctx behind include/fvhip.h's fvhip_handle): device mesh,
+ *   state scratch, residual stages with the halo exchange, Jacobian and matrix-free operator, and the
+ *   work space of the implicit solver (implicit.cpp). Shared by fvhip_api.cpp and implicit.cpp.
+ * No exception crosses the ABI: entry points wrap their bodies in guard().
+ */
+#ifndef FVHIP_CTX_HPP
+#define FVHIP_CTX_HPP
+
+#include "../../include/fvhip.h"
+#include "layout.hpp"
+#include "kernels.hpp"
+#include "jacobian.hpp"
+#include "mesh.hpp"
+#include "partition.hpp"
+#include "halo.hpp"
+#include "ode.hpp"
+#include <rccl/rccl.h>
+#include <hip/hip_runtime.h>
+#include <cstring>
+#include <algorithm>
+#include <cmath>
+#include <string>
+#include <vector>
+#include <map>
+#include <stdexcept>
+#include <memory>
+#include <functional>
+
+#include "krylov.hpp"
+
+namespace fvhip_detail {
+
+inline thread_local std::string g_err;      ///< fvhip_last_error() text, shared by every TU
+
+struct HipError : std::runtime_error { using std::runtime_error::runtime_error; };
+
+inline void hipCheck(hipError_t e, const char* what) {
+	if(e != hipSuccess) throw HipError(std::string(what) + ": " + hipGetErrorString(e));
+}
+#define HC(x) hipCheck((x), #x)
+
+inline void ncclCheck(ncclResult_t e, const char* what) {
+	if(e != ncclSuccess) throw std::runtime_error(std::string(what) + ": " + ncclGetErrorString(e));
+}
+#define NC(x) ncclCheck((x), #x)
+
+template <typename F>
+inline int guard(F&& f) {
+	try { f(); return 0; }
+	catch(const std::exception& e) { g_err = e.what(); return 1; }
+	catch(...) { g_err = "unknown error"; return 1; }
+}
+
+template <typename T>
+inline T* upload(const std::vector<T>& v, std::vector<void*>& owned) {
+	if(v.empty()) return nullptr;
+	void* p = nullptr;
+	HC(hipMalloc(&p, v.size()*sizeof(T)));
+	HC(hipMemcpy(p, v.data(), v.size()*sizeof(T), hipMemcpyHostToDevice));
+	owned.push_back(p);
+	return static_cast<T*>(p);
+}
+
+inline double* dalloc(size_t n, std::vector<void*>& owned) {
+	if(n == 0) n = 1;
+	void* p = nullptr;
+	HC(hipMalloc(&p, n*sizeof(double)));
+	owned.push_back(p);
+	return static_cast<double*>(p);
+}
+
+/// interleave int pairs / 4-tuples for vector loads
+inline std::vector<int> pack2(const std::vector<int>& a, const std::vector<int>& b) {
+	std::vector<int> o(2*a.size());
+	for(size_t i = 0; i < a.size(); i++) { o[2*i] = a[i]; o[2*i+1] = b[i]; }
+	return o;
+}
+
+}
+
+using namespace fvhip;
+using namespace fvhip_detail;
+
+struct fvhip_ctx
+{
+	int device = 0;
+	hipStream_t stream = nullptr;
+	fvhip_flow_config cfg{};
+	std::vector<int> bc_type, bc_tag;
+	std::vector<double> bc_vals;
+	Layout L;
+	DevMesh M{};
+	DevPhys P{};
+	std::vector<void*> owned;
+	int* d_perm = nullptr;
+	// state scratch
+	double *d_u = nullptr, *d_up = nullptr, *d_grad = nullptr, *d_lgrad = nullptr, *d_phi = nullptr;
+	double *d_ubc = nullptr, *d_ug = nullptr, *d_r = nullptr, *d_dtm = nullptr;
+	// mat-free state
+	double *d_mf_u = nullptr, *d_mf_r = nullptr, *d_mf_mdt = nullptr, *d_mf_aux = nullptr, *d_mf_y = nullptr;
+	double mf_eps = 1e-7;
+	const double *mf_u = nullptr, *mf_r = nullptr, *mf_mdt = nullptr;   // device state of the operator
+	double *d_part = nullptr, *d_pm = nullptr;
+	double *d_rn_part = nullptr, *d_rn = nullptr;   // residual-norm reduction of the explicit driver
+	/// work space of the implicit solver (implicit.cpp), allocated on first use
+	struct ImplicitWork {
+		int m = 0;                                  ///< GMRES restart length the basis holds
+		double* V = nullptr;                        ///< Krylov basis [m+1][4*ncell]
+		double *z = nullptr, *aux = nullptr;        ///< [4*(ncell+nghost)]: operator inputs (ghost rows)
+		double *w = nullptr, *t = nullptr, *s = nullptr, *du = nullptr, *yg = nullptr;   ///< [4*ncell]
+		double *jd = nullptr, *jlo = nullptr, *jup = nullptr, *dinv = nullptr;            ///< 4x4 blocks
+		double *part = nullptr, *red = nullptr, *coef = nullptr, *pm = nullptr;           ///< reductions
+		double *h_red = nullptr, *h_coef = nullptr;                                      ///< pinned host
+	} iw;
+	std::vector<void*> owned_host;                  ///< pinned host allocations
+	// Jacobian
+	JacMesh J{};
+	bool jac_ready = false;
+	double *d_jb = nullptr, *d_jlo = nullptr, *d_jup = nullptr, *d_jdiag = nullptr;
+	std::vector<double> h_stage;
+	// partitioned meshes: halo exchange with the neighbour ranks (RCCL, or in-process for a group)
+	int rank = 0, nparts = 1;
+	bool use_staged = false;      ///< force the staged (gradient + sweep) path even if fused applies
+	ncclComm_t comm = nullptr;
+	bool in_group = false;
+	int* d_send = nullptr;
+	int* d_border = nullptr;
+	int nborder = 0;
+	double* d_sendbuf = nullptr;
+	int nsend = 0;
+	// profiling
+	bool prof = false;
+	struct Rec { std::string name; hipEvent_t a, b; };
+	std::vector<Rec> recs;
+	std::map<std::string, std::pair<double,int>> acc;
+
+	~fvhip_ctx() {
+		(void)hipSetDevice(device);
+		if(comm) (void)ncclCommDestroy(comm);
+		for(auto& r : recs) { (void)hipEventDestroy(r.a); (void)hipEventDestroy(r.b); }
+		for(void* p : owned) (void)hipFree(p);
+		for(void* p : owned_host) (void)hipHostFree(p);
+		if(stream) (void)hipStreamDestroy(stream);
+	}
+
+	template <typename F>
+	void timed(const std::string& name, F&& launch) {
+		if(!prof) { launch(); return; }
+		Rec r; r.name = name;
+		HC(hipEventCreate(&r.a)); HC(hipEventCreate(&r.b));
+		HC(hipEventRecord(r.a, stream));
+		launch();
+		HC(hipEventRecord(r.b, stream));
+		recs.push_back(r);
+	}
+	void collect() {
+		HC(hipStreamSynchronize(stream));
+		for(auto& r : recs) {
+			float ms = 0;
+			HC(hipEventElapsedTime(&ms, r.a, r.b));
+			auto& a = acc[r.name]; a.first += ms; a.second += 1;
+			(void)hipEventDestroy(r.a); (void)hipEventDestroy(r.b);
+		}
+		recs.clear();
+	}
+
+	/// kernels of the selected numerics mode (exact: bitwise parity; fast: stated tolerance)
+#define KOPS(fn) (cfg.fast_math ? fast::fn : exact::fn)
+	int recKind() const {
+		if(!cfg.order2) return SR_FIRST;
+		return cfg.reconstruction == FVHIP_REC_VANALBADA ? SR_MUSCL : SR_LINEAR;
+	}
+	int viscKind() const {
+		if(!cfg.viscous_sim) return SV_NONE;
+		return cfg.const_visc ? SV_CONST : SV_SUTHERLAND;
+	}
+
+	bool halo() const { return !L.nbr_rank.empty(); }
+	int ntotal() const { return L.ncell + L.nghost; }
+
+	// --- residual stages (FlowFV::compute_residual, flow_spatial.cpp:636-816); between them the
+	// ghost rows of u, of the gradients and of limiter data are exchanged on partitioned meshes ---
+	void stage_gradients(const double* u) {
+		if(L.nghost > 0)
+			timed("k_ghost_prim", [&]{ launch_cons2prim_rows(P.gas, u, d_up, L.ncell, L.nghost, stream); });
+		if(cfg.gradientscheme == FVHIP_GRAD_LEASTSQUARES) {
+			timed("k_prep_grad_wls", [&]{ KOPS(launch_prep_grad_wls)(M, P, u, d_up, d_ubc, d_ug, d_grad, stream); });
+		} else {
+			timed("k_prep", [&]{ KOPS(launch_prep)(M, P, u, d_up, d_ubc, d_ug, true, stream); });
+			if(cfg.gradientscheme == FVHIP_GRAD_GREENGAUSS)
+				timed("k_grad_gg", [&]{ KOPS(launch_grad_gg)(M, d_up, d_ug, d_grad, stream); });
+			else KOPS(launch_fill)(d_grad, 0.0, 8LL*ntotal(), stream);
+		}
+	}
+	bool limited() const {
+		return cfg.reconstruction == FVHIP_REC_BARTHJESPERSEN || cfg.reconstruction == FVHIP_REC_VENKATAKRISHNAN;
+	}
+	void stage_limiter() {
+		const int venk = cfg.reconstruction == FVHIP_REC_VENKATAKRISHNAN;
+		timed("k_limiter", [&]{ KOPS(launch_limiter)(M, P, venk, d_up, d_ug, d_grad, d_phi, stream); });
+	}
+	void stage_weno() { timed("k_weno", [&]{ KOPS(launch_weno)(M, P, d_grad, d_lgrad, stream); }); }
+	void stage_sweep(const double* u, double* r, bool dt, double* dtm, bool overwrite) {
+		const int rk = recKind();
+		SweepBuffers B{};
+		B.u = u; B.r = r; B.dtm = dtm; B.overwrite = overwrite ? 1 : 0;
+		if(rk != SR_FIRST) {
+			B.up = d_up; B.grad = d_grad; B.rgrad = d_grad; B.ubc = d_ubc; B.ug = d_ug;
+			if(limited()) B.phi = d_phi;
+			if(cfg.reconstruction == FVHIP_REC_WENO) B.rgrad = d_lgrad;
+		}
+		const char* nm = nullptr;
+		// name is only known after launch; record under a generic label then rename
+		timed("k_sweep", [&]{ nm = KOPS(launch_sweep)(M, P, B, cfg.conv_numflux, rk, viscKind(), dt, stream); });
+		if(prof && !recs.empty() && recs.back().name == "k_sweep" && nm) recs.back().name = nm;
+		HC(hipGetLastError());
+	}
+
+	void stage_border_gradients(const double* u) {
+		timed("k_grad_wls_list", [&]{ KOPS(launch_grad_wls_list)(M, P, u, d_border, nborder, d_grad, stream); });
+	}
+
+	/// one-launch residual (WLS + MUSCL / unlimited linear, inviscid)
+	bool fused() const { return !L.fz_ext_start.empty() && !use_staged; }
+	void stage_fused(const double* u, double* r, bool dt, double* dtm, bool overwrite) {
+		SweepBuffers B{};
+		B.u = u; B.r = r; B.dtm = dtm; B.overwrite = overwrite ? 1 : 0;
+		B.grad = d_grad;     // received gradients of ghost cells (partitioned meshes)
+		const char* nm = nullptr;
+		timed("k_residual_wls", [&]{ nm = KOPS(launch_residual_wls)(M, P, B, cfg.conv_numflux, recKind(), dt, stream); });
+		if(prof && !recs.empty() && recs.back().name == "k_residual_wls" && nm) recs.back().name = nm;
+		HC(hipGetLastError());
+	}
+
+	/// pack the rows of `arr` (width doubles per cell) that the neighbours hold as ghosts
+	void pack(const double* arr, int width) {
+		timed("k_pack", [&]{ launch_pack_rows(d_send, nsend, arr, width, d_sendbuf, stream); });
+	}
+	/// RCCL point-to-point exchange with every neighbour rank, on this handle's stream
+	void exchange_rccl(double* arr, int width) {
+		if(!halo()) return;
+		if(!comm) throw std::runtime_error("partitioned handle: call fvhip_comm_init (or use a group) first");
+		pack(arr, width);
+		NC(ncclGroupStart());
+		for(size_t k = 0; k < L.nbr_rank.size(); k++) {
+			const int q = L.nbr_rank[k];
+			const size_t ns = static_cast<size_t>(L.send_start[k+1] - L.send_start[k]);
+			const size_t ng = static_cast<size_t>(L.ghost_start[k+1] - L.ghost_start[k]);
+			NC(ncclSend(d_sendbuf + static_cast<size_t>(width)*L.send_start[k], width*ns, ncclDouble, q, comm, stream));
+			NC(ncclRecv(arr + static_cast<size_t>(width)*(L.ncell + L.ghost_start[k]), width*ng, ncclDouble, q, comm, stream));
+		}
+		NC(ncclGroupEnd());
+	}
+
+	/// the device sweep: -r(u) added (or written) into r, time steps into dtm. On a partitioned
+	/// mesh u must have room for the ghost rows (ncell+nghost rows), which this fills.
+	void residual(const double* u, double* r, bool dt, double* dtm, bool overwrite) {
+		std::vector<fvhip_ctx*> one{this};
+		residual_seq(one, {u}, {r}, dt, {dtm}, overwrite, GroupExchange());
+	}
+
+	typedef std::function<double*(size_t)> ArrayOf;
+	typedef std::function<void(const ArrayOf&, int)> GroupExchange;
+
+	/// The residual as a sequence of stages over one or several handles (several: the ranks of a
+	/// partition held by one process, exchanging through device copies, see fvhip_group_*)
+	static void residual_seq(std::vector<fvhip_ctx*>& hs, const std::vector<const double*>& us,
+	                         const std::vector<double*>& rs, bool dt, const std::vector<double*>& dts,
+	                         bool overwrite, const GroupExchange& exg) {
+		auto exchange = [&](const ArrayOf& arr_of, int width) {
+			if(exg) { exg(arr_of, width); return; }
+			for(size_t i = 0; i < hs.size(); i++) hs[i]->exchange_rccl(arr_of(i), width);
+		};
+		fvhip_ctx* h0 = hs[0];
+		if(h0->fused()) {
+			if(h0->halo()) {
+				// ghost rows of u, then the gradients of the cells other ranks hold as ghosts
+				exchange([&](size_t i) { return const_cast<double*>(us[i]); }, 4);
+				for(size_t i = 0; i < hs.size(); i++) hs[i]->stage_border_gradients(us[i]);
+				exchange([&](size_t i) { return hs[i]->d_grad; }, 8);
+			}
+			for(size_t i = 0; i < hs.size(); i++) hs[i]->stage_fused(us[i], rs[i], dt, dts[i], overwrite);
+			return;
+		}
+		exchange([&](size_t i) { return const_cast<double*>(us[i]); }, 4);
+		if(h0->recKind() != SR_FIRST) {
+			for(size_t i = 0; i < hs.size(); i++) hs[i]->stage_gradients(us[i]);
+			exchange([&](size_t i) { return hs[i]->d_grad; }, 8);
+			if(h0->limited()) {
+				for(fvhip_ctx* h : hs) h->stage_limiter();
+				exchange([&](size_t i) { return hs[i]->d_phi; }, 4);
+			}
+			if(h0->cfg.reconstruction == FVHIP_REC_WENO) {
+				for(fvhip_ctx* h : hs) h->stage_weno();
+				exchange([&](size_t i) { return hs[i]->d_lgrad; }, 8);
+			}
+		}
+		for(size_t i = 0; i < hs.size(); i++) hs[i]->stage_sweep(us[i], rs[i], dt, dts[i], overwrite);
+	}
+
+	/// face-ordered mesh view and block buffers for the Jacobian, built on first use
+	void ensureJacobian() {
+		const int jf = cfg.conv_numflux_jac;
+		if(jf == FVHIP_FLUX_VANLEER) throw std::runtime_error(" ! VanLeerFlux: Not implemented!");   // anumericalflux.cpp:253-257
+		if(jf == FVHIP_FLUX_AUSMPLUS) throw std::runtime_error(" ! AUSMPlusFlux: Not implemented!"); // :556-560
+		if(jf < 0 || jf > 6) throw std::invalid_argument("unknown Jacobian flux");
+		for(int i = 0; i < cfg.nbc; i++)
+			if(bc_type[i] == FVHIP_BC_SUBSONIC_INFLOW)   // InFlow::computeGhostStateAndJacobian, abc.cpp:178-185
+				throw std::runtime_error("subsonic inflow BC has no Jacobian (Not implemented!)");
+		if(jac_ready) return;
+		auto& o = owned;
+		J.ncell = L.ncell; J.nbface = L.nbface; J.ninface = L.ninface;
+		J.if_LR = reinterpret_cast<const int2*>(upload(pack2(L.if_L, L.if_R), o));
+		J.if_n = reinterpret_cast<const double2*>(upload(L.if_n, o));
+		J.if_len = upload(L.if_len, o);
+		J.bf_L = M.bf_L; J.bf_bc = M.bf_bc; J.bf_n = M.bf_n; J.bf_rcbp = M.bf_rcbp; J.rc = M.rc;
+		J.bf_len = upload(L.bf_len, o);
+		J.cell_rfaces = reinterpret_cast<const int4*>(upload(L.cell_rfaces, o));
+		J.cell_nbr_fo = M.cell_nbr_fo;
+		d_jb = dalloc(16*static_cast<size_t>(std::max(L.nbface,1)), o);
+		jac_ready = true;
+	}
+
+	/// Spatial::assemble_jacobian into (diag internal order, lower/upper reference face order)
+	void assemble(const double* u, double* diag, double* lower, double* upper) {
+		ensureJacobian();
+		timed("k_jac_faces", [&]{ launch_jac_faces(J, P, cfg.conv_numflux_jac, viscKind(), u, d_jb, lower, upper, stream); });
+		timed("k_jac_diag", [&]{ launch_jac_diag(J, d_jb, lower, upper, diag, stream); });
+		HC(hipGetLastError());
+	}
+
+	/// reduction scratch of the device drivers (global sums, GMRES coefficients)
+	void ensureReductions() {
+		if(iw.red) return;
+		auto& o = owned;
+		iw.red = dalloc(KRY_MAXK + 2, o); iw.coef = dalloc(KRY_MAXK + 2, o); iw.pm = dalloc(2, o);
+		iw.part = dalloc(kry_scratch(2), o);
+		for(double** hp : {&iw.h_red, &iw.h_coef}) {
+			void* p = nullptr;
+			HC(hipHostMalloc(&p, (KRY_MAXK + 2)*sizeof(double), hipHostMallocDefault));
+			owned_host.push_back(p);
+			*hp = static_cast<double*>(p);
+		}
+	}
+	/// operand buffers of the matrix-free operator and GMRES (ghost rows where an operator reads them)
+	void ensureVectors() {
+		ensureReductions();
+		if(iw.z) return;
+		const size_t N = static_cast<size_t>(L.ncell), NT = N + static_cast<size_t>(L.nghost);
+		auto& o = owned;
+		iw.z = dalloc(4*NT, o); iw.aux = dalloc(4*NT, o);
+		iw.w = dalloc(4*N, o); iw.t = dalloc(4*N, o); iw.s = dalloc(4*N, o); iw.du = dalloc(4*N, o);
+		iw.yg = dalloc(4*N, o);
+	}
+	/// implicit-solver work space for GMRES(m): the above, the Jacobian blocks and the Krylov basis
+	void ensureImplicit(int m) {
+		ensureJacobian();
+		if(m < 1) throw std::invalid_argument("GMRES restart length must be positive");
+		ensureVectors();
+		const size_t N = static_cast<size_t>(L.ncell);
+		const size_t Fi = static_cast<size_t>(std::max(L.ninface, 1));
+		auto& o = owned;
+		if(m > KRY_MAXK) throw std::invalid_argument("GMRES restart length exceeds " + std::to_string(KRY_MAXK));
+		if(!iw.jd) {
+			iw.jd = dalloc(16*N, o); iw.jlo = dalloc(16*Fi, o); iw.jup = dalloc(16*Fi, o); iw.dinv = dalloc(16*N, o);
+		}
+		if(iw.m < m) {                  // a larger basis: the old one stays owned until destroy
+			iw.V = dalloc(4*N*static_cast<size_t>(m + 1), o);
+			iw.part = dalloc(kry_scratch(m + 2), o);
+			iw.m = m;
+		}
+	}
+
+	/// MatrixFreeSpatialJacobian::apply on device vectors (internal order), single domain (the
+	/// partitioned operator is sys_matfree, implicit.cpp)
+	void matfree(const double* x, double* y) {
+		if(!mf_u || !mf_r || !mf_mdt) throw std::runtime_error("matrix-free operator: state not set");
+		const size_t N = static_cast<size_t>(L.ncell);
+		if(!d_part) { d_part = dalloc(mf_partials(), owned); d_pm = dalloc(2, owned); }
+		if(!d_mf_aux) { d_mf_aux = dalloc(4*N, owned); d_mf_y = dalloc(4*N, owned); }
+		timed("k_mf_norm", [&]{ launch_mf_norm(4LL*L.ncell, x, mf_eps, d_part, d_pm, stream); });
+		timed("k_mf_perturb", [&]{ launch_mf_perturb(4LL*L.ncell, mf_u, x, d_pm, d_mf_aux, stream); });
+		residual(d_mf_aux, d_mf_y, false, nullptr, true);
+		timed("k_mf_combine", [&]{ launch_mf_combine(L.ncell, mf_mdt, x, d_mf_y, mf_r, d_pm, y, stream); });
+		HC(hipGetLastError());
+	}
+};
+
+/// all ranks of one partition driven from one process (fvhip_group_*)
+struct fvhip_group_s { std::vector<fvhip_ctx*> hs; };
+
+namespace fvhip_detail {
+/// in-process halo transport of a group: pack on every rank, then device copies into the ghost blocks
+fvhip_ctx::GroupExchange groupExchange(const fvhip_group_s* g);
+/// MatrixFreeSpatialJacobian::apply over all ranks of a partition (global |x|), implicit.cpp
+void sysMatfree(const std::vector<fvhip_ctx*>& hs, const fvhip_ctx::GroupExchange& exg,
+                const std::vector<const double*>& x, const std::vector<double*>& y);
+}
+
+#endif

@@ -1,0 +1,417 @@
+/** \file implicit.cpp
+ * \brief Device-resident pseudo-time solvers over one global system:
+ *   SteadyForwardEulerSolver::solve (aodesolver.cpp:135-282) and SteadyBackwardEulerSolver::solve
+ *   (aodesolver.cpp:363-638), plus the partitioned matrix-free operator.
+ *
+ * The reference hands each linear system to PETSc (KSPSolve, aodesolver.cpp:483; GMRES with a
+ * block-Jacobi/ILU or SOR preconditioner from the .solverc files). Here it is solved on the device
+ * by restarted GMRES: right-preconditioned (the residual it monitors is the true one), classical
+ * Gram-Schmidt with one re-orthogonalisation (two fused multi-dot reductions, i.e. two small host
+ * round trips, per Arnoldi step instead of j+1 with modified Gram-Schmidt), preconditioned by
+ * block-Jacobi sweeps on the assembled first-order Jacobian. PETSc's ILU/SOR are sequential
+ * recurrences; a block-Jacobi sweep is one launch over all cells, and several sweeps approach the
+ * block Gauss-Seidel effect. The matrix-free operator (alinalg.cpp:142-233) uses the assembled
+ * blocks as preconditioner, as the reference's KSPSetOperators(A_mf, M) does (casesolvers.cpp:170).
+ *
+ * A system is either one handle (one GPU, or one rank of a partition with its RCCL communicator:
+ * partial sums combined by ncclAllReduce) or all ranks of a partition driven from one process (a
+ * group: halo rows by device copies, partial sums added on the host in handle order).
+ */
+#include "ctx.hpp"
+
+#include <cmath>
+#include <vector>
+
+namespace fvhip_detail {
+
+struct System
+{
+	std::vector<fvhip_ctx*> hs;
+	fvhip_ctx::GroupExchange exg;        ///< in-process halo transport of a group, else empty
+
+	size_t size() const { return hs.size(); }
+	bool halo() const { return hs[0]->halo(); }
+	template <typename F> void each(F&& f) {
+		for(size_t i = 0; i < hs.size(); i++) { HC(hipSetDevice(hs[i]->device)); f(i, hs[i]); }
+	}
+	void exchange(const fvhip_ctx::ArrayOf& arr, int width) {
+		if(!halo()) return;
+		if(exg) { exg(arr, width); return; }
+		each([&](size_t i, fvhip_ctx* h) { h->exchange_rccl(arr(i), width); });
+	}
+	/// global sums of the k values every handle left in its iw.red: returned on the host and, if
+	/// to_device, present in every handle's iw.red afterwards
+	std::vector<double> allsum(int k, bool to_device) {
+		each([&](size_t, fvhip_ctx* h) {
+			if(h->comm) NC(ncclAllReduce(h->iw.red, h->iw.red, k, ncclDouble, ncclSum, h->comm, h->stream));
+			HC(hipMemcpyAsync(h->iw.h_red, h->iw.red, k*sizeof(double), hipMemcpyDeviceToHost, h->stream));
+		});
+		std::vector<double> tot(k, 0.0);
+		each([&](size_t, fvhip_ctx* h) {
+			HC(hipStreamSynchronize(h->stream));
+			for(int j = 0; j < k; j++) tot[j] += h->iw.h_red[j];
+		});
+		if(hs.size() > 1 && to_device)
+			each([&](size_t, fvhip_ctx* h) {
+				std::copy(tot.begin(), tot.end(), h->iw.h_red);
+				HC(hipMemcpyAsync(h->iw.red, h->iw.h_red, k*sizeof(double), hipMemcpyHostToDevice, h->stream));
+			});
+		return tot;
+	}
+	void sync() { each([&](size_t, fvhip_ctx* h) { HC(hipStreamSynchronize(h->stream)); }); }
+};
+
+typedef fvhip_ctx::ArrayOf ArrayOf;
+
+/// MatrixFreeSpatialJacobian::apply (alinalg.cpp:142-233) over a system: |x| is the global norm,
+/// the perturbed state gets its ghost rows from the residual's own exchange
+static void matfreeApply(System& S, const ArrayOf& x, const ArrayOf& y)
+{
+	S.each([&](size_t i, fvhip_ctx* h) {
+		if(!h->mf_u || !h->mf_r || !h->mf_mdt) throw std::runtime_error("matrix-free operator: state not set");
+		launch_mdot(4LL*h->L.ncell, 0, nullptr, 0, x(i), true, h->iw.part, h->iw.red, h->stream);
+	});
+	S.allsum(1, true);
+	std::vector<const double*> aux;
+	std::vector<double*> yg, none(S.size(), nullptr);
+	S.each([&](size_t i, fvhip_ctx* h) {
+		launch_pertmag(h->iw.red, h->mf_eps, h->iw.pm, h->stream);
+		launch_mf_perturb(4LL*h->L.ncell, h->mf_u, x(i), h->iw.pm, h->iw.aux, h->stream);
+		aux.push_back(h->iw.aux);
+		yg.push_back(h->iw.yg);
+	});
+	fvhip_ctx::residual_seq(S.hs, aux, yg, false, none, true, S.exg);
+	S.each([&](size_t i, fvhip_ctx* h) {
+		launch_mf_combine(h->L.ncell, h->mf_mdt, x(i), h->iw.yg, h->mf_r, h->iw.pm, y(i), h->stream);
+		HC(hipGetLastError());
+	});
+}
+
+/// The linear operator and preconditioner of one implicit step
+struct LinOp
+{
+	System& S;
+	bool matfree = false;
+	int sweeps = 1;
+	std::vector<const double*> D, Lo, Up;     ///< per handle: diagonal / lower / upper blocks
+
+	/// y = A x with the assembled blocks; x has ghost rows, which are filled here
+	void blocks(const ArrayOf& x, const ArrayOf& y) {
+		S.exchange(x, 4);
+		S.each([&](size_t i, fvhip_ctx* h) {
+			h->timed("k_block_apply", [&]{ launch_block_apply(h->J, D[i], Lo[i], Up[i], x(i), y(i), h->stream); });
+		});
+	}
+	void apply(const ArrayOf& x, const ArrayOf& y) {
+		if(matfree) matfreeApply(S, x, y);
+		else blocks(x, y);
+	}
+	/// z = M^-1 v: `sweeps` block-Jacobi sweeps on A z = v from z = 0 (z has ghost rows)
+	void precondition(const ArrayOf& v, const ArrayOf& z) {
+		S.each([&](size_t i, fvhip_ctx* h) {
+			h->timed("k_bjac_apply", [&]{ launch_bjac_apply(h->L.ncell, h->iw.dinv, v(i), z(i), h->stream); });
+		});
+		for(int s = 1; s < sweeps; s++) {
+			blocks(z, [&](size_t i) { return S.hs[i]->iw.t; });
+			S.each([&](size_t i, fvhip_ctx* h) {
+				h->timed("k_bjac_correct", [&]{ launch_bjac_correct(h->L.ncell, h->iw.dinv, v(i), h->iw.t, z(i), h->stream); });
+			});
+		}
+	}
+	/// block inverses of the current diagonal blocks
+	void setup() {
+		S.each([&](size_t i, fvhip_ctx* h) {
+			h->timed("k_bjac_invert", [&]{ launch_bjac_invert(h->L.ncell, D[i], h->iw.dinv, h->stream); });
+		});
+	}
+};
+
+struct GmresOut { int iters; double rnorm0, rnorm; };
+
+/// Restarted GMRES(m) for A x = b, x0 = 0; stops when |b - A x| <= rtol |b| or after maxit
+/// Arnoldi steps in total (KSPSolve with -ksp_rtol, -ksp_max_it, -ksp_gmres_restart)
+static GmresOut gmres(System& S, LinOp& A, const ArrayOf& b, const ArrayOf& x, double rtol, int maxit, int m)
+{
+	auto n4 = [&](size_t i) { return 4LL*S.hs[i]->L.ncell; };
+	auto V = [&](size_t i, int j) { return S.hs[i]->iw.V + static_cast<size_t>(j)*static_cast<size_t>(n4(i)); };
+	const ArrayOf z = [&](size_t i) { return S.hs[i]->iw.z; };
+	const ArrayOf w = [&](size_t i) { return S.hs[i]->iw.w; };
+	const ArrayOf sv = [&](size_t i) { return S.hs[i]->iw.s; };
+	auto norm = [&](const ArrayOf& v) {
+		S.each([&](size_t i, fvhip_ctx* h) { launch_mdot(n4(i), 0, nullptr, 0, v(i), true, h->iw.part, h->iw.red, h->stream); });
+		return std::sqrt(S.allsum(1, false)[0]);
+	};
+	S.each([&](size_t i, fvhip_ctx* h) { exact::launch_fill(x(i), 0.0, n4(i), h->stream); });
+	const double beta0 = norm(b);
+	GmresOut out{0, beta0, beta0};
+	if(!(beta0 > 0.0) || maxit <= 0) return out;
+
+	std::vector<double> H(static_cast<size_t>(m+1)*m, 0.0), cs(m), sn(m), g(m+1), y(m);
+	auto Hij = [&](int i, int j) -> double& { return H[static_cast<size_t>(j)*(m+1) + i]; };
+	double beta = beta0;
+	bool first = true;
+	while(true) {
+		if(first) S.each([&](size_t i, fvhip_ctx* h) { launch_axpby(n4(i), 1.0/beta, b(i), 0.0, V(i,0), h->stream); });
+		else {
+			// restart: r = b - A x (x into the ghosted operand buffer first)
+			S.each([&](size_t i, fvhip_ctx* h) {
+				HC(hipMemcpyAsync(z(i), x(i), n4(i)*sizeof(double), hipMemcpyDeviceToDevice, h->stream));
+			});
+			A.apply(z, w);
+			S.each([&](size_t i, fvhip_ctx* h) { launch_axpby(n4(i), 1.0, b(i), -1.0, w(i), h->stream); });
+			beta = norm(w);
+			out.rnorm = beta;
+			if(beta <= rtol*beta0) break;
+			S.each([&](size_t i, fvhip_ctx* h) { launch_axpby(n4(i), 1.0/beta, w(i), 0.0, V(i,0), h->stream); });
+		}
+		std::fill(g.begin(), g.end(), 0.0);
+		g[0] = beta;
+		int j = 0;
+		bool done = false;
+		while(j < m && out.iters < maxit) {
+			A.precondition([&](size_t i) { return V(i,j); }, z);
+			A.apply(z, w);
+			// classical Gram-Schmidt twice; the second pass also returns |w|^2 before its update
+			S.each([&](size_t i, fvhip_ctx* h) {
+				launch_mdot(n4(i), j+1, V(i,0), n4(i), w(i), false, h->iw.part, h->iw.red, h->stream);
+			});
+			const std::vector<double> h1 = S.allsum(j+1, true);
+			S.each([&](size_t i, fvhip_ctx* h) {
+				launch_maxpy(n4(i), j+1, V(i,0), n4(i), h->iw.red, w(i), h->stream);
+				launch_mdot(n4(i), j+1, V(i,0), n4(i), w(i), true, h->iw.part, h->iw.red, h->stream);
+			});
+			const std::vector<double> h2 = S.allsum(j+2, true);
+			S.each([&](size_t i, fvhip_ctx* h) { launch_maxpy(n4(i), j+1, V(i,0), n4(i), h->iw.red, w(i), h->stream); });
+			double corr = 0.0;
+			for(int k = 0; k <= j; k++) { Hij(k,j) = h1[k] + h2[k]; corr += h2[k]*h2[k]; }
+			double hn2 = h2[j+1] - corr;
+			if(!(hn2 > 1e-4*h2[j+1])) { const double t = norm(w); hn2 = t*t; }   // cancellation: measure
+			const double hn = std::sqrt(hn2);
+			Hij(j+1,j) = hn;
+			if(hn > 0.0) S.each([&](size_t i, fvhip_ctx* h) { launch_axpby(n4(i), 1.0/hn, w(i), 0.0, V(i,j+1), h->stream); });
+			// Givens rotations of the Hessenberg column
+			for(int k = 0; k < j; k++) {
+				const double t = cs[k]*Hij(k,j) + sn[k]*Hij(k+1,j);
+				Hij(k+1,j) = -sn[k]*Hij(k,j) + cs[k]*Hij(k+1,j);
+				Hij(k,j) = t;
+			}
+			const double d = std::hypot(Hij(j,j), Hij(j+1,j));
+			cs[j] = d > 0.0 ? Hij(j,j)/d : 1.0;
+			sn[j] = d > 0.0 ? Hij(j+1,j)/d : 0.0;
+			Hij(j,j) = d; Hij(j+1,j) = 0.0;
+			g[j+1] = -sn[j]*g[j];
+			g[j] = cs[j]*g[j];
+			j++;
+			out.iters++;
+			out.rnorm = std::fabs(g[j]);
+			if(!std::isfinite(out.rnorm)) throw std::runtime_error("GMRES: non-finite residual");
+			if(out.rnorm <= rtol*beta0 || hn == 0.0) { done = true; break; }
+		}
+		// x += M^-1 V y with H y = g (upper triangular after the rotations)
+		for(int k = j-1; k >= 0; k--) {
+			double s = g[k];
+			for(int l = k+1; l < j; l++) s -= Hij(k,l)*y[l];
+			y[k] = s/Hij(k,k);
+		}
+		S.each([&](size_t i, fvhip_ctx* h) {
+			std::copy(y.begin(), y.begin() + j, h->iw.h_coef);
+			HC(hipMemcpyAsync(h->iw.coef, h->iw.h_coef, j*sizeof(double), hipMemcpyHostToDevice, h->stream));
+			launch_lincomb(n4(i), j, V(i,0), n4(i), h->iw.coef, sv(i), h->stream);
+		});
+		A.precondition(sv, z);
+		S.each([&](size_t i, fvhip_ctx* h) { launch_axpby(n4(i), 1.0, z(i), 1.0, x(i), h->stream); });
+		S.sync();            // h_coef is rewritten by the next cycle
+		if(done || out.iters >= maxit) break;
+		first = false;
+	}
+	return out;
+}
+
+/// SteadySolver::expResidualRamp (aodesolver.cpp:110-120)
+static double expResidualRamp(double cflmin, double cflmax, double prevcfl, double resratio,
+                              double paramup, double paramdown)
+{
+	const double newcfl = resratio > 1.0 ? prevcfl * std::pow(resratio, paramup)
+		: prevcfl * std::pow(resratio, paramdown);
+	if(newcfl < cflmin) return cflmin;
+	else if(newcfl > cflmax) return cflmax;
+	else return newcfl;
+}
+
+static void checkImplicit(const fvhip_implicit_config& c)
+{
+	if(c.restart < 1 || c.restart > KRY_MAXK) throw std::invalid_argument("restart must be in [1, 128]");
+	if(c.prec_sweeps < 1) throw std::invalid_argument("prec_sweeps must be >= 1");
+	if(!(c.min_relax > 0.0)) throw std::domain_error("Minimum relaxation factor is invalid!");  // nonlinearrelaxation.cpp:20-21
+	if(c.matrix_free && !(c.mf_eps > 0.0)) throw std::invalid_argument("matrix-free difference step must be positive");
+}
+
+/// SteadyBackwardEulerSolver::solve (aodesolver.cpp:363-638) on device states us (internal order,
+/// ghost rows included on partitioned handles)
+static void backwardEuler(System& S, const std::vector<double*>& us, const fvhip_implicit_config& c,
+                          fvhip_solve_stats* st, double* hist)
+{
+	checkImplicit(c);
+	S.each([&](size_t, fvhip_ctx* h) { h->ensureImplicit(c.restart); h->mf_eps = c.mf_eps; });
+	LinOp A{S};
+	A.matfree = c.matrix_free != 0;
+	A.sweeps = c.prec_sweeps;
+	for(fvhip_ctx* h : S.hs) { A.D.push_back(h->iw.jd); A.Lo.push_back(h->iw.jlo); A.Up.push_back(h->iw.jup); }
+	std::vector<const double*> cu(us.begin(), us.end());
+	std::vector<double*> rs, dts;
+	for(fvhip_ctx* h : S.hs) { rs.push_back(h->d_r); dts.push_back(h->d_dtm); }
+	const ArrayOf bs = [&](size_t i) { return S.hs[i]->d_r; };
+	const ArrayOf xs = [&](size_t i) { return S.hs[i]->iw.du; };
+
+	double curCFL = 0, resi = 1.0, resiold = 1.0, initres = 1.0;
+	int step = 0, lin = 0;
+	while(resi/initres > c.tol && step < c.maxiter) {
+		// r = 0 + (-r(u)) with local time steps (:421-452); fills the ghost rows of u
+		fvhip_ctx::residual_seq(S.hs, cu, rs, true, dts, true, S.exg);
+		S.each([&](size_t i, fvhip_ctx* h) { h->assemble(us[i], h->iw.jd, h->iw.jlo, h->iw.jup); });   // :456-457
+		curCFL = expResidualRamp(c.cflinit, c.cflfin, curCFL, resiold/resi, 0.25, 0.3);           // :462
+		S.each([&](size_t, fvhip_ctx* h) {                                                          // :467
+			h->timed("k_pseudo_time", [&]{ launch_pseudo_time(h->L.ncell, h->M.area, curCFL, h->d_dtm, h->iw.jd, h->stream); });
+		});
+		A.setup();
+		if(A.matfree)                                                                               // :386-394
+			S.each([&](size_t i, fvhip_ctx* h) { h->mf_u = us[i]; h->mf_r = h->d_r; h->mf_mdt = h->d_dtm; });
+		const GmresOut g = gmres(S, A, bs, xs, c.lin_rtol, c.lin_maxit, c.restart);                  // :483
+		lin += g.iters;
+		S.each([&](size_t i, fvhip_ctx* h) {                                                        // :494-512
+			launch_relaxed_update(h->L.ncell, h->P.gas, c.min_relax, h->iw.du, us[i], h->stream);
+			launch_energy_sumsq(h->L.ncell, h->d_r, h->M.area, h->iw.part, h->iw.red, h->stream);   // :516-526
+			HC(hipGetLastError());
+		});
+		resiold = resi;
+		resi = std::sqrt(S.allsum(1, false)[0]);                                                    // :528-530
+		if(!std::isfinite(resi))
+			throw std::runtime_error("Steady backward Euler diverged - residual is Nan or inf!");  // :533-534
+		if(step == 0) initres = resi;
+		step++;
+		if(hist) hist[step-1] = resi;
+	}
+	if(A.matfree) S.each([&](size_t, fvhip_ctx* h) { h->mf_u = h->mf_r = h->mf_mdt = nullptr; });
+	st->steps = step;
+	st->lin_iters = lin;
+	st->resratio = resi/initres;
+	st->converged = (step < c.maxiter && resi/initres <= c.tol) ? 1 : 0;                            // :618-632
+	st->cfl = curCFL;
+}
+
+/// SteadyForwardEulerSolver::solve (aodesolver.cpp:135-282): u += cflinit dtm/area r (the ramped
+/// CFL is only reported by the reference, :194, :208)
+static void forwardEuler(System& S, const std::vector<double*>& us, double cfl, double tol, int maxiter,
+                         int* steps, double* resratio, double* hist)
+{
+	S.each([&](size_t, fvhip_ctx* h) { h->ensureReductions(); });
+	std::vector<const double*> cu(us.begin(), us.end());
+	std::vector<double*> rs, dts;
+	for(fvhip_ctx* h : S.hs) { rs.push_back(h->d_r); dts.push_back(h->d_dtm); }
+	double resi = 1.0, initres = 1.0;
+	int step = 0;
+	while(resi/initres > tol && step < maxiter) {
+		fvhip_ctx::residual_seq(S.hs, cu, rs, true, dts, true, S.exg);                          // :180-189
+		S.each([&](size_t i, fvhip_ctx* h) {
+			launch_fe_update(h->L.ncell, h->d_r, h->d_dtm, h->M.area, cfl, us[i], h->stream);   // :204-209
+			launch_energy_sumsq(h->L.ncell, h->d_r, h->M.area, h->iw.part, h->iw.red, h->stream);
+			HC(hipGetLastError());
+		});
+		resi = std::sqrt(S.allsum(1, false)[0]);                                                  // :214-230
+		if(step == 0) initres = resi;
+		if(hist) hist[step] = resi;
+		step++;
+		if(!std::isfinite(resi))
+			throw std::runtime_error("Steady forward Euler diverged - residual is Nan or inf!");  // :250-251
+	}
+	if(steps) *steps = step;
+	if(resratio) *resratio = resi/initres;
+}
+
+static System single(fvhip_ctx* h)
+{
+	if(h->in_group) throw std::runtime_error("handle belongs to a group: use the fvhip_group_* entry point");
+	if(h->halo() && !h->comm) throw std::runtime_error("partitioned handle: call fvhip_comm_init (or use a group) first");
+	return System{{h}, {}};
+}
+
+static System ofGroup(fvhip_group_s* g) { return System{g->hs, groupExchange(g)}; }
+
+void sysMatfree(const std::vector<fvhip_ctx*>& hs, const fvhip_ctx::GroupExchange& exg,
+                const std::vector<const double*>& x, const std::vector<double*>& y)
+{
+	System S{hs, exg};
+	S.each([&](size_t, fvhip_ctx* h) { h->ensureVectors(); });
+	const ArrayOf xo = [&](size_t i) { return const_cast<double*>(x[i]); };
+	const ArrayOf yo = [&](size_t i) { return y[i]; };
+	matfreeApply(S, xo, yo);
+}
+
+}
+
+extern "C" {
+
+int fvhip_steady_backward_euler_device(fvhip_handle h, double* d_u, const fvhip_implicit_config* cfg,
+                                       fvhip_solve_stats* stats, double* reshistory)
+{
+	return guard([&] {
+		if(!cfg || !stats) throw std::invalid_argument("null argument");
+		System S = single(h);
+		backwardEuler(S, {d_u}, *cfg, stats, reshistory);
+		S.sync();
+	});
+}
+
+int fvhip_group_steady_backward_euler_device(fvhip_group g, double* const* d_u, const fvhip_implicit_config* cfg,
+                                             fvhip_solve_stats* stats, double* reshistory)
+{
+	return guard([&] {
+		if(!cfg || !stats) throw std::invalid_argument("null argument");
+		System S = ofGroup(g);
+		backwardEuler(S, std::vector<double*>(d_u, d_u + S.size()), *cfg, stats, reshistory);
+		S.sync();
+	});
+}
+
+int fvhip_steady_forward_euler_device(fvhip_handle h, double* d_u, double cfl, double tol, int maxiter,
+                                      int* steps, double* resratio, double* reshistory)
+{
+	return guard([&] {
+		System S = single(h);
+		forwardEuler(S, {d_u}, cfl, tol, maxiter, steps, resratio, reshistory);
+		S.sync();
+	});
+}
+
+int fvhip_group_steady_forward_euler_device(fvhip_group g, double* const* d_u, double cfl, double tol, int maxiter,
+                                            int* steps, double* resratio, double* reshistory)
+{
+	return guard([&] {
+		System S = ofGroup(g);
+		forwardEuler(S, std::vector<double*>(d_u, d_u + S.size()), cfl, tol, maxiter, steps, resratio, reshistory);
+		S.sync();
+	});
+}
+
+int fvhip_gmres_blocks_device(fvhip_handle h, const double* d_diag, const double* d_lower, const double* d_upper,
+                              const double* d_b, double* d_x, double rtol, int maxit, int restart, int sweeps,
+                              int* iters, double* resnorm)
+{
+	return guard([&] {
+		if(restart < 1 || restart > KRY_MAXK) throw std::invalid_argument("restart must be in [1, 128]");
+		if(sweeps < 1) throw std::invalid_argument("sweeps must be >= 1");
+		System S = single(h);
+		h->ensureImplicit(restart);
+		LinOp A{S};
+		A.sweeps = sweeps;
+		A.D = {d_diag}; A.Lo = {d_lower}; A.Up = {d_upper};
+		A.setup();
+		const GmresOut g = gmres(S, A, [&](size_t) { return const_cast<double*>(d_b); },
+		                         [&](size_t) { return d_x; }, rtol, maxit, restart);
+		S.sync();
+		if(iters) *iters = g.iters;
+		if(resnorm) *resnorm = g.rnorm;
+	});
+}
+
+}

@@ -1,0 +1,255 @@
+/** \file krylov.hip
+ * \brief Device linear algebra of the implicit pseudo-time solver (declarations and sources in
+ *   krylov.hpp). One thread per cell for the 4x4 block kernels (128 B of blocks and 64 B of
+ *   vectors per cell, HBM-bound); the multi-dot reads w once per group of KRY_GROUP basis vectors
+ *   and reduces with a fixed grid and a fixed tree, so every GMRES coefficient is reproducible.
+ */
+#include "krylov.hpp"
+
+namespace fvhip {
+
+constexpr int KRY_BLOCKS = 512;   ///< partial sums per dot product (= ode.hip's ODE_RED_BLOCKS)
+constexpr int KRY_GROUP = 4;      ///< dot products per block row of the multi-dot
+
+static inline int nblk(long long n, int b) { return static_cast<int>((n + b - 1)/b); }
+
+/// fixed-tree sum over the block of NV values per thread; thread 0 writes out[q*stride]
+template <int NV>
+__device__ __forceinline__ void block_sum(double (&acc)[NV], double* out, int stride)
+{
+	__shared__ double s[NV][256];
+	const int t = static_cast<int>(threadIdx.x);
+	#pragma unroll
+	for(int q = 0; q < NV; q++) s[q][t] = acc[q];
+	__syncthreads();
+	for(int w = 128; w > 0; w >>= 1) {
+		if(t < w) {
+			#pragma unroll
+			for(int q = 0; q < NV; q++) s[q][t] += s[q][t + w];
+		}
+		__syncthreads();
+	}
+	if(t == 0) {
+		#pragma unroll
+		for(int q = 0; q < NV; q++) out[q*stride] = s[q][0];
+	}
+}
+
+/// y = B x for a row-major 4x4 block
+__device__ __forceinline__ void blk_mv(const double* __restrict__ B, const double4 x, double* y)
+{
+	const double4* b4 = reinterpret_cast<const double4*>(B);
+	#pragma unroll
+	for(int i = 0; i < 4; i++) {
+		const double4 r = b4[i];
+		y[i] = r.x*x.x + r.y*x.y + r.z*x.z + r.w*x.w;
+	}
+}
+
+// -------------------------------------------------------------------------------------------------
+// point-block Jacobi
+// -------------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256)
+void k_bjac_invert(int n, const double* __restrict__ diag, double* __restrict__ dinv)
+{
+	const int c = blockIdx.x*blockDim.x + threadIdx.x;
+	if(c >= n) return;
+	double a[4][4], b[4][4];
+	const double4* d4 = reinterpret_cast<const double4*>(diag + 16*static_cast<size_t>(c));
+	#pragma unroll
+	for(int i = 0; i < 4; i++) {
+		const double4 v = d4[i];
+		a[i][0] = v.x; a[i][1] = v.y; a[i][2] = v.z; a[i][3] = v.w;
+		#pragma unroll
+		for(int j = 0; j < 4; j++) b[i][j] = i == j ? 1.0 : 0.0;
+	}
+	#pragma unroll
+	for(int k = 0; k < 4; k++) {
+		// bring the largest |a[i][k]|, i >= k, to row k with selects (static register indices only)
+		#pragma unroll
+		for(int i = k+1; i < 4; i++) {
+			const bool sw = fabs(a[i][k]) > fabs(a[k][k]);
+			#pragma unroll
+			for(int j = 0; j < 4; j++) {
+				const double ta = a[k][j], tb = b[k][j];
+				a[k][j] = sw ? a[i][j] : ta; a[i][j] = sw ? ta : a[i][j];
+				b[k][j] = sw ? b[i][j] : tb; b[i][j] = sw ? tb : b[i][j];
+			}
+		}
+		const double piv = 1.0/a[k][k];
+		#pragma unroll
+		for(int j = 0; j < 4; j++) { a[k][j] *= piv; b[k][j] *= piv; }
+		#pragma unroll
+		for(int i = 0; i < 4; i++) {
+			if(i == k) continue;
+			const double f = a[i][k];
+			#pragma unroll
+			for(int j = 0; j < 4; j++) { a[i][j] -= f*a[k][j]; b[i][j] -= f*b[k][j]; }
+		}
+	}
+	double4* o = reinterpret_cast<double4*>(dinv + 16*static_cast<size_t>(c));
+	#pragma unroll
+	for(int i = 0; i < 4; i++) o[i] = make_double4(b[i][0], b[i][1], b[i][2], b[i][3]);
+}
+
+__global__ __launch_bounds__(256)
+void k_bjac_apply(int n, const double* __restrict__ dinv, const double* __restrict__ x, double* __restrict__ y)
+{
+	const int c = blockIdx.x*blockDim.x + threadIdx.x;
+	if(c >= n) return;
+	double o[4];
+	blk_mv(dinv + 16*static_cast<size_t>(c), reinterpret_cast<const double4*>(x)[c], o);
+	reinterpret_cast<double4*>(y)[c] = make_double4(o[0], o[1], o[2], o[3]);
+}
+
+__global__ __launch_bounds__(256)
+void k_bjac_correct(int n, const double* __restrict__ dinv, const double* __restrict__ b,
+                    const double* __restrict__ y, double* __restrict__ z)
+{
+	const int c = blockIdx.x*blockDim.x + threadIdx.x;
+	if(c >= n) return;
+	const double4 bb = reinterpret_cast<const double4*>(b)[c], yy = reinterpret_cast<const double4*>(y)[c];
+	double o[4];
+	blk_mv(dinv + 16*static_cast<size_t>(c), make_double4(bb.x-yy.x, bb.y-yy.y, bb.z-yy.z, bb.w-yy.w), o);
+	double4 zz = reinterpret_cast<double4*>(z)[c];
+	zz.x += o[0]; zz.y += o[1]; zz.z += o[2]; zz.w += o[3];
+	reinterpret_cast<double4*>(z)[c] = zz;
+}
+
+// -------------------------------------------------------------------------------------------------
+// reductions and vector updates
+// -------------------------------------------------------------------------------------------------
+/// block row y of the grid: products j0 = KRY_GROUP*y .. j0+KRY_GROUP-1 (j == k is w . w)
+__global__ __launch_bounds__(256)
+void k_mdot_partial(long long n, int k, int kt, const double* __restrict__ V, long long ld,
+                    const double* __restrict__ w, double* __restrict__ part)
+{
+	const int j0 = KRY_GROUP*static_cast<int>(blockIdx.y);
+	const double* vp[KRY_GROUP];
+	#pragma unroll
+	for(int q = 0; q < KRY_GROUP; q++) vp[q] = (j0 + q < k) ? V + static_cast<long long>(j0 + q)*ld : w;
+	double acc[KRY_GROUP];
+	#pragma unroll
+	for(int q = 0; q < KRY_GROUP; q++) acc[q] = 0.0;
+	for(long long i = blockIdx.x*256LL + threadIdx.x; i < n; i += 256LL*gridDim.x) {
+		const double wi = w[i];
+		#pragma unroll
+		for(int q = 0; q < KRY_GROUP; q++) if(j0 + q < kt) acc[q] += vp[q][i]*wi;
+	}
+	block_sum<KRY_GROUP>(acc, part + static_cast<size_t>(j0)*KRY_BLOCKS + blockIdx.x, KRY_BLOCKS);
+}
+
+/// out[b] = sum of the np partials of product b (one block per product)
+__global__ __launch_bounds__(256)
+void k_sum_partials(int np, const double* __restrict__ part, double* __restrict__ out)
+{
+	const double* p = part + static_cast<size_t>(blockIdx.x)*np;
+	double acc[1] = {0.0};
+	for(int i = threadIdx.x; i < np; i += 256) acc[0] += p[i];
+	block_sum<1>(acc, out + blockIdx.x, 1);
+}
+
+__global__ __launch_bounds__(256)
+void k_maxpy(long long n, int k, const double* __restrict__ V, long long ld, const double* __restrict__ h,
+             double* __restrict__ w)
+{
+	const long long i = blockIdx.x*256LL + threadIdx.x;
+	if(i >= n) return;
+	double s = 0.0;
+	for(int j = 0; j < k; j++) s += h[j]*V[j*ld + i];
+	w[i] -= s;
+}
+
+__global__ __launch_bounds__(256)
+void k_lincomb(long long n, int k, const double* __restrict__ V, long long ld, const double* __restrict__ c,
+               double* __restrict__ out)
+{
+	const long long i = blockIdx.x*256LL + threadIdx.x;
+	if(i >= n) return;
+	double s = 0.0;
+	for(int j = 0; j < k; j++) s += c[j]*V[j*ld + i];
+	out[i] = s;
+}
+
+__global__ __launch_bounds__(256)
+void k_axpby(long long n, double a, const double* __restrict__ x, double b, double* __restrict__ y)
+{
+	const long long i = blockIdx.x*256LL + threadIdx.x;
+	if(i >= n) return;
+	y[i] = b == 0.0 ? a*x[i] : a*x[i] + b*y[i];
+}
+
+__global__ void k_pertmag(const double* __restrict__ sq, double eps, double* __restrict__ pm)
+{
+	if(threadIdx.x == 0 && blockIdx.x == 0) {
+		const double xnorm = sqrt(sq[0]);
+		pm[0] = xnorm;
+		pm[1] = eps/xnorm;
+	}
+}
+
+__global__ __launch_bounds__(256)
+void k_energy_partial(int n, const double* __restrict__ r, const double* __restrict__ area, double* __restrict__ part)
+{
+	double acc[1] = {0.0};
+	for(int e = blockIdx.x*256 + threadIdx.x; e < n; e += 256*gridDim.x)
+		acc[0] += r[4*static_cast<size_t>(e)+3]*r[4*static_cast<size_t>(e)+3]*area[e];
+	block_sum<1>(acc, part + blockIdx.x, 1);
+}
+
+__global__ __launch_bounds__(256)
+void k_relaxed_update(int n, gd::Gas G, double minfactor, const double* __restrict__ du, double* __restrict__ u)
+{
+	const int c = blockIdx.x*blockDim.x + threadIdx.x;
+	if(c >= n) return;
+	const double4 a = reinterpret_cast<const double4*>(u)[c];
+	const double4 d = reinterpret_cast<const double4*>(du)[c];
+	const double uu[4] = {a.x, a.y, a.z, a.w}, dd[4] = {d.x, d.y, d.z, d.w};
+	const double om = relaxation_factor(G, minfactor, dd, uu);
+	reinterpret_cast<double4*>(u)[c] = make_double4(uu[0] + om*dd[0], uu[1] + om*dd[1], uu[2] + om*dd[2],
+	                                                uu[3] + om*dd[3]);
+}
+
+// -------------------------------------------------------------------------------------------------
+// launchers
+// -------------------------------------------------------------------------------------------------
+void launch_bjac_invert(int n, const double* diag, double* dinv, hipStream_t s)
+{ if(n > 0) k_bjac_invert<<<nblk(n,256), 256, 0, s>>>(n, diag, dinv); }
+void launch_bjac_apply(int n, const double* dinv, const double* x, double* y, hipStream_t s)
+{ if(n > 0) k_bjac_apply<<<nblk(n,256), 256, 0, s>>>(n, dinv, x, y); }
+void launch_bjac_correct(int n, const double* dinv, const double* b, const double* y, double* z, hipStream_t s)
+{ if(n > 0) k_bjac_correct<<<nblk(n,256), 256, 0, s>>>(n, dinv, b, y, z); }
+
+size_t kry_scratch(int k)
+{
+	return static_cast<size_t>(KRY_BLOCKS)*static_cast<size_t>((k + KRY_GROUP)/KRY_GROUP*KRY_GROUP);
+}
+
+void launch_mdot(long long n, int k, const double* V, long long ld, const double* w, bool self,
+                 double* part, double* out, hipStream_t s)
+{
+	const int kt = k + (self ? 1 : 0);
+	if(kt <= 0) return;
+	k_mdot_partial<<<dim3(KRY_BLOCKS, (kt + KRY_GROUP - 1)/KRY_GROUP), 256, 0, s>>>(n, k, kt, V, ld, w, part);
+	k_sum_partials<<<kt, 256, 0, s>>>(KRY_BLOCKS, part, out);
+}
+
+void launch_maxpy(long long n, int k, const double* V, long long ld, const double* h, double* w, hipStream_t s)
+{ if(n > 0 && k > 0) k_maxpy<<<nblk(n,256), 256, 0, s>>>(n, k, V, ld, h, w); }
+void launch_lincomb(long long n, int k, const double* V, long long ld, const double* c, double* out, hipStream_t s)
+{ if(n > 0) k_lincomb<<<nblk(n,256), 256, 0, s>>>(n, k, V, ld, c, out); }
+void launch_axpby(long long n, double a, const double* x, double b, double* y, hipStream_t s)
+{ if(n > 0) k_axpby<<<nblk(n,256), 256, 0, s>>>(n, a, x, b, y); }
+void launch_pertmag(const double* sq, double eps, double* pm, hipStream_t s)
+{ k_pertmag<<<1, 64, 0, s>>>(sq, eps, pm); }
+
+void launch_energy_sumsq(int n, const double* r, const double* area, double* part, double* out, hipStream_t s)
+{
+	k_energy_partial<<<KRY_BLOCKS, 256, 0, s>>>(n, r, area, part);
+	k_sum_partials<<<1, 256, 0, s>>>(KRY_BLOCKS, part, out);
+}
+
+void launch_relaxed_update(int n, const gd::Gas& G, double minfactor, const double* du, double* u, hipStream_t s)
+{ if(n > 0) k_relaxed_update<<<nblk(n,256), 256, 0, s>>>(n, G, minfactor, du, u); }
+
+}

@@ -1,0 +1,73 @@
+/** \file krylov.hpp
+ * \brief Device linear algebra of the implicit pseudo-time solver (krylov.hip): the point-block
+ *   Jacobi preconditioner on the assembled 4x4 Jacobian blocks, deterministic multi-dot products
+ *   and multi-AXPYs for restarted GMRES, and the nonlinear update of
+ *   SteadyBackwardEulerSolver::solve (aodesolver.cpp:494-530, nonlinearrelaxation.cpp:24-38).
+ *
+ * They replace what the reference hands to PETSc (KSPSolve with GMRES and a block-Jacobi / SOR
+ * preconditioner, aodesolver.cpp:483, casesolvers.cpp:166-201), so that Krylov vectors never leave
+ * HBM. Every reduction uses a fixed partition and a fixed tree: results are
+ * bitwise reproducible from run to run.
+ */
+#ifndef FVHIP_KRYLOV_HPP
+#define FVHIP_KRYLOV_HPP
+
+#include <hip/hip_runtime.h>
+#include <cstddef>
+#include "gasdyn.hpp"
+
+namespace fvhip {
+
+constexpr int KRY_MAXK = 128;     ///< largest GMRES restart length
+
+/// FlowSimpleUpdate::getLocalRelaxationFactor (nonlinearrelaxation.cpp:24-38) with
+/// IdealGasPhysics::getDeltaPressureFromConserved (aphysics_defs.hpp:67-80) as written there: its
+/// momentum loop runs over i = 2 .. NDIM+1 (y-momentum and energy), and that is what is restated.
+/// minfactor >= 1 means FullUpdate (nonlinearrelaxation.hpp:32-38): omega = 1.
+FVHIP_HD double relaxation_factor(const gd::Gas& G, double minfactor, const double* du, const double* u)
+{
+	if(minfactor >= 1.0) return 1.0;
+	const double p = gd::pressure_cons(G, u);
+	double unew[4];
+	for(int i = 0; i < 4; i++) unew[i] = u[i] + du[i];
+	double dp = 0;
+	for(int i = 2; i < 4; i++)
+		dp -= ((u[i]+unew[i])*(u[0]+unew[0])/2.0*du[i] - (unew[i]*unew[i]+u[i]*u[i])/2.0*du[0]);
+	dp = (G.g-1.0)*(du[3] - 1.0/(2*u[0]*unew[0])*dp);
+	const double rdp = fabs(dp)/p;
+	const double drho = fabs(du[0])/u[0];
+	const double danger = rdp < drho ? drho : rdp;      // std::max(dp, drho)
+	double omega = minfactor;
+	if(danger < 1.0-minfactor) omega = 1.0-danger;
+	return omega;
+}
+
+/// dinv[c] = diag[c]^-1 (Gauss-Jordan with row pivoting), c < ncell
+void launch_bjac_invert(int ncell, const double* diag, double* dinv, hipStream_t s);
+/// y[c] = dinv[c] x[c]
+void launch_bjac_apply(int ncell, const double* dinv, const double* x, double* y, hipStream_t s);
+/// z[c] += dinv[c] (b[c] - y[c]): one block-Jacobi sweep on A z = b, given y = A z
+void launch_bjac_correct(int ncell, const double* dinv, const double* b, const double* y, double* z, hipStream_t s);
+
+/// doubles of scratch `part` launch_mdot needs for up to k products
+size_t kry_scratch(int k);
+/// out[j] = V_j . w for j < k (V_j = V + j*ld) and, if self, out[k] = w . w; fixed-order sums
+void launch_mdot(long long n, int k, const double* V, long long ld, const double* w, bool self,
+                 double* part, double* out, hipStream_t s);
+/// w -= sum_{j<k} h[j] V_j  (h: k doubles on the device; ascending j for every element)
+void launch_maxpy(long long n, int k, const double* V, long long ld, const double* h, double* w, hipStream_t s);
+/// out = sum_{j<k} c[j] V_j  (c on the device)
+void launch_lincomb(long long n, int k, const double* V, long long ld, const double* c, double* out, hipStream_t s);
+/// y = a*x + b*y  (b == 0: y = a*x and y is not read)
+void launch_axpby(long long n, double a, const double* x, double b, double* y, hipStream_t s);
+/// pm[0] = sqrt(sq[0]), pm[1] = eps/pm[0]: the matrix-free step from a global sum of squares
+/// (alinalg.cpp:159-167)
+void launch_pertmag(const double* sq, double eps, double* pm, hipStream_t s);
+/// out[0] = sum_e r[e][3]^2 area[e] (aodesolver.cpp:216-223, 516-526), fixed order
+void launch_energy_sumsq(int ncell, const double* r, const double* area, double* part, double* out, hipStream_t s);
+/// u[c] += omega(du[c], u[c]) du[c] (aodesolver.cpp:506-511)
+void launch_relaxed_update(int ncell, const gd::Gas& G, double minfactor, const double* du, double* u,
+                           hipStream_t s);
+
+}
+#endif

@@ -171,18 +171,68 @@ int fvhip_jacobian_pattern(fvhip_handle h, int* rowptr, int* colind);
 int fvhip_assemble_jacobian_bsr(fvhip_handle h, const double* u, const int* rowptr, const int* colind,
                                 double* vals);
 
-/** SteadyForwardEulerSolver::solve (aodesolver.cpp:170-240) on the device: explicit local-time-step
- *  iterations on d_u (internal order) until ||r||/||r0|| <= tol or maxiter steps; reshistory [maxiter]
- *  (may be NULL) receives the residual norms sqrt(sum r_energy^2 area) */
+/* ---------------------------------------------------------------------------------------------
+ * Pseudo-time solvers on the device. States are device arrays in the
+ * internal cell order; on partitioned handles they have owned + ghost rows. Partitioned handles
+ * need their RCCL communicator (fvhip_comm_init); the fvhip_group_* variants drive all ranks of a
+ * partition from one process.
+ * -------------------------------------------------------------------------------------------- */
+/** SteadyForwardEulerSolver::solve (aodesolver.cpp:135-282): explicit local-time-step iterations
+ *  u += cfl dtm/area r until ||r||/||r0|| <= tol or maxiter steps; reshistory [maxiter] (may be
+ *  NULL) receives the residual norms sqrt(sum r_energy^2 area) */
 int fvhip_steady_forward_euler_device(fvhip_handle h, double* d_u, double cfl, double tol, int maxiter,
                                       int* steps, double* resratio, double* reshistory);
+int fvhip_group_steady_forward_euler_device(fvhip_group g, double* const* d_u, double cfl, double tol, int maxiter,
+                                            int* steps, double* resratio, double* reshistory);
+
+/** SteadySolverConfig of the main (or starter) solve (aodesolver.hpp, controlparser.cpp:150-206) and
+ *  the linear-solver options of the reference's .solverc files */
+typedef struct fvhip_implicit_config {
+	double cflinit, cflfin;   /* pseudotime cfl_min / cfl_max (exponential ramp, aodesolver.cpp:110-120) */
+	double tol;               /* stop when ||r||/||r0|| <= tol */
+	int maxiter;              /* max_timesteps */
+	int matrix_free;          /* -matrix_free_jacobian: Krylov products by finite differences
+	                             (alinalg.cpp:142-233), the assembled blocks precondition */
+	double mf_eps;            /* -matrix_free_difference_step (reference default 1e-7) */
+	double lin_rtol;          /* -ksp_rtol: |b - A du| <= lin_rtol |b| */
+	int lin_maxit;            /* -ksp_max_it: Arnoldi steps per pseudo-time step */
+	int restart;              /* -ksp_gmres_restart (PETSc default 30; at most 128) */
+	int prec_sweeps;          /* block-Jacobi sweeps per preconditioner application (1: point-block Jacobi) */
+	double min_relax;         /* nonlinear_update_scheme: >= 1 "full"; else "robust_flow" with
+	                             min_nonlinear_relaxation_factor = min_relax (nonlinearrelaxation.cpp) */
+} fvhip_implicit_config;
+
+typedef struct fvhip_solve_stats {
+	int steps;                /* pseudo-time steps taken */
+	int converged;            /* the reference's test: steps < maxiter and ratio <= tol (aodesolver.cpp:618-632) */
+	int lin_iters;            /* total Krylov iterations */
+	double resratio;          /* final ||r||/||r0|| */
+	double cfl;               /* CFL of the last step */
+} fvhip_solve_stats;
+
+/** SteadyBackwardEulerSolver::solve (aodesolver.cpp:363-638) with the linear systems solved on the
+ *  device by restarted GMRES (instead of PETSc's KSPSolve, :483); reshistory [maxiter] may be NULL */
+int fvhip_steady_backward_euler_device(fvhip_handle h, double* d_u, const fvhip_implicit_config* cfg,
+                                       fvhip_solve_stats* stats, double* reshistory);
+int fvhip_group_steady_backward_euler_device(fvhip_group g, double* const* d_u, const fvhip_implicit_config* cfg,
+                                             fvhip_solve_stats* stats, double* reshistory);
+/** The linear solver alone: GMRES(restart) with `sweeps` block-Jacobi sweeps as right preconditioner
+ *  on the block operator (d_diag internal order [ncell][16], d_lower/d_upper [ninface][16]); solves
+ *  A x = b from x = 0 until |b - A x| <= rtol |b| or maxit iterations */
+int fvhip_gmres_blocks_device(fvhip_handle h, const double* d_diag, const double* d_lower, const double* d_upper,
+                              const double* d_b, double* d_x, double rtol, int maxit, int restart, int sweeps,
+                              int* iters, double* resnorm);
 
 /** MatrixFreeSpatialJacobian: set_state(u, r = -r(u), mdt = area/(CFL*dt)) then y = J x */
 int fvhip_matfree_set_state(fvhip_handle h, const double* u, const double* r, const double* mdt);
 int fvhip_matfree_apply(fvhip_handle h, const double* x, double* y);
-/** Device variants (internal order). set_state keeps the pointers, as the reference keeps the Vecs. */
+/** Device variants (internal order). set_state keeps the pointers, as the reference keeps the Vecs.
+ *  On a partitioned handle |x| is the global norm and d_u needs room for the ghost rows. */
 int fvhip_matfree_set_state_device(fvhip_handle h, const double* d_u, const double* d_r, const double* d_mdt);
 int fvhip_matfree_apply_device(fvhip_handle h, const double* d_x, double* d_y);
+int fvhip_group_matfree_set_state_device(fvhip_group g, const double* const* d_u, const double* const* d_r,
+                                         const double* const* d_mdt);
+int fvhip_group_matfree_apply_device(fvhip_group g, const double* const* d_x, double* const* d_y);
 /** -matrix_free_difference_step (default 1e-7, alinalg.cpp:124-129) */
 int fvhip_matfree_set_eps(fvhip_handle h, double eps);
 

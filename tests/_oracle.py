@@ -201,6 +201,30 @@ class OracleSpatial:
             pass
 
 
+def relaxed_update(u, du, gamma, minfactor):
+    """u + omega du per cell: SteadyBackwardEulerSolver's update (aodesolver.cpp:506-511) with
+    FlowSimpleUpdate::getLocalRelaxationFactor (nonlinearrelaxation.cpp:24-38) and
+    IdealGasPhysics::getDeltaPressureFromConserved as written (aphysics_defs.hpp:67-80, whose loop
+    runs over i = 2 .. NDIM+1); minfactor >= 1 is FullUpdate (omega = 1). Same operation order as
+    the reference, elementwise IEEE arithmetic."""
+    u = np.asarray(u, np.float64)
+    du = np.asarray(du, np.float64)
+    if minfactor >= 1.0:
+        return u + 1.0 * du
+    p = (gamma - 1.0) * (u[:, 3] - 0.5 * ((0.0 + u[:, 1] * u[:, 1]) + u[:, 2] * u[:, 2]) / u[:, 0])
+    unew = u + du
+    dp = np.zeros(u.shape[0])
+    for i in (2, 3):
+        dp = dp - ((u[:, i] + unew[:, i]) * (u[:, 0] + unew[:, 0]) / 2.0 * du[:, i]
+                   - (unew[:, i] * unew[:, i] + u[:, i] * u[:, i]) / 2.0 * du[:, 0])
+    dp = (gamma - 1.0) * (du[:, 3] - 1.0 / (2 * u[:, 0] * unew[:, 0]) * dp)
+    rdp = np.abs(dp) / p
+    drho = np.abs(du[:, 0]) / u[:, 0]
+    danger = np.where(rdp < drho, drho, rdp)                  # std::max(dp, drho)
+    omega = np.where(danger < 1.0 - minfactor, 1.0 - danger, minfactor)
+    return u + omega[:, None] * du
+
+
 def flux(ftype, gas, ul, ur, n):
     out = np.zeros(4)
     _chk(lib().orc_flux(FLUXES[ftype] if isinstance(ftype, str) else ftype, _d(np.asarray(gas, np.float64)),

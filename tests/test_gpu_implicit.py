@@ -1,0 +1,298 @@
+"""Implicit pseudo-time solver on the device (BASELINE.json configs 3-5):
+SteadyBackwardEulerSolver::solve (aodesolver.cpp:363-638) with the linear systems solved by device
+GMRES + block-Jacobi sweeps instead of PETSc's KSPSolve (aodesolver.cpp:483).
+
+PETSc is not in this image, so the linear algebra is checked against a direct sparse solve of the
+same blocks (scipy), and a whole step against a host restatement assembled from the oracle
+(residual, Jacobian, pseudo-time term aodesolver.cpp:300-329, relaxation nonlinearrelaxation.cpp).
+Bars:
+  * GMRES on the assembled blocks: |b - A x| <= 1e-11 |b| (checked in numpy), x equal to the direct
+    solution to 1e-8 of max|x|; block-Jacobi sweeps cut the iteration count;
+  * one implicit step with a tight linear solve: the update u1 - u0 equal to the host restatement's
+    to 1e-8 of its size per variable, the residual norm to 1e-12;
+  * Flow_Euler_Cylinder_HLLC_MatFreeVsMat (tests/solvers/testmatrixfree.cpp:65 with matfree.ctrl /
+    matfree.solverc): matrix-free and assembled solves both converge, in the same number of steps;
+  * a 3-rank partition (in-process group) takes the same implicit steps as one GPU: same linear
+    iteration count, u to 1e-9 of the update size (only the order of the dot-product sums differs;
+    measured 2e-15 assembled, 2e-11 matrix-free);
+    its explicit steps are bitwise those of one GPU; its matrix-free operator matches one GPU's;
+  * testcases/naca0012 functional regression (CL 1e-6, CDp 1e-6 relative) reached implicitly.
+"""
+import numpy as np
+import pytest
+import scipy.sparse as sp
+import scipy.sparse.linalg as spla
+
+import fvens_amd as fa
+import _oracle as orc
+import cases
+from test_gpu_residual import get_mesh
+
+pytestmark = pytest.mark.gpu
+
+
+def _torch():
+    import torch
+    return torch
+
+
+def block_matrix(m, D, lower, upper):
+    """CSR matrix of the face-block storage: A[c][c] = D[c], A[R][L] = lower, A[L][R] = upper"""
+    N, nb = m.nelem, m.nbface
+    L = m.intfac[nb:, 0].astype(np.int64)
+    R = m.intfac[nb:, 1].astype(np.int64)
+    ii, jj = np.meshgrid(np.arange(4), np.arange(4), indexing="ij")
+    rows, cols, vals = [], [], []
+    for rc, cc, blk in ((np.arange(N), np.arange(N), D), (R, L, lower), (L, R, upper)):
+        rows.append((4 * rc[:, None, None] + ii[None]).ravel())
+        cols.append((4 * cc[:, None, None] + jj[None]).ravel())
+        vals.append(np.asarray(blk).reshape(-1))
+    return sp.csr_matrix((np.concatenate(vals), (np.concatenate(rows), np.concatenate(cols))), shape=(4 * N, 4 * N))
+
+
+def pseudo_time_system(m, om, p, n, u, cfl):
+    """Host restatement of one implicit step's system: -r(u), dtm, Jacobian blocks + area/(cfl dt) I"""
+    ref = orc.OracleSpatial(om, p, n)
+    N = m.nelem
+    r = np.zeros((N, 4))
+    dtm = np.zeros(N)
+    ref.compute_residual(u, r, True, dtm)
+    D, lo, up = ref.jacobian(u)
+    mdt = m.area[:N] / (cfl * dtm)
+    return r, dtm, D + mdt[:, None, None] * np.eye(4)[None], lo, up
+
+
+def to_device(a, perm=None):
+    torch = _torch()
+    a = a if perm is None else a[perm]
+    return torch.tensor(np.ascontiguousarray(a), device="cuda")
+
+
+def test_gmres_blocks_matches_direct_solve():
+    m, om = get_mesh("naca_small")
+    p = cases.physics("naca")
+    n = cases.numerics("ROE", "LEASTSQUARES", "VANALBADA")
+    u = cases.state(m, p, 4)
+    r, dtm, D, lo, up = pseudo_time_system(m, om, p, n, u, 20.0)
+    A = block_matrix(m, D, lo, up)
+    N, Fi = m.nelem, m.naface - m.nbface
+    b = np.random.default_rng(0).standard_normal((N, 4))
+    x_ref = spla.spsolve(A.tocsc(), b.ravel()).reshape(N, 4)
+    dev = fa.FlowFV(m, p, n)
+    perm = dev.permutation()
+    dd, dl, dup = to_device(D.reshape(N, 16), perm), to_device(lo.reshape(Fi, 16)), to_device(up.reshape(Fi, 16))
+    db = to_device(b, perm)
+    dx = _torch().zeros_like(db)
+    iters = {}
+    for sweeps in (1, 3):
+        it, rn = dev.gmres_blocks_device(dd.data_ptr(), dl.data_ptr(), dup.data_ptr(), db.data_ptr(), dx.data_ptr(),
+                                         1e-12, 3000, 60, sweeps)
+        x = np.empty_like(b)
+        x[perm] = dx.cpu().numpy()
+        res = np.linalg.norm(A @ x.ravel() - b.ravel())
+        assert res <= 1e-11 * np.linalg.norm(b), (sweeps, it, res, rn)
+        np.testing.assert_allclose(x, x_ref, rtol=0, atol=1e-8 * np.abs(x_ref).max())
+        iters[sweeps] = it
+    assert iters[3] < iters[1], iters
+    dev.close()
+
+
+@pytest.mark.parametrize("min_relax", [1.0, 0.2])
+def test_one_backward_euler_step_matches_host(min_relax):
+    m, om = get_mesh("naca_small")
+    p = cases.physics("naca")
+    n = cases.numerics("ROE", "LEASTSQUARES", "VANALBADA")
+    u0 = cases.state(m, p, 8)
+    cfl = 5.0
+    r, dtm, D, lo, up = pseudo_time_system(m, om, p, n, u0, cfl)
+    du = spla.spsolve(block_matrix(m, D, lo, up).tocsc(), r.ravel()).reshape(-1, 4)
+    u1 = orc.relaxed_update(u0, du, p.gamma, min_relax)
+    res0 = np.sqrt(np.sum(r[:, 3] * r[:, 3] * m.area[:m.nelem]))
+    dev = fa.FlowFV(m, p, n)
+    perm = dev.permutation()
+    dU = to_device(u0, perm)
+    cfg = fa.ImplicitConfig(cflinit=cfl, cflfin=cfl, tol=0.0, maxiter=1, lin_rtol=1e-13, lin_maxit=3000, restart=60,
+                            prec_sweeps=2, min_relax=min_relax)
+    st, hist = dev.steady_backward_euler_device(dU.data_ptr(), cfg)
+    assert st["steps"] == 1 and st["cfl"] == cfl
+    u = np.empty_like(u0)
+    u[perm] = dU.cpu().numpy()
+    scale = np.abs(u1 - u0).max(axis=0)
+    assert np.all(np.abs(u - u1).max(axis=0) <= 1e-8 * scale), np.abs(u - u1).max(axis=0) / scale
+    assert abs(hist[0] - res0) <= 1e-12 * res0
+    dev.close()
+
+
+def test_matfree_vs_matrix_same_steps():
+    """tests/solvers/testmatrixfree.cpp:65 (matfree.ctrl: HLLC, first order, CFL 50-3000, tol 1e-8,
+    100 steps, full update; matfree.solverc: GMRES rtol 1e-2, 30 iterations; step 1e-6)"""
+    m, _ = get_mesh("2dcylinder2.msh")
+    p = cases.physics("cyl")
+    n = cases.numerics("HLLC", "NONE", "NONE", order2=False)
+    u0 = np.tile(cases.freestream(p), (m.nelem, 1))
+    steps = {}
+    for mf in (False, True):
+        dev = fa.FlowFV(m, p, n)
+        dU = to_device(u0, dev.permutation())
+        cfg = fa.ImplicitConfig(cflinit=50.0, cflfin=3000.0, tol=1e-8, maxiter=100, matrix_free=mf, mf_eps=1e-6,
+                                lin_rtol=1e-2, lin_maxit=30, restart=30, prec_sweeps=4, min_relax=1.0)
+        st, hist = dev.steady_backward_euler_device(dU.data_ptr(), cfg)
+        assert st["converged"], (mf, st)
+        steps[mf] = st["steps"]
+        dev.close()
+    print("steps", steps)
+    assert steps[True] == steps[False], steps
+
+
+def _partitioned(m, p, n, u0, nparts):
+    torch = _torch()
+    part = fa.partition_rcb(m, nparts)
+    sps = [fa.FlowFV(m, p, n, partition=part, rank=k) for k in range(nparts)]
+    dus, glob = [], []
+    for k, spk in enumerate(sps):
+        g = np.nonzero(part == k)[0][spk.permutation()]
+        glob.append(g)
+        d = torch.full((spk.nown + spk.nghost, 4), float("nan"), dtype=torch.float64, device="cuda")
+        d[:spk.nown] = torch.tensor(u0[g], device="cuda")
+        dus.append(d)
+    return sps, dus, glob
+
+
+def _gather(u0, sps, dus, glob):
+    u = np.full_like(u0, np.nan)
+    for k, spk in enumerate(sps):
+        u[glob[k]] = dus[k][:spk.nown].cpu().numpy()
+    return u
+
+
+def test_partitioned_backward_euler_matches_single():
+    m, _ = get_mesh("naca_small")
+    p = cases.physics("naca")
+    n = cases.numerics("ROE", "LEASTSQUARES", "VANALBADA")
+    u0 = cases.state(m, p, 2)
+    # the finite-difference operator is noisy at ~1e-11 (|x| is summed in another order, and
+    # r(u + eps x/|x|) - r(u) amplifies the rounding by |x|/eps), which later steps amplify further:
+    # one matrix-free step, three assembled ones
+    for mf, nsteps in ((False, 3), (True, 1)):
+        cfg = fa.ImplicitConfig(cflinit=10.0, cflfin=200.0, tol=0.0, maxiter=nsteps, matrix_free=mf, mf_eps=1e-6,
+                                lin_rtol=1e-4, lin_maxit=60, restart=20, prec_sweeps=2, min_relax=0.2)
+        one = fa.FlowFV(m, p, n)
+        perm = one.permutation()
+        dU = to_device(u0, perm)
+        st1, h1 = one.steady_backward_euler_device(dU.data_ptr(), cfg)
+        u1 = np.empty_like(u0)
+        u1[perm] = dU.cpu().numpy()
+        one.close()
+        sps, dus, glob = _partitioned(m, p, n, u0, 3)
+        grp = fa.FlowFVGroup(sps)
+        st, h = grp.steady_backward_euler_device([d.data_ptr() for d in dus], cfg)
+        u = _gather(u0, sps, dus, glob)
+        grp.close()
+        for s in sps:
+            s.close()
+        assert st["steps"] == st1["steps"] == nsteps
+        assert st["lin_iters"] == st1["lin_iters"], (mf, st, st1)
+        np.testing.assert_allclose(h, h1, rtol=1e-10)
+        scale = np.abs(u1 - u0).max(axis=0)
+        assert np.all(np.abs(u - u1).max(axis=0) <= 1e-9 * scale), (mf, np.abs(u - u1).max(axis=0) / scale)
+
+
+def test_partitioned_forward_euler_bitwise():
+    m, _ = get_mesh("naca_small")
+    p = cases.physics("naca")
+    n = cases.numerics("ROE", "LEASTSQUARES", "VANALBADA")
+    u0 = np.tile(cases.freestream(p), (m.nelem, 1))
+    one = fa.FlowFV(m, p, n)
+    perm = one.permutation()
+    dU = to_device(u0, perm)
+    s1, r1, h1 = one.steady_forward_euler_device(dU.data_ptr(), 0.5, 0.0, 20)
+    u1 = np.empty_like(u0)
+    u1[perm] = dU.cpu().numpy()
+    one.close()
+    sps, dus, glob = _partitioned(m, p, n, u0, 4)
+    grp = fa.FlowFVGroup(sps)
+    s, r, h = grp.steady_forward_euler_device([d.data_ptr() for d in dus], 0.5, 0.0, 20)
+    u = _gather(u0, sps, dus, glob)
+    grp.close()
+    for spk in sps:
+        spk.close()
+    assert s == s1 == 20
+    np.testing.assert_array_equal(u, u1)
+    np.testing.assert_allclose(h, h1, rtol=1e-12)
+
+
+def test_partitioned_matfree_matches_single():
+    torch = _torch()
+    m, _ = get_mesh("naca_small")
+    p = cases.physics("naca")
+    n = cases.numerics("ROE", "LEASTSQUARES", "VANALBADA")
+    u0 = cases.state(m, p, 6)
+    N = m.nelem
+    rng = np.random.default_rng(3)
+    x = rng.standard_normal((N, 4))
+    mdt = m.area[:N] * (1.0 + rng.random(N))
+    res = rng.standard_normal((N, 4))
+    one = fa.FlowFV(m, p, n)
+    perm = one.permutation()
+    du, dr, dm, dx = to_device(u0, perm), to_device(res, perm), to_device(mdt, perm), to_device(x, perm)
+    dy = torch.zeros_like(dx)
+    one.matfree_set_state_device(du.data_ptr(), dr.data_ptr(), dm.data_ptr())
+    one.matfree_set_eps(1e-6)
+    one.matfree_apply_device(dx.data_ptr(), dy.data_ptr())
+    one.synchronize()
+    y1 = np.empty_like(x)
+    y1[perm] = dy.cpu().numpy()
+    one.close()
+    sps, dus, glob = _partitioned(m, p, n, u0, 3)
+    grp = fa.FlowFVGroup(sps)
+    rs = [to_device(res[g]) for g in glob]
+    ms = [to_device(mdt[g]) for g in glob]
+    xs = [to_device(x[g]) for g in glob]
+    ys = [torch.zeros_like(t) for t in xs]
+    for spk in sps:
+        spk.matfree_set_eps(1e-6)
+    grp.matfree_set_state_device([d.data_ptr() for d in dus], [t.data_ptr() for t in rs], [t.data_ptr() for t in ms])
+    grp.matfree_apply_device([t.data_ptr() for t in xs], [t.data_ptr() for t in ys])
+    torch.cuda.synchronize()
+    y = np.full_like(x, np.nan)
+    for k in range(len(sps)):
+        y[glob[k]] = ys[k].cpu().numpy()
+    grp.close()
+    for spk in sps:
+        spk.close()
+    assert np.abs(y - y1).max() <= 1e-7 * np.abs(y1).max()
+
+
+def test_naca0012_implicit_functional_regression():
+    """testcases/naca0012 SpatialFlow_Euler_NACA0012_MUSCL_LeastSquares_HLLC_FunctionalRegression
+    (transonic-sanity-test-muscl.ctrl + opts.solverc) with the device implicit solver: starter =
+    first-order HLLC (initialization: CFL 50-1000, tol 1e-1, 20 steps, casesolvers.cpp:225-314),
+    main = HLLC + least squares + Van Albada (CFL 500-5000, tol 1e-7), robust_flow update (0.2),
+    Jacobian 'consistent' (HLLC), -ksp_rtol 1e-1, -ksp_max_it 30. The reference preconditions with
+    SOR; block-Jacobi sweeps here, so its step count may differ (max_timesteps raised 170 -> 600).
+    Bars: CL (the reference's 1e-6) and CDp (1e-6) relative to regr-MUSCL_LeastSquares_HLLC.txt."""
+    m = fa.UMesh.read_gmsh(cases.fixture_mesh("naca0012luo"))
+    om = orc.OracleMesh.read(cases.fixture_mesh("naca0012luo"))
+    p = cases.physics("naca")
+    n1 = cases.numerics("HLLC", "NONE", "NONE", order2=False)
+    n2 = cases.numerics("HLLC", "LEASTSQUARES", "VANALBADA")
+    start, main = fa.FlowFV(m, p, n1), fa.FlowFV(m, p, n2)
+    perm = main.permutation()
+    assert np.array_equal(perm, start.permutation())
+    u0 = np.tile(cases.freestream(p), (m.nelem, 1))
+    dU = to_device(u0, perm)
+    lin = dict(lin_rtol=1e-1, lin_maxit=30, restart=30, prec_sweeps=4, min_relax=0.2)
+    st0, _ = start.steady_backward_euler_device(dU.data_ptr(), fa.ImplicitConfig(cflinit=50.0, cflfin=1000.0,
+                                                                                 tol=1e-1, maxiter=20, **lin))
+    st, hist = main.steady_backward_euler_device(dU.data_ptr(), fa.ImplicitConfig(cflinit=500.0, cflfin=5000.0,
+                                                                                 tol=1e-7, maxiter=600, **lin))
+    u = np.empty_like(u0)
+    u[perm] = dU.cpu().numpy()
+    ref = orc.OracleSpatial(om, p, n2)
+    cl, cdp, _ = ref.surface(u, ref.getGradients(u), 2)
+    print(f"starter {st0} main {st} CL {cl!r} CDp {cdp!r}")
+    assert st["converged"], st
+    assert abs(cl - 0.154112792928976) / 0.154112792928976 <= 1e-6
+    assert abs(cdp - 0.0115814414408097) / 0.0115814414408097 <= 1e-6
+    start.close()
+    main.close()
