@@ -30,6 +30,44 @@ struct Gas {
 
 FVHIP_HD double dot2(const double* a, const double* b) { double d = 0; d += a[0]*b[0]; d += a[1]*b[1]; return d; }
 
+/// a/b and sqrt(x), correctly rounded, for the parity kernels. On the device these are the compiler's
+/// own f64 sequences -- division: v_rcp, two Newton steps, Markstein's correction; square root:
+/// v_rsq and Goldschmidt steps -- without their range scaling and special-value fix-ups
+/// (v_div_scale / v_div_fmas / v_div_fixup; ldexp and class selects). For operands whose result is
+/// a normal number, which every division and root of the sweep has (densities, pressures, sound
+/// speeds, eps-shifted limiter denominators, face lengths), they execute the same instructions on the
+/// same values, i.e. they return bitwise a/b and sqrt(x), in 8 instead of 11 and 10 instead of 19
+/// instructions (the sweep is FP64-issue bound). Host builds and the fast-math kernels use / and sqrt.
+FVHIP_HD double div_rn(double a, double b) {
+#if defined(__HIP_DEVICE_COMPILE__) && !defined(FVHIP_FAST)
+	double r = __builtin_amdgcn_rcp(b);
+	double e = fma(-b, r, 1.0);
+	r = fma(r, e, r);
+	e = fma(-b, r, 1.0);
+	r = fma(r, e, r);
+	const double q = a*r;
+	e = fma(-b, q, a);
+	return fma(e, r, q);
+#else
+	return a/b;
+#endif
+}
+FVHIP_HD double sqrt_rn(double x) {
+#if defined(__HIP_DEVICE_COMPILE__) && !defined(FVHIP_FAST)
+	const double y = __builtin_amdgcn_rsq(x);
+	double g = x*y, h = y*0.5;
+	const double r = fma(-h, g, 0.5);
+	g = fma(g, r, g);
+	h = fma(h, r, h);
+	double d = fma(-g, g, x);
+	g = fma(d, h, g);
+	d = fma(-g, g, x);
+	return fma(d, h, g);
+#else
+	return sqrt(x);
+#endif
+}
+
 FVHIP_HD void directional_flux(const Gas& G, const double* uc, const double* n, double vn, double p, double* f) {
 	f[0] = vn*uc[0];
 	f[1] = vn*uc[1] + p*n[0];
@@ -39,31 +77,31 @@ FVHIP_HD void directional_flux(const Gas& G, const double* uc, const double* n, 
 
 /// getVarsFromConserved: velocity, normal velocity, pressure, total enthalpy
 FVHIP_HD void flow_vars(const Gas& G, const double* uc, const double* n, double* v, double& vn, double& p, double& H) {
-	v[0] = uc[1]/uc[0];
-	v[1] = uc[2]/uc[0];
+	v[0] = div_rn(uc[1], uc[0]);
+	v[1] = div_rn(uc[2], uc[0]);
 	vn = dot2(v,n);
 	const double vm2 = dot2(v,v);
 	p = (G.g-1.0)*(uc[3] - 0.5*uc[0]*vm2);
-	H = (uc[3]+p)/uc[0];
+	H = div_rn(uc[3]+p, uc[0]);
 }
 
 FVHIP_HD double pressure_cons(const Gas& G, const double* uc) {
-	return (G.g-1.0)*(uc[3] - 0.5*dot2(&uc[1],&uc[1])/uc[0]);
+	return (G.g-1.0)*(uc[3] - div_rn(0.5*dot2(&uc[1],&uc[1]), uc[0]));
 }
-FVHIP_HD double sound_speed(const Gas& G, double rho, double p) { return sqrt(G.g * p/rho); }
+FVHIP_HD double sound_speed(const Gas& G, double rho, double p) { return sqrt_rn(div_rn(G.g * p, rho)); }
 FVHIP_HD double sound_speed_cons(const Gas& G, const double* uc) { return sound_speed(G, uc[0], pressure_cons(G, uc)); }
-FVHIP_HD double temperature(const Gas& G, double rho, double p) { return p/rho * G.g*G.Minf*G.Minf; }
-FVHIP_HD double energy_from_pressure(const Gas& G, double p, double d, double vm2) { return p/(G.g-1.0) + 0.5*d*vm2; }
+FVHIP_HD double temperature(const Gas& G, double rho, double p) { return div_rn(p, rho) * G.g*G.Minf*G.Minf; }
+FVHIP_HD double energy_from_pressure(const Gas& G, double p, double d, double vm2) { return div_rn(p, G.g-1.0) + 0.5*d*vm2; }
 FVHIP_HD double energy_from_temperature(const Gas& G, double T, double d, double vm2) {
-	return d * (T/(G.g*(G.g-1.0)*G.Minf*G.Minf) + 0.5*vm2);
+	return d * (div_rn(T, G.g*(G.g-1.0)*G.Minf*G.Minf) + 0.5*vm2);
 }
-FVHIP_HD double freestream_pressure(const Gas& G) { return (1.0/(G.g*G.Minf*G.Minf)); }
+FVHIP_HD double freestream_pressure(const Gas& G) { return div_rn(1.0, G.g*G.Minf*G.Minf); }
 
 /// conserved -> (rho, vx, vy, p); in-place safe
 FVHIP_HD void cons2prim(const Gas& G, const double* uc, double* up) {
 	const double rho = uc[0];
 	const double p = pressure_cons(G, uc);
-	const double vx = uc[1]/rho, vy = uc[2]/rho;
+	const double vx = div_rn(uc[1], rho), vy = div_rn(uc[2], rho);
 	up[0] = rho; up[1] = vx; up[2] = vy; up[3] = p;
 }
 /// (rho, vx, vy, p) -> conserved; in-place safe
@@ -75,15 +113,15 @@ FVHIP_HD void prim2cons(const Gas& G, const double* up, double* uc) {
 /// conserved -> (rho, vx, vy, T)
 FVHIP_HD void cons2prim2(const Gas& G, const double* uc, double* up) {
 	const double p = pressure_cons(G, uc);
-	up[0] = uc[0]; up[1] = uc[1]/uc[0]; up[2] = uc[2]/uc[0];
+	up[0] = uc[0]; up[1] = div_rn(uc[1], uc[0]); up[2] = div_rn(uc[2], uc[0]);
 	up[3] = temperature(G, uc[0], p);
 }
 FVHIP_HD double grad_temperature(const Gas& G, double rho, double grho, double p, double gp) {
-	return (gp*rho - p*grho) / (rho*rho) * G.g*G.Minf*G.Minf;
+	return div_rn(gp*rho - p*grho, rho*rho) * G.g*G.Minf*G.Minf;
 }
 FVHIP_HD double sutherland(const Gas& G, const double* uc) {
 	const double T = temperature(G, uc[0], pressure_cons(G, uc));
-	return (1.0+G.sC/G.Tinf)/(T+G.sC/G.Tinf) * pow(T,1.5) / G.Reinf;
+	return div_rn(div_rn(1.0+div_rn(G.sC, G.Tinf), T+div_rn(G.sC, G.Tinf)) * pow(T,1.5), G.Reinf);
 }
 
 /// Roe averages (anumericalflux.hpp:175-189)
@@ -91,14 +129,14 @@ struct RoeAvg { double R, rho, v[2], vm2, vn, H, c; };
 FVHIP_HD RoeAvg roe_average(const Gas& G, const double* ul, const double* ur, const double* n,
                             const double* vi, double Hi, const double* vj, double Hj) {
 	RoeAvg a;
-	a.R = sqrt(ur[0]/ul[0]);
+	a.R = sqrt_rn(div_rn(ur[0], ul[0]));
 	a.rho = a.R*ul[0];
-	a.v[0] = (a.R*vj[0] + vi[0])/(a.R + 1.0);
-	a.v[1] = (a.R*vj[1] + vi[1])/(a.R + 1.0);
-	a.H = (a.R*Hj + Hi)/(a.R + 1.0);
+	a.v[0] = div_rn(a.R*vj[0] + vi[0], a.R + 1.0);
+	a.v[1] = div_rn(a.R*vj[1] + vi[1], a.R + 1.0);
+	a.H = div_rn(a.R*Hj + Hi, a.R + 1.0);
 	a.vm2 = dot2(a.v,a.v);
 	a.vn = dot2(a.v,n);
-	a.c = sqrt( (G.g-1.0)*(a.H - a.vm2*0.5) );
+	a.c = sqrt_rn( (G.g-1.0)*(a.H - a.vm2*0.5) );
 	return a;
 }
 
@@ -116,13 +154,13 @@ FVHIP_HD void flux_llf(const Gas& G, const double* ul, const double* ur, const d
 	// getDirectionalFluxFromConserved recomputes vn and p from the conserved state (aphysics.cpp:28-35)
 	double fl[4], fr[4];
 	{
-		const double vn = dot2(&ul[1],n)/ul[0];
-		const double p = (G.g-1.0)*(ul[3] - 0.5*dot2(&ul[1],&ul[1])/ul[0]);
+		const double vn = div_rn(dot2(&ul[1],n), ul[0]);
+		const double p = (G.g-1.0)*(ul[3] - div_rn(0.5*dot2(&ul[1],&ul[1]), ul[0]));
 		directional_flux(G, ul, n, vn, p, fl);
 	}
 	{
-		const double vn = dot2(&ur[1],n)/ur[0];
-		const double p = (G.g-1.0)*(ur[3] - 0.5*dot2(&ur[1],&ur[1])/ur[0]);
+		const double vn = div_rn(dot2(&ur[1],n), ur[0]);
+		const double p = (G.g-1.0)*(ur[3] - div_rn(0.5*dot2(&ur[1],&ur[1]), ur[0]));
 		directional_flux(G, ur, n, vn, p, fr);
 	}
 	for(int k = 0; k < 4; k++) f[k] = 0.5*( fl[k] + fr[k] - eig*(ur[k]-ul[k]) );
@@ -136,7 +174,7 @@ FVHIP_HD void flux_vanleer(const Gas& G, const double* ul, const double* ur, con
 	flow_vars(G, ul, n, vi, vni, pi, Hi);
 	flow_vars(G, ur, n, vj, vnj, pj, Hj);
 	const double ci = sound_speed(G, ul[0], pi), cj = sound_speed(G, ur[0], pj);
-	const double Mni = vni/ci, Mnj = vnj/cj;
+	const double Mni = div_rn(vni, ci), Mnj = div_rn(vnj, cj);
 	double fp[4], fm[4];
 	if(Mni < -1.0) { fp[0] = fp[1] = fp[2] = fp[3] = 0; }
 	else if(Mni > 1.0) directional_flux(G, ul, n, vni, pi, fp);
@@ -164,7 +202,7 @@ FVHIP_HD void flux_ausm(const Gas& G, const double* ul, const double* ur, const 
 	flow_vars(G, ul, n, vi, vni, pi, Hi);
 	flow_vars(G, ur, n, vj, vnj, pj, Hj);
 	const double ci = sound_speed(G, ul[0], pi), cj = sound_speed(G, ur[0], pj);
-	const double Mni = vni/ci, Mnj = vnj/cj;
+	const double Mni = div_rn(vni, ci), Mnj = div_rn(vnj, cj);
 	double ML, MR, pL, pR;
 	if(fabs(Mni) <= 1.0) { ML = 0.25*(Mni+1)*(Mni+1); pL = ML*pi*(2.0-Mni); }
 	else if(Mni < -1.0) { ML = 0; pL = 0; }
@@ -222,14 +260,14 @@ FVHIP_HD void flux_roe(const Gas& G, const double* ul, const double* ur, const d
 	// |eigenvalues| with Harten's entropy fix, delta = 1e-4 c (anumericalflux.cpp:664, 686-692)
 	double l0 = fabs(a.vn-a.c), l1 = fabs(a.vn), l3 = fabs(a.vn+a.c);
 	const double delta = 1.0e-4*a.c;
-	if(l0 < delta) l0 = (l0*l0 + delta*delta)/(2.0*delta);
-	if(l1 < delta) l1 = (l1*l1 + delta*delta)/(2.0*delta);
-	if(l3 < delta) l3 = (l3*l3 + delta*delta)/(2.0*delta);
+	if(l0 < delta) l0 = div_rn(l0*l0 + delta*delta, 2.0*delta);
+	if(l1 < delta) l1 = div_rn(l1*l1 + delta*delta, 2.0*delta);
+	if(l3 < delta) l3 = div_rn(l3*l3 + delta*delta, 2.0*delta);
 	const double devn = vnj-vni, dep = pj-pi, derho = ur[0]-ul[0];
-	const double a0 = l0*(dep-a.rho*a.c*devn)/(2.0*a.c*a.c);
-	const double a1 = l1*(derho - dep/(a.c*a.c));
+	const double a0 = div_rn(l0*(dep-a.rho*a.c*devn), 2.0*a.c*a.c);
+	const double a1 = l1*(derho - div_rn(dep, a.c*a.c));
 	const double a2 = l1*a.rho;
-	const double a3 = l3*(dep+a.rho*a.c*devn)/(2.0*a.c*a.c);
+	const double a3 = div_rn(l3*(dep+a.rho*a.c*devn), 2.0*a.c*a.c);
 	double d0 = a0, d1 = a0*(a.v[0]-a.c*n[0]), d2 = a0*(a.v[1]-a.c*n[1]), d3 = a0*(a.H-a.c*a.vn);
 	d0 += a1;
 	d1 += a1*a.v[0] +      a2*(vj[0]-vi[0] - devn*n[0]);
@@ -265,8 +303,8 @@ FVHIP_HD void flux_hll(const Gas& G, const double* ul, const double* ur, const d
 	einfeldt(vni, ci, vnj, cj, a, sl, sr);
 	const double sr0 = sr > 0 ? 0 : sr;
 	const double sl0 = sl > 0 ? 0 : sl;
-	const double t1 = (sr0 - sl0)/(sr-sl); const double t2 = 1.0 - t1;
-	const double t3 = 0.5*(sr*fabs(sl)-sl*fabs(sr))/(sr-sl);
+	const double t1 = div_rn(sr0 - sl0, sr-sl); const double t2 = 1.0 - t1;
+	const double t3 = div_rn(0.5*(sr*fabs(sl)-sl*fabs(sr)), sr-sl);
 	f[0] = t1*vnj*ur[0] + t2*vni*ul[0]                     - t3*(ur[0]-ul[0]);
 	f[1] = t1*(vnj*ur[1]+pj*n[0]) + t2*(vni*ul[1]+pi*n[0]) - t3*(ur[1]-ul[1]);
 	f[2] = t1*(vnj*ur[2]+pj*n[1]) + t2*(vni*ul[2]+pi*n[1]) - t3*(ur[2]-ul[2]);
@@ -276,10 +314,10 @@ FVHIP_HD void flux_hll(const Gas& G, const double* ul, const double* ur, const d
 /// HLLC star state (anumericalflux.cpp:1069-1081), returned as the flux correction s*(u* - u)
 FVHIP_HD void hllc_side(const double* u, const double* n, double vn, double p, double ss, double sm, double* f) {
 	const double pstar = u[0]*(vn-ss)*(vn-sm) + p;
-	const double us0 = u[0] * (ss - vn)/(ss-sm);
-	const double us1 = ( (ss-vn)*u[1] + (pstar-p)*n[0] )/(ss-sm);
-	const double us2 = ( (ss-vn)*u[2] + (pstar-p)*n[1] )/(ss-sm);
-	const double us3 = ( (ss-vn)*u[3] - p*vn + pstar*sm )/(ss-sm);
+	const double us0 = div_rn(u[0] * (ss - vn), ss-sm);
+	const double us1 = div_rn( (ss-vn)*u[1] + (pstar-p)*n[0], ss-sm );
+	const double us2 = div_rn( (ss-vn)*u[2] + (pstar-p)*n[1], ss-sm );
+	const double us3 = div_rn( (ss-vn)*u[3] - p*vn + pstar*sm, ss-sm );
 	f[0] += ss * (us0 - u[0]);
 	f[1] += ss * (us1 - u[1]);
 	f[2] += ss * (us2 - u[2]);
@@ -294,8 +332,8 @@ FVHIP_HD void flux_hllc(const Gas& G, const double* ul, const double* ur, const 
 	const RoeAvg a = roe_average(G, ul, ur, n, vi, Hi, vj, Hj);
 	double sl, sr;
 	einfeldt(vni, ci, vnj, cj, a, sl, sr);
-	const double sm = ( ur[0]*vnj*(sr-vnj) - ul[0]*vni*(sl-vni) + pi-pj )
-		/ ( ur[0]*(sr-vnj) - ul[0]*(sl-vni) );
+	const double sm = div_rn( ur[0]*vnj*(sr-vnj) - ul[0]*vni*(sl-vni) + pi-pj,
+		ur[0]*(sr-vnj) - ul[0]*(sl-vni) );
 	if(sl > 0)
 		directional_flux(G, ul, n, vni, pi, f);
 	else if(sl <= 0 && sm > 0) {
@@ -344,13 +382,13 @@ FVHIP_HD void ghost_state(const Gas& G, const BCDev& bc, const double* uinf, con
                           const double* n, double* gs) {
 	switch(bc.type) {
 	case 2: {  // INFLOW_OUTFLOW (abc.cpp:46-81)
-		const double vni = dot2(&ins[1],n)/ins[0];
+		const double vni = div_rn(dot2(&ins[1],n), ins[0]);
 		const double ci = sound_speed_cons(G, ins);
-		const double Mni = vni/ci;
+		const double Mni = div_rn(vni, ci);
 		if(Mni <= 0) { gs[0] = uinf[0]; gs[1] = uinf[1]; gs[2] = uinf[2]; gs[3] = uinf[3]; }
 		else if(Mni < 1) {
 			const double pinf = freestream_pressure(G);
-			const double e = energy_from_pressure(G, pinf, ins[0], dot2(&ins[1],&ins[1])/(ins[0]*ins[0]));
+			const double e = energy_from_pressure(G, pinf, ins[0], div_rn(dot2(&ins[1],&ins[1]), ins[0]*ins[0]));
 			gs[0] = ins[0]; gs[1] = ins[1]; gs[2] = ins[2]; gs[3] = e;
 		}
 		else { gs[0] = ins[0]; gs[1] = ins[1]; gs[2] = ins[2]; gs[3] = ins[3]; }
@@ -376,7 +414,7 @@ FVHIP_HD void ghost_state(const Gas& G, const BCDev& bc, const double* uinf, con
 		gs[0] = uinf[0]; gs[1] = uinf[1]; gs[2] = uinf[2]; gs[3] = uinf[3];
 		break;
 	case 0: {  // SLIP_WALL (abc.cpp:219-229)
-		const double vni = dot2(&ins[1],n)/ins[0];
+		const double vni = div_rn(dot2(&ins[1],n), ins[0]);
 		const double r = ins[0], e = ins[3];
 		const double m0 = ins[1] - 2.0*vni*n[0]*ins[0];
 		const double m1 = ins[2] - 2.0*vni*n[1]*ins[0];
@@ -395,10 +433,10 @@ FVHIP_HD void ghost_state(const Gas& G, const BCDev& bc, const double* uinf, con
 		const double p = pressure_cons(G, ins);
 		const double gtemp = 2.0*bc.v1 - temperature(G, ins[0], p);
 		const double r = ins[0];
-		const double m0 = r*( 2.0*bc.v0*n[1] - ins[1]/ins[0]);
-		const double m1 = r*(-2.0*bc.v0*n[0] - ins[2]/ins[0]);
+		const double m0 = r*( 2.0*bc.v0*n[1] - div_rn(ins[1], ins[0]));
+		const double m1 = r*(-2.0*bc.v0*n[0] - div_rn(ins[2], ins[0]));
 		double mm[2] = {m0, m1};
-		const double vm2 = dot2(mm,mm)/(r*r);
+		const double vm2 = div_rn(dot2(mm,mm), r*r);
 		gs[0] = r; gs[1] = m0; gs[2] = m1; gs[3] = energy_from_temperature(G, gtemp, r, vm2);
 		break;
 	}
@@ -437,20 +475,20 @@ FVHIP_HD void viscous_flux(const Gas& G, const double* n, const double* rcl, con
 		double dr[2], dist = 0;
 		dr[0] = rcr[0]-rcl[0]; dist += dr[0]*dr[0];
 		dr[1] = rcr[1]-rcl[1]; dist += dr[1]*dr[1];
-		dist = sqrt(dist);
-		dr[0] /= dist; dr[1] /= dist;
+		dist = sqrt_rn(dist);
+		dr[0] = div_rn(dr[0], dist); dr[1] = div_rn(dr[1], dist);
 		for(int i = 0; i < 4; i++) {
 			double davg[2];
 			davg[0] = 0.5*(gL[i] + gR[i]);
 			davg[1] = 0.5*(gL[4+i] + gR[4+i]);
-			const double corr = (tr[i]-tl[i])/dist;
+			const double corr = div_rn(tr[i]-tl[i], dist);
 			const double ddr = dot2(davg,dr);
 			grad[0][i] = davg[0] - ddr*dr[0] + corr*dr[0];
 			grad[1][i] = davg[1] - ddr*dr[1] + corr*dr[1];
 		}
 	}
 	const double muRe = CONSTVISC ? 1.0/G.Reinf : 0.5*( sutherland(G, ul) + sutherland(G, ur) );
-	const double kd = muRe / (G.Minf*G.Minf*(G.g-1.0)*G.Pr);
+	const double kd = div_rn(muRe, G.Minf*G.Minf*(G.g-1.0)*G.Pr);
 	double ldiv = 0;
 	ldiv += grad[0][1]; ldiv += grad[1][2];
 	ldiv *= 2.0/3.0*muRe;
@@ -462,8 +500,8 @@ FVHIP_HD void viscous_flux(const Gas& G, const double* n, const double* rcl, con
 	vf[0] = 0;
 	for(int i = 0; i < 2; i++) { double t = 0; t -= s[i][0]*n[0]; t -= s[i][1]*n[1]; vf[i+1] = t; }
 	double va[2];
-	va[0] = 0.5*( ul[1]/ul[0] + ur[1]/ur[0] );
-	va[1] = 0.5*( ul[2]/ul[0] + ur[2]/ur[0] );
+	va[0] = 0.5*( div_rn(ul[1], ul[0]) + div_rn(ur[1], ur[0]) );
+	va[1] = 0.5*( div_rn(ul[2], ul[0]) + div_rn(ur[2], ur[0]) );
 	double e = 0;
 	for(int i = 0; i < 2; i++) {
 		double comp = 0;

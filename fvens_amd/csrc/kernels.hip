@@ -117,7 +117,7 @@ __global__ void __launch_bounds__(256) k_grad_wls(DevMesh M, const double* __res
 		w2 += (rcc.x-rn[k].x)*(rcc.x-rn[k].x);
 		w2 += (rcc.y-rn[k].y)*(rcc.y-rn[k].y);
 		const double dr0 = rcc.x-rn[k].x, dr1 = rcc.y-rn[k].y;
-		w2 = 1.0/(w2);
+		w2 = div_rn(1.0, w2);
 		#pragma unroll
 		for(int iv = 0; iv < 4; iv++) {
 			const double du = uc[iv] - un[k][iv];
@@ -203,7 +203,7 @@ __global__ void __launch_bounds__(256) k_prep_grad_wls(DevMesh M, DevPhys P, con
 		w2 += (rcc.x-rn[k].x)*(rcc.x-rn[k].x);
 		w2 += (rcc.y-rn[k].y)*(rcc.y-rn[k].y);
 		const double dr0 = rcc.x-rn[k].x, dr1 = rcc.y-rn[k].y;
-		w2 = 1.0/(w2);
+		w2 = div_rn(1.0, w2);
 		#pragma unroll
 		for(int iv = 0; iv < 4; iv++) {
 			const double du = uc[iv] - un[k][iv];
@@ -260,7 +260,7 @@ __global__ void __launch_bounds__(256) k_grad_wls_list(DevMesh M, DevPhys P, con
 		w2 += (rcc.x-rn.x)*(rcc.x-rn.x);
 		w2 += (rcc.y-rn.y)*(rcc.y-rn.y);
 		const double dr0 = rcc.x-rn.x, dr1 = rcc.y-rn.y;
-		w2 = 1.0/(w2);
+		w2 = div_rn(1.0, w2);
 		#pragma unroll
 		for(int iv = 0; iv < 4; iv++) {
 			const double du = uc[iv] - un[iv];
@@ -287,7 +287,7 @@ __global__ void __launch_bounds__(256) k_grad_gg(DevMesh M, const double* __rest
 	const int4 cs = M.cell_slots[c];
 	const int e[4] = {cs.x, cs.y, cs.z, cs.w};
 	double g[8] = {0,0,0,0,0,0,0,0};
-	const double ainv = 1.0/M.area[c];
+	const double ainv = div_rn(1.0, M.area[c]);
 	#pragma unroll
 	for(int k = 0; k < 4; k++) {
 		if(e[k] < 0) break;
@@ -305,12 +305,12 @@ __global__ void __launch_bounds__(256) k_grad_gg(DevMesh M, const double* __rest
 		double dL = 0, dR = 0;
 		dL += (mid.x-rl.x)*(mid.x-rl.x); dR += (mid.x-rr.x)*(mid.x-rr.x);
 		dL += (mid.y-rl.y)*(mid.y-rl.y); dR += (mid.y-rr.y)*(mid.y-rr.y);
-		dL = 1.0/sqrt(dL);
-		dR = 1.0/sqrt(dR);
+		dL = div_rn(1.0, sqrt_rn(dL));
+		dR = div_rn(1.0, sqrt_rn(dR));
 		const bool right = e[k] & 1;
 		#pragma unroll
 		for(int iv = 0; iv < 4; iv++) {
-			const double ut = (uL[iv]*dL + uR[iv]*dR)/(dL+dR) * len;
+			const double ut = div_rn(uL[iv]*dL + uR[iv]*dR, dL+dR) * len;
 			if(!right) { g[iv*2+0] += (ut*nn.x)*ainv; g[iv*2+1] += (ut*nn.y)*ainv; }
 			else       { g[iv*2+0] -= (ut*nn.x)*ainv; g[iv*2+1] -= (ut*nn.y)*ainv; }
 		}
@@ -366,7 +366,7 @@ __global__ void __launch_bounds__(256) k_limiter(DevMesh M, const double* __rest
 			if(VENK) {
 				const double dm = uf - uc[iv];
 				const double dp = dm < 0 ? dmin : dmax;
-				ph = (dp*dp + 2*dp*dm + eps2)/(dp*dp + dp*dm + 2*dm*dm + eps2);
+				ph = div_rn(dp*dp + 2*dp*dm + eps2, dp*dp + dp*dm + 2*dm*dm + eps2);
 			} else {
 				const double diff = uf - uc[iv];
 				if(diff > 0) ph = 1 < dmax/diff ? 1 : dmax/diff;
@@ -423,7 +423,7 @@ __global__ void __launch_bounds__(256) k_weno(DevMesh M, double lambda, const do
 /// MUSCL / Van Albada pieces (musclreconstruction.cpp:33-59)
 __device__ __forceinline__ double muscl_phi(double d, double du) {
 	const double eps = 1e-8;
-	double ph = (2.0*d * du + eps) / (d*d + du*du + eps);
+	double ph = div_rn(2.0*d * du + eps, d*d + du*du + eps);
 	return ph < 0.0 ? 0.0 : ph;
 }
 __device__ __forceinline__ double muscl_left(double ui, double uj, double dm, double ph) {
@@ -623,19 +623,19 @@ __global__ void __launch_bounds__(SLOTS_MAX) k_sweep(const DevMesh M, const DevP
 
 		if(DT) {
 			const double ci = sound_speed_cons(G, ul), cj = sound_speed_cons(G, ur);
-			const double vni = dot2(&ul[1],n)/ul[0];
-			const double vnj = dot2(&ur[1],n)/ur[0];
+			const double vni = div_rn(dot2(&ul[1],n), ul[0]);
+			const double vnj = div_rn(dot2(&ur[1],n), ur[0]);
 			sri = (fabs(vni)+ci)*len;
 			srj = (fabs(vnj)+cj)*len;
 			if(VISC != SV_NONE) {
 				const double mui = VISC == SV_CONST ? 1.0/G.Reinf : sutherland(G, ul);
 				const double muj = VISC == SV_CONST ? 1.0/G.Reinf : sutherland(G, ur);
-				const double ai = 4.0/(3*ul[0]), bi = G.g/ul[0];
-				const double aj = 4.0/(3*ur[0]), bj = G.g/ur[0];
+				const double ai = div_rn(4.0, 3*ul[0]), bi = div_rn(G.g, ul[0]);
+				const double aj = div_rn(4.0, 3*ur[0]), bj = div_rn(G.g, ur[0]);
 				const double coi = (ai < bi) ? bi : ai;          // std::max
 				const double coj = (aj < bj) ? bj : aj;
-				sri += coi*mui/G.Pr * len*len/M.area[lr.x];
-				if(!bnd) srj += coj*muj/G.Pr * len*len/M.area[lr.y];
+				sri += div_rn(div_rn(coi*mui, G.Pr) * len*len, M.area[lr.x]);
+				if(!bnd) srj += div_rn(div_rn(coj*muj, G.Pr) * len*len, M.area[lr.y]);
 			}
 		}
 	}
@@ -672,7 +672,7 @@ __global__ void __launch_bounds__(SLOTS_MAX) k_sweep(const DevMesh M, const DevP
 			}
 		}
 		st4(B.r, c, r);
-		if(DT) B.dtm[c] = M.area[c]/integ;
+		if(DT) B.dtm[c] = div_rn(M.area[c], integ);
 	}
 }
 
@@ -771,7 +771,7 @@ __global__ void __launch_bounds__(SLOTS_MAX, 4) k_residual_wls(const DevMesh M, 
 			w2 += (rcc.x-rn.x)*(rcc.x-rn.x);
 			w2 += (rcc.y-rn.y)*(rcc.y-rn.y);
 			const double dr0 = rcc.x-rn.x, dr1 = rcc.y-rn.y;
-			w2 = 1.0/(w2);
+			w2 = div_rn(1.0, w2);
 			#pragma unroll
 			for(int iv = 0; iv < 4; iv++) {
 				const double du = uc[iv] - un[iv];
@@ -876,8 +876,8 @@ __global__ void __launch_bounds__(SLOTS_MAX, 4) k_residual_wls(const DevMesh M, 
 		for(int k = 0; k < 4; k++) f[k] *= len;
 		if(DT) {
 			const double ci = sound_speed_cons(G, ul), cj = sound_speed_cons(G, ur);
-			const double vni = dot2(&ul[1],n)/ul[0];
-			const double vnj = dot2(&ur[1],n)/ur[0];
+			const double vni = div_rn(dot2(&ul[1],n), ul[0]);
+			const double vnj = div_rn(dot2(&ur[1],n), ur[0]);
 			sri = (fabs(vni)+ci)*len;
 			srj = (fabs(vnj)+cj)*len;
 		}
@@ -915,7 +915,7 @@ __global__ void __launch_bounds__(SLOTS_MAX, 4) k_residual_wls(const DevMesh M, 
 			}
 		}
 		st4(B.r, c, r);
-		if(DT) B.dtm[c] = M.area[c]/integ;
+		if(DT) B.dtm[c] = div_rn(M.area[c], integ);
 	}
 	(void)N;
 }
