@@ -332,11 +332,15 @@ class FlowFV:
     def matfree_apply_device(self, d_x, d_y):
         check(_ffi.lib().fvhip_matfree_apply_device(self._h, ctypes.c_void_p(d_x), ctypes.c_void_p(d_y)))
 
-    def compute_residual_device(self, d_u, d_r, d_dtm=None, gettimesteps=False, overwrite=True, staged=False):
-        """staged=True forces the gradient + sweep kernels where the fused one-launch residual applies"""
+    def compute_residual_device(self, d_u, d_r, d_dtm=None, gettimesteps=False, overwrite=True, staged=False,
+                                pipelined=False):
+        """staged=True forces the gradient + sweep kernels one after the other, pipelined=True the
+        gradient chunks overlapped with the sweep groups (FVHIP_RES_STAGED / FVHIP_RES_PIPELINED);
+        every path gives the same bits"""
         check(_ffi.lib().fvhip_compute_residual_device(self._h, ctypes.c_void_p(d_u), ctypes.c_void_p(d_r),
                                                        int(gettimesteps), ctypes.c_void_p(d_dtm or 0),
-                                                       (1 if overwrite else 0) | (2 if staged else 0)))
+                                                       (1 if overwrite else 0) | (2 if staged else 0) |
+                                                       (4 if pipelined else 0)))
 
     def permutation(self):
         p = np.zeros(self.nown, np.int32)

@@ -122,6 +122,13 @@ struct fvhip_ctx
 	// partitioned meshes: halo exchange with the neighbour ranks (RCCL, or in-process for a group)
 	int rank = 0, nparts = 1;
 	bool use_staged = false;      ///< force the staged (gradient + sweep) path even if fused applies
+	bool use_pipe = false;        ///< force the pipelined staged path even if fused applies
+	// pipelined staged residual (single domain): the sweep groups run on stream2 behind the
+	// gradient chunks of `stream`
+	int* d_pipe_patch = nullptr;
+	hipStream_t stream2 = nullptr;
+	std::vector<hipEvent_t> pipe_ev;
+	hipEvent_t pipe_start = nullptr, pipe_done = nullptr;
 	ncclComm_t comm = nullptr;
 	bool in_group = false;
 	int* d_send = nullptr;
@@ -139,19 +146,25 @@ struct fvhip_ctx
 		(void)hipSetDevice(device);
 		if(comm) (void)ncclCommDestroy(comm);
 		for(auto& r : recs) { (void)hipEventDestroy(r.a); (void)hipEventDestroy(r.b); }
+		for(hipEvent_t e : pipe_ev) (void)hipEventDestroy(e);
+		if(pipe_start) (void)hipEventDestroy(pipe_start);
+		if(pipe_done) (void)hipEventDestroy(pipe_done);
+		if(stream2) (void)hipStreamDestroy(stream2);
 		for(void* p : owned) (void)hipFree(p);
 		for(void* p : owned_host) (void)hipHostFree(p);
 		if(stream) (void)hipStreamDestroy(stream);
 	}
 
 	template <typename F>
-	void timed(const std::string& name, F&& launch) {
+	void timed(const std::string& name, F&& launch) { timed_on(stream, name, launch); }
+	template <typename F>
+	void timed_on(hipStream_t st, const std::string& name, F&& launch) {
 		if(!prof) { launch(); return; }
 		Rec r; r.name = name;
 		HC(hipEventCreate(&r.a)); HC(hipEventCreate(&r.b));
-		HC(hipEventRecord(r.a, stream));
+		HC(hipEventRecord(r.a, st));
 		launch();
-		HC(hipEventRecord(r.b, stream));
+		HC(hipEventRecord(r.b, st));
 		recs.push_back(r);
 	}
 	void collect() {
@@ -185,7 +198,7 @@ struct fvhip_ctx
 		if(L.nghost > 0)
 			timed("k_ghost_prim", [&]{ launch_cons2prim_rows(P.gas, u, d_up, L.ncell, L.nghost, stream); });
 		if(cfg.gradientscheme == FVHIP_GRAD_LEASTSQUARES) {
-			timed("k_prep_grad_wls", [&]{ KOPS(launch_prep_grad_wls)(M, P, u, d_up, d_ubc, d_ug, d_grad, stream); });
+			timed("k_prep_grad_wls", [&]{ KOPS(launch_prep_grad_wls)(M, P, u, d_up, d_ubc, d_ug, d_grad, stream, 0, -1); });
 		} else {
 			timed("k_prep", [&]{ KOPS(launch_prep)(M, P, u, d_up, d_ubc, d_ug, true, stream); });
 			if(cfg.gradientscheme == FVHIP_GRAD_GREENGAUSS)
@@ -201,10 +214,13 @@ struct fvhip_ctx
 		timed("k_limiter", [&]{ KOPS(launch_limiter)(M, P, venk, d_up, d_ug, d_grad, d_phi, stream); });
 	}
 	void stage_weno() { timed("k_weno", [&]{ KOPS(launch_weno)(M, P, d_grad, d_lgrad, stream); }); }
-	void stage_sweep(const double* u, double* r, bool dt, double* dtm, bool overwrite) {
+	void stage_sweep(const double* u, double* r, bool dt, double* dtm, bool overwrite,
+	                 const int* plist = nullptr, int pcount = 0, hipStream_t st = nullptr) {
+		if(!st) st = stream;
 		const int rk = recKind();
 		SweepBuffers B{};
 		B.u = u; B.r = r; B.dtm = dtm; B.overwrite = overwrite ? 1 : 0;
+		B.plist = plist; B.pcount = pcount;
 		if(rk != SR_FIRST) {
 			B.up = d_up; B.grad = d_grad; B.rgrad = d_grad; B.ubc = d_ubc; B.ug = d_ug;
 			if(limited()) B.phi = d_phi;
@@ -212,7 +228,7 @@ struct fvhip_ctx
 		}
 		const char* nm = nullptr;
 		// name is only known after launch; record under a generic label then rename
-		timed("k_sweep", [&]{ nm = KOPS(launch_sweep)(M, P, B, cfg.conv_numflux, rk, viscKind(), dt, stream); });
+		timed_on(st, "k_sweep", [&]{ nm = KOPS(launch_sweep)(M, P, B, cfg.conv_numflux, rk, viscKind(), dt, st); });
 		if(prof && !recs.empty() && recs.back().name == "k_sweep" && nm) recs.back().name = nm;
 		HC(hipGetLastError());
 	}
@@ -222,7 +238,40 @@ struct fvhip_ctx
 	}
 
 	/// one-launch residual (WLS + MUSCL / unlimited linear, inviscid)
-	bool fused() const { return !L.fz_ext_start.empty() && !use_staged; }
+	bool fused() const { return !L.fz_ext_start.empty() && !use_staged && !use_pipe; }
+	/// pipelined staged residual (single domain, WLS + MUSCL / unlimited linear, viscous too), on
+	/// request only: on C4 it measured 0.55 ms against 0.46 ms for the serial staged path (the
+	/// FP64-bound sweep groups and the HBM-bound gradient chunks slow each other down, and every
+	/// group has its own tail)
+	bool pipelined() const { return !L.pipe_cell_start.empty() && !halo() && !use_staged && use_pipe; }
+	/// gradient chunks on `stream`; each sweep group on stream2 waits for the last chunk it reads.
+	/// Same kernels and arithmetic as the staged path, so bitwise its result.
+	void residual_pipelined(const double* u, double* r, bool dt, double* dtm, bool overwrite) {
+		const int K = static_cast<int>(L.pipe_cell_start.size()) - 1;
+		if(!stream2) {
+			HC(hipStreamCreateWithFlags(&stream2, hipStreamNonBlocking));
+			pipe_ev.resize(K);
+			for(hipEvent_t& e : pipe_ev) HC(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+			HC(hipEventCreateWithFlags(&pipe_start, hipEventDisableTiming));
+			HC(hipEventCreateWithFlags(&pipe_done, hipEventDisableTiming));
+		}
+		HC(hipEventRecord(pipe_start, stream));          // everything the caller queued before
+		HC(hipStreamWaitEvent(stream2, pipe_start, 0));
+		for(int k = 0; k < K; k++) {
+			timed("k_prep_grad_wls", [&]{
+				KOPS(launch_prep_grad_wls)(M, P, u, d_up, d_ubc, d_ug, d_grad, stream, L.pipe_cell_start[k], L.pipe_cell_start[k+1]);
+			});
+			HC(hipEventRecord(pipe_ev[k], stream));
+		}
+		for(int k = 0; k < K; k++) {
+			const int n = L.pipe_group_start[k+1] - L.pipe_group_start[k];
+			if(n == 0) continue;
+			HC(hipStreamWaitEvent(stream2, pipe_ev[k], 0));
+			stage_sweep(u, r, dt, dtm, overwrite, d_pipe_patch + L.pipe_group_start[k], n, stream2);
+		}
+		HC(hipEventRecord(pipe_done, stream2));
+		HC(hipStreamWaitEvent(stream, pipe_done, 0));   // the residual completes on `stream`
+	}
 	void stage_fused(const double* u, double* r, bool dt, double* dtm, bool overwrite) {
 		SweepBuffers B{};
 		B.u = u; B.r = r; B.dtm = dtm; B.overwrite = overwrite ? 1 : 0;
@@ -273,6 +322,10 @@ struct fvhip_ctx
 			for(size_t i = 0; i < hs.size(); i++) hs[i]->exchange_rccl(arr_of(i), width);
 		};
 		fvhip_ctx* h0 = hs[0];
+		if(hs.size() == 1 && !exg && h0->pipelined()) {
+			h0->residual_pipelined(us[0], rs[0], dt, dts[0], overwrite);
+			return;
+		}
 		if(h0->fused()) {
 			if(h0->halo()) {
 				// ghost rows of u, then the gradients of the cells other ranks hold as ghosts

@@ -105,6 +105,7 @@ static fvhip_ctx* createCtx(const MeshTopo& T, const fvhip_flow_config* cfg, int
 		M.fz_slot_lr = reinterpret_cast<const int2*>(upload(L.fz_slot_lr, o));
 		M.fz_max_cells = L.fz_max_cells;
 	}
+	if(!L.pipe_patch.empty()) h->d_pipe_patch = upload(L.pipe_patch, o);
 	h->d_perm = upload(L.perm, o);
 	h->nsend = static_cast<int>(L.send_cells.size());
 	h->nborder = static_cast<int>(L.border_cells.size());
@@ -245,8 +246,9 @@ int fvhip_compute_residual_device(fvhip_handle h, const double* d_u, double* d_r
 	return guard([&] {
 		HC(hipSetDevice(h->device));
 		h->use_staged = (flags & FVHIP_RES_STAGED) != 0;
+		h->use_pipe = (flags & FVHIP_RES_PIPELINED) != 0;
 		h->residual(d_u, d_r, gettimesteps != 0, d_dtm, (flags & FVHIP_RES_OVERWRITE) != 0);
-		h->use_staged = false;
+		h->use_staged = h->use_pipe = false;
 	});
 }
 

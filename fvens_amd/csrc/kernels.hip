@@ -142,13 +142,14 @@ __global__ void __launch_bounds__(256) k_grad_wls(DevMesh M, const double* __res
 /// block are gathered from global memory.
 __global__ void __launch_bounds__(256) k_prep_grad_wls(DevMesh M, DevPhys P, const double* __restrict__ u,
                                                        double* __restrict__ up, double* __restrict__ ubc,
-                                                       double* __restrict__ ug, double* __restrict__ grad)
+                                                       double* __restrict__ ug, double* __restrict__ grad,
+                                                       int c_begin, int c_end)
 {
 	__shared__ __attribute__((aligned(16))) double s_up[256][4];
 	__shared__ __attribute__((aligned(16))) double2 s_rc[256];
 	const int N = M.ncell;        // owned + ghost: neighbour codes >= N are boundary faces
-	const int NO = M.nown;
-	const int cb = xcd_chunk(static_cast<int>((NO + 255) >> 8))*256;
+	const int NO = c_end;         // this launch's cells: [c_begin, c_end) of the owned cells
+	const int cb = c_begin + xcd_chunk(static_cast<int>((c_end - c_begin + 255) >> 8))*256;
 	if(cb >= NO) return;
 	const int t = static_cast<int>(threadIdx.x);
 	const int c = cb + t;
@@ -458,10 +459,11 @@ __global__ void __launch_bounds__(SLOTS_MAX) k_sweep(const DevMesh M, const DevP
 	__shared__ __attribute__((aligned(16))) double sbuf[S::BUF];
 
 	// XCD-aware mapping: consecutive patches (which share halo cells) land on the same XCD
-	const int np = M.npatch;
+	const int np = B.plist ? B.pcount : M.npatch;
 	const int q = (np + 7) >> 3;
-	const int p = (blockIdx.x & 7) * q + (blockIdx.x >> 3);
-	if(p >= np) return;
+	const int pi = (blockIdx.x & 7) * q + (blockIdx.x >> 3);
+	if(pi >= np) return;
+	const int p = B.plist ? B.plist[pi] : pi;
 	const int s0 = M.patch_slot[p], s1 = M.patch_slot[p+1];
 	const int c0 = M.patch_cell[p], c1 = M.patch_cell[p+1];
 	const int nc = c1 - c0;
@@ -703,10 +705,11 @@ template <int FLUX, int REC, bool DT>
 __global__ void __launch_bounds__(SLOTS_MAX, 4) k_residual_wls(const DevMesh M, const DevPhys P, const SweepBuffers B)
 {
 	extern __shared__ __attribute__((aligned(16))) double fz[];
-	const int np = M.npatch;
+	const int np = B.plist ? B.pcount : M.npatch;
 	const int q = (np + 7) >> 3;
-	const int p = (blockIdx.x & 7) * q + (blockIdx.x >> 3);
-	if(p >= np) return;
+	const int pi = (blockIdx.x & 7) * q + (blockIdx.x >> 3);
+	if(pi >= np) return;
+	const int p = B.plist ? B.plist[pi] : pi;
 	const int s0 = M.patch_slot[p], s1 = M.patch_slot[p+1];
 	const int c0 = M.patch_cell[p], c1 = M.patch_cell[p+1];
 	const int nc = c1 - c0;
@@ -962,8 +965,12 @@ void launch_prep(const DevMesh& M, const DevPhys& P, const double* u, double* up
 void launch_grad_wls(const DevMesh& M, const double* up, const double* ug, double* grad, hipStream_t s)
 { if(M.nown > 0) k_grad_wls<<<nblk(M.nown,256), 256, 0, s>>>(M, up, ug, grad); }
 void launch_prep_grad_wls(const DevMesh& M, const DevPhys& P, const double* u, double* up, double* ubc,
-                          double* ug, double* grad, hipStream_t s)
-{ if(M.nown > 0) k_prep_grad_wls<<<xcd_blocks((M.nown + 255)/256), 256, 0, s>>>(M, P, u, up, ubc, ug, grad); }
+                          double* ug, double* grad, hipStream_t s, int c_begin, int c_end)
+{
+	if(c_end < 0) c_end = M.nown;
+	if(c_end > c_begin)
+		k_prep_grad_wls<<<xcd_blocks((c_end - c_begin + 255)/256), 256, 0, s>>>(M, P, u, up, ubc, ug, grad, c_begin, c_end);
+}
 void launch_grad_wls_list(const DevMesh& M, const DevPhys& P, const double* u, const int* list, int n,
                           double* grad, hipStream_t s)
 { if(n > 0) k_grad_wls_list<<<nblk(n,256), 256, 0, s>>>(M, P, u, list, n, grad); }
@@ -1037,8 +1044,8 @@ const char* launch_sweep(const DevMesh& M, const DevPhys& P, const SweepBuffers&
 		case 5: fn = pick2<5>(rec, visc, dt, phi); break;
 		default: fn = pick2<6>(rec, visc, dt, phi); break;
 	}
-	const int q = (M.npatch + 7) / 8;
-	if(M.npatch > 0) hipLaunchKernelGGL(fn, dim3(8*q), dim3(SLOTS_MAX), 0, s, M, P, B);
+	const int np = B.plist ? B.pcount : M.npatch;
+	if(np > 0) hipLaunchKernelGGL(fn, dim3(8*((np + 7)/8)), dim3(SLOTS_MAX), 0, s, M, P, B);
 	return kSweepNames[flux < 0 || flux > 6 ? 6 : flux];
 }
 
@@ -1075,8 +1082,8 @@ const char* launch_residual_wls(const DevMesh& M, const DevPhys& P, const SweepB
 	const size_t lds = std::max(static_cast<size_t>(M.fz_max_cells)*FZW, static_cast<size_t>(6*SLOTS_MAX))*sizeof(double);
 	(void)hipFuncSetAttribute(reinterpret_cast<const void*>(fn), hipFuncAttributeMaxDynamicSharedMemorySize,
 	                          static_cast<int>(lds));
-	const int q = (M.npatch + 7) / 8;
-	if(M.npatch > 0) hipLaunchKernelGGL(fn, dim3(8*q), dim3(SLOTS_MAX), lds, s, M, P, B);
+	const int np = B.plist ? B.pcount : M.npatch;
+	if(np > 0) hipLaunchKernelGGL(fn, dim3(8*((np + 7)/8)), dim3(SLOTS_MAX), lds, s, M, P, B);
 	return kFusedNames[flux < 0 || flux > 6 ? 6 : flux];
 }
 

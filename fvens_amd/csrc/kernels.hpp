@@ -68,6 +68,8 @@ struct SweepBuffers
 	double* r;            // [N][4]
 	double* dtm;          // [N]
 	int overwrite;
+	const int* plist;     // patches to sweep (pcount of them), or null: all patches
+	int pcount;
 };
 
 // Host launchers (all asynchronous on stream). kernels.hip is compiled twice: namespace `exact`
@@ -78,7 +80,7 @@ void launch_prep(const DevMesh& M, const DevPhys& P, const double* u, double* up
                  bool cells, hipStream_t s); \
 void launch_grad_wls(const DevMesh& M, const double* up, const double* ug, double* grad, hipStream_t s); \
 void launch_prep_grad_wls(const DevMesh& M, const DevPhys& P, const double* u, double* up, double* ubc, \
-                          double* ug, double* grad, hipStream_t s); \
+                          double* ug, double* grad, hipStream_t s, int c_begin = 0, int c_end = -1); \
 void launch_grad_wls_list(const DevMesh& M, const DevPhys& P, const double* u, const int* list, int n, \
                           double* grad, hipStream_t s); \
 void launch_grad_gg(const DevMesh& M, const double* up, const double* ug, double* grad, hipStream_t s); \

@@ -291,7 +291,48 @@ Layout buildLayout(const MeshTopo& T, const fvhip_flow_config& cfg, bool renumbe
 		for(int c = 0; c < N; c++) Lo.venk_eps2[c] = std::pow(cfg.limiter_param*T.clength[Lo.perm[c]], 3);
 	}
 	if(fused) buildFused(Lo);
+	if(Lo.nghost == 0 && pipelineEligible(cfg)) buildPipeline(Lo, PIPE_CHUNKS);
 	return Lo;
+}
+
+bool pipelineEligible(const fvhip_flow_config& cfg)
+{
+	return cfg.order2 && cfg.gradientscheme == FVHIP_GRAD_LEASTSQUARES &&
+	       (cfg.reconstruction == FVHIP_REC_VANALBADA || cfg.reconstruction == FVHIP_REC_NONE);
+}
+
+void buildPipeline(Layout& Lo, int chunks)
+{
+	const int N = Lo.ncell;
+	const int npatch = static_cast<int>(Lo.patch_cell.size()) - 1;
+	if(chunks < 1 || N == 0) { Lo.pipe_cell_start.clear(); return; }
+	// chunk boundaries on 256-cell blocks of the gradient kernel
+	const int nblk = (N + 255)/256;
+	Lo.pipe_cell_start.assign(1, 0);
+	for(int k = 1; k < chunks; k++) {
+		const int b = static_cast<int>((static_cast<long long>(nblk)*k)/chunks)*256;
+		if(b > Lo.pipe_cell_start.back() && b < N) Lo.pipe_cell_start.push_back(b);
+	}
+	Lo.pipe_cell_start.push_back(N);
+	const int K = static_cast<int>(Lo.pipe_cell_start.size()) - 1;
+	auto chunkOf = [&](int c) {
+		return static_cast<int>(std::upper_bound(Lo.pipe_cell_start.begin(), Lo.pipe_cell_start.end(), c)
+		                        - Lo.pipe_cell_start.begin()) - 1;
+	};
+	// a patch reads the primitive states and gradients of its cells and of the far side of its cut
+	// faces (and the ghost states of its own boundary faces, written with its cells)
+	std::vector<int> dep(npatch, 0);
+	for(int p = 0; p < npatch; p++)
+		for(int s = Lo.patch_slot[p]; s < Lo.patch_slot[p+1]; s++) {
+			dep[p] = std::max(dep[p], chunkOf(Lo.slot_L[s]));
+			if(Lo.slot_R[s] < N) dep[p] = std::max(dep[p], chunkOf(Lo.slot_R[s]));
+		}
+	Lo.pipe_group_start.assign(K+1, 0);
+	for(int p = 0; p < npatch; p++) Lo.pipe_group_start[dep[p]+1]++;
+	for(int k = 0; k < K; k++) Lo.pipe_group_start[k+1] += Lo.pipe_group_start[k];
+	Lo.pipe_patch.assign(npatch, -1);
+	std::vector<int> pos(Lo.pipe_group_start.begin(), Lo.pipe_group_start.end() - 1);
+	for(int p = 0; p < npatch; p++) Lo.pipe_patch[pos[dep[p]]++] = p;
 }
 
 bool fusedEligible(const fvhip_flow_config& cfg)

@@ -81,9 +81,16 @@ struct Layout
 	                                       ///<  -2-bf (boundary face), -1 (none); row offset = 4*(c0 + ext_start)
 	std::vector<int> fz_slot_lr;           ///< [S][2] local L, R (R boundary: -2-bf)
 	int fz_max_cells = 0;
+	// pipelined staged residual (single domain, WLS): the gradient kernel runs in chunks of cells on
+	// one stream while the sweep runs, on a second stream, the patches whose cells and halo cells
+	// all lie in finished chunks; patches are grouped by the last chunk they read
+	std::vector<int> pipe_cell_start;      ///< [K+1] gradient chunks (internal cell ranges)
+	std::vector<int> pipe_patch;           ///< patches ordered by group, ascending index within one
+	std::vector<int> pipe_group_start;     ///< [K+1] ranges into pipe_patch
 };
 
 constexpr int FUSED_LDS_CELLS = 704;     ///< staged cells per patch: 704 x 112 B = 77 KB (2 blocks/CU)
+constexpr int PIPE_CHUNKS = 8;          ///< gradient chunks of the pipelined staged residual
 constexpr int FUSED_GLOBAL = 1 << 20;    ///< neighbour codes >= this are global internal ids + FUSED_GLOBAL
 
 /// whether cfg takes the fused residual kernel (WLS + MUSCL/unlimited linear, inviscid). On a
@@ -91,6 +98,11 @@ constexpr int FUSED_GLOBAL = 1 << 20;    ///< neighbour codes >= this are global
 bool fusedEligible(const fvhip_flow_config& cfg);
 /// builds the fz_* arrays (owned-only meshes)
 void buildFused(Layout& Lo);
+
+/// whether cfg takes the pipelined staged residual (order 2, WLS, MUSCL/unlimited linear; viscous
+/// allowed) and, if so, builds the pipe_* schedule with `chunks` gradient chunks (single domain)
+bool pipelineEligible(const fvhip_flow_config& cfg);
+void buildPipeline(Layout& Lo, int chunks);
 
 /// Builds the layout from the reference's mesh arrays. bc_of_tag maps a boundary marker to the
 /// index of its BC in the config. Throws std::runtime_error on unsupported meshes.

@@ -146,6 +146,10 @@ int fvhip_compute_residual(fvhip_handle h, const double* u, double* r, int getti
 /** flags: FVHIP_RES_STAGED = use the gradient kernel + sweep kernel even where the one-launch
  *  fused residual applies (WLS + MUSCL/unlimited linear, inviscid, single domain); same results */
 #define FVHIP_RES_STAGED 2
+/** flags: FVHIP_RES_PIPELINED = gradient kernel in chunks on the handle's stream, overlapped with
+ *  the sweep of the patches whose inputs are ready on a second stream (single domain, WLS +
+ *  MUSCL/unlimited linear, viscous too); same results. Opt-in: slower than the serial path on C4 */
+#define FVHIP_RES_PIPELINED 4
 int fvhip_compute_residual_device(fvhip_handle h, const double* d_u, double* d_r, int gettimesteps,
                                   double* d_dtm, int flags);
 /** FlowFV_base::getGradients: conserved-variable gradients, GradBlock layout [nelem][4 vars][2 dims] */

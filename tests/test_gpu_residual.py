@@ -275,3 +275,37 @@ def test_fused_equals_staged_bitwise(flux, rec, meshkey, kind):
     np.testing.assert_array_equal(out[0][1], out[1][1])
     kt = dev.kernel_times() if False else None
     dev.close()
+
+
+# ------------------------------------------------------------------------------------------------
+# pipelined staged residual (gradient chunks overlapped with sweep groups on a second stream) vs
+# the serial staged path: same kernels, so bitwise; viscous configurations take it by default
+# ------------------------------------------------------------------------------------------------
+@pytest.mark.parametrize("meshkey,kind,flux,rec", [("naca_small", "naca", "ROE", "VANALBADA"),
+                                                   ("naca_c2", "naca", "ROE", "VANALBADA"),
+                                                   ("naca_small", "visc", "ROE", "NONE"),
+                                                   ("naca_small", "viscconst", "HLLC", "VANALBADA"),
+                                                   ("plate_small", "plate", "HLLC", "NONE"),
+                                                   ("2dcylinderhybrid.msh", "cyl", "LLF", "NONE")])
+def test_pipelined_equals_staged_bitwise(meshkey, kind, flux, rec):
+    import torch
+    m, _ = get_mesh(meshkey)
+    p = cases.physics(kind)
+    n = cases.numerics(flux, "LEASTSQUARES", rec)
+    u = cases.state(m, p, 9)
+    dev = fa.FlowFV(m, p, n)
+    perm = dev.permutation()
+    du = torch.tensor(u[perm], device="cuda")
+    out = []
+    for mode in ("staged", "pipelined"):
+        dr = torch.full((m.nelem, 4), float("nan"), dtype=torch.float64, device="cuda")
+        dt = torch.full((m.nelem,), float("nan"), dtype=torch.float64, device="cuda")
+        for _ in range(2):      # the second call reuses the streams and events
+            dev.compute_residual_device(du.data_ptr(), dr.data_ptr(), dt.data_ptr(), True, True,
+                                        staged=mode == "staged", pipelined=mode == "pipelined")
+        dev.synchronize()
+        out.append((dr.cpu().numpy(), dt.cpu().numpy()))
+    np.testing.assert_array_equal(out[0][0], out[1][0])
+    np.testing.assert_array_equal(out[0][1], out[1][1])
+    assert np.all(np.isfinite(out[1][0]))
+    dev.close()
