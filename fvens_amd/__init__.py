@@ -371,9 +371,10 @@ class FlowFV:
         return out
 
     def layout_stats(self):
-        s = (ctypes.c_longlong * 9)()
+        s = (ctypes.c_longlong * 10)()
         check(_ffi.lib().fvhip_layout_stats(self._h, s))
-        keys = ("cells", "faces", "slots", "patches", "max_slots", "bfaces", "ghosts", "neighbours", "send_rows")
+        keys = ("cells", "faces", "slots", "patches", "max_slots", "bfaces", "ghosts", "neighbours", "send_rows",
+                "interior_patches")
         return dict(zip(keys, [int(x) for x in s]))
 
     def close(self):

@@ -131,6 +131,10 @@ struct fvhip_ctx
 	hipEvent_t pipe_start = nullptr, pipe_done = nullptr;
 	ncclComm_t comm = nullptr;
 	bool in_group = false;
+	// halo exchange overlapped with the interior patches of the fused residual (RCCL handles)
+	int* d_fz_order = nullptr;
+	hipStream_t comm_stream = nullptr;
+	hipEvent_t ev_u = nullptr, ev_halo = nullptr;
 	int* d_send = nullptr;
 	int* d_border = nullptr;
 	int nborder = 0;
@@ -150,6 +154,9 @@ struct fvhip_ctx
 		if(pipe_start) (void)hipEventDestroy(pipe_start);
 		if(pipe_done) (void)hipEventDestroy(pipe_done);
 		if(stream2) (void)hipStreamDestroy(stream2);
+		if(ev_u) (void)hipEventDestroy(ev_u);
+		if(ev_halo) (void)hipEventDestroy(ev_halo);
+		if(comm_stream) (void)hipStreamDestroy(comm_stream);
 		for(void* p : owned) (void)hipFree(p);
 		for(void* p : owned_host) (void)hipHostFree(p);
 		if(stream) (void)hipStreamDestroy(stream);
@@ -233,8 +240,9 @@ struct fvhip_ctx
 		HC(hipGetLastError());
 	}
 
-	void stage_border_gradients(const double* u) {
-		timed("k_grad_wls_list", [&]{ KOPS(launch_grad_wls_list)(M, P, u, d_border, nborder, d_grad, stream); });
+	void stage_border_gradients(const double* u, hipStream_t st = nullptr) {
+		if(!st) st = stream;
+		timed_on(st, "k_grad_wls_list", [&]{ KOPS(launch_grad_wls_list)(M, P, u, d_border, nborder, d_grad, st); });
 	}
 
 	/// one-launch residual (WLS + MUSCL / unlimited linear, inviscid)
@@ -272,9 +280,12 @@ struct fvhip_ctx
 		HC(hipEventRecord(pipe_done, stream2));
 		HC(hipStreamWaitEvent(stream, pipe_done, 0));   // the residual completes on `stream`
 	}
-	void stage_fused(const double* u, double* r, bool dt, double* dtm, bool overwrite) {
+	void stage_fused(const double* u, double* r, bool dt, double* dtm, bool overwrite,
+	                 const int* plist = nullptr, int pcount = 0) {
 		SweepBuffers B{};
 		B.u = u; B.r = r; B.dtm = dtm; B.overwrite = overwrite ? 1 : 0;
+		B.plist = plist; B.pcount = pcount;
+		if(plist && pcount == 0) return;
 		B.grad = d_grad;     // received gradients of ghost cells (partitioned meshes)
 		const char* nm = nullptr;
 		timed("k_residual_wls", [&]{ nm = KOPS(launch_residual_wls)(M, P, B, cfg.conv_numflux, recKind(), dt, stream); });
@@ -283,23 +294,46 @@ struct fvhip_ctx
 	}
 
 	/// pack the rows of `arr` (width doubles per cell) that the neighbours hold as ghosts
-	void pack(const double* arr, int width) {
-		timed("k_pack", [&]{ launch_pack_rows(d_send, nsend, arr, width, d_sendbuf, stream); });
+	void pack(const double* arr, int width, hipStream_t st = nullptr) {
+		if(!st) st = stream;
+		timed_on(st, "k_pack", [&]{ launch_pack_rows(d_send, nsend, arr, width, d_sendbuf, st); });
 	}
-	/// RCCL point-to-point exchange with every neighbour rank, on this handle's stream
-	void exchange_rccl(double* arr, int width) {
+	/// RCCL point-to-point exchange with every neighbour rank, on stream st (default: the handle's)
+	void exchange_rccl(double* arr, int width, hipStream_t st = nullptr) {
 		if(!halo()) return;
 		if(!comm) throw std::runtime_error("partitioned handle: call fvhip_comm_init (or use a group) first");
-		pack(arr, width);
+		if(!st) st = stream;
+		pack(arr, width, st);
 		NC(ncclGroupStart());
 		for(size_t k = 0; k < L.nbr_rank.size(); k++) {
 			const int q = L.nbr_rank[k];
 			const size_t ns = static_cast<size_t>(L.send_start[k+1] - L.send_start[k]);
 			const size_t ng = static_cast<size_t>(L.ghost_start[k+1] - L.ghost_start[k]);
-			NC(ncclSend(d_sendbuf + static_cast<size_t>(width)*L.send_start[k], width*ns, ncclDouble, q, comm, stream));
-			NC(ncclRecv(arr + static_cast<size_t>(width)*(L.ncell + L.ghost_start[k]), width*ng, ncclDouble, q, comm, stream));
+			NC(ncclSend(d_sendbuf + static_cast<size_t>(width)*L.send_start[k], width*ns, ncclDouble, q, comm, st));
+			NC(ncclRecv(arr + static_cast<size_t>(width)*(L.ncell + L.ghost_start[k]), width*ng, ncclDouble, q, comm, st));
 		}
 		NC(ncclGroupEnd());
+	}
+
+	/// fused residual of one RCCL rank: the halo exchange (ghost u, border gradients, ghost
+	/// gradients) runs on comm_stream while the interior patches run on `stream`; the border
+	/// patches follow once the halo has arrived
+	void residual_fused_overlapped(const double* u, double* r, bool dt, double* dtm, bool overwrite) {
+		if(!comm_stream) {
+			HC(hipStreamCreateWithFlags(&comm_stream, hipStreamNonBlocking));
+			HC(hipEventCreateWithFlags(&ev_u, hipEventDisableTiming));
+			HC(hipEventCreateWithFlags(&ev_halo, hipEventDisableTiming));
+		}
+		double* uu = const_cast<double*>(u);
+		HC(hipEventRecord(ev_u, stream));                 // u as the caller left it
+		HC(hipStreamWaitEvent(comm_stream, ev_u, 0));
+		exchange_rccl(uu, 4, comm_stream);
+		stage_border_gradients(u, comm_stream);
+		exchange_rccl(d_grad, 8, comm_stream);
+		HC(hipEventRecord(ev_halo, comm_stream));
+		stage_fused(u, r, dt, dtm, overwrite, d_fz_order, L.fz_ninner);
+		HC(hipStreamWaitEvent(stream, ev_halo, 0));
+		stage_fused(u, r, dt, dtm, overwrite, d_fz_order + L.fz_ninner, static_cast<int>(L.fz_order.size()) - L.fz_ninner);
 	}
 
 	/// the device sweep: -r(u) added (or written) into r, time steps into dtm. On a partitioned
@@ -328,10 +362,18 @@ struct fvhip_ctx
 		}
 		if(h0->fused()) {
 			if(h0->halo()) {
-				// ghost rows of u, then the gradients of the cells other ranks hold as ghosts
+				if(hs.size() == 1 && !exg) { h0->residual_fused_overlapped(us[0], rs[0], dt, dts[0], overwrite); return; }
+				// interior patches need no halo data: they run first, then the exchange of the ghost
+				// rows of u and of the gradients of the cells other ranks hold as ghosts, then the rest
+				for(size_t i = 0; i < hs.size(); i++)
+					hs[i]->stage_fused(us[i], rs[i], dt, dts[i], overwrite, hs[i]->d_fz_order, hs[i]->L.fz_ninner);
 				exchange([&](size_t i) { return const_cast<double*>(us[i]); }, 4);
 				for(size_t i = 0; i < hs.size(); i++) hs[i]->stage_border_gradients(us[i]);
 				exchange([&](size_t i) { return hs[i]->d_grad; }, 8);
+				for(size_t i = 0; i < hs.size(); i++)
+					hs[i]->stage_fused(us[i], rs[i], dt, dts[i], overwrite, hs[i]->d_fz_order + hs[i]->L.fz_ninner,
+					                   static_cast<int>(hs[i]->L.fz_order.size()) - hs[i]->L.fz_ninner);
+				return;
 			}
 			for(size_t i = 0; i < hs.size(); i++) hs[i]->stage_fused(us[i], rs[i], dt, dts[i], overwrite);
 			return;

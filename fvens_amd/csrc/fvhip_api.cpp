@@ -106,6 +106,7 @@ static fvhip_ctx* createCtx(const MeshTopo& T, const fvhip_flow_config* cfg, int
 		M.fz_max_cells = L.fz_max_cells;
 	}
 	if(!L.pipe_patch.empty()) h->d_pipe_patch = upload(L.pipe_patch, o);
+	if(L.nghost > 0 && !L.fz_order.empty()) h->d_fz_order = upload(L.fz_order, o);
 	h->d_perm = upload(L.perm, o);
 	h->nsend = static_cast<int>(L.send_cells.size());
 	h->nborder = static_cast<int>(L.border_cells.size());
@@ -544,6 +545,7 @@ int fvhip_layout_stats(fvhip_handle h, long long* s)
 		s[0] = h->L.ncell; s[1] = h->L.naface; s[2] = static_cast<long long>(h->L.slot_L.size());
 		s[3] = static_cast<long long>(h->L.patch_cell.size()) - 1; s[4] = h->L.max_slots; s[5] = h->L.nbface;
 		s[6] = h->L.nghost; s[7] = static_cast<long long>(h->L.nbr_rank.size()); s[8] = h->nsend;
+		s[9] = h->L.fz_ninner;
 	});
 }
 

@@ -350,6 +350,7 @@ void buildFused(Layout& Lo)
 	Lo.fz_slot_lr.assign(2*Lo.slot_L.size(), -1);
 	Lo.fz_max_cells = 0;
 	std::vector<int> lidx(N, -1);          // patch-local index of a cell while its patch is built
+	std::vector<char> innerp(npatch, 0);
 	for(int p = 0; p < npatch; p++) {
 		const int c0 = Lo.patch_cell[p], c1 = Lo.patch_cell[p+1], nc = c1 - c0;
 		const size_t e0 = Lo.fz_ext.size();
@@ -380,9 +381,21 @@ void buildFused(Layout& Lo)
 			Lo.fz_slot_lr[2*static_cast<size_t>(s)+1] = code(Lo.slot_R[s]);
 		}
 		Lo.fz_max_cells = std::max(Lo.fz_max_cells, nl);
+		// interior patch: stages no ghost cell and reads none from global memory, so it needs no
+		// halo data and can run while the exchange is in flight
+		bool inner = true;
+		for(size_t k = e0; k < Lo.fz_ext.size(); k++) if(Lo.fz_ext[k] >= Lo.ncell) inner = false;
+		const size_t g0 = 4*(static_cast<size_t>(c0) + e0);
+		for(size_t k = g0; k < Lo.fz_gnbr.size(); k++)
+			if(Lo.fz_gnbr[k] >= FUSED_GLOBAL && Lo.fz_gnbr[k] - FUSED_GLOBAL >= Lo.ncell) inner = false;
+		innerp[p] = inner ? 1 : 0;
 		for(int c = c0; c < c1; c++) lidx[c] = -1;
 		for(size_t k = e0; k < Lo.fz_ext.size(); k++) lidx[Lo.fz_ext[k]] = -1;
 	}
+	Lo.fz_order.clear();
+	for(int p = 0; p < npatch; p++) if(innerp[p]) Lo.fz_order.push_back(p);
+	Lo.fz_ninner = static_cast<int>(Lo.fz_order.size());
+	for(int p = 0; p < npatch; p++) if(!innerp[p]) Lo.fz_order.push_back(p);
 }
 
 }

@@ -81,6 +81,8 @@ struct Layout
 	                                       ///<  -2-bf (boundary face), -1 (none); row offset = 4*(c0 + ext_start)
 	std::vector<int> fz_slot_lr;           ///< [S][2] local L, R (R boundary: -2-bf)
 	int fz_max_cells = 0;
+	std::vector<int> fz_order;             ///< patches needing no halo data first (fz_ninner), then the rest
+	int fz_ninner = 0;
 	// pipelined staged residual (single domain, WLS): the gradient kernel runs in chunks of cells on
 	// one stream while the sweep runs, on a second stream, the patches whose cells and halo cells
 	// all lie in finished chunks; patches are grouped by the last chunk they read

@@ -79,6 +79,10 @@ def test_partitioned_c2_eight_ranks():
     r, dt, r1, dt1, stats = run_partitioned(*CONFIGS[7], 8)
     np.testing.assert_array_equal(r, r1)
     np.testing.assert_array_equal(dt, dt1)
+    # the fused residual runs most patches before the halo arrives (overlapped with the exchange)
+    for s in stats:
+        assert 0 < s["interior_patches"] < s["patches"]
+        assert s["interior_patches"] >= 0.7 * s["patches"], s
 
 
 def test_partitioned_fast_math_within_tolerance():
