@@ -100,6 +100,7 @@ def main():
     ap.add_argument("--cpu-sweeps", type=int, default=3)
     ap.add_argument("--no-fast", action="store_true", help="skip the fast-math mode measurement")
     ap.add_argument("--scaling", choices=["weak", "strong"], default="weak")
+    ap.add_argument("--no-pipelined", action="store_true", help="skip the pipelined staged path")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -215,7 +216,7 @@ def main():
               "sweep_roofline_frac": round(sweep_algorithmic_bytes(*cnt) / (ssweep * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
               "sweep_algorithmic_bytes": sweep_algorithmic_bytes(*cnt)}
     pipelined = None
-    if world == 1:
+    if world == 1 and not args.no_pipelined:
         pms, pk, _ = measure(False, "pipelined")
         pipelined = {"ms_per_step": round(pms, 5), "value": round(F / (pms * 1e-3) / 1e6, 3),
                      "kernels_ms_summed_over_chunks": {k: round(v, 5) for k, v in pk.items()},

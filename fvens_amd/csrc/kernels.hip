@@ -53,6 +53,25 @@ __device__ __forceinline__ void st8(double* p, int i, const double* o) {
 	q[0] = make_double4(o[0], o[1], o[2], o[3]); q[1] = make_double4(o[4], o[5], o[6], o[7]);
 }
 
+/// Boundary ghost state out of line (abc.cpp via gasdyn.hpp ghost_state): boundary faces are rare
+/// (~sqrt(N)), but every BC type inlined into the hot kernels' unrolled neighbour loops costs
+/// registers, i.e. occupancy, on every cell and face. Arguments and result travel in registers.
+__device__ __noinline__ double4 ghost_ool(const Gas G, const BCDev bc, const double4 uinf, const double4 ins,
+                                          const double2 nn)
+{
+	const double ui[4] = {uinf.x, uinf.y, uinf.z, uinf.w}, in[4] = {ins.x, ins.y, ins.z, ins.w};
+	const double n[2] = {nn.x, nn.y};
+	double gs[4];
+	ghost_state(G, bc, ui, in, n, gs);
+	return make_double4(gs[0], gs[1], gs[2], gs[3]);
+}
+__device__ __forceinline__ void ghost(const DevPhys& P, int bc, const double* ins, const double* n, double* gs)
+{
+	const double4 g = ghost_ool(P.gas, P.bc[bc], make_double4(P.uinf[0], P.uinf[1], P.uinf[2], P.uinf[3]),
+	                            make_double4(ins[0], ins[1], ins[2], ins[3]), make_double2(n[0], n[1]));
+	gs[0] = g.x; gs[1] = g.y; gs[2] = g.z; gs[3] = g.w;
+}
+
 // ------------------------------------------------------------------------------------------------
 // preparation
 // ------------------------------------------------------------------------------------------------
@@ -183,7 +202,7 @@ __global__ void __launch_bounds__(256) k_prep_grad_wls(DevMesh M, DevPhys P, con
 			const double2 nn = M.bf_n[bf];
 			const double n[2] = {nn.x, nn.y};
 			double gs[4];
-			ghost_state(G, P.bc[M.bf_bc[bf]], P.uinf, ucons, n, gs);
+			ghost(P, M.bf_bc[bf], ucons, n, gs);
 			st4(ubc, bf, gs);
 			cons2prim(G, gs, un[k]);
 			st4(ug, bf, un[k]);
@@ -248,7 +267,7 @@ __global__ void __launch_bounds__(256) k_grad_wls_list(DevMesh M, DevPhys P, con
 			const double2 nn = M.bf_n[bf];
 			const double n[2] = {nn.x, nn.y};
 			double gs[4];
-			ghost_state(G, P.bc[M.bf_bc[bf]], P.uinf, ucons, n, gs);
+			ghost(P, M.bf_bc[bf], ucons, n, gs);
 			cons2prim(G, gs, un);
 			rn = M.bf_rcbp[bf];
 		} else {
@@ -516,7 +535,7 @@ __global__ void __launch_bounds__(SLOTS_MAX) k_sweep(const DevMesh M, const DevP
 
 		if(REC == SR_FIRST) {
 			get4(lr.x, S::UC, B.u, ul);
-			if(bnd) ghost_state(G, P.bc[M.bf_bc[bf]], P.uinf, ul, n, ur);
+			if(bnd) ghost(P, M.bf_bc[bf], ul, n, ur);
 			else    get4(lr.y, S::UC, B.u, ur);
 		}
 		else if(REC == SR_MUSCL) {
@@ -555,7 +574,7 @@ __global__ void __launch_bounds__(SLOTS_MAX) k_sweep(const DevMesh M, const DevP
 					ul[i] = muscl_left(ui[i], uj[i], dm, muscl_phi(dm, du));
 				}
 				prim2cons(G, ul, ul);
-				ghost_state(G, P.bc[M.bf_bc[bf]], P.uinf, ul, n, ur);
+				ghost(P, M.bf_bc[bf], ul, n, ur);
 			}
 		}
 		else {  // SR_LINEAR: unlimited, WENO-limited gradients or BJ/Venkatakrishnan limiter values
@@ -590,7 +609,7 @@ __global__ void __launch_bounds__(SLOTS_MAX) k_sweep(const DevMesh M, const DevP
 				}
 				prim2cons(G, ur, ur);
 			} else {
-				ghost_state(G, P.bc[M.bf_bc[bf]], P.uinf, ul, n, ur);
+				ghost(P, M.bf_bc[bf], ul, n, ur);
 			}
 		}
 
@@ -696,7 +715,7 @@ __device__ __forceinline__ double4 ghost_prim_of_cell(const DevMesh& M, const De
 	const double n[2] = {nn.x, nn.y};
 	double ucons[4], gs[4], gp[4];
 	ld4(u, cell, ucons);
-	ghost_state(P.gas, P.bc[M.bf_bc[bf]], P.uinf, ucons, n, gs);
+	ghost(P, M.bf_bc[bf], ucons, n, gs);
 	cons2prim(P.gas, gs, gp);
 	return make_double4(gp[0], gp[1], gp[2], gp[3]);
 }
@@ -844,7 +863,7 @@ __global__ void __launch_bounds__(SLOTS_MAX, 4) k_residual_wls(const DevMesh M, 
 					ul[i] = muscl_left(ui[i], uj[i], dm, muscl_phi(dm, du));
 				}
 				prim2cons(G, ul, ul);
-				ghost_state(G, P.bc[M.bf_bc[bf]], P.uinf, ul, n, ur);
+				ghost(P, M.bf_bc[bf], ul, n, ur);
 			}
 		} else {  // unlimited linear
 			const double2 gp = M.slot_gr[s];
@@ -871,7 +890,7 @@ __global__ void __launch_bounds__(SLOTS_MAX, 4) k_residual_wls(const DevMesh M, 
 				}
 				prim2cons(G, ur, ur);
 			} else {
-				ghost_state(G, P.bc[M.bf_bc[bf]], P.uinf, ul, n, ur);
+				ghost(P, M.bf_bc[bf], ul, n, ur);
 			}
 		}
 		inviscid_flux<FLUX>(G, ul, ur, n, f);
