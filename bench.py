@@ -93,8 +93,8 @@ def pmc_traffic(kernel_symbol, workload_cells):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=50)
-    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--steps", type=int, default=200)
+    ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--scale", type=int, default=1, help="divide the C4 mesh dimensions (debug)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-sweeps", type=int, default=3)
@@ -187,17 +187,18 @@ def main():
         return 1e3 * elapsed / args.steps, {k: v[0] / args.steps for k, v in kt.items()}, stats
 
     t_setup = time.time() - t0
-    ms_per_step, kernels_ms, stats = measure(False)
-    # this rank's algorithmic bytes (its owned cells, its faces incl. both copies of cut faces)
-    cnt = (stats["cells"], stats["faces"], stats["bfaces"])
 
     def dominant(km):
         k = max(km, key=km.get)
         return k, km[k]
 
+    # the secondary paths run first: by the time the primary (library default) path is timed the
+    # GPU has been busy for seconds and its clocks have settled (kernel times fall ~15 % over the
+    # first ~100 ms of a cold run)
     fast = None
     if not args.no_fast:
-        fms, fk, _ = measure(True)
+        fms, fk, stats = measure(True)
+        cnt = (stats["cells"], stats["faces"], stats["bfaces"])
         fname, fsms = dominant(fk)
         fab = kernel_bytes(fname, *cnt) / (fsms * 1e-3) / 1e9
         ftr = pmc_traffic("fast::" + kernel_symbol(fname), N) if world == 1 else None
@@ -209,7 +210,9 @@ def main():
                              "(tests/test_gpu_residual.py::test_fast_math_within_tolerance)"}
     # the two-kernel path (WLS gradient kernel + face sweep), same results bit for bit: one after
     # the other, and pipelined (gradient chunks overlapped with the sweep groups on a second stream)
-    sms, sk, _ = measure(False, "staged")
+    sms, sk, stats = measure(False, "staged")
+    # this rank's algorithmic bytes (its owned cells, its faces incl. both copies of cut faces)
+    cnt = (stats["cells"], stats["faces"], stats["bfaces"])
     sname, ssweep = [(k, v) for k, v in sk.items() if k.startswith("k_sweep")][0]
     staged = {"ms_per_step": round(sms, 5), "value": round(F / (sms * 1e-3) / 1e6, 3),
               "kernels_ms": {k: round(v, 5) for k, v in sk.items()},
@@ -222,6 +225,8 @@ def main():
                      "kernels_ms_summed_over_chunks": {k: round(v, 5) for k, v in pk.items()},
                      "hbm_GBs_both_kernels": round((sweep_algorithmic_bytes(*cnt) + prep_algorithmic_bytes(*cnt))
                                                    / (pms * 1e-3) / 1e9, 1)}
+    # the primary measurement: the library's default path for this configuration
+    ms_per_step, kernels_ms, stats = measure(False)
     sweep_name, sweep_ms = dominant(kernels_ms)
     sweep_name = [sweep_name]
 

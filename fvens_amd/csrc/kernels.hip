@@ -1099,8 +1099,16 @@ const char* launch_residual_wls(const DevMesh& M, const DevPhys& P, const SweepB
 		default: fn = pickFused<6>(rec, dt); break;
 	}
 	const size_t lds = std::max(static_cast<size_t>(M.fz_max_cells)*FZW, static_cast<size_t>(6*SLOTS_MAX))*sizeof(double);
-	(void)hipFuncSetAttribute(reinterpret_cast<const void*>(fn), hipFuncAttributeMaxDynamicSharedMemorySize,
-	                          static_cast<int>(lds));
+	// raise the dynamic-LDS limit once per instantiation to the largest patch the layout allows
+	// (hipFuncSetAttribute is a host-side runtime call: not on every launch)
+	static bool configured[7][2][2] = {};
+	bool& done = configured[flux < 0 || flux > 6 ? 6 : flux][rec == SR_MUSCL ? 1 : 0][dt ? 1 : 0];
+	if(!done) {
+		const size_t maxlds = std::max(static_cast<size_t>(FUSED_LDS_CELLS)*FZW, static_cast<size_t>(6*SLOTS_MAX))*sizeof(double);
+		(void)hipFuncSetAttribute(reinterpret_cast<const void*>(fn), hipFuncAttributeMaxDynamicSharedMemorySize,
+		                          static_cast<int>(maxlds));
+		done = true;
+	}
 	const int np = B.plist ? B.pcount : M.npatch;
 	if(np > 0) hipLaunchKernelGGL(fn, dim3(8*((np + 7)/8)), dim3(SLOTS_MAX), lds, s, M, P, B);
 	return kFusedNames[flux < 0 || flux > 6 ? 6 : flux];
