@@ -193,6 +193,55 @@ private:
 	const FlowFV_HIP* spatial;
 };
 
+/// SteadyForwardEulerSolver (aodesolver.hpp:113-131) with the state kept on the device
+class SteadyForwardEulerSolver_HIP
+{
+public:
+	SteadyForwardEulerSolver_HIP(const FlowFV_HIP* s, double cflinit, double tol, int maxiter)
+		: spatial(s), cfl(cflinit), tol(tol), maxiter(maxiter) { }
+	/// d_u: device state in the library's internal cell order; throws like the reference's
+	/// Tolerance_error when the tolerance is not reached (aodesolver.cpp:263-268)
+	StatusCode solve(double* d_u) {
+		hist.assign(maxiter > 0 ? maxiter : 1, 0.0);
+		check(fvhip_steady_forward_euler_device(spatial->handle(), d_u, cfl, tol, maxiter, &steps, &ratio, hist.data()));
+		hist.resize(steps);
+		if(steps == maxiter)     // the reference's test, even if the last step reached tol
+			throw std::runtime_error("Steady forward Euler did not converge to specified tolerance!");
+		return 0;
+	}
+	int steps = 0;
+	double ratio = 1.0;
+	std::vector<double> hist;     ///< energy-residual norm per step
+private:
+	const FlowFV_HIP* spatial;
+	double cfl, tol;
+	int maxiter;
+};
+
+/// SteadyBackwardEulerSolver (aodesolver.hpp:133-189) with the linear systems solved on the device
+/// (GMRES + block-Jacobi instead of PETSc's KSP; fvhip_implicit_config holds SteadySolverConfig and
+/// the -ksp_* / -matrix_free_* options)
+class SteadyBackwardEulerSolver_HIP
+{
+public:
+	SteadyBackwardEulerSolver_HIP(const FlowFV_HIP* s, const fvhip_implicit_config& c) : spatial(s), conf(c) { }
+	/// d_u: device state (internal order); throws like Tolerance_error / Numerical_error
+	/// (aodesolver.cpp:618-632) when the solve does not converge
+	StatusCode solve(double* d_u) {
+		hist.assign(conf.maxiter > 0 ? conf.maxiter : 1, 0.0);
+		check(fvhip_steady_backward_euler_device(spatial->handle(), d_u, &conf, &stats, hist.data()));
+		hist.resize(stats.steps);
+		if(!stats.converged)
+			throw std::runtime_error("Steady backward Euler did not converge to specified tolerance!");
+		return 0;
+	}
+	fvhip_solve_stats stats{};
+	std::vector<double> hist;     ///< energy-residual norm per step
+private:
+	const FlowFV_HIP* spatial;
+	fvhip_implicit_config conf;
+};
+
 /// Batched InviscidFlux::get_flux / get_jacobian on the device (anumericalflux.hpp:32-45)
 class InviscidFlux_HIP
 {

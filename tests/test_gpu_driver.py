@@ -29,8 +29,34 @@ def build_driver():
     return EXE
 
 
+def build_implicit_driver():
+    src = os.path.join(HERE, "native", "implicit_driver.cpp")
+    hdr = os.path.join(ROOT, "fvens_amd", "host", "flowfv_hip.hpp")
+    lib = os.path.join(ROOT, "fvens_amd", "libfvhip.so")
+    exe = os.path.join(HERE, "_build", "implicit_driver")
+    os.makedirs(os.path.dirname(exe), exist_ok=True)
+    if (not os.path.exists(exe) or os.path.getmtime(exe) < max(os.path.getmtime(src), os.path.getmtime(hdr),
+                                                             os.path.getmtime(lib))):
+        subprocess.run(["g++", "-std=c++17", "-O2", "-Wall", src, "-o", exe, "-L" + os.path.dirname(lib),
+                        "-lfvhip", "-Wl,-rpath," + os.path.dirname(lib)], check=True, capture_output=True)
+    return exe
+
+
 def test_driver_builds_against_wrapper():
     assert os.path.exists(build_driver())
+    assert os.path.exists(build_implicit_driver())
+
+
+@pytest.mark.gpu
+def test_implicit_driver_matfree_vs_matrix():
+    """SteadyBackwardEulerSolver_HIP (C++ wrapper) on the reference's MatFreeVsMat settings: both
+    operators converge, in the same number of pseudo-steps (testmatrixfree.cpp:65)"""
+    r = subprocess.run([build_implicit_driver(), os.path.join(HERE, "fixtures", "meshes", "2dcylinder2.msh")],
+                       capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stdout + r.stderr
+    line = [ln for ln in r.stdout.splitlines() if ln.startswith("steps ")][0]
+    a, b = [int(x) for x in line.split()[1:]]
+    assert a == b and 0 < a < 100, r.stdout
 
 
 @pytest.mark.gpu
