@@ -81,6 +81,7 @@ class ImplicitConfig:
     restart: int = 30               # -ksp_gmres_restart
     prec_sweeps: int = 1            # block-Jacobi sweeps per preconditioner application
     min_relax: float = 1.0          # nonlinear_update_scheme: >= 1 "full", else "robust_flow" factor
+    prec_single: bool = False       # preconditioner blocks stored in fp32 (operator stays fp64)
 
     def _struct(self):
         c = _ffi.FvImplicitConfig()
@@ -88,6 +89,7 @@ class ImplicitConfig:
         c.matrix_free, c.mf_eps = int(self.matrix_free), float(self.mf_eps)
         c.lin_rtol, c.lin_maxit, c.restart = float(self.lin_rtol), int(self.lin_maxit), int(self.restart)
         c.prec_sweeps, c.min_relax = int(self.prec_sweeps), float(self.min_relax)
+        c.prec_single = int(self.prec_single)
         return c
 
 

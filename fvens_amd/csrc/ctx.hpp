@@ -110,6 +110,7 @@ struct fvhip_ctx
 		double *z = nullptr, *aux = nullptr;        ///< [4*(ncell+nghost)]: operator inputs (ghost rows)
 		double *w = nullptr, *t = nullptr, *s = nullptr, *du = nullptr, *yg = nullptr;   ///< [4*ncell]
 		double *jd = nullptr, *jlo = nullptr, *jup = nullptr, *dinv = nullptr;            ///< 4x4 blocks
+		float *slo = nullptr, *sup = nullptr, *sdinv = nullptr;   ///< fp32 copies for the preconditioner
 		double *part = nullptr, *red = nullptr, *coef = nullptr, *pm = nullptr;           ///< reductions
 		double *h_red = nullptr, *h_coef = nullptr;                                      ///< pinned host
 	} iw;
@@ -465,6 +466,16 @@ struct fvhip_ctx
 			iw.part = dalloc(kry_scratch(m + 2), o);
 			iw.m = m;
 		}
+	}
+
+	/// fp32 copies of the preconditioner blocks (fvhip_implicit_config::prec_single)
+	void ensureSinglePrecond() {
+		if(iw.sdinv) return;
+		const size_t N = static_cast<size_t>(L.ncell);
+		const size_t Fi = static_cast<size_t>(std::max(L.ninface, 1));
+		iw.sdinv = reinterpret_cast<float*>(dalloc(8*N, owned));
+		iw.slo = reinterpret_cast<float*>(dalloc(8*Fi, owned));
+		iw.sup = reinterpret_cast<float*>(dalloc(8*Fi, owned));
 	}
 
 	/// MatrixFreeSpatialJacobian::apply on device vectors (internal order), single domain (the

@@ -6,8 +6,9 @@
  * The reference hands each linear system to PETSc (KSPSolve, aodesolver.cpp:483; GMRES with a
  * block-Jacobi/ILU or SOR preconditioner from the .solverc files). Here it is solved on the device
  * by restarted GMRES: right-preconditioned (the residual it monitors is the true one), classical
- * Gram-Schmidt with one re-orthogonalisation (two fused multi-dot reductions, i.e. two small host
- * round trips, per Arnoldi step instead of j+1 with modified Gram-Schmidt), preconditioned by
+ * Gram-Schmidt with selective (DGKS) re-orthogonalisation (one fused multi-dot reduction, i.e. one
+ * small host round trip, per Arnoldi step in the common case, a second only when the projection
+ * cancelled more than half of |w|^2; modified Gram-Schmidt would take j+1), preconditioned by
  * block-Jacobi sweeps on the assembled first-order Jacobian. PETSc's ILU/SOR are sequential
  * recurrences; a block-Jacobi sweep is one launch over all cells, and several sweeps approach the
  * block Gauss-Seidel effect. The matrix-free operator (alinalg.cpp:142-233) uses the assembled
@@ -92,6 +93,7 @@ struct LinOp
 {
 	System& S;
 	bool matfree = false;
+	bool single = false;                      ///< preconditioner blocks in fp32 (iw.sdinv/slo/sup)
 	int sweeps = 1;
 	std::vector<const double*> D, Lo, Up;     ///< per handle: diagonal / lower / upper blocks
 
@@ -106,15 +108,26 @@ struct LinOp
 		if(matfree) matfreeApply(S, x, y);
 		else blocks(x, y);
 	}
-	/// z = M^-1 v: `sweeps` block-Jacobi sweeps on A z = v from z = 0 (z has ghost rows)
+	/// z = M^-1 v: `sweeps` block-Jacobi sweeps on A z = v from z = 0 (z has ghost rows). The iterates
+	/// alternate between z and aux (both with ghost rows) so that the last one lands in z.
 	void precondition(const ArrayOf& v, const ArrayOf& z) {
+		const ArrayOf aux = [&](size_t i) { return S.hs[i]->iw.aux; };
+		auto buf = [&](int k) -> const ArrayOf& { return ((sweeps - 1 - k) % 2 == 0) ? z : aux; };
 		S.each([&](size_t i, fvhip_ctx* h) {
-			h->timed("k_bjac_apply", [&]{ launch_bjac_apply(h->L.ncell, h->iw.dinv, v(i), z(i), h->stream); });
+			h->timed("k_bjac_apply", [&]{
+				if(single) launch_bjac_apply(h->L.ncell, h->iw.sdinv, v(i), buf(0)(i), h->stream);
+				else launch_bjac_apply(h->L.ncell, h->iw.dinv, v(i), buf(0)(i), h->stream);
+			});
 		});
-		for(int s = 1; s < sweeps; s++) {
-			blocks(z, [&](size_t i) { return S.hs[i]->iw.t; });
+		for(int k = 1; k < sweeps; k++) {
+			const ArrayOf& zin = buf(k-1);
+			const ArrayOf& zout = buf(k);
+			S.exchange(zin, 4);
 			S.each([&](size_t i, fvhip_ctx* h) {
-				h->timed("k_bjac_correct", [&]{ launch_bjac_correct(h->L.ncell, h->iw.dinv, v(i), h->iw.t, z(i), h->stream); });
+				h->timed("k_bjac_sweep", [&]{
+					if(single) launch_bjac_sweep(h->J, h->iw.sdinv, h->iw.slo, h->iw.sup, v(i), zin(i), zout(i), h->stream);
+					else launch_bjac_sweep(h->J, h->iw.dinv, Lo[i], Up[i], v(i), zin(i), zout(i), h->stream);
+				});
 			});
 		}
 	}
@@ -122,6 +135,17 @@ struct LinOp
 	void setup() {
 		S.each([&](size_t i, fvhip_ctx* h) {
 			h->timed("k_bjac_invert", [&]{ launch_bjac_invert(h->L.ncell, D[i], h->iw.dinv, h->stream); });
+			if(single) {
+				h->ensureSinglePrecond();
+				const long long nf = 16LL*std::max(h->L.ninface, 0);
+				h->timed("k_to_single", [&]{
+					launch_to_single(16LL*h->L.ncell, h->iw.dinv, h->iw.sdinv, h->stream);
+					if(sweeps > 1) {
+						launch_to_single(nf, Lo[i], h->iw.slo, h->stream);
+						launch_to_single(nf, Up[i], h->iw.sup, h->stream);
+					}
+				});
+			}
 		});
 	}
 };
@@ -171,21 +195,28 @@ static GmresOut gmres(System& S, LinOp& A, const ArrayOf& b, const ArrayOf& x, d
 		while(j < m && out.iters < maxit) {
 			A.precondition([&](size_t i) { return V(i,j); }, z);
 			A.apply(z, w);
-			// classical Gram-Schmidt twice; the second pass also returns |w|^2 before its update
+			// classical Gram-Schmidt with selective (DGKS) reorthogonalisation: every multi-dot pass
+			// also returns |w|^2, so |w - V h|^2 follows by Pythagoras; a second pass runs only when
+			// the projection removed more than half of |w|^2 (loss of orthogonality possible)
 			S.each([&](size_t i, fvhip_ctx* h) {
-				launch_mdot(n4(i), j+1, V(i,0), n4(i), w(i), false, h->iw.part, h->iw.red, h->stream);
-			});
-			const std::vector<double> h1 = S.allsum(j+1, true);
-			S.each([&](size_t i, fvhip_ctx* h) {
-				launch_maxpy(n4(i), j+1, V(i,0), n4(i), h->iw.red, w(i), h->stream);
 				launch_mdot(n4(i), j+1, V(i,0), n4(i), w(i), true, h->iw.part, h->iw.red, h->stream);
 			});
-			const std::vector<double> h2 = S.allsum(j+2, true);
+			const std::vector<double> h1 = S.allsum(j+2, true);
 			S.each([&](size_t i, fvhip_ctx* h) { launch_maxpy(n4(i), j+1, V(i,0), n4(i), h->iw.red, w(i), h->stream); });
 			double corr = 0.0;
-			for(int k = 0; k <= j; k++) { Hij(k,j) = h1[k] + h2[k]; corr += h2[k]*h2[k]; }
-			double hn2 = h2[j+1] - corr;
-			if(!(hn2 > 1e-4*h2[j+1])) { const double t = norm(w); hn2 = t*t; }   // cancellation: measure
+			for(int k = 0; k <= j; k++) { Hij(k,j) = h1[k]; corr += h1[k]*h1[k]; }
+			double hn2 = h1[j+1] - corr;
+			if(!(hn2 > 0.5*h1[j+1])) {
+				S.each([&](size_t i, fvhip_ctx* h) {
+					launch_mdot(n4(i), j+1, V(i,0), n4(i), w(i), true, h->iw.part, h->iw.red, h->stream);
+				});
+				const std::vector<double> h2 = S.allsum(j+2, true);
+				S.each([&](size_t i, fvhip_ctx* h) { launch_maxpy(n4(i), j+1, V(i,0), n4(i), h->iw.red, w(i), h->stream); });
+				corr = 0.0;
+				for(int k = 0; k <= j; k++) { Hij(k,j) += h2[k]; corr += h2[k]*h2[k]; }
+				hn2 = h2[j+1] - corr;
+				if(!(hn2 > 1e-4*h2[j+1])) { const double t = norm(w); hn2 = t*t; }   // cancellation: measure
+			}
 			const double hn = std::sqrt(hn2);
 			Hij(j+1,j) = hn;
 			if(hn > 0.0) S.each([&](size_t i, fvhip_ctx* h) { launch_axpby(n4(i), 1.0/hn, w(i), 0.0, V(i,j+1), h->stream); });
@@ -256,6 +287,7 @@ static void backwardEuler(System& S, const std::vector<double*>& us, const fvhip
 	LinOp A{S};
 	A.matfree = c.matrix_free != 0;
 	A.sweeps = c.prec_sweeps;
+	A.single = c.prec_single != 0;
 	for(fvhip_ctx* h : S.hs) { A.D.push_back(h->iw.jd); A.Lo.push_back(h->iw.jlo); A.Up.push_back(h->iw.jup); }
 	std::vector<const double*> cu(us.begin(), us.end());
 	std::vector<double*> rs, dts;

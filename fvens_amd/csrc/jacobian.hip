@@ -163,6 +163,28 @@ void k_pseudo_time(int ncell, const double* __restrict__ area, double cfl, doubl
 // -------------------------------------------------------------------------------------------------
 // y = A x with the face-based blocks; per cell: diag first, then faces in ascending reference order
 // -------------------------------------------------------------------------------------------------
+/// s[i] = sum_k B[i][k] x[k] for a row-major 4x4 block, rows read as double4 (k ascending)
+__device__ __forceinline__ void blk_row_dots(const double* __restrict__ B, const double4 x, double (&s)[4])
+{
+	const double4* b4 = reinterpret_cast<const double4*>(B);
+#pragma unroll
+	for(int i = 0; i < 4; i++) {
+		const double4 r = b4[i];
+		s[i] = r.x*x.x + r.y*x.y + r.z*x.z + r.w*x.w;
+	}
+}
+/// the same for an fp32 block (entries widened to fp64, fp64 arithmetic)
+__device__ __forceinline__ void blk_row_dots(const float* __restrict__ B, const double4 x, double (&s)[4])
+{
+	const float4* b4 = reinterpret_cast<const float4*>(B);
+#pragma unroll
+	for(int i = 0; i < 4; i++) {
+		const float4 r = b4[i];
+		s[i] = static_cast<double>(r.x)*x.x + static_cast<double>(r.y)*x.y + static_cast<double>(r.z)*x.z
+		     + static_cast<double>(r.w)*x.w;
+	}
+}
+
 __global__ __launch_bounds__(256)
 void k_block_apply(JacMesh J, const double* __restrict__ diag, const double* __restrict__ lower,
                    const double* __restrict__ upper, const double* __restrict__ x, double* __restrict__ y)
@@ -171,16 +193,7 @@ void k_block_apply(JacMesh J, const double* __restrict__ diag, const double* __r
 	if(c >= J.ncell) return;
 	const double4* x4 = reinterpret_cast<const double4*>(x);
 	double acc[4];
-	{
-		const double4 xc = x4[c];
-		const double xv[4] = {xc.x, xc.y, xc.z, xc.w};
-		const double* D = diag + 16*static_cast<size_t>(c);
-		for(int i = 0; i < 4; i++) {
-			double s = D[i*4]*xv[0];
-			for(int k = 1; k < 4; k++) s += D[i*4+k]*xv[k];
-			acc[i] = s;
-		}
-	}
+	blk_row_dots(diag + 16*static_cast<size_t>(c), x4[c], acc);
 	const int4 fc = J.cell_rfaces[c];
 	const int4 nb = J.cell_nbr_fo[c];
 	const int codes[4] = {fc.x, fc.y, fc.z, fc.w};
@@ -192,15 +205,47 @@ void k_block_apply(JacMesh J, const double* __restrict__ diag, const double* __r
 		const int f = code >> 1;
 		if(f < J.nbface) continue;
 		const double* B = ((code & 1) ? lower : upper) + 16*static_cast<size_t>(f - J.nbface);
-		const double4 xo = x4[nbrs[j]];
-		const double xv[4] = {xo.x, xo.y, xo.z, xo.w};
-		for(int i = 0; i < 4; i++) {
-			double s = B[i*4]*xv[0];
-			for(int k = 1; k < 4; k++) s += B[i*4+k]*xv[k];
-			acc[i] += s;
-		}
+		double s[4];
+		blk_row_dots(B, x4[nbrs[j]], s);
+#pragma unroll
+		for(int i = 0; i < 4; i++) acc[i] += s[i];
 	}
 	reinterpret_cast<double4*>(y)[c] = make_double4(acc[0], acc[1], acc[2], acc[3]);
+}
+
+/// One block-Jacobi sweep fused into one pass: zout = D^-1 (v - sum_faces B zin[nbr]), the
+/// off-diagonal half of k_block_apply followed by the diagonal solve (zin needs its ghost rows).
+/// Same iterate as zin + D^-1 (v - A zin) up to rounding, without reading D or writing A zin.
+template <typename T>
+__global__ __launch_bounds__(256)
+void k_bjac_sweep(JacMesh J, const T* __restrict__ dinv, const T* __restrict__ lower,
+                  const T* __restrict__ upper, const double* __restrict__ v, const double* __restrict__ zin,
+                  double* __restrict__ zout)
+{
+	const int c = blockIdx.x*blockDim.x + threadIdx.x;
+	if(c >= J.ncell) return;
+	const double4* z4 = reinterpret_cast<const double4*>(zin);
+	const double4 vc = reinterpret_cast<const double4*>(v)[c];
+	double acc[4] = {vc.x, vc.y, vc.z, vc.w};
+	const int4 fc = J.cell_rfaces[c];
+	const int4 nb = J.cell_nbr_fo[c];
+	const int codes[4] = {fc.x, fc.y, fc.z, fc.w};
+	const int nbrs[4] = {nb.x, nb.y, nb.z, nb.w};
+#pragma unroll
+	for(int j = 0; j < 4; j++) {
+		const int code = codes[j];
+		if(code < 0) continue;
+		const int f = code >> 1;
+		if(f < J.nbface) continue;
+		const T* B = ((code & 1) ? lower : upper) + 16*static_cast<size_t>(f - J.nbface);
+		double s[4];
+		blk_row_dots(B, z4[nbrs[j]], s);
+#pragma unroll
+		for(int i = 0; i < 4; i++) acc[i] -= s[i];
+	}
+	double o[4];
+	blk_row_dots(dinv + 16*static_cast<size_t>(c), make_double4(acc[0], acc[1], acc[2], acc[3]), o);
+	reinterpret_cast<double4*>(zout)[c] = make_double4(o[0], o[1], o[2], o[3]);
 }
 
 // -------------------------------------------------------------------------------------------------
@@ -337,6 +382,17 @@ void launch_block_apply(const JacMesh& J, const double* diag, const double* lowe
                         const double* x, double* y, hipStream_t s)
 {
 	hipLaunchKernelGGL(k_block_apply, dim3(nblk(J.ncell,256)), dim3(256), 0, s, J, diag, lower, upper, x, y);
+}
+
+void launch_bjac_sweep(const JacMesh& J, const double* dinv, const double* lower, const double* upper,
+                       const double* v, const double* zin, double* zout, hipStream_t s)
+{
+	hipLaunchKernelGGL(k_bjac_sweep<double>, dim3(nblk(J.ncell,256)), dim3(256), 0, s, J, dinv, lower, upper, v, zin, zout);
+}
+void launch_bjac_sweep(const JacMesh& J, const float* dinv, const float* lower, const float* upper,
+                       const double* v, const double* zin, double* zout, hipStream_t s)
+{
+	hipLaunchKernelGGL(k_bjac_sweep<float>, dim3(nblk(J.ncell,256)), dim3(256), 0, s, J, dinv, lower, upper, v, zin, zout);
 }
 
 void launch_mf_norm(long long n, const double* x, double eps, double* part, double* pm, hipStream_t s)

@@ -34,6 +34,12 @@ void launch_jac_diag(const JacMesh& J, const double* bblk, const double* lower, 
 void launch_pseudo_time(int ncell, const double* area, double cfl, double* dtm, double* diag, hipStream_t s);
 void launch_block_apply(const JacMesh& J, const double* diag, const double* lower, const double* upper,
                         const double* x, double* y, hipStream_t s);
+/// zout = D^-1 (v - (A - D) zin): one block-Jacobi sweep (dinv: inverted diagonal blocks)
+void launch_bjac_sweep(const JacMesh& J, const double* dinv, const double* lower, const double* upper,
+                       const double* v, const double* zin, double* zout, hipStream_t s);
+/// the same with fp32 blocks (fp64 vectors and arithmetic)
+void launch_bjac_sweep(const JacMesh& J, const float* dinv, const float* lower, const float* upper,
+                       const double* v, const double* zin, double* zout, hipStream_t s);
 /// pm[0] = |x|, pm[1] = eps/|x|; part: mf_partials() doubles of scratch
 void launch_mf_norm(long long n, const double* x, double eps, double* part, double* pm, hipStream_t s);
 void launch_mf_perturb(long long n, const double* u, const double* x, const double* pm, double* aux, hipStream_t s);

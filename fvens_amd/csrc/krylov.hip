@@ -92,14 +92,37 @@ void k_bjac_invert(int n, const double* __restrict__ diag, double* __restrict__ 
 	for(int i = 0; i < 4; i++) o[i] = make_double4(b[i][0], b[i][1], b[i][2], b[i][3]);
 }
 
+/// y = B x for a row-major fp32 4x4 block, entries widened to fp64
+__device__ __forceinline__ void blk_mv(const float* __restrict__ B, const double4 x, double* y)
+{
+	const float4* b4 = reinterpret_cast<const float4*>(B);
+	#pragma unroll
+	for(int i = 0; i < 4; i++) {
+		const float4 r = b4[i];
+		y[i] = static_cast<double>(r.x)*x.x + static_cast<double>(r.y)*x.y + static_cast<double>(r.z)*x.z
+		     + static_cast<double>(r.w)*x.w;
+	}
+}
+
+template <typename T>
 __global__ __launch_bounds__(256)
-void k_bjac_apply(int n, const double* __restrict__ dinv, const double* __restrict__ x, double* __restrict__ y)
+void k_bjac_apply(int n, const T* __restrict__ dinv, const double* __restrict__ x, double* __restrict__ y)
 {
 	const int c = blockIdx.x*blockDim.x + threadIdx.x;
 	if(c >= n) return;
 	double o[4];
 	blk_mv(dinv + 16*static_cast<size_t>(c), reinterpret_cast<const double4*>(x)[c], o);
 	reinterpret_cast<double4*>(y)[c] = make_double4(o[0], o[1], o[2], o[3]);
+}
+
+__global__ __launch_bounds__(256)
+void k_to_single(long long n, const double* __restrict__ a, float* __restrict__ b)
+{
+	const long long i = blockIdx.x*256LL + threadIdx.x;
+	if(i >= n/4) return;
+	const double4 v = reinterpret_cast<const double4*>(a)[i];
+	reinterpret_cast<float4*>(b)[i] = make_float4(static_cast<float>(v.x), static_cast<float>(v.y),
+	                                              static_cast<float>(v.z), static_cast<float>(v.w));
 }
 
 __global__ __launch_bounds__(256)
@@ -216,7 +239,11 @@ void k_relaxed_update(int n, gd::Gas G, double minfactor, const double* __restri
 void launch_bjac_invert(int n, const double* diag, double* dinv, hipStream_t s)
 { if(n > 0) k_bjac_invert<<<nblk(n,256), 256, 0, s>>>(n, diag, dinv); }
 void launch_bjac_apply(int n, const double* dinv, const double* x, double* y, hipStream_t s)
-{ if(n > 0) k_bjac_apply<<<nblk(n,256), 256, 0, s>>>(n, dinv, x, y); }
+{ if(n > 0) k_bjac_apply<double><<<nblk(n,256), 256, 0, s>>>(n, dinv, x, y); }
+void launch_bjac_apply(int n, const float* dinv, const double* x, double* y, hipStream_t s)
+{ if(n > 0) k_bjac_apply<float><<<nblk(n,256), 256, 0, s>>>(n, dinv, x, y); }
+void launch_to_single(long long n, const double* a, float* b, hipStream_t s)
+{ if(n > 0) k_to_single<<<nblk(n/4,256), 256, 0, s>>>(n, a, b); }
 void launch_bjac_correct(int n, const double* dinv, const double* b, const double* y, double* z, hipStream_t s)
 { if(n > 0) k_bjac_correct<<<nblk(n,256), 256, 0, s>>>(n, dinv, b, y, z); }
 

@@ -46,6 +46,9 @@ FVHIP_HD double relaxation_factor(const gd::Gas& G, double minfactor, const doub
 void launch_bjac_invert(int ncell, const double* diag, double* dinv, hipStream_t s);
 /// y[c] = dinv[c] x[c]
 void launch_bjac_apply(int ncell, const double* dinv, const double* x, double* y, hipStream_t s);
+void launch_bjac_apply(int ncell, const float* dinv, const double* x, double* y, hipStream_t s);
+/// b = fp32(a), n a multiple of 4
+void launch_to_single(long long n, const double* a, float* b, hipStream_t s);
 /// z[c] += dinv[c] (b[c] - y[c]): one block-Jacobi sweep on A z = b, given y = A z
 void launch_bjac_correct(int ncell, const double* dinv, const double* b, const double* y, double* z, hipStream_t s);
 

@@ -204,6 +204,9 @@ typedef struct fvhip_implicit_config {
 	int prec_sweeps;          /* block-Jacobi sweeps per preconditioner application (1: point-block Jacobi) */
 	double min_relax;         /* nonlinear_update_scheme: >= 1 "full"; else "robust_flow" with
 	                             min_nonlinear_relaxation_factor = min_relax (nonlinearrelaxation.cpp) */
+	int prec_single;          /* 1: the preconditioner's blocks (inverted diagonal, lower, upper) are kept in
+	                             fp32 (sweeps read half the bytes; vectors and arithmetic stay fp64). The
+	                             operator itself is unchanged, so the solution tolerance is too. */
 } fvhip_implicit_config;
 
 typedef struct fvhip_solve_stats {

@@ -9,7 +9,8 @@ Bars:
   * GMRES on the assembled blocks: |b - A x| <= 1e-11 |b| (checked in numpy), x equal to the direct
     solution to 1e-8 of max|x|; block-Jacobi sweeps cut the iteration count;
   * one implicit step with a tight linear solve: the update u1 - u0 equal to the host restatement's
-    to 1e-8 of its size per variable, the residual norm to 1e-12;
+    to 1e-8 of its size per variable, the residual norm to 1e-12 (also with the preconditioner's
+    blocks in fp32: the operator is unchanged, so is the solution);
   * Flow_Euler_Cylinder_HLLC_MatFreeVsMat (tests/solvers/testmatrixfree.cpp:65 with matfree.ctrl /
     matfree.solverc): matrix-free and assembled solves both converge, in the same number of steps;
   * a 3-rank partition (in-process group) takes the same implicit steps as one GPU: same linear
@@ -97,8 +98,8 @@ def test_gmres_blocks_matches_direct_solve():
     dev.close()
 
 
-@pytest.mark.parametrize("min_relax", [1.0, 0.2])
-def test_one_backward_euler_step_matches_host(min_relax):
+@pytest.mark.parametrize("min_relax,single", [(1.0, False), (0.2, False), (1.0, True)])
+def test_one_backward_euler_step_matches_host(min_relax, single):
     m, om = get_mesh("naca_small")
     p = cases.physics("naca")
     n = cases.numerics("ROE", "LEASTSQUARES", "VANALBADA")
@@ -112,7 +113,7 @@ def test_one_backward_euler_step_matches_host(min_relax):
     perm = dev.permutation()
     dU = to_device(u0, perm)
     cfg = fa.ImplicitConfig(cflinit=cfl, cflfin=cfl, tol=0.0, maxiter=1, lin_rtol=1e-13, lin_maxit=3000, restart=60,
-                            prec_sweeps=2, min_relax=min_relax)
+                            prec_sweeps=2, min_relax=min_relax, prec_single=single)
     st, hist = dev.steady_backward_euler_device(dU.data_ptr(), cfg)
     assert st["steps"] == 1 and st["cfl"] == cfl
     u = np.empty_like(u0)

@@ -1,0 +1,101 @@
+#!/usr/bin/env python3
+"""Secondary benchmark: device implicit pseudo-time steps (SteadyBackwardEulerSolver::solve,
+aodesolver.cpp:363-638) on the bench mesh — residual + analytic first-order Jacobian + GMRES with
+block-Jacobi sweeps + relaxed update per step, matrix-free and assembled operator.
+
+Starts as the reference's transonic-implicit.ctrl does (freestream, first-order initialisation
+solve), then times K second-order steps (tolerance 0 so every step runs) after W warm-up steps;
+prints one JSON line per operator kind with ms/step, linear iterations per step and ms per linear
+iteration. Not the headline metric (bench.py is); one GPU.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, "tests"))
+
+
+CASES = {   # physics, flux, gradients, reconstruction
+    "naca": ("naca", "ROE", "LEASTSQUARES", "VANALBADA"),
+    "naca-venkat": ("naca", "ROE", "LEASTSQUARES", "VENKATAKRISHNAN"),
+    "plate": ("plate", "HLLC", "LEASTSQUARES", "NONE"),
+}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--case", default="naca", choices=sorted(CASES),
+                    help="naca: bench.py's C4 workload; naca-venkat: BASELINE config 3 numerics on it; "
+                         "plate: config 2, laminar flat plate, ~1M quads")
+    ap.add_argument("--scale", type=int, default=1, help="divide the mesh dimensions by this")
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--init-steps", type=int, default=10, help="first-order initialisation steps")
+    ap.add_argument("--cfl", type=float, default=25.0)
+    ap.add_argument("--restart", type=int, default=30)
+    ap.add_argument("--lin-maxit", type=int, default=30)
+    ap.add_argument("--sweeps", type=int, default=4)
+    ap.add_argument("--prec-single", action="store_true", help="preconditioner blocks in fp32")
+    args = ap.parse_args()
+
+    import torch
+    torch.cuda.set_device(0)
+    import fvens_amd as fa
+    import cases
+    from bench import c4_mesh
+
+    kind, flux, grad, rec = CASES[args.case]
+    if kind == "plate":
+        nx = ny = 1024 // args.scale
+        mesh, dims = fa.UMesh.flat_plate(nx, ny), dict(nx=nx, ny=ny)
+    else:
+        mesh, dims = c4_mesh(fa, args.scale)
+    p = cases.physics(kind)
+    n = cases.numerics(flux, grad, rec)
+    n1 = cases.numerics(flux, grad, rec, order2=False)
+    sp1 = fa.FlowFV(mesh, p, n1, device=0)
+    sp = fa.FlowFV(mesh, p, n, device=0)
+    perm = sp.permutation()
+    assert np.array_equal(perm, sp1.permutation())
+    u0 = np.tile(cases.freestream(p), (mesh.nelem, 1))[perm]
+    # the reference's start-up (transonic-implicit.ctrl): a first-order initialisation solve, then the
+    # second-order main solve. Its CFL ramps (25/50 -> 500) blow up on this O-grid's 1e-5 wall cells
+    # during the start-up transient (measured), so the CFL is held fixed
+    dinit = torch.tensor(u0, dtype=torch.float64, device="cuda")
+    ini = fa.ImplicitConfig(cflinit=args.cfl, cflfin=args.cfl, tol=0.0, maxiter=args.init_steps,
+                            lin_rtol=1e-2, lin_maxit=args.lin_maxit, restart=args.restart, prec_sweeps=args.sweeps)
+    st0, _ = sp1.steady_backward_euler_device(dinit.data_ptr(), ini)
+    torch.cuda.synchronize()
+    for mf in (False, True):
+        du = dinit.clone()
+        cfg = fa.ImplicitConfig(cflinit=args.cfl, cflfin=args.cfl, tol=0.0, maxiter=args.warmup, matrix_free=mf,
+                                lin_rtol=1e-2, lin_maxit=args.lin_maxit, restart=args.restart,
+                                prec_sweeps=args.sweeps, prec_single=args.prec_single)
+        sp.steady_backward_euler_device(du.data_ptr(), cfg)      # warm-up: allocations, clocks
+        torch.cuda.synchronize()
+        du = dinit.clone()
+        cfg.maxiter = args.steps
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        st, hist = sp.steady_backward_euler_device(du.data_ptr(), cfg)
+        torch.cuda.synchronize()
+        dt = time.perf_counter() - t0
+        k = max(st["steps"], 1)
+        out = {"metric": "implicit_step_time", "case": args.case, "operator": "matrix-free" if mf else "assembled",
+               "ms_per_step": round(dt / k * 1e3, 3), "steps": st["steps"],
+               "lin_iters_per_step": round(st["lin_iters"] / k, 2),
+               "ms_per_lin_iter": round(dt * 1e3 / max(st["lin_iters"], 1), 4),
+               "resratio": st["resratio"], "cells": mesh.nelem, "faces": mesh.naface, "dims": dims,
+               "restart": args.restart, "prec_sweeps": args.sweeps, "prec_single": args.prec_single, "cfl": args.cfl,
+               "init": {"steps": st0["steps"], "resratio": st0["resratio"]}}
+        print(json.dumps(out), flush=True)
+
+
+if __name__ == "__main__":
+    main()
