@@ -249,6 +249,16 @@ class FlowFV:
         check(_ffi.lib().fvhip_get_gradients(self._h, dptr(u), dptr(g)))
         return g
 
+    def surface_data_device(self, d_u, marker):
+        """FlowFV_base::computeSurfaceData (flow_spatial.cpp:130-310) for the device state d_u
+        (internal order): ((CL, CDp, CDsf), per-face (x, y, Cp, Cf) of this handle's faces of `marker`)"""
+        funcs = np.zeros(3)
+        faces = np.zeros((max(self.mesh.nbface, 1), 4))
+        nf = np.zeros(1, np.int32)
+        check(_ffi.lib().fvhip_surface_data_device(self._h, ctypes.c_void_p(d_u), int(marker), dptr(funcs),
+                                                   dptr(faces), iptr(nf)))
+        return tuple(float(x) for x in funcs), faces[:int(nf[0])]
+
     def assemble_jacobian(self, u, diag=None, lower=None, upper=None):
         """Spatial::assemble_jacobian (aspatial.cpp:242-340): blocks are ADDED into diag [nelem][4][4],
         lower/upper [ninface][4][4] (A[R][L] += lower, A[L][R] += upper); zeros if not given."""

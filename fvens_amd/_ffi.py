@@ -74,6 +74,8 @@ _SIGS = {
     "fvhip_compute_residual_device": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
                                                      ctypes.c_int, ctypes.c_void_p, ctypes.c_int]),
     "fvhip_get_gradients": (ctypes.c_int, [ctypes.c_void_p, c_dbl_p, c_dbl_p]),
+    "fvhip_surface_data_device": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, c_dbl_p, c_dbl_p,
+                                                 c_int_p]),
     "fvhip_assemble_jacobian": (ctypes.c_int, [ctypes.c_void_p, c_dbl_p, c_dbl_p, c_dbl_p, c_dbl_p]),
     "fvhip_assemble_jacobian_device": (ctypes.c_int, [ctypes.c_void_p] + [ctypes.c_void_p] * 4),
     "fvhip_add_pseudo_time_term_device": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_double, ctypes.c_void_p,

@@ -15,6 +15,7 @@
 #include "partition.hpp"
 #include "halo.hpp"
 #include "ode.hpp"
+#include "surface.hpp"
 #include <rccl/rccl.h>
 #include <hip/hip_runtime.h>
 #include <cstring>
@@ -466,6 +467,32 @@ struct fvhip_ctx
 			iw.part = dalloc(kry_scratch(m + 2), o);
 			iw.m = m;
 		}
+	}
+
+	/// the boundary faces of one marker for the surface functionals, uploaded on first use
+	struct SurfCache { SurfaceFaces S{}; double *faceout = nullptr, *contrib = nullptr, *sums = nullptr; };
+	std::map<int, SurfCache> surf;
+	SurfCache& surfaceFaces(int marker) {
+		auto it = surf.find(marker);
+		if(it != surf.end()) return it->second;
+		std::vector<int> Lc;
+		std::vector<double> geo;
+		for(int f = 0; f < L.nbface; f++) {
+			if(L.bf_tag[f] != marker) continue;
+			Lc.push_back(L.bf_L[f]);
+			const double g5[5] = {L.bf_n[2*f], L.bf_n[2*f+1], L.bf_len[f], L.bf_gr[2*f], L.bf_gr[2*f+1]};
+			geo.insert(geo.end(), g5, g5 + 5);
+		}
+		SurfCache c;
+		c.S.n = static_cast<int>(Lc.size());
+		if(c.S.n > 0) {
+			c.S.L = upload(Lc, owned);
+			c.S.geo = upload(geo, owned);
+			c.faceout = dalloc(4*Lc.size(), owned);
+			c.contrib = dalloc(4*Lc.size(), owned);
+		}
+		c.sums = dalloc(4, owned);
+		return surf.emplace(marker, c).first->second;
 	}
 
 	/// fp32 copies of the preconditioner blocks (fvhip_implicit_config::prec_single)

@@ -5,6 +5,8 @@
  */
 #include "ctx.hpp"
 
+#include <cmath>
+
 namespace fvhip_detail {
 
 fvhip_ctx::GroupExchange groupExchange(const fvhip_group_s* g)
@@ -306,6 +308,39 @@ int fvhip_get_gradients(fvhip_handle h, const double* u, double* grads)
 		HC(hipMemcpyAsync(st.data(), h->d_grad, 8*N*sizeof(double), hipMemcpyDeviceToHost, h->stream));
 		HC(hipStreamSynchronize(h->stream));
 		fromInternal(h, st.data(), grads, 8);
+	});
+}
+
+int fvhip_surface_data_device(fvhip_handle h, const double* d_u, int marker, double* funcs, double* faces,
+                              int* nfaces)
+{
+	return guard([&] {
+		if(!funcs) throw std::invalid_argument("funcs must not be NULL");
+		HC(hipSetDevice(h->device));
+		fvhip_ctx::SurfCache& c = h->surfaceFaces(marker);
+		double* u = const_cast<double*>(d_u);
+		h->exchange_rccl(u, 4);   // ghost rows for the border cells' gradients (partitioned handles)
+		// getGradients (flow_spatial.cpp:95-112): ghost states, then the scheme on conserved variables
+		exact::launch_prep(h->M, h->P, u, h->d_up, h->d_ubc, h->d_ug, false, h->stream);
+		switch(h->cfg.gradientscheme) {
+			case FVHIP_GRAD_LEASTSQUARES: exact::launch_grad_wls(h->M, u, h->d_ubc, h->d_grad, h->stream); break;
+			case FVHIP_GRAD_GREENGAUSS: exact::launch_grad_gg(h->M, u, h->d_ubc, h->d_grad, h->stream); break;
+			default: exact::launch_fill(h->d_grad, 0.0, 8LL*h->L.ncell, h->stream);
+		}
+		// flowDirectionVector(aoa) with zero side-slip and getFreestreamPressure, on the host as there
+		const double aoa = h->cfg.aoa;
+		const double wx = std::cos(aoa)*std::cos(0.0), wy = std::sin(aoa)*std::cos(0.0);      // mathutils.hpp:67-75
+		const double pinf = 1.0/(h->cfg.gamma*h->cfg.Minf*h->cfg.Minf);                          // aphysics_defs.hpp:465-467
+		launch_surface(c.S, u, h->d_grad, h->P.gas, pinf, wx, wy, c.faceout, c.contrib, c.sums, h->stream);
+		HC(hipGetLastError());
+		if(h->comm) NC(ncclAllReduce(c.sums, c.sums, 4, ncclDouble, ncclSum, h->comm, h->stream));   // :297-299
+		double s[4];
+		HC(hipMemcpyAsync(s, c.sums, sizeof s, hipMemcpyDeviceToHost, h->stream));
+		if(faces && c.S.n > 0)
+			HC(hipMemcpyAsync(faces, c.faceout, 4*static_cast<size_t>(c.S.n)*sizeof(double), hipMemcpyDeviceToHost, h->stream));
+		HC(hipStreamSynchronize(h->stream));
+		funcs[0] = s[0]/s[3]; funcs[1] = s[1]/s[3]; funcs[2] = s[2]/s[3];                          // :302
+		if(nfaces) *nfaces = c.S.n;
 	});
 }
 

@@ -220,6 +220,7 @@ Layout buildLayout(const MeshTopo& T, const fvhip_flow_config& cfg, bool renumbe
 
 	// --- boundary faces ---
 	Lo.bf_L.resize(nb); Lo.bf_bc.resize(nb); Lo.bf_n.resize(2*static_cast<size_t>(nb)); Lo.bf_rcbp.resize(2*static_cast<size_t>(nb));
+	Lo.bf_tag.resize(nb); Lo.bf_gr.resize(2*static_cast<size_t>(nb));
 	for(int f = 0; f < nb; f++) {
 		Lo.bf_L[f] = Lo.iperm[Lref(f)];
 		const int tag = T.btag[f];
@@ -229,6 +230,8 @@ Layout buildLayout(const MeshTopo& T, const fvhip_flow_config& cfg, bool renumbe
 		Lo.bf_bc[f] = bi;
 		Lo.bf_n[2*f] = T.facemetric[3*static_cast<size_t>(f)]; Lo.bf_n[2*f+1] = T.facemetric[3*static_cast<size_t>(f)+1];
 		Lo.bf_rcbp[2*f] = T.rcbp[2*f]; Lo.bf_rcbp[2*f+1] = T.rcbp[2*f+1];
+		Lo.bf_tag[f] = tag;
+		Lo.bf_gr[2*f] = T.gr[2*static_cast<size_t>(f)]; Lo.bf_gr[2*f+1] = T.gr[2*static_cast<size_t>(f)+1];
 	}
 	// --- interior faces (reference order) ---
 	Lo.if_L.resize(F-nb); Lo.if_R.resize(F-nb); Lo.if_slot.assign(F-nb, -1);

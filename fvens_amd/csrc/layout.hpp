@@ -57,6 +57,8 @@ struct Layout
 	std::vector<int> bf_bc;                ///< index into the BC table
 	std::vector<double> bf_n;              ///< [nb][2]
 	std::vector<double> bf_rcbp;           ///< [nb][2]
+	std::vector<int> bf_tag;               ///< [nb] boundary marker (gbtags(face,0))
+	std::vector<double> bf_gr;             ///< [nb][2] face centre (node average, aspatial.cpp:53-61)
 	// interior faces (reference order, for the Jacobian): internal L, R
 	std::vector<int> if_L, if_R;
 	std::vector<int> if_slot;              ///< one slot carrying the face's geometry

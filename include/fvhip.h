@@ -11,6 +11,7 @@
  *   fvhip_compute_residual   FlowFV::compute_residual                      spatial/flow_spatial.cpp:636-816
  *                            (virtual Spatial::compute_residual            spatial/aspatial.hpp:62-63)
  *   fvhip_get_gradients      FlowFV_base::getGradients                     spatial/flow_spatial.cpp:95-112
+ *   fvhip_surface_data_device FlowFV_base::computeSurfaceData              spatial/flow_spatial.cpp:130-310
  *   fvhip_assemble_jacobian  Spatial::assemble_jacobian                    spatial/aspatial.cpp:242-340
  *   fvhip_matfree_set_state  MatrixFreeSpatialJacobian::set_state          linalg/alinalg.cpp:131-140
  *   fvhip_matfree_apply      MatrixFreeSpatialJacobian::apply              linalg/alinalg.cpp:142-233
@@ -154,6 +155,12 @@ int fvhip_compute_residual_device(fvhip_handle h, const double* d_u, double* d_r
                                   double* d_dtm, int flags);
 /** FlowFV_base::getGradients: conserved-variable gradients, GradBlock layout [nelem][4 vars][2 dims] */
 int fvhip_get_gradients(fvhip_handle h, const double* u, double* grads);
+/** FlowFV_base::computeSurfaceData (spatial/flow_spatial.cpp:130-310) for the device state d_u (internal
+ *  order; on a partitioned handle with room for its ghost rows, which are exchanged): funcs[3] =
+ *  {CL, CDp, CDsf} over the faces of boundary marker `marker` (summed over ranks); if faces is not
+ *  NULL it receives (x, y, Cp, Cf) per face [nfaces][4] (host, this rank's faces in reference order). */
+int fvhip_surface_data_device(fvhip_handle h, const double* d_u, int marker, double* funcs, double* faces,
+                              int* nfaces);
 
 /** Spatial::assemble_jacobian into block-sparse storage: diag [nelem][16] (diagonal blocks),
  *  lower/upper [ninface][16] for interior faces in face order (A[R][L] += L, A[L][R] += U). */

@@ -291,7 +291,9 @@ def test_naca0012_implicit_functional_regression():
     u[perm] = dU.cpu().numpy()
     ref = orc.OracleSpatial(om, p, n2)
     cl, cdp, _ = ref.surface(u, ref.getGradients(u), 2)
+    (dcl, dcdp, _), _ = main.surface_data_device(dU.data_ptr(), 2)     # the product's computeSurfaceData
     print(f"starter {st0} main {st} CL {cl!r} CDp {cdp!r}")
+    assert dcl == cl and dcdp == cdp
     assert st["converged"], st
     assert abs(cl - 0.154112792928976) / 0.154112792928976 <= 1e-6
     assert abs(cdp - 0.0115814414408097) / 0.0115814414408097 <= 1e-6
