@@ -125,12 +125,15 @@ def main():
     n = cases.numerics("ROE", "LEASTSQUARES", "VANALBADA")
     u = cases.state(mesh, p, seed=42)
     N, F, Fb = mesh.nelem, mesh.naface, mesh.nbface
-    part, uid = None, None
+    part = None
     if world > 1:
         part = fa.partition_rcb(mesh, world)
+
+    def new_uid():
+        """a fresh RCCL unique id for every communicator (an id bootstraps exactly one)"""
         obj = [fa.comm_unique_id() if rank == 0 else None]
         dist.broadcast_object_list(obj, src=0)
-        uid = obj[0]
+        return obj[0]
 
     def barrier(sp):
         if dist is not None:
@@ -143,7 +146,7 @@ def main():
         n.fast_math = fast
         if world > 1:
             sp = fa.FlowFV(mesh, p, n, device=torch.cuda.current_device(), partition=part, rank=rank)
-            sp.comm_init(world, rank, uid)
+            sp.comm_init(world, rank, new_uid())
             owned = np.nonzero(part == rank)[0]
         else:
             sp = fa.FlowFV(mesh, p, n, device=torch.cuda.current_device())
