@@ -119,9 +119,20 @@ FVHIP_HD void cons2prim2(const Gas& G, const double* uc, double* up) {
 FVHIP_HD double grad_temperature(const Gas& G, double rho, double grho, double p, double gp) {
 	return div_rn(gp*rho - p*grho, rho*rho) * G.g*G.Minf*G.Minf;
 }
+/// T^1.5 of Sutherland's law. The reference calls std::pow(T,1.5); device code forms T*sqrt(T)
+/// (within 2 ulp of it; the device pow is a ~150-instruction log/exp sequence and not glibc's bits
+/// either, so Sutherland terms are compared to the reference to 1e-12 in both cases) -- three of them
+/// per face in the viscous sweep.
+FVHIP_HD double pow15(double T) {
+#if defined(__HIP_DEVICE_COMPILE__)
+	return T*sqrt_rn(T);
+#else
+	return pow(T, 1.5);
+#endif
+}
 FVHIP_HD double sutherland(const Gas& G, const double* uc) {
 	const double T = temperature(G, uc[0], pressure_cons(G, uc));
-	return div_rn(div_rn(1.0+div_rn(G.sC, G.Tinf), T+div_rn(G.sC, G.Tinf)) * pow(T,1.5), G.Reinf);
+	return div_rn(div_rn(1.0+div_rn(G.sC, G.Tinf), T+div_rn(G.sC, G.Tinf)) * pow15(T), G.Reinf);
 }
 
 /// Roe averages (anumericalflux.hpp:175-189)
@@ -448,17 +459,19 @@ FVHIP_HD void ghost_state(const Gas& G, const BCDev& bc, const double* uinf, con
 
 // ---------------------------------------------------------------------------------------------
 // Viscous face flux (flow_spatial.cpp:348-395, aspatial.cpp:172-205, viscousphysics.cpp:14-122)
-// gl, gr: primitive gradients in GradBlock layout [var][dim]; zero-gradient first order if !order2
+// gl, gr: primitive gradients in GradBlock layout [var][dim]; zero-gradient first order if !order2.
+// ORDER2: pl, pr are the cells' primitive states (rho, vx, vy, p) = cons2prim(u) -- the residual
+// stages them already, bit for bit what getPrimitive2StatesAndGradients derives from the conserved
+// states; first order: pl, pr are the conserved states (converted here with cons2prim2).
 // ---------------------------------------------------------------------------------------------
 template <bool ORDER2, bool CONSTVISC>
 FVHIP_HD void viscous_flux(const Gas& G, const double* n, const double* rcl, const double* rcr,
-                           const double* ucl, const double* ucr, const double* gl, const double* grr,
+                           const double* pl, const double* pr, const double* gl, const double* grr,
                            const double* ul, const double* ur, double* vf) {
 	double tl[4], tr[4], gL[8], gR[8];          // gL[dim*4 + var]
 	if(ORDER2) {
 		for(int i = 0; i < 2; i++) for(int j = 0; j < 4; j++) { gL[i*4+j] = gl[j*2+i]; gR[i*4+j] = grr[j*2+i]; }
-		cons2prim(G, ucl, tl);
-		cons2prim(G, ucr, tr);
+		for(int i = 0; i < 4; i++) { tl[i] = pl[i]; tr[i] = pr[i]; }
 		for(int j = 0; j < 2; j++) {
 			gL[j*4+3] = grad_temperature(G, tl[0], gL[j*4], tl[3], gL[j*4+3]);
 			gR[j*4+3] = grad_temperature(G, tr[0], gR[j*4], tr[3], gR[j*4+3]);
@@ -466,8 +479,8 @@ FVHIP_HD void viscous_flux(const Gas& G, const double* n, const double* rcl, con
 		tl[3] = temperature(G, tl[0], tl[3]);
 		tr[3] = temperature(G, tr[0], tr[3]);
 	} else {
-		cons2prim2(G, ucl, tl);
-		cons2prim2(G, ucr, tr);
+		cons2prim2(G, pl, tl);
+		cons2prim2(G, pr, tr);
 		for(int i = 0; i < 8; i++) { gL[i] = 0; gR[i] = 0; }
 	}
 	double grad[2][4];

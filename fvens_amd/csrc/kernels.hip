@@ -456,16 +456,17 @@ __device__ __forceinline__ double muscl_right(double ui, double uj, double dp, d
 }
 
 /// Per-cell words (doubles) staged in LDS for a sweep variant, one 16-byte-aligned row per cell:
-///   order 2: [up 4][reconstruction gradient 8][rc 2] (+[u 4] if viscous) (+[phi 4] if limiter)
+///   order 2: [up 4][reconstruction gradient 8][rc 2] (+[phi 4] if limiter); the viscous flux
+///            takes its primitive states from up as well
 ///   order 1: [u 4] (+[rc 2] if viscous)
 template <int REC, int VISC, bool PHI> struct Stage {
 	static constexpr bool O2 = REC != SR_FIRST;
 	static constexpr bool V = VISC != SV_NONE;
 	static constexpr int UP = 0, RG = 4;
 	static constexpr int RC = O2 ? 12 : 4;
-	static constexpr int UC = O2 ? 14 : 0;
-	static constexpr int PH = V ? 18 : 14;
-	static constexpr int W0 = O2 ? (14 + (V ? 4 : 0) + (PHI ? 4 : 0)) : (V ? 6 : 4);
+	static constexpr int UC = 0;            // order 1 only
+	static constexpr int PH = 14;
+	static constexpr int W0 = O2 ? (14 + (PHI ? 4 : 0)) : (V ? 6 : 4);
 	static constexpr int W = (W0 + 1) & ~1;
 	static constexpr int BUF = (W > 6 ? W : 6) * SLOTS_MAX;   // flux staging reuses the buffer
 };
@@ -499,7 +500,6 @@ __global__ void __launch_bounds__(SLOTS_MAX) k_sweep(const DevMesh M, const DevP
 			ld4(B.up, c, a); st4(row + S::UP, 0, a);
 			ld8(B.rgrad, c, a); st8(row + S::RG, 0, a);
 			const double2 r = M.rc[c]; *reinterpret_cast<double2*>(row + S::RC) = r;
-			if(S::V) { ld4(B.u, c, a); st4(row + S::UC, 0, a); }
 			if(PHI) { ld4(B.phi, c, a); st4(row + S::PH, 0, a); }
 		} else {
 			ld4(B.u, c, a); st4(row + S::UC, 0, a);
@@ -618,17 +618,20 @@ __global__ void __launch_bounds__(SLOTS_MAX) k_sweep(const DevMesh M, const DevP
 		for(int k = 0; k < 4; k++) f[k] *= len;
 
 		if(VISC != SV_NONE) {
+			// order 2: primitive states (up / ghost ug); order 1: conserved states
 			double ucl[4], ucr[4], gl[8], gr[8];
 			const double2 rl = getrc(lr.x);
 			double2 rr;
-			get4(lr.x, S::UC, B.u, ucl);
+			if(REC == SR_FIRST) get4(lr.x, S::UC, B.u, ucl);
+			else get4(lr.x, S::UP, B.up, ucl);
 			if(bnd) {
 				rr = M.bf_rcbp[bf];
 				if(REC == SR_FIRST) { for(int k = 0; k < 4; k++) ucr[k] = ur[k]; }
-				else ld4(B.ubc, bf, ucr);
+				else ld4(B.ug, bf, ucr);
 			} else {
 				rr = getrc(lr.y);
-				get4(lr.y, S::UC, B.u, ucr);
+				if(REC == SR_FIRST) get4(lr.y, S::UC, B.u, ucr);
+				else get4(lr.y, S::UP, B.up, ucr);
 			}
 			if(REC != SR_FIRST) {
 				const int cr = bnd ? lr.x : lr.y;
