@@ -58,9 +58,11 @@ def prep_algorithmic_bytes(N, F, Fb):
 
 
 def kernel_bytes(label, N, F, Fb):
-    """algorithmic bytes of one launch of the kernel `label` (profiling name)"""
-    if label.startswith("k_residual_wls"):
-        return residual_algorithmic_bytes(N, F, Fb)
+    """algorithmic bytes of one launch of the residual kernel `label` (profiling name): SURVEY.md 8(d)'s
+    per-face figure for the second-order sweep (124.0 B/face on C4) plus the time-step bytes, the same
+    for the one-launch residual and for the staged sweep -- they perform the same operation; the
+    one-launch kernel's own compulsory traffic is lower (residual_algorithmic_bytes: gradients stay
+    in LDS), which is why it is faster, not a different amount of algorithmic work"""
     return sweep_algorithmic_bytes(N, F, Fb)
 
 
@@ -281,7 +283,9 @@ def main():
                          "traffic": int(tr[0]) if tr else None,
                          "traffic_source": tr[1] if tr else None,
                          "kernel": sweep_name[0] if sweep_name else None,
-                         "kernel_ms": round(sweep_ms, 5), "algorithmic_bytes": ab},
+                         "kernel_ms": round(sweep_ms, 5), "algorithmic_bytes": ab,
+                         "bytes_basis": "SURVEY.md 8(d) 32F + 144N + 48Fb (124.0 B/face on C4) + 16N time step",
+                         "compulsory_bytes_one_launch": residual_algorithmic_bytes(*cnt)},
             "kernels_ms": {k: round(v, 5) for k, v in kernels_ms.items()},
             "cpu_baseline": cpu,
             "fast_math": fast,
