@@ -771,35 +771,46 @@ __global__ void __launch_bounds__(SLOTS_MAX, 4) k_residual_wls(const DevMesh M, 
 		const double2 rcc = *reinterpret_cast<const double2*>(row + 12);
 		const int4 nb4 = gnbr[i];
 		const int nb[4] = {nb4.x, nb4.y, nb4.z, nb4.w};
+		// gather first: the global (ring-2) states of all neighbours are requested before any is
+		// used, so a ring-1 cell waits for one memory round trip instead of one per neighbour
+		double un[4][4];
+		double2 rn[4];
+		#pragma unroll
+		for(int k = 0; k < 4; k++) {
+			if(nb[k] >= FUSED_GLOBAL) {
+				const int g = nb[k] - FUSED_GLOBAL;
+				ld4(B.u, g, un[k]);
+				rn[k] = M.rc[g];
+			}
+		}
+		#pragma unroll
+		for(int k = 0; k < 4; k++) {
+			if(nb[k] == -1) continue;
+			if(nb[k] >= 0 && nb[k] < FUSED_GLOBAL) {
+				ld4(&fz[nb[k]*FZW], 0, un[k]);
+				rn[k] = *reinterpret_cast<const double2*>(&fz[nb[k]*FZW + 12]);
+			} else if(nb[k] >= FUSED_GLOBAL) {
+				double t4[4] = {un[k][0], un[k][1], un[k][2], un[k][3]};
+				cons2prim(G, t4, un[k]);
+			} else {
+				const int bf = -2 - nb[k];
+				const double4 gp = ghost_prim_of_cell(M, P, B.u, c, bf);
+				un[k][0] = gp.x; un[k][1] = gp.y; un[k][2] = gp.z; un[k][3] = gp.w;
+				rn[k] = M.bf_rcbp[bf];
+			}
+		}
 		double f[8] = {0,0,0,0,0,0,0,0};
 		#pragma unroll
 		for(int k = 0; k < 4; k++) {
 			if(nb[k] == -1) break;
-			double un[4];
-			double2 rn;
-			if(nb[k] >= 0 && nb[k] < FUSED_GLOBAL) {
-				ld4(&fz[nb[k]*FZW], 0, un);
-				rn = *reinterpret_cast<const double2*>(&fz[nb[k]*FZW + 12]);
-			} else if(nb[k] >= FUSED_GLOBAL) {
-				const int g = nb[k] - FUSED_GLOBAL;
-				double t4[4];
-				ld4(B.u, g, t4);
-				rn = M.rc[g];
-				cons2prim(G, t4, un);
-			} else {
-				const int bf = -2 - nb[k];
-				const double4 gp = ghost_prim_of_cell(M, P, B.u, c, bf);
-				un[0] = gp.x; un[1] = gp.y; un[2] = gp.z; un[3] = gp.w;
-				rn = M.bf_rcbp[bf];
-			}
 			double w2 = 0;
-			w2 += (rcc.x-rn.x)*(rcc.x-rn.x);
-			w2 += (rcc.y-rn.y)*(rcc.y-rn.y);
-			const double dr0 = rcc.x-rn.x, dr1 = rcc.y-rn.y;
+			w2 += (rcc.x-rn[k].x)*(rcc.x-rn[k].x);
+			w2 += (rcc.y-rn[k].y)*(rcc.y-rn[k].y);
+			const double dr0 = rcc.x-rn[k].x, dr1 = rcc.y-rn[k].y;
 			w2 = div_rn(1.0, w2);
 			#pragma unroll
 			for(int iv = 0; iv < 4; iv++) {
-				const double du = uc[iv] - un[iv];
+				const double du = uc[iv] - un[k][iv];
 				f[iv*2+0] += w2*dr0*du;
 				f[iv*2+1] += w2*dr1*du;
 			}
