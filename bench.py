@@ -88,8 +88,23 @@ def pmc_traffic(kernel_symbol, workload_cells):
             continue
         for k, v in d.get("kernels", {}).items():
             if k.endswith(kernel_symbol):
-                best = (v["hbm_bytes_corrected"], os.path.relpath(f, ROOT))
+                best = (v["hbm_bytes_corrected"], os.path.relpath(f, ROOT), v.get("SQ_INSTS_VALU"))
     return best
+
+
+HBM_MEASURED_GBS = 6290.0          # MI355X_MICROARCH.md: float4 copy, 79 % of the spec
+FP64_LANE_OPS = 256 * 64 * 2.4e9   # FP64 VALU issue: 64 lanes/CU/clock (78.6 TFLOPS FMA spec) at 2.4 GHz
+
+
+def valu_roofline(valu_wave_instrs, kernel_ms):
+    """the face kernels are FP64-issue bound: VALU wave-instructions per launch (PMC SQ_INSTS_VALU of
+    the committed profile) x 64 lanes / launch time, against the FP64 issue rate (every VALU
+    instruction counted at the FP64 rate, so the fraction is a lower bound)"""
+    if not valu_wave_instrs:
+        return None
+    a = valu_wave_instrs * 64 / (kernel_ms * 1e-3)
+    return {"bound": "fp64-valu", "achieved": round(a / 1e12, 2), "peak": round(FP64_LANE_OPS / 1e12, 2),
+            "unit": "T lane-ops/s", "frac": round(a / FP64_LANE_OPS, 4), "valu_wave_instrs": int(valu_wave_instrs)}
 
 
 def main():
@@ -285,7 +300,9 @@ def main():
                          "kernel": sweep_name[0] if sweep_name else None,
                          "kernel_ms": round(sweep_ms, 5), "algorithmic_bytes": ab,
                          "bytes_basis": "SURVEY.md 8(d) 32F + 144N + 48Fb (124.0 B/face on C4) + 16N time step",
-                         "compulsory_bytes_one_launch": residual_algorithmic_bytes(*cnt)},
+                         "compulsory_bytes_one_launch": residual_algorithmic_bytes(*cnt),
+                         "frac_of_measured_peak": round(achieved / HBM_MEASURED_GBS, 4)},
+            "valu_roofline": valu_roofline(tr[2] if tr else None, sweep_ms),
             "kernels_ms": {k: round(v, 5) for k, v in kernels_ms.items()},
             "cpu_baseline": cpu,
             "fast_math": fast,
