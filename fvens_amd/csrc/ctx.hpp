@@ -207,7 +207,10 @@ struct fvhip_ctx
 		if(L.nghost > 0)
 			timed("k_ghost_prim", [&]{ launch_cons2prim_rows(P.gas, u, d_up, L.ncell, L.nghost, stream); });
 		if(cfg.gradientscheme == FVHIP_GRAD_LEASTSQUARES) {
-			timed("k_prep_grad_wls", [&]{ KOPS(launch_prep_grad_wls)(M, P, u, d_up, d_ubc, d_ug, d_grad, stream, 0, -1); });
+			// limited reconstructions: the limiter values come out of the same kernel
+			const int lim = fusedLimiter() ? (cfg.reconstruction == FVHIP_REC_VENKATAKRISHNAN ? 2 : 1) : 0;
+			timed("k_prep_grad_wls", [&]{ KOPS(launch_prep_grad_wls)(M, P, u, d_up, d_ubc, d_ug, d_grad, stream, 0, -1,
+			                                                         lim, d_phi); });
 		} else {
 			timed("k_prep", [&]{ KOPS(launch_prep)(M, P, u, d_up, d_ubc, d_ug, true, stream); });
 			if(cfg.gradientscheme == FVHIP_GRAD_GREENGAUSS)
@@ -218,7 +221,10 @@ struct fvhip_ctx
 	bool limited() const {
 		return cfg.reconstruction == FVHIP_REC_BARTHJESPERSEN || cfg.reconstruction == FVHIP_REC_VENKATAKRISHNAN;
 	}
+	/// WLS gradients compute the limiter in the same pass (k_prep_grad_wls<LIM>)
+	bool fusedLimiter() const { return limited() && cfg.gradientscheme == FVHIP_GRAD_LEASTSQUARES; }
 	void stage_limiter() {
+		if(fusedLimiter()) return;
 		const int venk = cfg.reconstruction == FVHIP_REC_VENKATAKRISHNAN;
 		timed("k_limiter", [&]{ KOPS(launch_limiter)(M, P, venk, d_up, d_ug, d_grad, d_phi, stream); });
 	}
@@ -269,7 +275,7 @@ struct fvhip_ctx
 		HC(hipStreamWaitEvent(stream2, pipe_start, 0));
 		for(int k = 0; k < K; k++) {
 			timed("k_prep_grad_wls", [&]{
-				KOPS(launch_prep_grad_wls)(M, P, u, d_up, d_ubc, d_ug, d_grad, stream, L.pipe_cell_start[k], L.pipe_cell_start[k+1]);
+				KOPS(launch_prep_grad_wls)(M, P, u, d_up, d_ubc, d_ug, d_grad, stream, L.pipe_cell_start[k], L.pipe_cell_start[k+1], 0, nullptr);
 			});
 			HC(hipEventRecord(pipe_ev[k], stream));
 		}

@@ -159,10 +159,56 @@ __global__ void __launch_bounds__(256) k_grad_wls(DevMesh M, const double* __res
 /// then the same WLS arithmetic as k_grad_wls. A block owns 256 consecutive (Hilbert-ordered)
 /// cells; their primitive states and centres are staged in LDS, so only neighbours outside the
 /// block are gathered from global memory.
+/// limiter values of one cell (k_limiter's arithmetic): uc its primitive state, g its gradient,
+/// un[j] / gp[j] the state across and the centre of its face j (any face order: dmin/dmax and the
+/// minimum over faces do not depend on it), nf faces
+template <bool VENK>
+__device__ __forceinline__ void cell_limiter(const double* uc, const double* g, const double (*un)[4],
+                                             const double2* gp, const bool* has, double2 r, double eps2,
+                                             double* out)
+{
+	#pragma unroll
+	for(int iv = 0; iv < 4; iv++) {
+		double dmin = 0, dmax = 0;
+		#pragma unroll
+		for(int j = 0; j < 4; j++) {
+			if(!has[j]) continue;
+			const double d = un[j][iv]-uc[iv];
+			if(d > dmax) dmax = d;
+			if(d < dmin) dmin = d;
+		}
+		double lim = 1.0;
+		#pragma unroll
+		for(int j = 0; j < 4; j++) {
+			if(!has[j]) continue;
+			double uf = uc[iv];
+			uf += 1.0*g[iv*2+0]*(gp[j].x - r.x);
+			uf += 1.0*g[iv*2+1]*(gp[j].y - r.y);
+			double ph;
+			if(VENK) {
+				const double dm = uf - uc[iv];
+				const double dp = dm < 0 ? dmin : dmax;
+				ph = div_rn(dp*dp + 2*dp*dm + eps2, dp*dp + dp*dm + 2*dm*dm + eps2);
+			} else {
+				const double diff = uf - uc[iv];
+				if(diff > 0) ph = 1 < dmax/diff ? 1 : dmax/diff;
+				else if(diff < 0) ph = 1 < dmin/diff ? 1 : dmin/diff;
+				else ph = 1;
+			}
+			if(ph < lim) lim = ph;
+		}
+		out[iv] = lim;
+	}
+}
+
+/// LIM (1 Barth-Jespersen, 2 Venkatakrishnan): the cell's limiter values follow from the same
+/// neighbour states with k_limiter's arithmetic (face centres in reference face order from
+/// cell_slots), so the separate limiter pass and its re-reads disappear
+template <int LIM>
 __global__ void __launch_bounds__(256) k_prep_grad_wls(DevMesh M, DevPhys P, const double* __restrict__ u,
                                                        double* __restrict__ up, double* __restrict__ ubc,
                                                        double* __restrict__ ug, double* __restrict__ grad,
-                                                       int c_begin, int c_end)
+                                                       int c_begin, int c_end, double* __restrict__ phi)
 {
 	__shared__ __attribute__((aligned(16))) double s_up[256][4];
 	__shared__ __attribute__((aligned(16))) double2 s_rc[256];
@@ -238,6 +284,20 @@ __global__ void __launch_bounds__(256) k_prep_grad_wls(DevMesh M, DevPhys P, con
 		g[iv*2+1] = V.z*f[iv*2+0] + V.w*f[iv*2+1];
 	}
 	st8(grad, c, g);
+	if(LIM) {
+		const int4 cs = M.cell_slots[c];
+		const int sl[4] = {cs.x, cs.y, cs.z, cs.w};
+		double2 gp[4];
+		bool has[4];
+		#pragma unroll
+		for(int k = 0; k < 4; k++) {
+			has[k] = nb[k] >= 0;
+			if(has[k]) gp[k] = M.slot_gr[sl[k] >> 1];
+		}
+		double out[4];
+		cell_limiter<LIM == 2>(uc, g, un, gp, has, rcc, LIM == 2 ? M.venk_eps2[c] : 0.0, out);
+		st4(phi, c, out);
+	}
 }
 
 /// WLS gradients of a list of owned cells (the cells other ranks hold as ghosts), all inputs from
@@ -364,39 +424,9 @@ __global__ void __launch_bounds__(256) k_limiter(DevMesh M, const double* __rest
 		if(nbr[j] >= N) ld4(ug, nbr[j]-N, un[j]); else ld4(up, nbr[j], un[j]);
 		gp[j] = M.slot_gr[fcs[j]];
 	}
+	const bool has[4] = {nbr[0] >= 0, nbr[1] >= 0, nbr[2] >= 0, nbr[3] >= 0};
 	double out[4];
-	#pragma unroll
-	for(int iv = 0; iv < 4; iv++) {
-		double dmin = 0, dmax = 0;
-		#pragma unroll
-		for(int j = 0; j < 4; j++) {
-			if(nbr[j] < 0) continue;
-			const double d = un[j][iv]-uc[iv];
-			if(d > dmax) dmax = d;
-			if(d < dmin) dmin = d;
-		}
-		double lim = 1.0;
-		#pragma unroll
-		for(int j = 0; j < 4; j++) {
-			if(nbr[j] < 0) continue;
-			double uf = uc[iv];
-			uf += 1.0*g[iv*2+0]*(gp[j].x - r.x);
-			uf += 1.0*g[iv*2+1]*(gp[j].y - r.y);
-			double ph;
-			if(VENK) {
-				const double dm = uf - uc[iv];
-				const double dp = dm < 0 ? dmin : dmax;
-				ph = div_rn(dp*dp + 2*dp*dm + eps2, dp*dp + dp*dm + 2*dm*dm + eps2);
-			} else {
-				const double diff = uf - uc[iv];
-				if(diff > 0) ph = 1 < dmax/diff ? 1 : dmax/diff;
-				else if(diff < 0) ph = 1 < dmin/diff ? 1 : dmin/diff;
-				else ph = 1;
-			}
-			if(ph < lim) lim = ph;
-		}
-		out[iv] = lim;
-	}
+	cell_limiter<VENK>(uc, g, un, gp, has, r, eps2, out);
 	st4(phi, c, out);
 }
 
@@ -998,11 +1028,14 @@ void launch_prep(const DevMesh& M, const DevPhys& P, const double* u, double* up
 void launch_grad_wls(const DevMesh& M, const double* up, const double* ug, double* grad, hipStream_t s)
 { if(M.nown > 0) k_grad_wls<<<nblk(M.nown,256), 256, 0, s>>>(M, up, ug, grad); }
 void launch_prep_grad_wls(const DevMesh& M, const DevPhys& P, const double* u, double* up, double* ubc,
-                          double* ug, double* grad, hipStream_t s, int c_begin, int c_end)
+                          double* ug, double* grad, hipStream_t s, int c_begin, int c_end, int lim, double* phi)
 {
 	if(c_end < 0) c_end = M.nown;
-	if(c_end > c_begin)
-		k_prep_grad_wls<<<xcd_blocks((c_end - c_begin + 255)/256), 256, 0, s>>>(M, P, u, up, ubc, ug, grad, c_begin, c_end);
+	if(c_end <= c_begin) return;
+	const dim3 g(xcd_blocks((c_end - c_begin + 255)/256)), b(256);
+	if(lim == 1) k_prep_grad_wls<1><<<g, b, 0, s>>>(M, P, u, up, ubc, ug, grad, c_begin, c_end, phi);
+	else if(lim == 2) k_prep_grad_wls<2><<<g, b, 0, s>>>(M, P, u, up, ubc, ug, grad, c_begin, c_end, phi);
+	else k_prep_grad_wls<0><<<g, b, 0, s>>>(M, P, u, up, ubc, ug, grad, c_begin, c_end, phi);
 }
 void launch_grad_wls_list(const DevMesh& M, const DevPhys& P, const double* u, const int* list, int n,
                           double* grad, hipStream_t s)

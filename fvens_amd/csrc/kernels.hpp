@@ -80,7 +80,8 @@ void launch_prep(const DevMesh& M, const DevPhys& P, const double* u, double* up
                  bool cells, hipStream_t s); \
 void launch_grad_wls(const DevMesh& M, const double* up, const double* ug, double* grad, hipStream_t s); \
 void launch_prep_grad_wls(const DevMesh& M, const DevPhys& P, const double* u, double* up, double* ubc, \
-                          double* ug, double* grad, hipStream_t s, int c_begin = 0, int c_end = -1); \
+                          double* ug, double* grad, hipStream_t s, int c_begin = 0, int c_end = -1, \
+                          int lim = 0, double* phi = nullptr); \
 void launch_grad_wls_list(const DevMesh& M, const DevPhys& P, const double* u, const int* list, int n, \
                           double* grad, hipStream_t s); \
 void launch_grad_gg(const DevMesh& M, const double* up, const double* ug, double* grad, hipStream_t s); \
