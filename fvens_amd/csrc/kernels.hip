@@ -948,6 +948,12 @@ __global__ void __launch_bounds__(SLOTS_MAX, 4) k_residual_wls(const DevMesh M, 
 			srj = (fabs(vnj)+cj)*len;
 		}
 	}
+	// the cell's face list (and area) are requested before the two barriers of the flux staging,
+	// once the face work no longer holds registers
+	const int c = c0 + t;
+	int4 cs = make_int4(-1, -1, -1, -1);
+	double carea = 0.0;
+	if(c < c1) { cs = M.cell_slots[c]; if(DT) carea = M.area[c]; }
 	__syncthreads();   // all staged rows read: reuse LDS for the face fluxes
 	double* sf = fz;
 	double* ssr = fz + 4*SLOTS_MAX;
@@ -958,13 +964,11 @@ __global__ void __launch_bounds__(SLOTS_MAX, 4) k_residual_wls(const DevMesh M, 
 	}
 	__syncthreads();
 
-	const int c = c0 + t;
 	if(c < c1) {
 		double r[4];
 		if(B.overwrite) { r[0] = r[1] = r[2] = r[3] = 0.0; }
 		else ld4(B.r, c, r);
 		double integ = 0.0;
-		const int4 cs = M.cell_slots[c];
 		const int e[4] = {cs.x, cs.y, cs.z, cs.w};
 		#pragma unroll
 		for(int k = 0; k < 4; k++) {
@@ -981,7 +985,7 @@ __global__ void __launch_bounds__(SLOTS_MAX, 4) k_residual_wls(const DevMesh M, 
 			}
 		}
 		st4(B.r, c, r);
-		if(DT) B.dtm[c] = div_rn(M.area[c], integ);
+		if(DT) B.dtm[c] = div_rn(carea, integ);
 	}
 	(void)N;
 }
