@@ -693,6 +693,12 @@ __global__ void __launch_bounds__(SLOTS_MAX) k_sweep(const DevMesh M, const DevP
 			}
 		}
 	}
+	// the cell's face list (and area) are requested before the two barriers of the flux staging,
+	// once the face work no longer holds registers
+	const int c = c0 + t;
+	int4 cs = make_int4(-1, -1, -1, -1);
+	double carea = 0.0;
+	if(c < c1) { cs = M.cell_slots[c]; if(DT) carea = M.area[c]; }
 	__syncthreads();   // every slot has read the staged cells: reuse the buffer for the fluxes
 	double* sf = sbuf;                  // [4][SLOTS_MAX]
 	double* ssr = sbuf + 4*SLOTS_MAX;   // [2][SLOTS_MAX]
@@ -703,13 +709,11 @@ __global__ void __launch_bounds__(SLOTS_MAX) k_sweep(const DevMesh M, const DevP
 	}
 	__syncthreads();
 
-	const int c = c0 + t;
 	if(c < c1) {
 		double r[4];
 		if(B.overwrite) { r[0] = r[1] = r[2] = r[3] = 0.0; }
 		else ld4(B.r, c, r);
 		double integ = 0.0;
-		const int4 cs = M.cell_slots[c];
 		const int e[4] = {cs.x, cs.y, cs.z, cs.w};
 		#pragma unroll
 		for(int k = 0; k < 4; k++) {
@@ -726,7 +730,7 @@ __global__ void __launch_bounds__(SLOTS_MAX) k_sweep(const DevMesh M, const DevP
 			}
 		}
 		st4(B.r, c, r);
-		if(DT) B.dtm[c] = div_rn(M.area[c], integ);
+		if(DT) B.dtm[c] = div_rn(carea, integ);
 	}
 }
 
