@@ -383,10 +383,10 @@ class FlowFV:
         return out
 
     def layout_stats(self):
-        s = (ctypes.c_longlong * 10)()
+        s = (ctypes.c_longlong * 12)()
         check(_ffi.lib().fvhip_layout_stats(self._h, s))
         keys = ("cells", "faces", "slots", "patches", "max_slots", "bfaces", "ghosts", "neighbours", "send_rows",
-                "interior_patches")
+                "interior_patches", "ring1_cells", "patches_over_block")
         return dict(zip(keys, [int(x) for x in s]))
 
     def close(self):

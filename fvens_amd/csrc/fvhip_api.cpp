@@ -581,6 +581,17 @@ int fvhip_layout_stats(fvhip_handle h, long long* s)
 		s[3] = static_cast<long long>(h->L.patch_cell.size()) - 1; s[4] = h->L.max_slots; s[5] = h->L.nbface;
 		s[6] = h->L.nghost; s[7] = static_cast<long long>(h->L.nbr_rank.size()); s[8] = h->nsend;
 		s[9] = h->L.fz_ninner;
+		// fused residual staging: ring-1 cells over all patches; patches staging more cells than a
+		// block has threads (their gradient phase takes two rounds)
+		s[10] = static_cast<long long>(h->L.fz_ext.size());
+		long long over = 0;
+		const long long np = static_cast<long long>(h->L.patch_cell.size()) - 1;
+		if(!h->L.fz_ext_start.empty())
+			for(long long p = 0; p < np; p++) {
+				const long long nl = (h->L.patch_cell[p+1] - h->L.patch_cell[p]) + (h->L.fz_ext_start[p+1] - h->L.fz_ext_start[p]);
+				if(nl > SLOTS_MAX) over++;
+			}
+		s[11] = over;
 	});
 }
 

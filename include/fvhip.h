@@ -268,9 +268,11 @@ void* fvhip_stream(fvhip_handle h);
 int fvhip_profile(fvhip_handle h, int enable);
 int fvhip_kernel_times(fvhip_handle h, int maxk, char* names, int namelen, double* ms, int* counts);
 
-/** Layout statistics (stats[10]): [0]=cells [1]=faces [2]=face slots incl. duplicated cut faces
+/** Layout statistics (stats[12]): [0]=cells [1]=faces [2]=face slots incl. duplicated cut faces
  *  [3]=patches [4]=max slots per patch [5]=boundary faces [6]=ghost cells [7]=neighbour ranks
- *  [8]=rows sent per exchange [9]=fused-residual patches that need no halo data (partitioned) */
+ *  [8]=rows sent per exchange [9]=fused-residual patches that need no halo data (partitioned)
+ *  [10]=ring-1 cells staged by the fused residual over all patches [11]=patches staging more cells
+ *  than a block has threads */
 int fvhip_layout_stats(fvhip_handle h, long long* stats);
 
 /** Point-wise numerical flux on the device (get_flux) for nf faces: ul, ur [nf][4], n [nf][2] */
