@@ -82,6 +82,7 @@ class ImplicitConfig:
     prec_sweeps: int = 1            # block-Jacobi sweeps per preconditioner application
     min_relax: float = 1.0          # nonlinear_update_scheme: >= 1 "full", else "robust_flow" factor
     prec_single: bool = False       # preconditioner blocks stored in fp32 (operator stays fp64)
+    prec_gs: bool = False           # multicolour block Gauss-Seidel sweeps instead of block-Jacobi
 
     def _struct(self):
         c = _ffi.FvImplicitConfig()
@@ -90,6 +91,7 @@ class ImplicitConfig:
         c.lin_rtol, c.lin_maxit, c.restart = float(self.lin_rtol), int(self.lin_maxit), int(self.restart)
         c.prec_sweeps, c.min_relax = int(self.prec_sweeps), float(self.min_relax)
         c.prec_single = int(self.prec_single)
+        c.prec_gs = int(self.prec_gs)
         return c
 
 

@@ -501,6 +501,38 @@ struct fvhip_ctx
 		return surf.emplace(marker, c).first->second;
 	}
 
+	/// multicolour block Gauss-Seidel (fvhip_implicit_config::prec_gs): greedy colouring of the owned
+	/// cells in internal (Hilbert) order over interior faces; ghost cells are not coloured (within a
+	/// sweep they hold the values of the last exchange)
+	std::vector<int> gs_colour_start;
+	int* d_gs_cells = nullptr;
+	void ensureColouring() {
+		if(d_gs_cells) return;
+		const int N = L.ncell;
+		std::vector<int> col(static_cast<size_t>(N), -1);
+		int ncol = 0;
+		for(int c = 0; c < N; c++) {
+			unsigned long long used = 0;
+			for(int j = 0; j < 4; j++) {
+				const int code = L.cell_rfaces[4*static_cast<size_t>(c)+j];
+				if(code < 0 || (code >> 1) < L.nbface) continue;
+				const int nb = L.cell_nbr_fo[4*static_cast<size_t>(c)+j];
+				if(nb >= 0 && nb < N && col[nb] >= 0) used |= 1ull << col[nb];
+			}
+			int k = 0;
+			while(used & (1ull << k)) k++;
+			col[c] = k;
+			ncol = std::max(ncol, k + 1);
+		}
+		gs_colour_start.assign(static_cast<size_t>(ncol) + 1, 0);
+		for(int c = 0; c < N; c++) gs_colour_start[col[c] + 1]++;
+		for(int k = 0; k < ncol; k++) gs_colour_start[k+1] += gs_colour_start[k];
+		std::vector<int> cells(static_cast<size_t>(std::max(N, 1)));
+		std::vector<int> pos(gs_colour_start.begin(), gs_colour_start.end() - 1);
+		for(int c = 0; c < N; c++) cells[pos[col[c]]++] = c;   // ascending within a colour
+		d_gs_cells = upload(cells, owned);
+	}
+
 	/// fp32 copies of the preconditioner blocks (fvhip_implicit_config::prec_single)
 	void ensureSinglePrecond() {
 		if(iw.sdinv) return;

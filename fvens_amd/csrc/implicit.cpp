@@ -94,6 +94,7 @@ struct LinOp
 	System& S;
 	bool matfree = false;
 	bool single = false;                      ///< preconditioner blocks in fp32 (iw.sdinv/slo/sup)
+	bool gs = false;                          ///< multicolour block Gauss-Seidel instead of Jacobi
 	int sweeps = 1;
 	std::vector<const double*> D, Lo, Up;     ///< per handle: diagonal / lower / upper blocks
 
@@ -111,6 +112,7 @@ struct LinOp
 	/// z = M^-1 v: `sweeps` block-Jacobi sweeps on A z = v from z = 0 (z has ghost rows). The iterates
 	/// alternate between z and aux (both with ghost rows) so that the last one lands in z.
 	void precondition(const ArrayOf& v, const ArrayOf& z) {
+		if(gs) { gaussSeidel(v, z); return; }
 		const ArrayOf aux = [&](size_t i) { return S.hs[i]->iw.aux; };
 		auto buf = [&](int k) -> const ArrayOf& { return ((sweeps - 1 - k) % 2 == 0) ? z : aux; };
 		S.each([&](size_t i, fvhip_ctx* h) {
@@ -131,16 +133,41 @@ struct LinOp
 			});
 		}
 	}
+	/// z = M^-1 v by `sweeps` multicolour block Gauss-Seidel sweeps from z = 0, colours in forward
+	/// then backward order on alternate sweeps (symmetric Gauss-Seidel pairs). Across ranks the
+	/// sweep is block-Jacobi: ghost rows are exchanged once per sweep -- the reference's PETSc
+	/// setting -pc_type bjacobi -sub_pc_type sor, with a colour order instead of a row order.
+	void gaussSeidel(const ArrayOf& v, const ArrayOf& z) {
+		S.each([&](size_t i, fvhip_ctx* h) {
+			exact::launch_fill(z(i), 0.0, 4LL*(h->L.ncell + h->L.nghost), h->stream);
+		});
+		for(int k = 0; k < sweeps; k++) {
+			if(k > 0) S.exchange(z, 4);
+			const bool fwd = (k % 2) == 0;
+			S.each([&](size_t i, fvhip_ctx* h) {
+				const int nc = static_cast<int>(h->gs_colour_start.size()) - 1;
+				h->timed("k_bgs_colour", [&]{
+					for(int q = 0; q < nc; q++) {
+						const int col = fwd ? q : nc - 1 - q;
+						const int b = h->gs_colour_start[col], n = h->gs_colour_start[col+1] - b;
+						if(single) launch_bgs_colour(h->J, h->iw.sdinv, h->iw.slo, h->iw.sup, v(i), z(i), h->d_gs_cells + b, n, h->stream);
+						else launch_bgs_colour(h->J, h->iw.dinv, Lo[i], Up[i], v(i), z(i), h->d_gs_cells + b, n, h->stream);
+					}
+				});
+			});
+		}
+	}
 	/// block inverses of the current diagonal blocks
 	void setup() {
 		S.each([&](size_t i, fvhip_ctx* h) {
 			h->timed("k_bjac_invert", [&]{ launch_bjac_invert(h->L.ncell, D[i], h->iw.dinv, h->stream); });
+			if(gs) h->ensureColouring();
 			if(single) {
 				h->ensureSinglePrecond();
 				const long long nf = 16LL*std::max(h->L.ninface, 0);
 				h->timed("k_to_single", [&]{
 					launch_to_single(16LL*h->L.ncell, h->iw.dinv, h->iw.sdinv, h->stream);
-					if(sweeps > 1) {
+					if(sweeps > 1 || gs) {
 						launch_to_single(nf, Lo[i], h->iw.slo, h->stream);
 						launch_to_single(nf, Up[i], h->iw.sup, h->stream);
 					}
@@ -288,6 +315,7 @@ static void backwardEuler(System& S, const std::vector<double*>& us, const fvhip
 	A.matfree = c.matrix_free != 0;
 	A.sweeps = c.prec_sweeps;
 	A.single = c.prec_single != 0;
+	A.gs = c.prec_gs != 0;
 	for(fvhip_ctx* h : S.hs) { A.D.push_back(h->iw.jd); A.Lo.push_back(h->iw.jlo); A.Up.push_back(h->iw.jup); }
 	std::vector<const double*> cu(us.begin(), us.end());
 	std::vector<double*> rs, dts;

@@ -248,6 +248,41 @@ void k_bjac_sweep(JacMesh J, const T* __restrict__ dinv, const T* __restrict__ l
 	reinterpret_cast<double4*>(zout)[c] = make_double4(o[0], o[1], o[2], o[3]);
 }
 
+/// One colour of a multicolour block Gauss-Seidel sweep, in place: z_c = D^-1 (v - sum_faces B z[nbr])
+/// for the listed cells, which share no face, so every neighbour value read is either from an
+/// earlier colour of this sweep or from the previous sweep (ghost rows: from the last exchange).
+template <typename T>
+__global__ __launch_bounds__(256)
+void k_bgs_colour(JacMesh J, const T* __restrict__ dinv, const T* __restrict__ lower, const T* __restrict__ upper,
+                  const double* __restrict__ v, double* z, const int* __restrict__ cells, int n)
+{
+	const int i = blockIdx.x*blockDim.x + threadIdx.x;
+	if(i >= n) return;
+	const int c = cells[i];
+	const double4* z4 = reinterpret_cast<const double4*>(z);
+	const double4 vc = reinterpret_cast<const double4*>(v)[c];
+	double acc[4] = {vc.x, vc.y, vc.z, vc.w};
+	const int4 fc = J.cell_rfaces[c];
+	const int4 nb = J.cell_nbr_fo[c];
+	const int codes[4] = {fc.x, fc.y, fc.z, fc.w};
+	const int nbrs[4] = {nb.x, nb.y, nb.z, nb.w};
+#pragma unroll
+	for(int j = 0; j < 4; j++) {
+		const int code = codes[j];
+		if(code < 0) continue;
+		const int f = code >> 1;
+		if(f < J.nbface) continue;
+		const T* B = ((code & 1) ? lower : upper) + 16*static_cast<size_t>(f - J.nbface);
+		double s[4];
+		blk_row_dots(B, z4[nbrs[j]], s);
+#pragma unroll
+		for(int k = 0; k < 4; k++) acc[k] -= s[k];
+	}
+	double o[4];
+	blk_row_dots(dinv + 16*static_cast<size_t>(c), make_double4(acc[0], acc[1], acc[2], acc[3]), o);
+	reinterpret_cast<double4*>(z)[c] = make_double4(o[0], o[1], o[2], o[3]);
+}
+
 // -------------------------------------------------------------------------------------------------
 // matrix-free pieces
 // -------------------------------------------------------------------------------------------------
@@ -394,6 +429,20 @@ void launch_bjac_sweep(const JacMesh& J, const float* dinv, const float* lower, 
 {
 	hipLaunchKernelGGL(k_bjac_sweep<float>, dim3(nblk(J.ncell,256)), dim3(256), 0, s, J, dinv, lower, upper, v, zin, zout);
 }
+
+template <typename T>
+void launch_bgs_colour_t(const JacMesh& J, const T* dinv, const T* lower, const T* upper, const double* v,
+                         double* z, const int* cells, int n, hipStream_t s)
+{
+	if(n > 0)
+		hipLaunchKernelGGL(k_bgs_colour<T>, dim3(nblk(n,256)), dim3(256), 0, s, J, dinv, lower, upper, v, z, cells, n);
+}
+void launch_bgs_colour(const JacMesh& J, const double* dinv, const double* lower, const double* upper,
+                       const double* v, double* z, const int* cells, int n, hipStream_t s)
+{ launch_bgs_colour_t(J, dinv, lower, upper, v, z, cells, n, s); }
+void launch_bgs_colour(const JacMesh& J, const float* dinv, const float* lower, const float* upper,
+                       const double* v, double* z, const int* cells, int n, hipStream_t s)
+{ launch_bgs_colour_t(J, dinv, lower, upper, v, z, cells, n, s); }
 
 void launch_mf_norm(long long n, const double* x, double eps, double* part, double* pm, hipStream_t s)
 {

@@ -40,6 +40,11 @@ void launch_bjac_sweep(const JacMesh& J, const double* dinv, const double* lower
 /// the same with fp32 blocks (fp64 vectors and arithmetic)
 void launch_bjac_sweep(const JacMesh& J, const float* dinv, const float* lower, const float* upper,
                        const double* v, const double* zin, double* zout, hipStream_t s);
+/// one colour of a multicolour block Gauss-Seidel sweep, in place on z (cells: that colour's cells)
+void launch_bgs_colour(const JacMesh& J, const double* dinv, const double* lower, const double* upper,
+                       const double* v, double* z, const int* cells, int n, hipStream_t s);
+void launch_bgs_colour(const JacMesh& J, const float* dinv, const float* lower, const float* upper,
+                       const double* v, double* z, const int* cells, int n, hipStream_t s);
 /// pm[0] = |x|, pm[1] = eps/|x|; part: mf_partials() doubles of scratch
 void launch_mf_norm(long long n, const double* x, double eps, double* part, double* pm, hipStream_t s);
 void launch_mf_perturb(long long n, const double* u, const double* x, const double* pm, double* aux, hipStream_t s);

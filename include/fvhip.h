@@ -214,6 +214,9 @@ typedef struct fvhip_implicit_config {
 	int prec_single;          /* 1: the preconditioner's blocks (inverted diagonal, lower, upper) are kept in
 	                             fp32 (sweeps read half the bytes; vectors and arithmetic stay fp64). The
 	                             operator itself is unchanged, so the solution tolerance is too. */
+	int prec_gs;              /* 1: multicolour block Gauss-Seidel sweeps (forward/backward colour order on
+	                             alternate sweeps; block-Jacobi across ranks, i.e. PETSc's bjacobi + sor)
+	                             instead of block-Jacobi sweeps */
 } fvhip_implicit_config;
 
 typedef struct fvhip_solve_stats {

@@ -10,7 +10,8 @@ Bars:
     solution to 1e-8 of max|x|; block-Jacobi sweeps cut the iteration count;
   * one implicit step with a tight linear solve: the update u1 - u0 equal to the host restatement's
     to 1e-8 of its size per variable, the residual norm to 1e-12 (also with the preconditioner's
-    blocks in fp32: the operator is unchanged, so is the solution);
+    blocks in fp32, and with multicolour block Gauss-Seidel sweeps: the operator is unchanged, so
+    is the solution);
   * Flow_Euler_Cylinder_HLLC_MatFreeVsMat (tests/solvers/testmatrixfree.cpp:65 with matfree.ctrl /
     matfree.solverc): matrix-free and assembled solves both converge, in the same number of steps;
   * a 3-rank partition (in-process group) takes the same implicit steps as one GPU: same linear
@@ -98,8 +99,9 @@ def test_gmres_blocks_matches_direct_solve():
     dev.close()
 
 
-@pytest.mark.parametrize("min_relax,single", [(1.0, False), (0.2, False), (1.0, True)])
-def test_one_backward_euler_step_matches_host(min_relax, single):
+@pytest.mark.parametrize("min_relax,single,gs", [(1.0, False, False), (0.2, False, False), (1.0, True, False),
+                                                 (1.0, False, True), (1.0, True, True)])
+def test_one_backward_euler_step_matches_host(min_relax, single, gs):
     m, om = get_mesh("naca_small")
     p = cases.physics("naca")
     n = cases.numerics("ROE", "LEASTSQUARES", "VANALBADA")
@@ -113,7 +115,7 @@ def test_one_backward_euler_step_matches_host(min_relax, single):
     perm = dev.permutation()
     dU = to_device(u0, perm)
     cfg = fa.ImplicitConfig(cflinit=cfl, cflfin=cfl, tol=0.0, maxiter=1, lin_rtol=1e-13, lin_maxit=3000, restart=60,
-                            prec_sweeps=2, min_relax=min_relax, prec_single=single)
+                            prec_sweeps=2, min_relax=min_relax, prec_single=single, prec_gs=gs)
     st, hist = dev.steady_backward_euler_device(dU.data_ptr(), cfg)
     assert st["steps"] == 1 and st["cfl"] == cfl
     u = np.empty_like(u0)
@@ -196,6 +198,39 @@ def test_partitioned_backward_euler_matches_single():
         np.testing.assert_allclose(h, h1, rtol=1e-10)
         scale = np.abs(u1 - u0).max(axis=0)
         assert np.all(np.abs(u - u1).max(axis=0) <= 1e-9 * scale), (mf, np.abs(u - u1).max(axis=0) / scale)
+
+
+def test_partitioned_gauss_seidel_same_solution():
+    """multicolour block Gauss-Seidel on a 3-rank group is block-Jacobi across ranks, so its linear
+    iterations differ from one GPU's; with tight linear solves the step is the same to 1e-8 of the
+    update, and it needs no more Krylov iterations than block-Jacobi sweeps on one GPU"""
+    m, _ = get_mesh("naca_small")
+    p = cases.physics("naca")
+    n = cases.numerics("ROE", "LEASTSQUARES", "VANALBADA")
+    u0 = cases.state(m, p, 2)
+    cfg = fa.ImplicitConfig(cflinit=10.0, cflfin=10.0, tol=0.0, maxiter=1, lin_rtol=1e-11, lin_maxit=400,
+                            restart=60, prec_sweeps=2, prec_gs=True)
+    one = fa.FlowFV(m, p, n)
+    perm = one.permutation()
+    dU = to_device(u0, perm)
+    st1, _ = one.steady_backward_euler_device(dU.data_ptr(), cfg)
+    u1 = np.empty_like(u0)
+    u1[perm] = dU.cpu().numpy()
+    cfg_j = fa.ImplicitConfig(**{**cfg.__dict__, "prec_gs": False})
+    dJ = to_device(u0, perm)
+    stj, _ = one.steady_backward_euler_device(dJ.data_ptr(), cfg_j)
+    one.close()
+    sps, dus, glob = _partitioned(m, p, n, u0, 3)
+    grp = fa.FlowFVGroup(sps)
+    st, _ = grp.steady_backward_euler_device([d.data_ptr() for d in dus], cfg)
+    u = _gather(u0, sps, dus, glob)
+    grp.close()
+    for s_ in sps:
+        s_.close()
+    print(f"lin iters: GS 1 GPU {st1['lin_iters']}, GS 3 ranks {st['lin_iters']}, Jacobi 1 GPU {stj['lin_iters']}")
+    assert st1["lin_iters"] <= stj["lin_iters"]
+    scale = np.abs(u1 - u0).max(axis=0)
+    assert np.all(np.abs(u - u1).max(axis=0) <= 1e-8 * scale), np.abs(u - u1).max(axis=0) / scale
 
 
 def test_partitioned_forward_euler_bitwise():

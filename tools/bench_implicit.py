@@ -42,6 +42,7 @@ def main():
     ap.add_argument("--lin-maxit", type=int, default=30)
     ap.add_argument("--sweeps", type=int, default=4)
     ap.add_argument("--prec-single", action="store_true", help="preconditioner blocks in fp32")
+    ap.add_argument("--gs", action="store_true", help="multicolour block Gauss-Seidel sweeps")
     args = ap.parse_args()
 
     import torch
@@ -69,14 +70,15 @@ def main():
     # during the start-up transient (measured), so the CFL is held fixed
     dinit = torch.tensor(u0, dtype=torch.float64, device="cuda")
     ini = fa.ImplicitConfig(cflinit=args.cfl, cflfin=args.cfl, tol=0.0, maxiter=args.init_steps,
-                            lin_rtol=1e-2, lin_maxit=args.lin_maxit, restart=args.restart, prec_sweeps=args.sweeps)
+                            lin_rtol=1e-2, lin_maxit=args.lin_maxit, restart=args.restart, prec_sweeps=args.sweeps,
+                            prec_single=args.prec_single, prec_gs=args.gs)
     st0, _ = sp1.steady_backward_euler_device(dinit.data_ptr(), ini)
     torch.cuda.synchronize()
     for mf in (False, True):
         du = dinit.clone()
         cfg = fa.ImplicitConfig(cflinit=args.cfl, cflfin=args.cfl, tol=0.0, maxiter=args.warmup, matrix_free=mf,
                                 lin_rtol=1e-2, lin_maxit=args.lin_maxit, restart=args.restart,
-                                prec_sweeps=args.sweeps, prec_single=args.prec_single)
+                                prec_sweeps=args.sweeps, prec_single=args.prec_single, prec_gs=args.gs)
         sp.steady_backward_euler_device(du.data_ptr(), cfg)      # warm-up: allocations, clocks
         torch.cuda.synchronize()
         du = dinit.clone()
@@ -92,7 +94,7 @@ def main():
                "lin_iters_per_step": round(st["lin_iters"] / k, 2),
                "ms_per_lin_iter": round(dt * 1e3 / max(st["lin_iters"], 1), 4),
                "resratio": st["resratio"], "cells": mesh.nelem, "faces": mesh.naface, "dims": dims,
-               "restart": args.restart, "prec_sweeps": args.sweeps, "prec_single": args.prec_single, "cfl": args.cfl,
+               "restart": args.restart, "prec_sweeps": args.sweeps, "prec_single": args.prec_single, "prec_gs": args.gs, "cfl": args.cfl,
                "init": {"steps": st0["steps"], "resratio": st0["resratio"]}}
         print(json.dumps(out), flush=True)
 
