@@ -118,6 +118,7 @@ def main():
     ap.add_argument("--no-fast", action="store_true", help="skip the fast-math mode measurement")
     ap.add_argument("--scaling", choices=["weak", "strong"], default="weak")
     ap.add_argument("--no-pipelined", action="store_true", help="skip the pipelined staged path")
+    ap.add_argument("--no-implicit", action="store_true", help="skip the implicit-step figure (1 GPU only)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -254,6 +255,16 @@ def main():
     achieved = ab / (sweep_ms * 1e-3) / 1e9
     value = F / (ms_per_step * 1e-3) / 1e6       # every face of the (global) mesh once per step
 
+    # secondary figure, one GPU: the device implicit pseudo-time step on the same
+    # mesh -- residual, analytic Jacobian, GMRES(30) with 4 block-Jacobi sweeps in fp32, update
+    implicit = None
+    if world == 1 and not args.no_implicit:
+        sys.path.insert(0, os.path.join(ROOT, "tools"))
+        from bench_implicit import implicit_steps
+        implicit = next(implicit_steps(mesh, "naca", steps=3, warmup=1, init_steps=5, sweeps=4, single=True,
+                                       operators=(False,)))
+        implicit.pop("faces", None)
+
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         import _oracle as orc
@@ -308,6 +319,7 @@ def main():
             "fast_math": fast,
             "staged_path": staged,
             "pipelined_path": pipelined,
+            "implicit_step": implicit,
         }
         print(json.dumps(out))
     if dist is not None:

@@ -48,7 +48,6 @@ def main():
     import torch
     torch.cuda.set_device(0)
     import fvens_amd as fa
-    import cases
     from bench import c4_mesh
 
     kind, flux, grad, rec = CASES[args.case]
@@ -57,46 +56,60 @@ def main():
         mesh, dims = fa.UMesh.flat_plate(nx, ny), dict(nx=nx, ny=ny)
     else:
         mesh, dims = c4_mesh(fa, args.scale)
+    for out in implicit_steps(mesh, args.case, steps=args.steps, warmup=args.warmup, init_steps=args.init_steps,
+                              cfl=args.cfl, restart=args.restart, lin_maxit=args.lin_maxit, sweeps=args.sweeps,
+                              single=args.prec_single, gs=args.gs):
+        out["dims"] = dims
+        print(json.dumps(out), flush=True)
+
+
+def implicit_steps(mesh, case="naca", steps=5, warmup=2, init_steps=10, cfl=25.0, restart=30, lin_maxit=30,
+                   sweeps=4, single=False, gs=False, operators=(False, True)):
+    """time `steps` second-order backward-Euler steps per operator kind (False: assembled, True:
+    matrix-free) after a first-order start; yields one dict per operator"""
+    import torch
+    import fvens_amd as fa
+    import cases
+    kind, flux, grad, rec = CASES[case]
     p = cases.physics(kind)
     n = cases.numerics(flux, grad, rec)
     n1 = cases.numerics(flux, grad, rec, order2=False)
-    sp1 = fa.FlowFV(mesh, p, n1, device=0)
-    sp = fa.FlowFV(mesh, p, n, device=0)
+    dev = torch.cuda.current_device()
+    sp1 = fa.FlowFV(mesh, p, n1, device=dev)
+    sp = fa.FlowFV(mesh, p, n, device=dev)
     perm = sp.permutation()
     assert np.array_equal(perm, sp1.permutation())
     u0 = np.tile(cases.freestream(p), (mesh.nelem, 1))[perm]
     # the reference's start-up (transonic-implicit.ctrl): a first-order initialisation solve, then the
     # second-order main solve. Its CFL ramps (25/50 -> 500) blow up on this O-grid's 1e-5 wall cells
     # during the start-up transient (measured), so the CFL is held fixed
+    lin = dict(lin_rtol=1e-2, lin_maxit=lin_maxit, restart=restart, prec_sweeps=sweeps, prec_single=single,
+               prec_gs=gs)
     dinit = torch.tensor(u0, dtype=torch.float64, device="cuda")
-    ini = fa.ImplicitConfig(cflinit=args.cfl, cflfin=args.cfl, tol=0.0, maxiter=args.init_steps,
-                            lin_rtol=1e-2, lin_maxit=args.lin_maxit, restart=args.restart, prec_sweeps=args.sweeps,
-                            prec_single=args.prec_single, prec_gs=args.gs)
-    st0, _ = sp1.steady_backward_euler_device(dinit.data_ptr(), ini)
+    st0, _ = sp1.steady_backward_euler_device(dinit.data_ptr(), fa.ImplicitConfig(
+        cflinit=cfl, cflfin=cfl, tol=0.0, maxiter=init_steps, **lin))
     torch.cuda.synchronize()
-    for mf in (False, True):
+    sp1.close()
+    for mf in operators:
         du = dinit.clone()
-        cfg = fa.ImplicitConfig(cflinit=args.cfl, cflfin=args.cfl, tol=0.0, maxiter=args.warmup, matrix_free=mf,
-                                lin_rtol=1e-2, lin_maxit=args.lin_maxit, restart=args.restart,
-                                prec_sweeps=args.sweeps, prec_single=args.prec_single, prec_gs=args.gs)
+        cfg = fa.ImplicitConfig(cflinit=cfl, cflfin=cfl, tol=0.0, maxiter=warmup, matrix_free=mf, **lin)
         sp.steady_backward_euler_device(du.data_ptr(), cfg)      # warm-up: allocations, clocks
-        torch.cuda.synchronize()
         du = dinit.clone()
-        cfg.maxiter = args.steps
+        cfg.maxiter = steps
         torch.cuda.synchronize()
         t0 = time.perf_counter()
         st, hist = sp.steady_backward_euler_device(du.data_ptr(), cfg)
         torch.cuda.synchronize()
         dt = time.perf_counter() - t0
         k = max(st["steps"], 1)
-        out = {"metric": "implicit_step_time", "case": args.case, "operator": "matrix-free" if mf else "assembled",
+        yield {"metric": "implicit_step_time", "case": case, "operator": "matrix-free" if mf else "assembled",
                "ms_per_step": round(dt / k * 1e3, 3), "steps": st["steps"],
                "lin_iters_per_step": round(st["lin_iters"] / k, 2),
                "ms_per_lin_iter": round(dt * 1e3 / max(st["lin_iters"], 1), 4),
-               "resratio": st["resratio"], "cells": mesh.nelem, "faces": mesh.naface, "dims": dims,
-               "restart": args.restart, "prec_sweeps": args.sweeps, "prec_single": args.prec_single, "prec_gs": args.gs, "cfl": args.cfl,
+               "resratio": st["resratio"], "cells": mesh.nelem, "faces": mesh.naface,
+               "restart": restart, "prec_sweeps": sweeps, "prec_single": single, "prec_gs": gs, "cfl": cfl,
                "init": {"steps": st0["steps"], "resratio": st0["resratio"]}}
-        print(json.dumps(out), flush=True)
+    sp.close()
 
 
 if __name__ == "__main__":

@@ -7,7 +7,7 @@ cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
 OUT=gpurun_out/prof
 mkdir -p $OUT
-ARGS="--steps 200 --warmup 20 --no-cpu-baseline --no-pipelined $*"
+ARGS="--steps 200 --warmup 20 --no-cpu-baseline --no-pipelined --no-implicit $*"
 run() {  # name timeout cmd...
   local name=$1 to=$2; shift 2
   echo "== $name"; date
