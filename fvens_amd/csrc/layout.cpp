@@ -78,10 +78,80 @@ Layout buildLayout(const MeshTopo& T, const fvhip_flow_config& cfg, bool renumbe
 	// owned cells are renumbered; ghosts (>= N) and boundary codes (>= NT) keep their value
 	auto toInt = [&](int refcell) { return refcell < N ? Lo.iperm[refcell] : refcell; };
 
-	// --- patches (greedy over internal cells, bounded slots and cells) ---
+	// --- patches, bounded slots and cells ---
+	// renumbered meshes: each patch is grown breadth-first over interior faces from the first
+	// unassigned cell in Hilbert order (and refilled from the next one when its region runs out), so
+	// patches are compact in the mesh graph: on C4 17.6 % ring-1 cells and 8.2 % duplicated cut faces
+	// against 35.2 % and 12.7 % for Hilbert ranges. The cells are then renumbered patch by patch
+	// (BFS order inside a patch). Otherwise: greedy ranges of the given order.
 	std::vector<int> mark(F, -1);
 	Lo.patch_cell.push_back(0);
-	{
+	if(renumber && N > 0) {
+		std::vector<int> order;                      // new -> old, patch by patch
+		order.reserve(N);
+		std::vector<char> taken(static_cast<size_t>(N), 0);
+		std::vector<int> queue, inq(static_cast<size_t>(N), -1);
+		// partitioned meshes: cells within two faces of a ghost cell go into patches of their own
+		// (built last), so that every other patch stages no ghost data -- its ring-1 cells and
+		// their neighbours are all owned -- and can run while the halo is in flight
+		std::vector<char> near(static_cast<size_t>(N), 0);
+		if(T.nghost > 0) {
+			std::vector<int> front;
+			for(int c = 0; c < N; c++)
+				for(int j = 0; j < nf(c); j++) {
+					const int nb = esu(c, j);
+					if(nb >= N && nb < NT) { near[c] = 1; front.push_back(c); break; }
+				}
+			for(const int c : std::vector<int>(front))
+				for(int j = 0; j < nf(c); j++) {
+					const int nb = esu(c, j);
+					if(nb >= 0 && nb < N && !near[nb]) near[nb] = 1;
+				}
+		}
+		int pid = 0;
+		for(int pass = 0; pass < 2; pass++) {
+			auto allowed = [&](int ref) { return (near[ref] != 0) == (pass == 1); };
+			size_t seed = 0;
+			for(;;) {
+				while(seed < static_cast<size_t>(N) && (taken[Lo.perm[seed]] || !allowed(Lo.perm[seed]))) seed++;
+				if(seed >= static_cast<size_t>(N)) break;
+				queue.clear();
+				size_t qi = 0;
+				int cs = 0, cc = 0;
+				for(;;) {
+					if(qi == queue.size()) {
+						// the patch's region is exhausted: continue from the next unassigned cell in
+						// Hilbert order (a nearby hole or fresh cells), so every patch fills up
+						if(cc > 0 && cs >= SLOTS_MAX - 4) break;
+						size_t sk = seed;
+						while(sk < static_cast<size_t>(N) && (taken[Lo.perm[sk]] || inq[Lo.perm[sk]] == pid
+						                                      || !allowed(Lo.perm[sk]))) sk++;
+						if(sk >= static_cast<size_t>(N)) break;
+						inq[Lo.perm[sk]] = pid;
+						queue.push_back(Lo.perm[sk]);
+					}
+					const int ref = queue[qi++];
+					int nnew = 0;
+					for(int j = 0; j < nf(ref); j++) if(mark[efc(ref,j)] != pid) nnew++;
+					if(cc > 0 && (cs + nnew > SLOTS_MAX || cc + 1 > CELLS_MAX)) continue;   // left for later patches
+					for(int j = 0; j < nf(ref); j++) mark[efc(ref,j)] = pid;
+					cs += nnew; cc++;
+					taken[ref] = 1;
+					order.push_back(ref);
+					for(int j = 0; j < nf(ref); j++) {
+						const int nb = esu(ref, j);
+						if(nb < 0 || nb >= N || taken[nb] || inq[nb] == pid || !allowed(nb)) continue;
+						inq[nb] = pid;
+						queue.push_back(nb);
+					}
+				}
+				Lo.patch_cell.push_back(static_cast<int>(order.size()));
+				pid++;
+			}
+		}
+		Lo.perm = order;
+		for(int i = 0; i < N; i++) Lo.iperm[Lo.perm[i]] = i;
+	} else {
 		int pid = 0, cs = 0, cc = 0;
 		for(int c = 0; c < N; c++) {
 			const int ref = Lo.perm[c];
