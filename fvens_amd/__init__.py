@@ -387,9 +387,7 @@ class FlowFV:
     def layout_stats(self):
         s = (ctypes.c_longlong * 12)()
         check(_ffi.lib().fvhip_layout_stats(self._h, s))
-        keys = ("cells", "faces", "slots", "patches", "max_slots", "bfaces", "ghosts", "neighbours", "send_rows",
-                "interior_patches", "ring1_cells", "patches_over_block")
-        return dict(zip(keys, [int(x) for x in s]))
+        return dict(zip(LAYOUT_KEYS[:12], [int(x) for x in s]))
 
     def close(self):
         if getattr(self, "_h", None):
@@ -465,6 +463,21 @@ def partition_info(mesh, part, rank):
                                           iptr(nbr), iptr(gs), iptr(ss), iptr(sg)))
     return dict(owned=nown, ghosts=ngh, bfaces=nb, faces=nf, cell_global=cg, nbr_rank=nbr[:nnbr],
                 ghost_start=gs, send_start=ss, send_global=sg[:nsend])
+
+
+LAYOUT_KEYS = ("cells", "faces", "slots", "patches", "max_slots", "bfaces", "ghosts", "neighbours", "send_rows",
+               "interior_patches", "ring1_cells", "patches_over_block", "ring2_cells", "max_staged_cells",
+               "slots_per_patch")
+
+
+def layout_probe(mesh, pconf, nconf):
+    """Layout statistics of the device layout a FlowFV would build, computed on the host only
+    (fvhip_layout_probe; no device needed)"""
+    cfg, keep = _config_struct(pconf, nconf)
+    s = (ctypes.c_longlong * 16)()
+    check(_ffi.lib().fvhip_layout_probe(ctypes.byref(mesh.view), ctypes.byref(cfg), s))
+    del keep
+    return dict(zip(LAYOUT_KEYS, [int(x) for x in s]))
 
 
 class FlowFVGroup:

@@ -9,7 +9,8 @@ import os
 import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libfvhip.so")
+# FVHIP_LIB selects another build of the library (experiments only); default: the in-tree build
+LIB_PATH = os.environ.get("FVHIP_LIB") or os.path.join(_HERE, "libfvhip.so")
 
 c_int_p = ctypes.POINTER(ctypes.c_int)
 c_dbl_p = ctypes.POINTER(ctypes.c_double)
@@ -114,6 +115,8 @@ _SIGS = {
     "fvhip_kernel_times": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_char_p, ctypes.c_int,
                                           c_dbl_p, c_int_p]),
     "fvhip_layout_stats": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(ctypes.c_longlong)]),
+    "fvhip_layout_probe": (ctypes.c_int, [ctypes.POINTER(FvMeshView), ctypes.POINTER(FvFlowConfig),
+                                          ctypes.POINTER(ctypes.c_longlong)]),
     "fvhip_local_flux": (ctypes.c_int, [ctypes.c_int, c_dbl_p, ctypes.c_int, c_dbl_p, c_dbl_p, c_dbl_p, c_dbl_p]),
     "fvhip_local_flux_jacobian": (ctypes.c_int, [ctypes.c_int, c_dbl_p, ctypes.c_int, c_dbl_p, c_dbl_p, c_dbl_p,
                                                  c_dbl_p, c_dbl_p]),
@@ -145,6 +148,8 @@ def lib():
             raise RuntimeError(f"{LIB_PATH} is missing; build it with __graft_entry__.build()")
         L = ctypes.CDLL(LIB_PATH)
         for name, (res, args) in _SIGS.items():
+            if os.environ.get("FVHIP_LIB") and not hasattr(L, name):
+                continue      # an older experiment build may lack newer entry points
             f = getattr(L, name)
             f.restype = res
             f.argtypes = args

@@ -103,6 +103,8 @@ static fvhip_ctx* createCtx(const MeshTopo& T, const fvhip_flow_config* cfg, int
 	if(!L.fz_ext_start.empty()) {
 		M.fz_ext_start = upload(L.fz_ext_start, o);
 		M.fz_ext = upload(L.fz_ext, o);
+		M.fz_n1 = upload(L.fz_n1, o);
+		M.fz_g_start = upload(L.fz_g_start, o);
 		M.fz_gnbr = reinterpret_cast<const int4*>(upload(L.fz_gnbr, o));
 		M.fz_slot_lr = reinterpret_cast<const int2*>(upload(L.fz_slot_lr, o));
 		M.fz_max_cells = L.fz_max_cells;
@@ -574,24 +576,41 @@ int fvhip_kernel_times(fvhip_handle h, int maxk, char* names, int namelen, doubl
 	return rc ? -1 : n;
 }
 
+/// layout statistics (include/fvhip.h fvhip_layout_stats / fvhip_layout_probe), n entries
+static void layoutStats(const Layout& L, long long* s, int n)
+{
+	long long v[16] = {};
+	v[0] = L.ncell; v[1] = L.naface; v[2] = static_cast<long long>(L.slot_L.size());
+	v[3] = static_cast<long long>(L.patch_cell.size()) - 1; v[4] = L.max_slots; v[5] = L.nbface;
+	v[6] = L.nghost; v[7] = static_cast<long long>(L.nbr_rank.size()); v[8] = static_cast<long long>(L.send_cells.size());
+	v[9] = L.fz_ninner;
+	// fused residual staging: ring-1 cells over all patches; patches staging more cells than a
+	// block has threads (their staging takes two rounds); ring-2 cells; most rows one patch stages
+	v[10] = static_cast<long long>(L.fz_ext.size()) - L.fz_ring2;
+	const long long np = static_cast<long long>(L.patch_cell.size()) - 1;
+	if(!L.fz_ext_start.empty())
+		for(long long p = 0; p < np; p++) {
+			const long long nl = (L.patch_cell[p+1] - L.patch_cell[p]) + (L.fz_ext_start[p+1] - L.fz_ext_start[p]);
+			if(nl > SLOTS_MAX) v[11]++;
+		}
+	v[12] = L.fz_ring2;
+	v[13] = L.fz_max_cells;
+	v[14] = SLOTS_MAX;
+	for(int i = 0; i < n && i < 16; i++) s[i] = v[i];
+}
+
 int fvhip_layout_stats(fvhip_handle h, long long* s)
 {
+	return guard([&] { layoutStats(h->L, s, 12); });
+}
+
+int fvhip_layout_probe(const fvhip_mesh* mesh, const fvhip_flow_config* cfg, long long* s)
+{
 	return guard([&] {
-		s[0] = h->L.ncell; s[1] = h->L.naface; s[2] = static_cast<long long>(h->L.slot_L.size());
-		s[3] = static_cast<long long>(h->L.patch_cell.size()) - 1; s[4] = h->L.max_slots; s[5] = h->L.nbface;
-		s[6] = h->L.nghost; s[7] = static_cast<long long>(h->L.nbr_rank.size()); s[8] = h->nsend;
-		s[9] = h->L.fz_ninner;
-		// fused residual staging: ring-1 cells over all patches; patches staging more cells than a
-		// block has threads (their gradient phase takes two rounds)
-		s[10] = static_cast<long long>(h->L.fz_ext.size());
-		long long over = 0;
-		const long long np = static_cast<long long>(h->L.patch_cell.size()) - 1;
-		if(!h->L.fz_ext_start.empty())
-			for(long long p = 0; p < np; p++) {
-				const long long nl = (h->L.patch_cell[p+1] - h->L.patch_cell[p]) + (h->L.fz_ext_start[p+1] - h->L.fz_ext_start[p]);
-				if(nl > SLOTS_MAX) over++;
-			}
-		s[11] = over;
+		if(!mesh || !cfg || !s) throw std::invalid_argument("null argument");
+		checkConfig(cfg);
+		const Layout L = buildLayout(topoFromMesh(*mesh), *cfg, true);
+		layoutStats(L, s, 16);
 	});
 }
 

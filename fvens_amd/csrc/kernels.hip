@@ -757,6 +757,67 @@ __device__ __forceinline__ double4 ghost_prim_of_cell(const DevMesh& M, const De
 	return make_double4(gp[0], gp[1], gp[2], gp[3]);
 }
 
+/// phase 0 of the fused residual: a staged row [up 4][gradient 8][rc 2] from the conserved state
+__device__ __forceinline__ void stage_row(const Gas& G, double* row, const double* ucons, double2 r)
+{
+	double b[4];
+	cons2prim(G, ucons, b);
+	st4(row, 0, b);
+	*reinterpret_cast<double2*>(row + 12) = r;
+}
+
+/// phase 1 of the fused residual: WLS gradient of staged row `row` (cell c) from the staged rows of
+/// its neighbours nb4 (patch-local indices, boundary codes -2-bf, -1 padding), k_prep_grad_wls
+/// arithmetic; a ghost cell takes the gradient received from its owner
+__device__ __forceinline__ void fused_wls_row(const DevMesh& M, const DevPhys& P, const SweepBuffers& B,
+                                              const double* fz, double* row, int c, int4 nb4, double4 V)
+{
+	if(c >= M.nown) {
+		double g[8];
+		ld8(B.grad, c, g);
+		st8(row + 4, 0, g);
+		return;
+	}
+	double uc[4];
+	ld4(row, 0, uc);
+	const double2 rcc = *reinterpret_cast<const double2*>(row + 12);
+	const int nb[4] = {nb4.x, nb4.y, nb4.z, nb4.w};
+	double f[8] = {0,0,0,0,0,0,0,0};
+	#pragma unroll
+	for(int k = 0; k < 4; k++) {
+		if(nb[k] == -1) break;
+		double un[4];
+		double2 rn;
+		if(nb[k] >= 0) {
+			ld4(&fz[nb[k]*FZW], 0, un);
+			rn = *reinterpret_cast<const double2*>(&fz[nb[k]*FZW + 12]);
+		} else {
+			const int bf = -2 - nb[k];
+			const double4 gp = ghost_prim_of_cell(M, P, B.u, c, bf);
+			un[0] = gp.x; un[1] = gp.y; un[2] = gp.z; un[3] = gp.w;
+			rn = M.bf_rcbp[bf];
+		}
+		double w2 = 0;
+		w2 += (rcc.x-rn.x)*(rcc.x-rn.x);
+		w2 += (rcc.y-rn.y)*(rcc.y-rn.y);
+		const double dr0 = rcc.x-rn.x, dr1 = rcc.y-rn.y;
+		w2 = div_rn(1.0, w2);
+		#pragma unroll
+		for(int iv = 0; iv < 4; iv++) {
+			const double du = uc[iv] - un[iv];
+			f[iv*2+0] += w2*dr0*du;
+			f[iv*2+1] += w2*dr1*du;
+		}
+	}
+	double g[8];
+	#pragma unroll
+	for(int iv = 0; iv < 4; iv++) {
+		g[iv*2+0] = V.x*f[iv*2+0] + V.y*f[iv*2+1];
+		g[iv*2+1] = V.z*f[iv*2+0] + V.w*f[iv*2+1];
+	}
+	st8(row + 4, 0, g);
+}
+
 template <int FLUX, int REC, bool DT>
 __global__ void __launch_bounds__(SLOTS_MAX, 4) k_residual_wls(const DevMesh M, const DevPhys P, const SweepBuffers B)
 {
@@ -770,104 +831,57 @@ __global__ void __launch_bounds__(SLOTS_MAX, 4) k_residual_wls(const DevMesh M, 
 	const int c0 = M.patch_cell[p], c1 = M.patch_cell[p+1];
 	const int nc = c1 - c0;
 	const int e0 = M.fz_ext_start[p];
-	const int nl = nc + (M.fz_ext_start[p+1] - e0);
-	const int4* gnbr = M.fz_gnbr + (c0 + e0);
+	const int nl = nc + (M.fz_ext_start[p+1] - e0);    // staged rows: patch, ring 1, ring 2
+	const int ng = nc + M.fz_n1[p];                      // rows whose gradients the patch computes
+	const int4* gnbr = M.fz_gnbr + M.fz_g_start[p];
 	const int N = M.ncell;
 	const Gas& G = P.gas;
 	const int t = static_cast<int>(threadIdx.x);
 	auto cellOf = [&](int i) { return i < nc ? c0 + i : M.fz_ext[e0 + (i - nc)]; };
 
-	// phase 0: primitive states and centres of the patch and ring-1 cells
-	for(int i = t; i < nl; i += SLOTS_MAX) {
+	// Every load of the patch is issued up front, so the patch waits for one memory round trip:
+	// this thread's first staged row (state, centre), the neighbour list and WLS inverse of the
+	// gradient it computes first, and the geometry of its face (all cells a patch reads are staged)
+	const int s = s0 + t;
+	const int cf = t < nl ? cellOf(t) : 0;
+	double ua[4] = {0, 0, 0, 0};
+	double2 rca = make_double2(0, 0);
+	int4 nb4a = make_int4(-1, -1, -1, -1);
+	double4 Va = make_double4(0, 0, 0, 0);
+	if(t < nl) {
+		ld4(B.u, cf, ua);
+		rca = M.rc[cf];
+		if(t < ng && cf < M.nown) { nb4a = gnbr[t]; Va = M.wls_V[cf]; }
+	}
+	int2 lrl = make_int2(0, -1);
+	double2 nn = make_double2(0, 0);
+	double len = 0;
+	if(s < s1) { lrl = M.fz_slot_lr[s]; nn = M.slot_n[s]; len = M.slot_len[s]; }
+
+	// phase 0: primitive states and centres of the staged cells
+	if(t < nl) stage_row(G, &fz[t*FZW], ua, rca);
+	for(int i = t + SLOTS_MAX; i < nl; i += SLOTS_MAX) {
 		const int c = cellOf(i);
-		double a[4], b[4];
+		double a[4];
 		ld4(B.u, c, a);
-		cons2prim(G, a, b);
-		double* row = &fz[i*FZW];
-		st4(row, 0, b);
-		*reinterpret_cast<double2*>(row + 12) = M.rc[c];
+		stage_row(G, &fz[i*FZW], a, M.rc[c]);
 	}
 	__syncthreads();
 
-	// phase 1: WLS gradients of the staged cells (k_prep_grad_wls arithmetic; each neighbour's
-	// contribution is accumulated as soon as it is read, in the same order)
-	for(int i = t; i < nl; i += SLOTS_MAX) {
+	// phase 1: WLS gradients of the patch and ring-1 cells from the staged states
+	// (k_prep_grad_wls arithmetic, neighbours in the same ascending reference face order)
+	if(t < ng) fused_wls_row(M, P, B, fz, &fz[t*FZW], cf, nb4a, Va);
+	for(int i = t + SLOTS_MAX; i < ng; i += SLOTS_MAX) {
 		const int c = cellOf(i);
-		double* row = &fz[i*FZW];
-		if(c >= M.nown) {                       // ghost cell: gradient received from its owner
-			double g[8];
-			ld8(B.grad, c, g);
-			st8(row + 4, 0, g);
-			continue;
-		}
-		double uc[4];
-		ld4(row, 0, uc);
-		const double2 rcc = *reinterpret_cast<const double2*>(row + 12);
-		const int4 nb4 = gnbr[i];
-		const int nb[4] = {nb4.x, nb4.y, nb4.z, nb4.w};
-		// gather first: the global (ring-2) states of all neighbours are requested before any is
-		// used, so a ring-1 cell waits for one memory round trip instead of one per neighbour
-		double un[4][4];
-		double2 rn[4];
-		#pragma unroll
-		for(int k = 0; k < 4; k++) {
-			if(nb[k] >= FUSED_GLOBAL) {
-				const int g = nb[k] - FUSED_GLOBAL;
-				ld4(B.u, g, un[k]);
-				rn[k] = M.rc[g];
-			}
-		}
-		#pragma unroll
-		for(int k = 0; k < 4; k++) {
-			if(nb[k] == -1) continue;
-			if(nb[k] >= 0 && nb[k] < FUSED_GLOBAL) {
-				ld4(&fz[nb[k]*FZW], 0, un[k]);
-				rn[k] = *reinterpret_cast<const double2*>(&fz[nb[k]*FZW + 12]);
-			} else if(nb[k] >= FUSED_GLOBAL) {
-				double t4[4] = {un[k][0], un[k][1], un[k][2], un[k][3]};
-				cons2prim(G, t4, un[k]);
-			} else {
-				const int bf = -2 - nb[k];
-				const double4 gp = ghost_prim_of_cell(M, P, B.u, c, bf);
-				un[k][0] = gp.x; un[k][1] = gp.y; un[k][2] = gp.z; un[k][3] = gp.w;
-				rn[k] = M.bf_rcbp[bf];
-			}
-		}
-		double f[8] = {0,0,0,0,0,0,0,0};
-		#pragma unroll
-		for(int k = 0; k < 4; k++) {
-			if(nb[k] == -1) break;
-			double w2 = 0;
-			w2 += (rcc.x-rn[k].x)*(rcc.x-rn[k].x);
-			w2 += (rcc.y-rn[k].y)*(rcc.y-rn[k].y);
-			const double dr0 = rcc.x-rn[k].x, dr1 = rcc.y-rn[k].y;
-			w2 = div_rn(1.0, w2);
-			#pragma unroll
-			for(int iv = 0; iv < 4; iv++) {
-				const double du = uc[iv] - un[k][iv];
-				f[iv*2+0] += w2*dr0*du;
-				f[iv*2+1] += w2*dr1*du;
-			}
-		}
-		const double4 V = M.wls_V[c];
-		double g[8];
-		#pragma unroll
-		for(int iv = 0; iv < 4; iv++) {
-			g[iv*2+0] = V.x*f[iv*2+0] + V.y*f[iv*2+1];
-			g[iv*2+1] = V.z*f[iv*2+0] + V.w*f[iv*2+1];
-		}
-		st8(row + 4, 0, g);
+		fused_wls_row(M, P, B, fz, &fz[i*FZW], c, c < M.nown ? gnbr[i] : make_int4(-1, -1, -1, -1),
+		              c < M.nown ? M.wls_V[c] : make_double4(0, 0, 0, 0));
 	}
 	__syncthreads();
 
 	// phase 2: one face per thread (k_sweep arithmetic)
-	const int s = s0 + t;
 	double f[4] = {0, 0, 0, 0};
 	double sri = 0, srj = 0;
 	if(s < s1) {
-		const int2 lrl = M.fz_slot_lr[s];
-		const double2 nn = M.slot_n[s];
-		const double len = M.slot_len[s];
 		const double n[2] = {nn.x, nn.y};
 		const bool bnd = lrl.y < -1;
 		const int bf = -2 - lrl.y;

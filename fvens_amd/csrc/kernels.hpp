@@ -41,8 +41,10 @@ struct DevMesh
 	const double2* bf_rcbp;    // [nb]
 	// fused residual (layout.hpp fz_*)
 	const int* fz_ext_start;   // [npatch+1]
-	const int* fz_ext;         // ring-1 cells
-	const int4* fz_gnbr;       // neighbour codes of staged cells
+	const int* fz_ext;         // ring-1 then ring-2 cells
+	const int* fz_n1;          // [npatch] ring-1 count
+	const int* fz_g_start;     // [npatch+1] first fz_gnbr row of each patch
+	const int4* fz_gnbr;       // neighbour codes of the cells whose gradients a patch computes
 	const int2* fz_slot_lr;    // [S] patch-local L, R
 	int fz_max_cells;
 };

@@ -166,14 +166,14 @@ Layout buildLayout(const MeshTopo& T, const fvhip_flow_config& cfg, bool renumbe
 		}
 		Lo.patch_cell.push_back(N);
 	}
-	// fused residual path: also cap the patch cells + ring-1 cells the patch stages in LDS
+	// fused residual path: also cap the patch cells + ring-1 + ring-2 cells the patch stages in LDS
 	const bool fused = fusedEligible(cfg);
 	if(fused) {
-		std::vector<int> ranges, mark2(NT, -1);
+		std::vector<int> ranges, mark2(NT, -1), r1;
 		int stamp = 0;
 		auto ring1 = [&](int c0, int c1) {
 			stamp++;
-			int n1 = 0;
+			r1.clear();
 			for(int c = c0; c < c1; c++) {
 				const int ref = Lo.perm[c];
 				for(int j = 0; j < nf(ref); j++) {
@@ -181,10 +181,22 @@ Layout buildLayout(const MeshTopo& T, const fvhip_flow_config& cfg, bool renumbe
 					if(nb < 0 || nb >= NT) continue;          // boundary face
 					const int ci = toInt(nb);
 					if(ci >= c0 && ci < c1) continue;
-					if(mark2[ci] != stamp) { mark2[ci] = stamp; n1++; }
+					if(mark2[ci] != stamp) { mark2[ci] = stamp; r1.push_back(ci); }
 				}
 			}
-			return n1;
+			int n2 = 0;                                       // ring 2: through owned ring-1 cells
+			for(const int ci : r1) {
+				if(ci >= N) continue;
+				const int ref = Lo.perm[ci];
+				for(int j = 0; j < nf(ref); j++) {
+					const int nb = esu(ref, j);
+					if(nb < 0 || nb >= NT) continue;
+					const int cj = toInt(nb);
+					if((cj >= c0 && cj < c1) || mark2[cj] == stamp) continue;
+					mark2[cj] = stamp; n2++;
+				}
+			}
+			return static_cast<int>(r1.size()) + n2;
 		};
 		std::vector<std::pair<int,int>> stack;
 		for(size_t k = 0; k + 1 < Lo.patch_cell.size(); k++) {
@@ -419,9 +431,11 @@ void buildFused(Layout& Lo)
 	const int N = Lo.ncell + Lo.nghost;      // ghost cells may be ring-1 cells (their gradients are received)
 	const int npatch = static_cast<int>(Lo.patch_cell.size()) - 1;
 	Lo.fz_ext_start.assign(1, 0); Lo.fz_ext.clear(); Lo.fz_n1.assign(npatch, 0);
+	Lo.fz_g_start.assign(1, 0);
 	Lo.fz_gnbr.clear();
 	Lo.fz_slot_lr.assign(2*Lo.slot_L.size(), -1);
 	Lo.fz_max_cells = 0;
+	Lo.fz_ring2 = 0;
 	std::vector<int> lidx(N, -1);          // patch-local index of a cell while its patch is built
 	std::vector<char> innerp(npatch, 0);
 	for(int p = 0; p < npatch; p++) {
@@ -429,38 +443,45 @@ void buildFused(Layout& Lo)
 		const size_t e0 = Lo.fz_ext.size();
 		for(int c = c0; c < c1; c++) lidx[c] = c - c0;
 		int nl = nc;
-		// ring 1: the other side of the patch's cut faces
 		auto add = [&](int c) {
 			if(c < 0 || c >= N || lidx[c] >= 0) return;
 			lidx[c] = nl++; Lo.fz_ext.push_back(c);
 		};
+		// ring 1: the other side of the patch's cut faces
 		for(int s = Lo.patch_slot[p]; s < Lo.patch_slot[p+1]; s++) { add(Lo.slot_L[s]); add(Lo.slot_R[s]); }
+		const int ng = nl;
+		// ring 2: the other neighbours of the owned ring-1 cells (their gradients read them)
+		for(int i = nc; i < ng; i++) {
+			const int c = Lo.fz_ext[e0 + (i - nc)];
+			if(c >= Lo.ncell) continue;
+			for(int j = 0; j < MAXF; j++) add(Lo.cell_nbr_fo[static_cast<size_t>(c)*MAXF+j]);
+		}
 		if(nl > FUSED_LDS_CELLS) throw std::logic_error("fused residual: patch exceeds its LDS budget");
-		Lo.fz_n1[p] = nl - nc;
+		Lo.fz_n1[p] = ng - nc;
+		Lo.fz_ring2 += nl - ng;
 		Lo.fz_ext_start.push_back(static_cast<int>(Lo.fz_ext.size()));
-		// neighbours of every staged cell, in the cell's ascending reference face order
+		// neighbours of every cell whose gradient the patch computes, in ascending reference face order
 		auto code = [&](int nb) {
 			if(nb < 0) return -1;
 			if(nb >= N) return -2 - (nb - N);
-			return lidx[nb] >= 0 ? lidx[nb] : FUSED_GLOBAL + nb;
+			if(lidx[nb] < 0) throw std::logic_error("fused residual: neighbour not staged");
+			return lidx[nb];
 		};
-		for(int i = 0; i < nl; i++) {
+		for(int i = 0; i < ng; i++) {
 			const int c = i < nc ? c0 + i : Lo.fz_ext[e0 + (i - nc)];
 			for(int j = 0; j < MAXF; j++)     // ghost cells: gradient received, no neighbour list
 				Lo.fz_gnbr.push_back(c < Lo.ncell ? code(Lo.cell_nbr_fo[static_cast<size_t>(c)*MAXF+j]) : -1);
 		}
+		Lo.fz_g_start.push_back(Lo.fz_g_start.back() + ng);
 		for(int s = Lo.patch_slot[p]; s < Lo.patch_slot[p+1]; s++) {
 			Lo.fz_slot_lr[2*static_cast<size_t>(s)] = code(Lo.slot_L[s]);
 			Lo.fz_slot_lr[2*static_cast<size_t>(s)+1] = code(Lo.slot_R[s]);
 		}
 		Lo.fz_max_cells = std::max(Lo.fz_max_cells, nl);
-		// interior patch: stages no ghost cell and reads none from global memory, so it needs no
-		// halo data and can run while the exchange is in flight
+		// interior patch: stages no ghost cell, so it needs no halo data and can run while the
+		// exchange is in flight
 		bool inner = true;
 		for(size_t k = e0; k < Lo.fz_ext.size(); k++) if(Lo.fz_ext[k] >= Lo.ncell) inner = false;
-		const size_t g0 = 4*(static_cast<size_t>(c0) + e0);
-		for(size_t k = g0; k < Lo.fz_gnbr.size(); k++)
-			if(Lo.fz_gnbr[k] >= FUSED_GLOBAL && Lo.fz_gnbr[k] - FUSED_GLOBAL >= Lo.ncell) inner = false;
 		innerp[p] = inner ? 1 : 0;
 		for(int c = c0; c < c1; c++) lidx[c] = -1;
 		for(size_t k = e0; k < Lo.fz_ext.size(); k++) lidx[Lo.fz_ext[k]] = -1;

@@ -18,8 +18,14 @@
 
 namespace fvhip {
 
-constexpr int SLOTS_MAX = 512;   ///< faces per patch = threads per sweep workgroup
-constexpr int CELLS_MAX = 512;
+#ifndef FVHIP_SLOTS
+#define FVHIP_SLOTS 512
+#endif
+#ifndef FVHIP_FUSED_ROWS
+#define FVHIP_FUSED_ROWS (FVHIP_SLOTS*11/8)   // 704 x 112 B = 77 KB for 512-slot patches (2 blocks/CU)
+#endif
+constexpr int SLOTS_MAX = FVHIP_SLOTS;   ///< faces per patch = threads per sweep workgroup
+constexpr int CELLS_MAX = FVHIP_SLOTS;
 constexpr int MAXF = 4;          ///< max faces per cell (linear tri/quad)
 
 struct Layout
@@ -73,15 +79,19 @@ struct Layout
 	std::vector<int> border_cells;         ///< unique send cells (their gradients are computed first)
 	std::vector<int> cell_global;          ///< [ncell+nghost] global cell of each internal cell
 	// fused residual (k_residual_wls): per patch, the ring-1 cells (far side of its cut faces) whose
-	// primitive states and gradients it recomputes; patch-local index = [patch cells | ring 1]
+	// primitive states and gradients it recomputes, and the ring-2 cells (the other neighbours of the
+	// owned ring-1 cells) whose primitive states those gradients read; every cell a patch reads is
+	// staged in LDS by one round of loads. Patch-local index = [patch cells | ring 1 | ring 2]
 	std::vector<int> fz_ext_start;         ///< [npatch+1]
-	std::vector<int> fz_ext;               ///< ring-1 cells (internal ids)
+	std::vector<int> fz_ext;               ///< ring-1 then ring-2 cells of each patch (internal ids)
 	std::vector<int> fz_n1;                ///< [npatch] ring-1 count
+	std::vector<int> fz_g_start;           ///< [npatch+1] row offset of each patch's fz_gnbr rows
 	std::vector<int> fz_gnbr;              ///< per patch [patch cells + ring 1][4]: neighbours in
-	                                       ///<  ascending reference face order: local index (< FUSED_GLOBAL),
-	                                       ///<  FUSED_GLOBAL + internal id (read from global memory),
-	                                       ///<  -2-bf (boundary face), -1 (none); row offset = 4*(c0 + ext_start)
+	                                       ///<  ascending reference face order: patch-local index,
+	                                       ///<  -2-bf (boundary face), -1 (none; also every entry of a
+	                                       ///<  ghost ring-1 cell, whose gradient is received)
 	std::vector<int> fz_slot_lr;           ///< [S][2] local L, R (R boundary: -2-bf)
+	int fz_ring2 = 0;                      ///< ring-2 cells staged over all patches
 	int fz_max_cells = 0;
 	std::vector<int> fz_order;             ///< patches needing no halo data first (fz_ninner), then the rest
 	int fz_ninner = 0;
@@ -93,9 +103,8 @@ struct Layout
 	std::vector<int> pipe_group_start;     ///< [K+1] ranges into pipe_patch
 };
 
-constexpr int FUSED_LDS_CELLS = 704;     ///< staged cells per patch: 704 x 112 B = 77 KB (2 blocks/CU)
+constexpr int FUSED_LDS_CELLS = FVHIP_FUSED_ROWS;   ///< staged cells per patch (rows of 112 B)
 constexpr int PIPE_CHUNKS = 8;          ///< gradient chunks of the pipelined staged residual
-constexpr int FUSED_GLOBAL = 1 << 20;    ///< neighbour codes >= this are global internal ids + FUSED_GLOBAL
 
 /// whether cfg takes the fused residual kernel (WLS + MUSCL/unlimited linear, inviscid). On a
 /// partitioned mesh, ghost cells in a patch's ring 1 take their received gradients.

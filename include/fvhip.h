@@ -277,6 +277,11 @@ int fvhip_kernel_times(fvhip_handle h, int maxk, char* names, int namelen, doubl
  *  [10]=ring-1 cells staged by the fused residual over all patches [11]=patches staging more cells
  *  than a block has threads */
 int fvhip_layout_stats(fvhip_handle h, long long* stats);
+/** The same statistics for a mesh and configuration without a device (host only: builds the layout
+ *  fvhip_create would upload). stats[16]: [0..11] as fvhip_layout_stats, [12]=ring-2 cells staged by
+ *  the fused residual over all patches, [13]=most cells one patch stages, [14]=faces per patch
+ *  (threads per face-sweep block), [15]=0 */
+int fvhip_layout_probe(const fvhip_mesh* mesh, const fvhip_flow_config* cfg, long long* stats);
 
 /** Point-wise numerical flux on the device (get_flux) for nf faces: ul, ur [nf][4], n [nf][2] */
 int fvhip_local_flux(int flux_type, const double* gas5, int nf, const double* ul, const double* ur,
