@@ -37,9 +37,14 @@ def c4_mesh(fa, scale, mult=1):
 
 def sweep_algorithmic_bytes(N, F, Fb):
     """32 B/face (L,R 8 + nx,ny,len 24) + 144 B/cell (prim 32 + grad 64 + centre 16
-    + residual write 32) + 48 B/boundary face (ghost centre 16 + ghost state 32) + 16 B/cell for the
-    time step (area read 8 + dtm write 8)."""
-    return 32 * F + 144 * N + 48 * Fb + 16 * N
+    + residual write 32) + 48 B/boundary face (ghost centre 16 + ghost state 32) + 8 B/cell for the
+    time-step accumulation ("Time-step accumulation adds 8 B/cell")"""
+    return 32 * F + 144 * N + 48 * Fb + 8 * N
+
+
+def sweep_bytes_area_dt(N, F, Fb):
+    """variant basis: the time step counted as area read 8 + dtm write 8 = 16 B/cell"""
+    return sweep_algorithmic_bytes(N, F, Fb) + 8 * N
 
 
 def residual_algorithmic_bytes(N, F, Fb):
@@ -107,6 +112,83 @@ def valu_roofline(valu_wave_instrs, kernel_ms):
             "unit": "T lane-ops/s", "frac": round(a / FP64_LANE_OPS, 4), "valu_wave_instrs": int(valu_wave_instrs)}
 
 
+def host_cpu_info():
+    """the cores this job may use: affinity CPUs / threads per core, capped by the cgroup CPU quota;
+    lscpu model name (all physical cores, OMP_PROC_BIND=close OMP_PLACES=cores)"""
+    import subprocess
+    info = {}
+    try:
+        out = subprocess.run(["lscpu"], capture_output=True, text=True, timeout=20).stdout
+        for line in out.splitlines():
+            k, _, v = line.partition(":")
+            info[k.strip()] = v.strip()
+    except Exception:
+        pass
+    aff = len(os.sched_getaffinity(0))
+    tpc = int(info.get("Thread(s) per core", "1") or 1)
+    quota = None
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()
+        if q != "max":
+            quota = int(q) // int(per)
+    except Exception:
+        pass
+    cores = max(1, aff // max(tpc, 1))
+    if quota:
+        cores = min(cores, quota)
+    return {"model": info.get("Model name"), "sockets": info.get("Socket(s)"),
+            "cores_per_socket": info.get("Core(s) per socket"), "threads_per_core": tpc,
+            "affinity_cpus": aff, "cgroup_cpu_quota": quota, "physical_cores_used": cores}
+
+
+def cpu_baseline(mesh, u, nrep):
+    """BASELINE.md's CPU baseline: the oracle's OpenMP restatement (the reference's omp parallel for /
+    omp atomic structure) on this host's physical cores, in a child process so that OMP_PROC_BIND /
+    OMP_PLACES take effect (torch has already loaded the OpenMP runtime here); median of `nrep` sweeps
+    after 3 warm-ups on all cores, and on 1 thread"""
+    import subprocess
+    import tempfile
+    hw = host_cpu_info()
+    nt = int(os.environ.get("FVHIP_CPU_THREADS", "0")) or hw["physical_cores_used"]
+    raw = mesh.raw()
+    fd, path = tempfile.mkstemp(suffix=".npz", dir="/tmp")
+    os.close(fd)
+    try:
+        np.savez(path, u=np.ascontiguousarray(u), **{k: np.asarray(v) for k, v in raw.items()})
+        res = {}
+        for threads, reps in ((nt, nrep), (1, max(3, nrep // 4))):
+            env = dict(os.environ, OMP_NUM_THREADS=str(threads), OMP_PROC_BIND="close", OMP_PLACES="cores")
+            out = subprocess.run([sys.executable, os.path.abspath(__file__), "--cpu-child", path, str(threads),
+                                  str(reps)], env=env, capture_output=True, text=True, timeout=900)
+            if out.returncode != 0:
+                raise RuntimeError("cpu baseline child failed: " + out.stderr[-2000:])
+            res[threads] = json.loads(out.stdout.strip().splitlines()[-1])
+    finally:
+        os.unlink(path)
+    F = mesh.naface
+    med_n, med_1 = res[nt]["median_s"], res[1]["median_s"]
+    return {"value": F / med_n / 1e6, "unit": "Mfaces/s", "cores": nt, "kind": "port",
+            "value_1_core": F / med_1 / 1e6, "host": hw,
+            "sample": f"full second-order residual sweeps of the same {mesh.nelem}-cell mesh and state by the C++ "
+                      f"restatement with the reference's omp parallel for / omp atomic structure (oracle/, -O2 "
+                      f"-fopenmp, no FMA), OMP_PROC_BIND=close OMP_PLACES=cores: median of {nrep} sweeps after 3 "
+                      f"warm-ups on {nt} threads = {med_n:.4f} s; median of {res[1]['nrep']} on 1 thread = "
+                      f"{med_1:.3f} s"}
+
+
+def cpu_child(path, threads, nrep):
+    """child of cpu_baseline: builds the oracle from the saved mesh and times it (prints one JSON line)"""
+    import _oracle as orc
+    import cases
+    d = np.load(path)
+    raw = {k: (int(d[k]) if d[k].ndim == 0 else d[k]) for k in d.files if k != "u"}
+    om = orc.OracleMesh.from_raw(raw)
+    ref = orc.OracleSpatial(om, cases.physics("naca"), cases.numerics("ROE", "LEASTSQUARES", "VANALBADA"))
+    med, times = ref.time_residual(np.ascontiguousarray(d["u"]), nrep, True, threads=threads, nwarm=3)
+    print(json.dumps({"median_s": med, "nrep": nrep, "threads": threads, "min_s": float(times.min()),
+                      "max_s": float(times.max())}))
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -114,7 +196,7 @@ def main():
     ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--scale", type=int, default=1, help="divide the C4 mesh dimensions (debug)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-sweeps", type=int, default=3)
+    ap.add_argument("--cpu-sweeps", type=int, default=20, help="timed CPU-baseline sweeps (median)")
     ap.add_argument("--no-fast", action="store_true", help="skip the fast-math mode measurement")
     ap.add_argument("--scaling", choices=["weak", "strong"], default="weak")
     ap.add_argument("--no-pipelined", action="store_true", help="skip the pipelined staged path")
@@ -267,20 +349,7 @@ def main():
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        import _oracle as orc
-        om = orc.OracleMesh.from_raw(mesh.raw())
-        ref = orc.OracleSpatial(om, p, n)
-        uu = np.ascontiguousarray(u)
-        nt = int(os.environ.get("OMP_NUM_THREADS", "0")) or min(16, os.cpu_count() or 1)
-        secs1 = ref.time_residual(uu, args.cpu_sweeps, True, threads=1)
-        secsn = ref.time_residual(uu, 4 * args.cpu_sweeps, True, threads=nt) if nt > 1 else secs1
-        cpu = {"value": F / secsn / 1e6, "unit": "Mfaces/s", "cores": nt, "kind": "port",
-               "value_1_core": F / secs1 / 1e6,
-               "sample": f"full second-order residual sweeps (+1 warm-up) of the same {N}-cell mesh and state by "
-                         f"the C++ restatement with the reference's omp parallel for / omp atomic structure "
-                         f"(oracle/, -O2 -fopenmp, no FMA): {4 * args.cpu_sweeps} sweeps on {nt} threads, "
-                         f"{secsn:.4f} s per sweep; {args.cpu_sweeps} sweeps on 1 thread, {secs1:.3f} s per sweep"}
-        del ref, om
+        cpu = cpu_baseline(mesh, u, args.cpu_sweeps)
 
     if rank == 0:
         # template of the timed sweep: k_sweep<FLUX=ROE(4), REC=MUSCL(1), VISC=none(0), DT, no PHI>
@@ -304,13 +373,17 @@ def main():
                        "parallelism": (f"RCB {world}-way partition, RCCL p2p halo (u + gradients)"
                                        if world > 1 else "single GPU"),
                        "layout": stats, "setup_s": round(t_setup, 2)},
-            "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "roofline": {"bound": "hbm",
+                         "limiter": "FP64 VALU issue and barrier latency between the kernel's phases, not HBM "
+                                    "bandwidth (PMC: valu_roofline below; DESIGN.md section 5)", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 4),
                          "traffic": int(tr[0]) if tr else None,
                          "traffic_source": tr[1] if tr else None,
                          "kernel": sweep_name[0] if sweep_name else None,
                          "kernel_ms": round(sweep_ms, 5), "algorithmic_bytes": ab,
-                         "bytes_basis": "SURVEY.md 8(d) 32F + 144N + 48Fb (124.0 B/face on C4) + 16N time step",
+                         "bytes_basis": "SURVEY.md 8(d) 32F + 144N + 48Fb (124.0 B/face on C4) + 8N time step",
+                         "frac_area_dt_basis": round(sweep_bytes_area_dt(*cnt) / (sweep_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+                         "area_dt_basis": "same + 8N (time step as area read 8 + dtm write 8 = 16 B/cell)",
                          "compulsory_bytes_one_launch": residual_algorithmic_bytes(*cnt),
                          "frac_of_measured_peak": round(achieved / HBM_MEASURED_GBS, 4)},
             "valu_roofline": valu_roofline(tr[2] if tr else None, sweep_ms),
@@ -327,4 +400,7 @@ def main():
 
 
 if __name__ == "__main__":
-    main()
+    if len(sys.argv) == 5 and sys.argv[1] == "--cpu-child":
+        cpu_child(sys.argv[2], int(sys.argv[3]), int(sys.argv[4]))
+    else:
+        main()

@@ -361,8 +361,10 @@ struct fvhip_ctx
 	                         bool overwrite, const GroupExchange& exg) {
 		auto exchange = [&](const ArrayOf& arr_of, int width) {
 			if(exg) { exg(arr_of, width); return; }
-			for(size_t i = 0; i < hs.size(); i++) hs[i]->exchange_rccl(arr_of(i), width);
+			for(size_t i = 0; i < hs.size(); i++) { HC(hipSetDevice(hs[i]->device)); hs[i]->exchange_rccl(arr_of(i), width); }
 		};
+		// every stage launches on the handle's own device (a group may span devices)
+		auto on = [&](size_t i) -> fvhip_ctx* { HC(hipSetDevice(hs[i]->device)); return hs[i]; };
 		fvhip_ctx* h0 = hs[0];
 		if(hs.size() == 1 && !exg && h0->pipelined()) {
 			h0->residual_pipelined(us[0], rs[0], dt, dts[0], overwrite);
@@ -374,32 +376,32 @@ struct fvhip_ctx
 				// interior patches need no halo data: they run first, then the exchange of the ghost
 				// rows of u and of the gradients of the cells other ranks hold as ghosts, then the rest
 				for(size_t i = 0; i < hs.size(); i++)
-					hs[i]->stage_fused(us[i], rs[i], dt, dts[i], overwrite, hs[i]->d_fz_order, hs[i]->L.fz_ninner);
+					on(i)->stage_fused(us[i], rs[i], dt, dts[i], overwrite, hs[i]->d_fz_order, hs[i]->L.fz_ninner);
 				exchange([&](size_t i) { return const_cast<double*>(us[i]); }, 4);
-				for(size_t i = 0; i < hs.size(); i++) hs[i]->stage_border_gradients(us[i]);
+				for(size_t i = 0; i < hs.size(); i++) on(i)->stage_border_gradients(us[i]);
 				exchange([&](size_t i) { return hs[i]->d_grad; }, 8);
 				for(size_t i = 0; i < hs.size(); i++)
-					hs[i]->stage_fused(us[i], rs[i], dt, dts[i], overwrite, hs[i]->d_fz_order + hs[i]->L.fz_ninner,
+					on(i)->stage_fused(us[i], rs[i], dt, dts[i], overwrite, hs[i]->d_fz_order + hs[i]->L.fz_ninner,
 					                   static_cast<int>(hs[i]->L.fz_order.size()) - hs[i]->L.fz_ninner);
 				return;
 			}
-			for(size_t i = 0; i < hs.size(); i++) hs[i]->stage_fused(us[i], rs[i], dt, dts[i], overwrite);
+			for(size_t i = 0; i < hs.size(); i++) on(i)->stage_fused(us[i], rs[i], dt, dts[i], overwrite);
 			return;
 		}
 		exchange([&](size_t i) { return const_cast<double*>(us[i]); }, 4);
 		if(h0->recKind() != SR_FIRST) {
-			for(size_t i = 0; i < hs.size(); i++) hs[i]->stage_gradients(us[i]);
+			for(size_t i = 0; i < hs.size(); i++) on(i)->stage_gradients(us[i]);
 			exchange([&](size_t i) { return hs[i]->d_grad; }, 8);
 			if(h0->limited()) {
-				for(fvhip_ctx* h : hs) h->stage_limiter();
+				for(size_t i = 0; i < hs.size(); i++) on(i)->stage_limiter();
 				exchange([&](size_t i) { return hs[i]->d_phi; }, 4);
 			}
 			if(h0->cfg.reconstruction == FVHIP_REC_WENO) {
-				for(fvhip_ctx* h : hs) h->stage_weno();
+				for(size_t i = 0; i < hs.size(); i++) on(i)->stage_weno();
 				exchange([&](size_t i) { return hs[i]->d_lgrad; }, 8);
 			}
 		}
-		for(size_t i = 0; i < hs.size(); i++) hs[i]->stage_sweep(us[i], rs[i], dt, dts[i], overwrite);
+		for(size_t i = 0; i < hs.size(); i++) on(i)->stage_sweep(us[i], rs[i], dt, dts[i], overwrite);
 	}
 
 	/// face-ordered mesh view and block buffers for the Jacobian, built on first use
@@ -547,6 +549,7 @@ struct fvhip_ctx
 	/// partitioned operator is sys_matfree, implicit.cpp)
 	void matfree(const double* x, double* y) {
 		if(!mf_u || !mf_r || !mf_mdt) throw std::runtime_error("matrix-free operator: state not set");
+		if(halo()) throw std::logic_error("fvhip_ctx::matfree is the single-domain operator (partitioned: sysMatfree)");
 		const size_t N = static_cast<size_t>(L.ncell);
 		if(!d_part) { d_part = dalloc(mf_partials(), owned); d_pm = dalloc(2, owned); }
 		if(!d_mf_aux) { d_mf_aux = dalloc(4*N, owned); d_mf_y = dalloc(4*N, owned); }

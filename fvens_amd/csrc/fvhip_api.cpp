@@ -299,6 +299,7 @@ int fvhip_get_gradients(fvhip_handle h, const double* u, double* grads)
 		std::vector<double>& st = h->h_stage;
 		toInternal(h, u, st.data(), 4);
 		HC(hipMemcpyAsync(h->d_u, st.data(), 4*N*sizeof(double), hipMemcpyHostToDevice, h->stream));
+		h->exchange_rccl(h->d_u, 4);   // ghost rows for the border cells (partitioned handles)
 		// ghost states from cell values, then the gradient scheme on CONSERVED variables
 		exact::launch_prep(h->M, h->P, h->d_u, h->d_up, h->d_ubc, h->d_ug, false, h->stream);
 		switch(h->cfg.gradientscheme) {
@@ -354,6 +355,7 @@ int fvhip_assemble_jacobian(fvhip_handle h, const double* u, double* diag, doubl
 		std::vector<double>& st = h->h_stage;
 		toInternal(h, u, st.data(), 4);
 		HC(hipMemcpyAsync(h->d_u, st.data(), 4*N*sizeof(double), hipMemcpyHostToDevice, h->stream));
+		h->exchange_rccl(h->d_u, 4);   // ghost rows: the cut-face blocks read them (partitioned handles)
 		HC(hipStreamSynchronize(h->stream));
 		if(!h->d_jdiag) {
 			h->d_jdiag = dalloc(16*N, h->owned);
@@ -474,7 +476,12 @@ int fvhip_matfree_apply(fvhip_handle h, const double* x, double* y)
 		toInternal(h, x, st.data(), 4);
 		double *dx = h->d_u, *dy = h->d_r;   // scratch: the operator's state lives in d_mf_*
 		HC(hipMemcpyAsync(dx, st.data(), 4*N*sizeof(double), hipMemcpyHostToDevice, h->stream));
-		h->matfree(dx, dy);
+		if(h->halo()) {
+			// partitioned: the operator over all ranks (global |x|; ghost rows of the perturbed state
+			// are exchanged inside the residual), as fvhip_matfree_apply_device does
+			if(!h->comm) throw std::runtime_error("partitioned handle: call fvhip_comm_init first");
+			sysMatfree({h}, fvhip_ctx::GroupExchange(), {dx}, {dy});
+		} else h->matfree(dx, dy);
 		HC(hipMemcpyAsync(st.data(), dy, 4*N*sizeof(double), hipMemcpyDeviceToHost, h->stream));
 		HC(hipStreamSynchronize(h->stream));
 		fromInternal(h, st.data(), y, 4);

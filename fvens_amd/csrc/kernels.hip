@@ -17,6 +17,10 @@
 #include "kernels.hpp"
 #include "layout.hpp"
 #include <algorithm>
+#include <mutex>
+#include <set>
+#include <stdexcept>
+#include <string>
 
 #ifndef FVHIP_NS
 #define FVHIP_NS exact
@@ -1168,15 +1172,24 @@ const char* launch_residual_wls(const DevMesh& M, const DevPhys& P, const SweepB
 		default: fn = pickFused<6>(rec, dt); break;
 	}
 	const size_t lds = std::max(static_cast<size_t>(M.fz_max_cells)*FZW, static_cast<size_t>(6*SLOTS_MAX))*sizeof(double);
-	// raise the dynamic-LDS limit once per instantiation to the largest patch the layout allows
-	// (hipFuncSetAttribute is a host-side runtime call: not on every launch)
-	static bool configured[7][2][2] = {};
-	bool& done = configured[flux < 0 || flux > 6 ? 6 : flux][rec == SR_MUSCL ? 1 : 0][dt ? 1 : 0];
-	if(!done) {
-		const size_t maxlds = std::max(static_cast<size_t>(FUSED_LDS_CELLS)*FZW, static_cast<size_t>(6*SLOTS_MAX))*sizeof(double);
-		(void)hipFuncSetAttribute(reinterpret_cast<const void*>(fn), hipFuncAttributeMaxDynamicSharedMemorySize,
-		                          static_cast<int>(maxlds));
-		done = true;
+	// raise the dynamic-LDS limit once per instantiation and device to the largest patch the layout
+	// allows (hipFuncSetAttribute is a host-side runtime call: not on every launch)
+	{
+		static std::mutex mu;
+		static std::set<std::pair<const void*, int>> configured;
+		int dev = 0;
+		if(hipGetDevice(&dev) != hipSuccess) throw std::runtime_error("k_residual_wls: hipGetDevice failed");
+		std::lock_guard<std::mutex> lock(mu);
+		if(configured.insert({reinterpret_cast<const void*>(fn), dev}).second) {
+			const size_t maxlds = std::max(static_cast<size_t>(FUSED_LDS_CELLS)*FZW, static_cast<size_t>(6*SLOTS_MAX))*sizeof(double);
+			const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(fn),
+			                                         hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(maxlds));
+			if(e != hipSuccess) {
+				configured.erase({reinterpret_cast<const void*>(fn), dev});
+				throw std::runtime_error(std::string("k_residual_wls: raising the dynamic LDS limit failed: ")
+				                         + hipGetErrorString(e));
+			}
+		}
 	}
 	const int np = B.plist ? B.pcount : M.npatch;
 	if(np > 0) hipLaunchKernelGGL(fn, dim3(8*((np + 7)/8)), dim3(SLOTS_MAX), lds, s, M, P, B);

@@ -8,6 +8,7 @@
 #include <string>
 #include <stdexcept>
 #include <chrono>
+#include <algorithm>
 #ifdef _OPENMP
 #include <omp.h>
 #endif
@@ -142,20 +143,27 @@ int orc_bc_ghost(int type, const double* gas, double aoa, const double* vals, co
 static struct OmpOne { OmpOne() { omp_set_num_threads(1); } } g_omp_one;
 int orc_set_threads(int n) { omp_set_num_threads(n < 1 ? 1 : n); return omp_get_max_threads(); }
 
-/// CPU baseline timing: nrep sweeps of compute_residual; returns seconds per sweep (median-free
-/// mean over nrep after one warm-up). Single-threaded restatement.
-double orc_time_residual(void* h, const double* u, int nrep, int gettimesteps)
+/// CPU baseline timing: nwarm untimed sweeps, then nrep sweeps of compute_residual
+/// each timed with std::chrono::steady_clock; times[nrep] receives the seconds of each sweep and the
+/// median is returned
+double orc_time_residual(void* h, const double* u, int nwarm, int nrep, int gettimesteps, double* times)
 {
 	Spatial& s = *static_cast<Spatial*>(h);
-	std::vector<double> r(4*static_cast<size_t>(s.m.nelem)), dtm(s.m.nelem);
-	s.compute_residual(u, r.data(), gettimesteps != 0, dtm.data());
-	const auto t0 = std::chrono::steady_clock::now();
-	for(int i = 0; i < nrep; i++) {
+	std::vector<double> r(4*static_cast<size_t>(s.m.nelem)), dtm(s.m.nelem), t(std::max(nrep, 1));
+	for(int i = 0; i < nwarm; i++) {
 		std::fill(r.begin(), r.end(), 0.0);
 		s.compute_residual(u, r.data(), gettimesteps != 0, dtm.data());
 	}
-	const auto t1 = std::chrono::steady_clock::now();
-	return std::chrono::duration<double>(t1-t0).count()/nrep;
+	for(int i = 0; i < nrep; i++) {
+		std::fill(r.begin(), r.end(), 0.0);
+		const auto t0 = std::chrono::steady_clock::now();
+		s.compute_residual(u, r.data(), gettimesteps != 0, dtm.data());
+		const auto t1 = std::chrono::steady_clock::now();
+		t[i] = std::chrono::duration<double>(t1-t0).count();
+		if(times) times[i] = t[i];
+	}
+	std::sort(t.begin(), t.begin() + nrep);
+	return nrep % 2 ? t[nrep/2] : 0.5*(t[nrep/2-1] + t[nrep/2]);
 }
 
 }

@@ -36,7 +36,7 @@ _SIGS = {
     "orc_flux": (ctypes.c_int, [ctypes.c_int, _dp, _dp, _dp, _dp, _dp]),
     "orc_flux_jacobian": (ctypes.c_int, [ctypes.c_int, _dp, _dp, _dp, _dp, _dp, _dp]),
     "orc_bc_ghost": (ctypes.c_int, [ctypes.c_int, _dp, ctypes.c_double, _dp, _dp, _dp, _dp, _dp]),
-    "orc_time_residual": (ctypes.c_double, [_vp, _dp, ctypes.c_int, ctypes.c_int]),
+    "orc_time_residual": (ctypes.c_double, [_vp, _dp, ctypes.c_int, ctypes.c_int, ctypes.c_int, _dp]),
     "orc_set_threads": (ctypes.c_int, [ctypes.c_int]),
 }
 
@@ -186,13 +186,16 @@ class OracleSpatial:
         _chk(lib().orc_surface(self._h, _d(u), _d(grads), marker, _d(out)))
         return out
 
-    def time_residual(self, u, nrep, gettimesteps=True, threads=1):
-        """seconds per sweep with `threads` OpenMP threads (the reference's omp structure)"""
+    def time_residual(self, u, nrep, gettimesteps=True, threads=1, nwarm=3):
+        """median seconds per sweep of `nrep` timed sweeps after `nwarm` untimed ones, with `threads`
+        OpenMP threads (the reference's omp structure); returns (median, per-sweep seconds)"""
         lib().orc_set_threads(int(threads))
+        times = np.zeros(max(int(nrep), 1))
         try:
-            return lib().orc_time_residual(self._h, _d(u), nrep, int(gettimesteps))
+            med = lib().orc_time_residual(self._h, _d(u), int(nwarm), int(nrep), int(gettimesteps), _d(times))
         finally:
             lib().orc_set_threads(1)
+        return med, times[:nrep]
 
     def __del__(self):
         try:
