@@ -115,6 +115,8 @@ class UMesh:
         self.ninface = self.naface - self.nbface - self.nconnface
 
         def arr(p, n, dt):
+            if n == 0:
+                return np.zeros(0, dt)
             return np.ctypeslib.as_array(p, shape=(n,)).astype(dt, copy=True)
         N, F, nb = self.nelem, self.naface, self.nbface
         self.coords = arr(v.coords, 2 * self.npoin, np.float64).reshape(-1, 2)
@@ -123,12 +125,15 @@ class UMesh:
         self.esuel = arr(v.esuel, N * self.maxnfael, np.int32).reshape(N, -1)
         self.elemface = arr(v.elemface, N * self.maxnfael, np.int32).reshape(N, -1)
         self.intfac = arr(v.intfac, 4 * F, np.int32).reshape(F, 4)
-        self.btags = arr(v.btags, nb * self.nbtag, np.int32).reshape(nb, -1)
+        self.btags = arr(v.btags, nb * self.nbtag, np.int32).reshape(nb, self.nbtag)
         self.facemetric = arr(v.facemetric, 3 * F, np.float64).reshape(F, 3)
         self.area = arr(v.area, N, np.float64)
         self.rc = arr(v.rc, 2 * (N + self.nconnface), np.float64).reshape(-1, 2)
         self.rcbp = arr(v.rcbp, 2 * nb, np.float64).reshape(-1, 2)
         self.gr = arr(v.gr, 2 * F, np.float64).reshape(F, 2)
+        nc = self.nconnface
+        self.connface = (arr(v.connface, 5 * nc, np.int32).reshape(nc, 5) if nc > 0
+                         else np.zeros((0, 5), np.int32))
 
     @classmethod
     def read_gmsh(cls, path):
@@ -153,6 +158,26 @@ class UMesh:
         h = ctypes.c_void_p()
         check(_ffi.lib().fvmesh_generate(2, nx, ny, 0, xlead, height, wallspacing, ctypes.byref(h)))
         return cls(h.value)
+
+    @staticmethod
+    def partition_trivial(nelem, nranks):
+        """TrivialReplicatedGlobalMeshPartitioner::compute_partition (meshpartitioning.cpp:354-367)"""
+        d = np.zeros(nelem, np.int32)
+        check(_ffi.lib().fvmesh_partition_trivial(int(nelem), int(nranks), iptr(d)))
+        return d
+
+    def restrict(self, elemdist, rank):
+        """restrictMeshToPartitions + preprocessMesh (meshpartitioning.cpp:24-159): rank `rank`'s
+        subdomain with its connectivity faces (the mesh each MPI rank of the reference holds)"""
+        d = np.ascontiguousarray(elemdist, np.int32)
+        h = ctypes.c_void_p()
+        check(_ffi.lib().fvmesh_restrict(self._h, iptr(d), int(rank), ctypes.byref(h)))
+        return UMesh(h.value)
+
+    def global_elem_index(self):
+        g = np.zeros(self.nelem, np.int32)
+        check(_ffi.lib().fvmesh_global_elem_index(self._h, iptr(g)))
+        return g
 
     def raw(self):
         """Pre-topology arrays (as read/generated): coords, inpoel, nnode, bface, nbtag"""
@@ -217,8 +242,9 @@ class FlowFV:
         h = ctypes.c_void_p()
         self.rank, self.nparts = rank, 1
         if partition is None:
+            # a per-rank mesh (nconnface > 0) is one MPI rank's subdomain of the reference
             check(_ffi.lib().fvhip_create(ctypes.byref(mesh.view), ctypes.byref(cfg), device, ctypes.byref(h)))
-            self.nown, self.nghost = mesh.nelem, 0
+            self.nown, self.nghost = mesh.nelem, mesh.nconnface
         else:
             part = np.ascontiguousarray(partition, np.int32)
             self.nparts = int(part.max()) + 1
@@ -228,6 +254,11 @@ class FlowFV:
         if partition is not None:
             st = self.layout_stats()
             self.nown, self.nghost = st["cells"], st["ghosts"]
+
+    def set_rank(self, rank, nranks):
+        """rank of a per-rank-mesh handle (before group use; comm_init implies it)"""
+        check(_ffi.lib().fvhip_set_rank(self._h, int(rank), int(nranks)))
+        self.rank, self.nparts = rank, nranks
 
     def comm_init(self, nranks, rank, uid):
         """RCCL communicator of the partition (uid: 128 bytes from comm_unique_id on rank 0)"""

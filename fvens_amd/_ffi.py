@@ -21,7 +21,7 @@ class FvMeshView(ctypes.Structure):
                 ("nelem", "npoin", "nbface", "naface", "nconnface", "maxnnode", "maxnfael", "nbtag")] + [
         ("coords", c_dbl_p), ("inpoel", c_int_p), ("nnode", c_int_p), ("esuel", c_int_p),
         ("elemface", c_int_p), ("intfac", c_int_p), ("btags", c_int_p), ("facemetric", c_dbl_p),
-        ("area", c_dbl_p), ("rc", c_dbl_p), ("rcbp", c_dbl_p), ("gr", c_dbl_p)]
+        ("area", c_dbl_p), ("rc", c_dbl_p), ("rcbp", c_dbl_p), ("gr", c_dbl_p), ("connface", c_int_p)]
 
 
 class FvFlowConfig(ctypes.Structure):
@@ -57,6 +57,7 @@ _SIGS = {
     "fvhip_create": (ctypes.c_int, [ctypes.POINTER(FvMeshView), ctypes.POINTER(FvFlowConfig), ctypes.c_int,
                                     ctypes.POINTER(ctypes.c_void_p)]),
     "fvhip_destroy": (ctypes.c_int, [ctypes.c_void_p]),
+    "fvhip_set_rank": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_int]),
     "fvhip_partition_rcb": (ctypes.c_int, [ctypes.POINTER(FvMeshView), ctypes.c_int, c_int_p]),
     "fvhip_partition_info": (ctypes.c_int, [ctypes.POINTER(FvMeshView), c_int_p, ctypes.c_int, c_int_p, c_int_p,
                                             c_int_p, c_int_p, c_int_p, c_int_p]),
@@ -126,6 +127,9 @@ _SIGS = {
     "fvmesh_write_gmsh": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_char_p]),
     "fvmesh_destroy": (ctypes.c_int, [ctypes.c_void_p]),
     "fvmesh_view": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(FvMeshView)]),
+    "fvmesh_partition_trivial": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, c_int_p]),
+    "fvmesh_restrict": (ctypes.c_int, [ctypes.c_void_p, c_int_p, ctypes.c_int, ctypes.POINTER(ctypes.c_void_p)]),
+    "fvmesh_global_elem_index": (ctypes.c_int, [ctypes.c_void_p, c_int_p]),
     "fvmesh_raw_info": (ctypes.c_int, [ctypes.c_void_p, c_int_p]),
     "fvmesh_raw_arrays": (ctypes.c_int, [ctypes.c_void_p, c_dbl_p, c_int_p, c_int_p, c_int_p]),
 }

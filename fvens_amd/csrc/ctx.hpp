@@ -123,6 +123,7 @@ struct fvhip_ctx
 	std::vector<double> h_stage;
 	// partitioned meshes: halo exchange with the neighbour ranks (RCCL, or in-process for a group)
 	int rank = 0, nparts = 1;
+	bool rankmesh = false;        ///< one rank's subdomain with connectivity faces (fvhip_create, nconnface > 0)
 	bool use_staged = false;      ///< force the staged (gradient + sweep) path even if fused applies
 	bool use_pipe = false;        ///< force the pipelined staged path even if fused applies
 	// pipelined staged residual (single domain): the sweep groups run on stream2 behind the

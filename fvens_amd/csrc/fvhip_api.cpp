@@ -149,7 +149,26 @@ int fvhip_create(const fvhip_mesh* mesh, const fvhip_flow_config* cfg, int devic
 {
 	return guard([&] {
 		if(!mesh || !cfg || !out) throw std::invalid_argument("null argument");
+		if(mesh->nconnface > 0) {
+			// one rank's subdomain: its rank comes with the communicator (or fvhip_set_rank)
+			fvhip_ctx* h = createCtx(topoFromRankMesh(*mesh), cfg, device);
+			h->rankmesh = true; h->rank = -1; h->nparts = 0;
+			*out = h;
+			return;
+		}
 		*out = createCtx(topoFromMesh(*mesh), cfg, device);
+	});
+}
+
+int fvhip_set_rank(fvhip_handle h, int rank, int nranks)
+{
+	return guard([&] {
+		if(!h->rankmesh) throw std::invalid_argument("fvhip_set_rank: not a per-rank mesh handle");
+		if(rank < 0 || rank >= nranks) throw std::invalid_argument("rank out of range");
+		for(int q : h->L.nbr_rank)
+			if(q < 0 || q >= nranks || q == rank) throw std::invalid_argument("connectivity faces name rank "
+			                                                                  + std::to_string(q));
+		h->rank = rank; h->nparts = nranks;
 	});
 }
 
@@ -203,6 +222,7 @@ int fvhip_comm_unique_id(void* id128)
 int fvhip_comm_init(fvhip_handle h, int nranks, int rank, const void* id128)
 {
 	return guard([&] {
+		if(h->rankmesh && h->rank < 0 && fvhip_set_rank(h, rank, nranks)) throw std::runtime_error(g_err);
 		if(nranks != h->nparts || rank != h->rank)
 			throw std::invalid_argument("communicator does not match the handle's partition");
 		HC(hipSetDevice(h->device));
@@ -693,6 +713,33 @@ int fvmesh_generate(int kind, int a, int b, int c, double x, double y, double z,
 int fvmesh_write_gmsh(fvmesh_handle m, const char* path) { return guard([&] { writeGmsh2(m->raw, path); }); }
 int fvmesh_destroy(fvmesh_handle m) { return guard([&] { delete m; }); }
 
+int fvmesh_partition_trivial(int nelem, int nranks, int* elemdist)
+{
+	return guard([&] {
+		const std::vector<int> d = partitionTrivial(nelem, nranks);
+		std::memcpy(elemdist, d.data(), d.size()*sizeof(int));
+	});
+}
+
+int fvmesh_restrict(fvmesh_handle g, const int* elemdist, int rank, fvmesh_handle* out)
+{
+	return guard([&] {
+		if(!g || !elemdist || !out) throw std::invalid_argument("null argument");
+		std::unique_ptr<fvmesh_s> m(new fvmesh_s());
+		m->mesh = restrictMesh(g->mesh, elemdist, rank);
+		m->raw = m->mesh.md;
+		*out = m.release();
+	});
+}
+
+int fvmesh_global_elem_index(fvmesh_handle h, int* gidx)
+{
+	return guard([&] {
+		const Mesh& M = h->mesh;
+		for(int i = 0; i < M.md.nelem; i++) gidx[i] = M.globalElemIndex.empty() ? i : M.globalElemIndex[i];
+	});
+}
+
 int fvmesh_view(fvmesh_handle h, fvhip_mesh* v)
 {
 	return guard([&] {
@@ -703,6 +750,7 @@ int fvmesh_view(fvmesh_handle h, fvhip_mesh* v)
 		v->esuel = M.esuel.data(); v->elemface = M.elemface.data(); v->intfac = M.intfac.data();
 		v->btags = M.btags.data(); v->facemetric = M.facemetric.data(); v->area = M.area.data();
 		v->rc = M.rc.data(); v->rcbp = M.rcbp.data(); v->gr = M.gr.data();
+		v->connface = M.connface.empty() ? nullptr : M.connface.data();
 	});
 }
 

@@ -823,7 +823,10 @@ __device__ __forceinline__ void fused_wls_row(const DevMesh& M, const DevPhys& P
 }
 
 template <int FLUX, int REC, bool DT>
-__global__ void __launch_bounds__(SLOTS_MAX, 4) k_residual_wls(const DevMesh M, const DevPhys P, const SweepBuffers B)
+#ifndef FVHIP_FUSED_WAVES
+#define FVHIP_FUSED_WAVES 4
+#endif
+__global__ void __launch_bounds__(SLOTS_MAX, FVHIP_FUSED_WAVES) k_residual_wls(const DevMesh M, const DevPhys P, const SweepBuffers B)
 {
 	extern __shared__ __attribute__((aligned(16))) double fz[];
 	const int np = B.plist ? B.pcount : M.npatch;

@@ -272,11 +272,17 @@ Mesh buildMesh(MeshData md)
 
 	// 1-rank restriction (drops unused points) then preprocessMesh's compute_topological
 	compactPoints(md);
-	buildEsup(md, esup_p, esup);
+	buildTopology(std::move(md), M, std::vector<int>());
+	return M;
+}
 
+namespace {
+
+/// compute_elementsSurroundingElements (mesh.cpp:467-541): neighbour across each local face, -1 if none
+std::vector<int> esuelOf(const MeshData& md, const std::vector<int>& esup_p, const std::vector<int>& esup)
+{
 	const int N = md.nelem, mf = md.maxnfael;
-	M.esuel.assign(static_cast<size_t>(N)*mf, -1);
-	// compute_elementsSurroundingElements (mesh.cpp:467-541): neighbour across each local face
+	std::vector<int> esuel(static_cast<size_t>(N)*mf, -1);
 	for(int ie = 0; ie < N; ie++) {
 		const int nn = md.nnode[ie];
 		for(int f = 0; f < md.nfael[ie]; f++) {
@@ -286,15 +292,33 @@ Mesh buildMesh(MeshData md)
 				if(je == ie) continue;
 				const int jf = faceWithNodes(md, je, a, b);
 				if(jf >= 0) {
-					M.esuel[static_cast<size_t>(ie)*mf+f] = je;
-					M.esuel[static_cast<size_t>(je)*mf+jf] = ie;
+					esuel[static_cast<size_t>(ie)*mf+f] = je;
+					esuel[static_cast<size_t>(je)*mf+jf] = ie;
 				}
 			}
 		}
 	}
+	return esuel;
+}
 
-	// compute_faceConnectivity (mesh.cpp:659-762), nconnface = 0 on a single domain
-	M.nconnface = 0;
+}
+
+/// preprocessMesh's compute_topological + compute_areas + compute_face_data (ameshutils.cpp:40-99,
+/// mesh.cpp:290-365, 659-762) and the Spatial ctor's centres (aspatial.cpp:36-119) for one rank's mesh;
+/// connface [nconnface][5] as the restriction set it (empty on a single domain)
+void buildTopology(MeshData md, Mesh& M, const std::vector<int>& connface)
+{
+	std::vector<int> esup_p, esup, helem, hface;
+	const int bw = md.nnofa + md.nbtag;
+	buildEsup(md, esup_p, esup);
+
+	const int N = md.nelem, mf = md.maxnfael;
+	M.esuel = esuelOf(md, esup_p, esup);
+
+	// compute_faceConnectivity (mesh.cpp:659-762): physical boundary faces, subdomain interior faces,
+	// then the connectivity faces in connface order (none on a single domain)
+	M.nconnface = static_cast<int>(connface.size()/5);
+	M.connface = connface;
 	int ninface = 0;
 	for(int ie = 0; ie < N; ie++)
 		for(int in = 0; in < md.nfael[ie]; in++) {
@@ -335,6 +359,17 @@ Mesh buildMesh(MeshData md)
 		}
 	}
 	if(fi != md.nbface + ninface) throw std::logic_error("buildMesh: face count mismatch");
+	// connectivity faces (mesh.cpp:744-757): L = the subdomain cell, R = ghost row nelem+icface, nodes
+	// in the cell's own order so the face points out of the subdomain
+	for(int ic = 0; ic < M.nconnface; ic++, fi++) {
+		const int inelem = connface[5*ic], lf = connface[5*ic+1], nn = md.nnode[inelem];
+		M.intfac[4*fi+0] = inelem;
+		M.esuel[static_cast<size_t>(inelem)*mf+lf] = N + ic;
+		M.elemface[static_cast<size_t>(inelem)*mf+lf] = fi;
+		M.intfac[4*fi+1] = N + ic;
+		M.intfac[4*fi+2] = nodeOf(md, inelem, (lf+0) % nn);
+		M.intfac[4*fi+3] = nodeOf(md, inelem, (lf+1) % nn);
+	}
 
 	// compute_areas (mesh.cpp:290-313)
 	auto X = [&](int p) { return md.coords[2*p]; };
@@ -395,6 +430,118 @@ Mesh buildMesh(MeshData md)
 	}
 
 	M.md = std::move(md);
+}
+
+// ------------------------------------------------------------------------------------------------
+// Subdomains (multi-rank meshes)
+// ------------------------------------------------------------------------------------------------
+
+std::vector<int> partitionTrivial(int nelem, int nranks)
+{
+	if(nranks < 1 || nelem < nranks) throw std::runtime_error("Not enough cells in this mesh for "
+	                                                            + std::to_string(nranks) + " processes!");
+	const int per = nelem / nranks;
+	std::vector<int> d(nelem, nranks-1);
+	for(int r = 0; r < nranks; r++)
+		for(int i = r*per; i < (r+1)*per; i++) d[i] = r;
+	return d;
+}
+
+Mesh restrictMesh(const Mesh& gm, const int* elemdist, int rank)
+{
+	const MeshData& g = gm.md;
+	if(gm.nconnface != 0) throw std::runtime_error("restrictMesh: expects the global mesh");
+	MeshData lm;
+	lm.maxnnode = g.maxnnode; lm.maxnfael = g.maxnfael; lm.nnofa = g.nnofa;
+	lm.nbtag = g.nbtag; lm.ndtag = g.ndtag;
+	// 1. cells of this rank in global order (extractInpoel, :161-182)
+	std::vector<int> glob;
+	for(int e = 0; e < g.nelem; e++)
+		if(elemdist[e] == rank) {
+			glob.push_back(e);
+			for(int j = 0; j < g.maxnnode; j++) lm.inpoel.push_back(g.inpoel[static_cast<size_t>(e)*g.maxnnode+j]);
+			for(int j = 0; j < g.ndtag; j++) lm.vol_regions.push_back(g.vol_regions[static_cast<size_t>(e)*g.ndtag+j]);
+			lm.nnode.push_back(g.nnode[e]);
+			lm.nfael.push_back(g.nfael[e]);
+		}
+	lm.nelem = static_cast<int>(glob.size());
+	if(lm.nelem == 0) throw std::runtime_error("restrictMesh: rank " + std::to_string(rank) + " owns no cells");
+	// 2. the points they use, in ascending global order (extractPointCoords, :184-223)
+	std::vector<int> pts;
+	for(int e = 0; e < lm.nelem; e++)
+		for(int j = 0; j < lm.nnode[e]; j++) pts.push_back(lm.inpoel[static_cast<size_t>(e)*lm.maxnnode+j]);
+	std::sort(pts.begin(), pts.end());
+	pts.erase(std::unique(pts.begin(), pts.end()), pts.end());
+	lm.npoin = static_cast<int>(pts.size());
+	std::vector<int> g2l(g.npoin, -1);
+	lm.coords.resize(2*static_cast<size_t>(lm.npoin));
+	for(int i = 0; i < lm.npoin; i++) {
+		g2l[pts[i]] = i;
+		lm.coords[2*i] = g.coords[2*static_cast<size_t>(pts[i])];
+		lm.coords[2*i+1] = g.coords[2*static_cast<size_t>(pts[i])+1];
+	}
+	// 3. local point numbers (:66-69)
+	for(int e = 0; e < lm.nelem; e++)
+		for(int j = 0; j < lm.nnode[e]; j++) {
+			int& v = lm.inpoel[static_cast<size_t>(e)*lm.maxnnode+j];
+			v = g2l[v];
+		}
+	// 4. the physical boundary faces whose cell is here, in global order (extractbfaces, :225-276)
+	const int gbw = g.nnofa + g.nbtag;
+	lm.nbface = 0;
+	for(int f = 0; f < g.nbface; f++) {
+		if(elemdist[gm.intfac[4*static_cast<size_t>(f)]] != rank) continue;
+		for(int j = 0; j < g.nnofa; j++) lm.bface.push_back(g2l[g.bface[static_cast<size_t>(f)*gbw+j]]);
+		for(int j = 0; j < g.nbtag; j++) lm.bface.push_back(g.bface[static_cast<size_t>(f)*gbw+g.nnofa+j]);
+		lm.nbface++;
+	}
+	// 5. local esuel; points on a physical boundary face (:76-82, :278-291)
+	std::vector<int> esup_p, esup;
+	buildEsup(lm, esup_p, esup);
+	const std::vector<int> esuel = esuelOf(lm, esup_p, esup);
+	std::vector<char> bpoin(lm.npoin, 0);
+	const int lbw = lm.nnofa + lm.nbtag;
+	for(int f = 0; f < lm.nbface; f++)
+		for(int j = 0; j < lm.nnofa; j++) bpoin[lm.bface[static_cast<size_t>(f)*lbw+j]] = 1;
+	// 6. connectivity faces: local faces without a local neighbour with a point off the physical
+	// boundary (getConnectivityFaceEIndices :293-331), matched to the global cell's face (:98-154)
+	std::vector<int> cf;
+	for(int e = 0; e < lm.nelem; e++)
+		for(int lf = 0; lf < lm.nfael[e]; lf++) {
+			if(esuel[static_cast<size_t>(e)*lm.maxnfael+lf] != -1) continue;
+			bool conn = false;
+			for(int k = 0; k < lm.nnofa; k++)
+				if(!bpoin[nodeOf(lm, e, (lf+k) % lm.nnode[e])]) { conn = true; break; }
+			if(!conn) continue;
+			const int ge = glob[e];
+			int nbrank = -1, nbcell = -1;
+			for(int jgf = 0; jgf < g.nfael[ge]; jgf++) {
+				bool matched = true;
+				for(int k = 0; k < g.nnofa; k++) {
+					const int gp = nodeOf(g, ge, (jgf+k) % g.nnode[ge]);
+					bool pm = false;
+					for(int l = 0; l < lm.nnofa; l++)
+						if(pts[nodeOf(lm, e, (lf+l) % lm.nnode[e])] == gp) { pm = true; break; }
+					if(!pm) { matched = false; break; }
+				}
+				if(matched) {
+					nbcell = gm.esuel[static_cast<size_t>(ge)*g.maxnfael+jgf];
+					nbrank = elemdist[nbcell];
+					break;
+				}
+			}
+			if(nbrank < 0) throw std::logic_error("Could not find connectivity face!");
+			const int c5[5] = {e, lf, nbrank, nbcell, gm.elemface[static_cast<size_t>(ge)*g.maxnfael+lf]};
+			cf.insert(cf.end(), c5, c5+5);
+		}
+	Mesh M;
+	buildTopology(std::move(lm), M, cf);
+	M.globalElemIndex = glob;
+	// ghost rows of the cell centres: the neighbours' centres (the owner computes them from the same
+	// points in the same order, so they equal the global mesh's)
+	for(int ic = 0; ic < M.nconnface; ic++)
+		for(int d = 0; d < 2; d++)
+			M.rc[2*(static_cast<size_t>(M.md.nelem)+ic)+d] = gm.rc[2*static_cast<size_t>(cf[5*ic+3])+d];
 	return M;
 }
 

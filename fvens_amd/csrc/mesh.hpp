@@ -50,6 +50,10 @@ struct Mesh
 	std::vector<double> rc;        ///< [nelem+nconnface][2] cell centres (vertex average)
 	std::vector<double> gr;        ///< [naface][2] face centres
 	std::vector<double> rcbp;      ///< [nbface][2] ghost cell centres about face midpoints
+	// one rank's subdomain (restrictMesh): connectivity faces and the global cell of each local cell
+	std::vector<int> connface;     ///< [nconnface][5] = {cell, local face, owner rank of the neighbour,
+	                               ///<  global neighbour cell, global face} (mesh.hpp:60-70)
+	std::vector<int> globalElemIndex; ///< [nelem] (empty on a single domain)
 };
 
 /// Reads a Gmsh 2.2 ASCII mesh exactly as readGmsh2 does (boundary edges must precede cells).
@@ -61,6 +65,20 @@ void writeGmsh2(const MeshData& m, const std::string& path);
 /// Full reference preprocessing for one rank: orientation fix, topology, areas, face data,
 /// centres. (constructMesh ameshutils.cpp:102-153 with a trivial 1-rank partition)
 Mesh buildMesh(MeshData md);
+
+/// preprocessMesh's topology + geometry for one rank's mesh whose connectivity faces are given
+/// (connface [nconnface][5]); ghost-row centres rc[nelem..] are left zero for the caller to fill
+void buildTopology(MeshData md, Mesh& M, const std::vector<int>& connface);
+
+/// TrivialReplicatedGlobalMeshPartitioner::compute_partition (meshpartitioning.cpp:354-367):
+/// nelem/nranks cells per rank in index order, the remainder to the last rank
+std::vector<int> partitionTrivial(int nelem, int nranks);
+
+/// ReplicatedGlobalMeshPartitioner::restrictMeshToPartitions (meshpartitioning.cpp:24-159) followed
+/// by preprocessMesh (ameshutils.cpp:40-99): rank `rank`'s subdomain of the (preprocessed) global
+/// mesh gm under the cell distribution elemdist, with its connectivity faces; the ghost rows of rc
+/// hold the centres of the neighbouring cells (what the Spatial ctor's ghost scatter puts there)
+Mesh restrictMesh(const Mesh& gm, const int* elemdist, int rank);
 
 /// Synthetic hybrid O-grid around a NACA 0012 aerofoil (chord 1, LE at origin).
 /// ntheta points around the surface, nquad quad layers at the wall, ntri triangle-split layers

@@ -90,6 +90,81 @@ MeshTopo topoFromMesh(const fvhip_mesh& m)
 	return T;
 }
 
+MeshTopo topoFromRankMesh(const fvhip_mesh& m)
+{
+	const int N = m.nelem, nb = m.nbface, F = m.naface, nc = m.nconnface;
+	if(nc <= 0 || !m.connface) throw std::invalid_argument("per-rank mesh: connface missing");
+	if(m.maxnfael > 4) throw std::runtime_error("cells with more than 4 faces are not supported");
+	const int cs = F - nc;                                  // gConnBFaceStart
+	auto C = [&](int ic, int k) { return m.connface[5*static_cast<size_t>(ic)+k]; };
+	std::vector<int> order(nc);
+	std::iota(order.begin(), order.end(), 0);
+	std::sort(order.begin(), order.end(), [&](int a, int b) {
+		return C(a,2) < C(b,2) || (C(a,2) == C(b,2) && (C(a,4) < C(b,4) || (C(a,4) == C(b,4) && a < b))); });
+	std::vector<int> gpos(nc);
+	for(int i = 0; i < nc; i++) gpos[order[i]] = i;
+	for(int ic = 0; ic < nc; ic++) {
+		const int f = cs + ic;
+		if(m.intfac[4*static_cast<size_t>(f)] != C(ic,0) || m.intfac[4*static_cast<size_t>(f)+1] != N + ic)
+			throw std::invalid_argument("per-rank mesh: connectivity faces are not the last faces of intfac");
+	}
+	MeshTopo T;
+	T.nown = N; T.nghost = nc; T.nbface = nb; T.naface = F;
+	const int NT = N + nc;
+	auto remap = [&](int code) {          // reference neighbour code -> local code
+		if(code < 0) return code;
+		if(code < N) return code;
+		if(code < N + nc) return N + gpos[code - N];
+		return code;                        // physical boundary: nelem+nconnface+iface = NT + iface
+	};
+	T.cell_global.resize(NT);
+	std::iota(T.cell_global.begin(), T.cell_global.begin() + N, 0);
+	T.ghost_row.resize(nc);
+	for(int ic = 0; ic < nc; ic++) { T.cell_global[N + gpos[ic]] = C(ic,3); T.ghost_row[gpos[ic]] = N + ic; }
+	T.nfael.resize(N);
+	T.cell_faces.assign(4*static_cast<size_t>(N), -1);
+	T.cell_esuel.assign(4*static_cast<size_t>(N), -1);
+	T.clength.resize(N);
+	for(int e = 0; e < N; e++) {
+		T.nfael[e] = m.nnode[e];
+		for(int j = 0; j < m.nnode[e]; j++) {
+			T.cell_faces[4*static_cast<size_t>(e)+j] = m.elemface[static_cast<size_t>(e)*m.maxnfael+j];
+			T.cell_esuel[4*static_cast<size_t>(e)+j] = remap(m.esuel[static_cast<size_t>(e)*m.maxnfael+j]);
+		}
+		T.clength[e] = cellLength(m, e);
+	}
+	T.rc.resize(2*static_cast<size_t>(NT));
+	for(int c = 0; c < N; c++) { T.rc[2*c] = m.rc[2*c]; T.rc[2*c+1] = m.rc[2*c+1]; }
+	for(int ic = 0; ic < nc; ic++)
+		for(int d = 0; d < 2; d++) T.rc[2*static_cast<size_t>(N + gpos[ic])+d] = m.rc[2*static_cast<size_t>(N + ic)+d];
+	T.area.assign(m.area, m.area + N);
+	T.face_global.resize(F); std::iota(T.face_global.begin(), T.face_global.end(), 0);
+	T.L.resize(F); T.R.resize(F);
+	for(int f = 0; f < F; f++) {
+		T.L[f] = m.intfac[4*static_cast<size_t>(f)];
+		T.R[f] = remap(m.intfac[4*static_cast<size_t>(f)+1]);
+	}
+	T.facemetric.assign(m.facemetric, m.facemetric + 3*static_cast<size_t>(F));
+	T.gr.assign(m.gr, m.gr + 2*static_cast<size_t>(F));
+	T.btag.resize(nb);
+	for(int f = 0; f < nb; f++) T.btag[f] = m.btags[static_cast<size_t>(f)*m.nbtag];
+	T.rcbp.assign(m.rcbp, m.rcbp + 2*static_cast<size_t>(nb));
+	// neighbour ranks and the exchange lists
+	T.ghost_start.push_back(0);
+	T.send_start.push_back(0);
+	for(int i = 0; i < nc; i++) {
+		const int q = C(order[i], 2);
+		if(T.nbr_rank.empty() || T.nbr_rank.back() != q) {
+			if(!T.nbr_rank.empty()) { T.ghost_start.push_back(i); T.send_start.push_back(i); }
+			T.nbr_rank.push_back(q);
+		}
+		T.send_cells.push_back(C(order[i], 0));
+	}
+	T.ghost_start.push_back(nc);
+	T.send_start.push_back(nc);
+	return T;
+}
+
 MeshTopo extractPartition(const fvhip_mesh& m, const int* part, int rank)
 {
 	if(m.nconnface != 0) throw std::runtime_error("extractPartition: expects the single-domain mesh");

@@ -45,10 +45,22 @@ struct MeshTopo
 	                                   ///<  nown+ghost_start[k] .. nown+ghost_start[k+1]-1
 	std::vector<int> send_start;       ///< [nnbr+1] ranges into send_cells
 	std::vector<int> send_cells;       ///< local owned cells each neighbour holds as ghosts (ascending global id)
+	std::vector<int> ghost_row;        ///< [nghost] per-rank meshes: reference row (nelem+icface) of each ghost
 };
 
 /// Whole mesh as one rank (no ghosts)
 MeshTopo topoFromMesh(const fvhip_mesh& m);
+
+/// One rank's subdomain as the reference's multi-rank driver holds it (restrictMeshToPartitions,
+/// meshpartitioning.cpp:24-159): mesh.connface [nconnface][5] lists its connectivity faces, which
+/// come last in face order with the local outward normal and R = nelem + icface (mesh.cpp:744-757).
+/// Each connectivity face gets a ghost cell of its own (the reference's ghost row nelem+icface),
+/// grouped by neighbour rank and ordered by GLOBAL face index (connface(.,4)) within a rank; each
+/// rank sends the rows of its connectivity-face cells in that same order, so both sides of every
+/// exchange agree without the index handshake of L2TraceVector::update_comm_pattern
+/// (tracevector.cpp:31-184). The result is the reference's per-rank residual: faces, orientation
+/// and accumulation order are the subdomain's own.
+MeshTopo topoFromRankMesh(const fvhip_mesh& m);
 
 /// Rank `rank`'s piece of a single-domain mesh partitioned by `part` (part[cell] in [0,nparts))
 MeshTopo extractPartition(const fvhip_mesh& m, const int* part, int rank);

@@ -95,6 +95,8 @@ typedef struct fvhip_mesh {
 	const double* rc;         /* [nelem+nconnface][2] */
 	const double* rcbp;       /* [nbface][2] */
 	const double* gr;         /* [naface][2] */
+	const int* connface;      /* [nconnface][5] gconnface (mesh.hpp:60-70): cell, local face, neighbour's
+	                             rank, global neighbour cell, global face; NULL when nconnface == 0 */
 } fvhip_mesh;
 
 typedef struct fvhip_ctx* fvhip_handle;
@@ -106,8 +108,17 @@ const char* fvhip_version(void);
 /** Number of visible HIP devices (0 if none; never fails) */
 int fvhip_device_count(void);
 
-/** Builds the device-resident discretisation for a mesh on a device */
+/** Builds the device-resident discretisation for a mesh on a device. A mesh with connectivity faces
+ *  (nconnface > 0) is one rank's subdomain as the reference's multi-rank driver holds it
+ *  (restrictMeshToPartitions, mesh/meshpartitioning.cpp:24-159): the residual is that rank's residual
+ *  of the reference (flow_spatial.cpp:636-816 with its connectivity faces; the face traces and ghost
+ *  gradients L2TraceVector / VecGhostUpdate exchange, tracevector.cpp:213-340, alinalg.cpp:17-29, come
+ *  from the library's RCCL exchange), once fvhip_comm_init (or fvhip_set_rank + a group) gave the rank.
+ *  Ghost rows of u are refreshed by the library's exchange (the rows the caller's VecGhostUpdate holds). */
 int fvhip_create(const fvhip_mesh* mesh, const fvhip_flow_config* cfg, int device, fvhip_handle* out);
+/** Rank of a per-rank-mesh handle within nranks (PETSC_COMM_WORLD's rank in the reference); needed
+ *  before fvhip_group_create, implied by fvhip_comm_init */
+int fvhip_set_rank(fvhip_handle h, int rank, int nranks);
 int fvhip_destroy(fvhip_handle h);
 
 /* ---------------------------------------------------------------------------------------------
@@ -302,6 +313,16 @@ int fvmesh_read_gmsh(const char* path, fvmesh_handle* out);
 int fvmesh_generate(int kind, int a, int b, int c, double x, double y, double z, fvmesh_handle* out);
 int fvmesh_write_gmsh(fvmesh_handle m, const char* path);
 int fvmesh_destroy(fvmesh_handle m);
+/** TrivialReplicatedGlobalMeshPartitioner::compute_partition (meshpartitioning.cpp:354-367): cell i
+ *  goes to rank i/(nelem/nranks), the remainder to the last rank */
+int fvmesh_partition_trivial(int nelem, int nranks, int* elemdist);
+/** ReplicatedGlobalMeshPartitioner::restrictMeshToPartitions (meshpartitioning.cpp:24-159) followed by
+ *  preprocessMesh (ameshutils.cpp:40-99): rank `rank`'s subdomain of global mesh g under the cell
+ *  distribution elemdist [nelem of g], with its connectivity faces; rc has nelem+nconnface rows, the
+ *  ghost rows holding the neighbouring cells' centres (the Spatial ctor's ghost scatter, aspatial.cpp:41-66) */
+int fvmesh_restrict(fvmesh_handle g, const int* elemdist, int rank, fvmesh_handle* out);
+/** UMesh::gglobalElemIndex of a subdomain from fvmesh_restrict: gidx [nelem] */
+int fvmesh_global_elem_index(fvmesh_handle m, int* gidx);
 /** Fills a fvhip_mesh view whose pointers stay valid until fvmesh_destroy */
 int fvmesh_view(fvmesh_handle m, fvhip_mesh* view);
 /** Raw (pre-topology) arrays: npoin, nelem, maxnnode, nbface, nbtag */

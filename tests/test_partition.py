@@ -102,3 +102,72 @@ def _exchange_worker(rank, world, port, nparts_check):
 def test_halo_exchange_gloo_two_ranks():
     port = 29500 + (os.getpid() % 500)
     mp.spawn(_exchange_worker, args=(2, port, 2), nprocs=2, join=True)
+
+
+def _read_dat(path, nelem, nconn):
+    """testhybrid-distb_part*.dat: '#Elements' then the global index of each local cell, '#ConnFaces'
+    then 4 columns per connectivity face (distributedmesh.cpp:19-42)"""
+    tok = open(path).read().split()
+    assert tok[0].startswith("#")
+    gidx = np.array(tok[1:1 + nelem], np.int32)
+    assert tok[1 + nelem].startswith("#")
+    conn = np.array(tok[2 + nelem:2 + nelem + 4 * nconn], np.int32).reshape(nconn, 4)
+    return gidx, conn
+
+
+@pytest.mark.parametrize("rank", [0, 1, 2])
+def test_subdomain_restriction_trivial_golden(rank):
+    """MeshPartition_SubdomainRestriction_Trivial (tests/mesh/CMakeLists.txt:57-67,
+    distributedmesh.cpp:46-99): the trivial 3-way partition of testhybrid.msh restricted to each rank
+    equals the reference's golden subdomain testhybrid_part{1,2,3}.msh (compareMeshes: cell and point
+    counts, nnode/nfael, inpoel, bface incl. tags, coords to 1 eps) and testhybrid-distb_part*.dat
+    (global cell index of each local cell, connface columns 0-3)"""
+    gm = fa.UMesh.read_gmsh(cases.fixture_mesh("testhybrid"))
+    d = fa.UMesh.partition_trivial(gm.nelem, 3)
+    lm = gm.restrict(d, rank)
+    ref = fa.UMesh.read_gmsh(cases.fixture_mesh("testhybrid_part%d" % (rank + 1)))
+    a, b = lm.raw(), ref.raw()
+    for k in ("npoin", "nelem", "nbface"):
+        assert a[k] == b[k], k
+    np.testing.assert_array_equal(a["nnode"], b["nnode"])
+    ia, ib = a["inpoel"].reshape(a["nelem"], -1), b["inpoel"].reshape(b["nelem"], -1)
+    for i, k in enumerate(a["nnode"]):          # compareMeshes: ginpoel(i, j) for j < gnnode(i)
+        np.testing.assert_array_equal(ia[i, :k], ib[i, :k])
+    np.testing.assert_array_equal(a["bface"], b["bface"])
+    assert np.abs(a["coords"] - b["coords"]).max() <= np.finfo(float).eps
+    gidx, conn = _read_dat(cases.fixture_mesh("testhybrid-distb_part%d" % (rank + 1)).replace(".msh", ".dat"),
+                           lm.nelem, lm.nconnface)
+    np.testing.assert_array_equal(lm.global_elem_index(), gidx)
+    np.testing.assert_array_equal(lm.connface[:, :4], conn)
+
+
+def test_subdomains_tile_the_global_mesh():
+    """every global interior face is a subdomain interior face of one rank or a connectivity face of
+    both neighbouring ranks, with the global face index in connface(.,4), and the per-rank faces keep
+    the reference's order (physical, interior, connectivity) and outward conn-face normals"""
+    gm = fa.UMesh.naca_ogrid(64, 4, 10)
+    nranks = 5
+    d = fa.UMesh.partition_trivial(gm.nelem, nranks)
+    nb = gm.nbface
+    seen = np.zeros(gm.naface, np.int32)
+    for r in range(nranks):
+        lm = gm.restrict(d, r)
+        g = lm.global_elem_index()
+        N, nc = lm.nelem, lm.nconnface
+        cs = lm.naface - nc
+        assert lm.nbface + lm.ninface == cs
+        # interior faces of the subdomain are global faces between two local cells
+        for f in range(lm.nbface, cs):
+            l, rr = lm.intfac[f, :2]
+            gf = gm.elemface[g[l]][list(lm.esuel[l]).index(rr)]
+            seen[gf] += 2
+        for ic, (c, lf, q, gn, gf) in enumerate(lm.connface):
+            f = cs + ic
+            assert tuple(lm.intfac[f, :2]) == (c, N + ic)
+            assert d[gn] == q != r and gm.elemface[g[c], lf] == gf
+            assert {gm.intfac[gf, 0], gm.intfac[gf, 1]} == {g[c], gn}
+            np.testing.assert_array_equal(lm.rc[N + ic], gm.rc[gn])
+            seen[gf] += 1
+            # the conn face points out of the subdomain
+            assert np.dot(lm.gr[f] - lm.rc[c], lm.facemetric[f, :2]) > 0
+    assert (seen[nb:] == 2).all()
