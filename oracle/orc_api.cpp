@@ -41,12 +41,38 @@ void* orc_mesh_from_raw(int npoin, const double* coords, int nelem, int maxnnode
 
 void orc_mesh_free(void* h) { delete static_cast<OMesh*>(h); }
 
-/// info: npoin, nelem, nbface, naface, ninface, maxnnode, maxnfael, nbtag
+/// subdomain `rank` of a preprocessed global mesh under elemdist (meshpartitioning.cpp:24-159)
+void* orc_mesh_restrict(void* gm, const int* elemdist, int rank)
+{
+	try {
+		const OMesh& g = *static_cast<OMesh*>(gm);
+		return new OMesh(orc_restrict(g, std::vector<int>(elemdist, elemdist + g.nelem), rank));
+	} catch(const std::exception& e) { g_err = e.what(); return nullptr; }
+}
+
+int orc_partition_trivial(int nelem, int nranks, int* elemdist)
+{
+	ORC_TRY(const std::vector<int> d = orc_partition_trivial(nelem, nranks); std::memcpy(elemdist, d.data(), d.size()*sizeof(int)))
+}
+
+/// compute_residual on all ranks of a partition (handles of Spatials over per-rank meshes)
+int orc_residual_ranks(int n, void** spatials, const double** u, double** res, int gettimesteps, double** dtm)
+{
+	ORC_TRY(
+		std::vector<const Spatial*> S;
+		for(int i = 0; i < n; i++) S.push_back(static_cast<const Spatial*>(spatials[i]));
+		compute_residual_ranks(S, std::vector<const double*>(u, u+n), std::vector<double*>(res, res+n),
+		                       gettimesteps != 0, gettimesteps ? std::vector<double*>(dtm, dtm+n) : std::vector<double*>(n, nullptr))
+	)
+}
+
+/// info: npoin, nelem, nbface, naface, ninface, maxnnode, maxnfael, nbtag, nconnface
 void orc_mesh_info(void* h, int* info)
 {
 	const OMesh& m = *static_cast<OMesh*>(h);
 	info[0] = m.npoin; info[1] = m.nelem; info[2] = m.nbface; info[3] = m.naface;
 	info[4] = m.ninface; info[5] = m.maxnnode; info[6] = m.maxnfael; info[7] = m.nbtag;
+	info[8] = m.nconnface;
 }
 
 /// Copies a named mesh array out. Names: coords inpoel bface esuel elemface intfac btags
@@ -62,6 +88,7 @@ int orc_mesh_get(void* h, const char* name, void* out)
 	else if(s == "intfac") cpi(m.intfac); else if(s == "btags") cpi(m.btags);
 	else if(s == "facemetric") cpd(m.facemetric); else if(s == "area") cpd(m.area);
 	else if(s == "rc") cpd(m.rc); else if(s == "gr") cpd(m.gr); else if(s == "rcbp") cpd(m.rcbp);
+	else if(s == "connface") cpi(m.connface); else if(s == "globalElemIndex") cpi(m.globalElemIndex);
 	else { g_err = "unknown array " + s; return -1; }
 	return 0;
 }

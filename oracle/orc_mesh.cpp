@@ -8,6 +8,7 @@
 #include <algorithm>
 #include <stdexcept>
 #include <iterator>
+#include <map>
 
 namespace orc {
 
@@ -203,10 +204,17 @@ void orc_preprocess(OMesh& m)
 				std::swap(m.bface[iface*bw+0], m.bface[iface*bw+1]);
 		}
 	}
-	// compute_topological (mesh.cpp:330-341); nconnface = 0 on one rank
+	m.nconnface = 0;
+	m.connface.clear();
+	orc_preprocess_rank(m);
+}
+
+void orc_preprocess_rank(OMesh& m)
+{
+	const int bw = m.nnofa+m.nbtag;
+	// compute_topological (mesh.cpp:330-341) with the connectivity faces already in m.connface
 	esupCompute(m);
 	esuelCompute(m);
-	m.nconnface = 0;
 	m.ninface = 0;
 	for(int ie = 0; ie < m.nelem; ie++)
 		for(int in = 0; in < m.nfael[ie]; in++) {
@@ -243,6 +251,18 @@ void orc_preprocess(OMesh& m)
 				faceindex++;
 			}
 		}
+	// connectivity faces (mesh.cpp:737-757)
+	const int connBFaceStart = m.nbface + m.ninface;
+	for(int iface = connBFaceStart; iface < m.naface; iface++) {
+		const int icface = iface - connBFaceStart;
+		const int inelem = m.gconnface(icface,0);
+		m.intfac[4*iface+0] = inelem;
+		m.esuel[static_cast<size_t>(inelem)*m.maxnfael+m.gconnface(icface,1)] = m.nelem+icface;
+		m.elemface[static_cast<size_t>(inelem)*m.maxnfael+m.gconnface(icface,1)] = iface;
+		m.intfac[4*iface+1] = m.nelem+icface;
+		for(int inode = 0; inode < m.nnofa; inode++)
+			m.intfac[4*iface+2+inode] = m.in(inelem, (m.gconnface(icface,1) + inode) % m.nnode[inelem]);
+	}
 
 	// compute_areas (mesh.cpp:290-313)
 	auto c = [&](int p, int d) { return m.coords[2*static_cast<size_t>(p)+d]; };
@@ -294,6 +314,133 @@ void orc_preprocess(OMesh& m)
 			m.rcbp[2*f+d] = 2.0*mid - m.rc[2*ie+d];
 		}
 	}
+}
+
+
+// meshpartitioning.cpp:354-367
+std::vector<int> orc_partition_trivial(int nelem, int nranks)
+{
+	const int numloceleminit = nelem / nranks;
+	std::vector<int> elemdist(nelem);
+	for(int irank = 0; irank < nranks; irank++)
+		for(int iel = irank*numloceleminit; iel < (irank+1)*numloceleminit; iel++) elemdist[iel] = irank;
+	for(int iel = nranks*numloceleminit; iel < nelem; iel++) elemdist[iel] = nranks-1;
+	return elemdist;
+}
+
+// meshpartitioning.cpp:24-159, then preprocessMesh (ameshutils.cpp:40-99) and the ghost-row centres
+// of the Spatial ctor's scatter (aspatial.cpp:41-66): the owner computes them from the same points in
+// the same order as gm does
+OMesh orc_restrict(const OMesh& gm, const std::vector<int>& elemdist, int rank)
+{
+	OMesh lm;
+	lm.nelem = 0;
+	for(int iel = 0; iel < gm.nelem; iel++) if(elemdist[iel] == rank) lm.nelem++;
+	lm.maxnnode = gm.maxnnode; lm.maxnfael = gm.maxnfael; lm.nnofa = gm.nnofa;
+	// 1. extractInpoel (:161-182)
+	lm.inpoel.assign(static_cast<size_t>(lm.nelem)*gm.maxnnode, 0);
+	lm.nfael.assign(lm.nelem, 0); lm.nnode.assign(lm.nelem, 0);
+	lm.nbtag = gm.nbtag; lm.ndtag = gm.ndtag;
+	lm.globalElemIndex.assign(lm.nelem, 0);
+	{
+		int lociel = 0;
+		for(int iel = 0; iel < gm.nelem; iel++)
+			if(elemdist[iel] == rank) {
+				lm.globalElemIndex[lociel] = iel;
+				for(int j = 0; j < gm.maxnnode; j++) lm.inpoel[static_cast<size_t>(lociel)*lm.maxnnode+j] = gm.in(iel,j);
+				lm.nnode[lociel] = gm.nnode[iel];
+				lm.nfael[lociel] = gm.nfael[iel];
+				lociel++;
+			}
+	}
+	// 2. extractPointCoords (:184-223)
+	std::vector<int> locpoints;
+	for(int iel = 0; iel < lm.nelem; iel++)
+		for(int inode = 0; inode < lm.nnode[iel]; inode++) locpoints.push_back(lm.in(iel,inode));
+	std::sort(locpoints.begin(), locpoints.end());
+	locpoints.erase(std::unique(locpoints.begin(), locpoints.end()), locpoints.end());
+	lm.npoin = static_cast<int>(locpoints.size());
+	lm.coords.assign(2*static_cast<size_t>(lm.npoin), 0);
+	std::map<int,int> g2l;
+	for(int i = 0; i < lm.npoin; i++) g2l[locpoints[i]] = i;
+	{
+		int globpointer = 0, locpointer = 0;
+		while(globpointer < gm.npoin && locpointer < lm.npoin) {
+			if(globpointer == locpoints[locpointer]) {
+				for(int i = 0; i < 2; i++) lm.coords[2*locpointer+i] = gm.coords[2*globpointer+i];
+				locpointer++;
+			}
+			globpointer++;
+		}
+	}
+	// 3. local point numbers (:66-69)
+	for(int iel = 0; iel < lm.nelem; iel++)
+		for(int j = 0; j < lm.nnode[iel]; j++)
+			lm.inpoel[static_cast<size_t>(iel)*lm.maxnnode+j] = g2l.at(lm.in(iel,j));
+	// 4. extractbfaces (:225-276)
+	const int gbw = gm.nnofa+gm.nbtag;
+	lm.nbface = 0;
+	for(int iface = 0; iface < gm.nbface; iface++) {
+		const int globelem = gm.L(iface);
+		if(elemdist[globelem] != rank) continue;
+		for(int j = 0; j < gm.nnofa; j++) lm.bface.push_back(g2l.at(gm.bface[iface*gbw+j]));
+		for(int j = 0; j < gm.nbtag; j++) lm.bface.push_back(gm.bface[iface*gbw+gm.nnofa+j]);
+		lm.nbface++;
+	}
+	// 5. (:79-82, 278-291)
+	esupCompute(lm);
+	esuelCompute(lm);
+	std::vector<bool> isBounPoin(lm.npoin, false);
+	const int lbw = lm.nnofa+lm.nbtag;
+	for(int iface = 0; iface < lm.nbface; iface++)
+		for(int inode = 0; inode < lm.nnofa; inode++) isBounPoin[lm.bface[iface*lbw+inode]] = true;
+	// 6. getConnectivityFaceEIndices (:293-331) and the connface rows (:91-156)
+	std::vector<std::vector<int>> connElemLocalFace(lm.nelem);
+	for(int iel = 0; iel < lm.nelem; iel++)
+		for(int iface = 0; iface < lm.nfael[iel]; iface++)
+			if(lm.gesuel(iel,iface) == -1) {
+				bool isconnface = false;
+				for(int inode = 0; inode < lm.nnofa; inode++)
+					if(!isBounPoin[lm.in(iel, (iface+inode) % lm.nnode[iel])]) { isconnface = true; break; }
+				if(isconnface) connElemLocalFace[iel].push_back(iface);
+			}
+	lm.nconnface = 0;
+	for(int i = 0; i < lm.nelem; i++) lm.nconnface += static_cast<int>(connElemLocalFace[i].size());
+	lm.connface.assign(5*static_cast<size_t>(lm.nconnface), 0);
+	int icofa = 0;
+	for(int iel = 0; iel < lm.nelem; iel++)
+		for(size_t iconface = 0; iconface < connElemLocalFace[iel].size(); iconface++) {
+			const int localConnFace = connElemLocalFace[iel][iconface];
+			int* c = &lm.connface[5*static_cast<size_t>(icofa)];
+			c[0] = iel; c[1] = localConnFace; c[2] = -1; c[3] = -1;
+			c[4] = gm.gelemface(lm.globalElemIndex[iel], localConnFace);
+			std::vector<int> locfacepoints(lm.nnofa);
+			for(int linofa = 0; linofa < lm.nnofa; linofa++)
+				locfacepoints[linofa] = lm.in(iel, (localConnFace+linofa) % lm.nnode[iel]);
+			const int glind = lm.globalElemIndex[iel];
+			for(int jgf = 0; jgf < gm.nfael[glind]; jgf++) {
+				bool matched = true;
+				for(int jnofa = 0; jnofa < gm.nnofa; jnofa++) {
+					const int globpoint = gm.in(glind, (jgf+jnofa) % gm.nnode[glind]);
+					bool pointmatched = false;
+					for(int linofa = 0; linofa < lm.nnofa; linofa++)
+						if(locpoints[locfacepoints[linofa]] == globpoint) { pointmatched = true; break; }
+					if(!pointmatched) { matched = false; break; }
+				}
+				if(matched) {
+					c[2] = elemdist[gm.gesuel(glind,jgf)];
+					c[3] = gm.gesuel(glind,jgf);
+					break;
+				}
+			}
+			if(c[2] < 0) throw std::logic_error("Could not find connectivity face!");
+			icofa++;
+		}
+	orc_preprocess_rank(lm);
+	for(int ic = 0; ic < lm.nconnface; ic++)
+		for(int d = 0; d < 2; d++)
+			lm.rc[2*(static_cast<size_t>(lm.nelem)+ic)+d] = gm.rc[2*static_cast<size_t>(lm.gconnface(ic,3))+d];
+	return lm;
 }
 
 }

@@ -5,7 +5,8 @@
  * Restated: meshreaders.cpp:66-265 (readGmsh2), mesh.cpp:55-82 (boundary orientation),
  * mesh.cpp:290-328 (areas, centres), mesh.cpp:346-365 (face metric), mesh.cpp:425-541 (esup,
  * esuel, with the reference's nested searches), mesh.cpp:560-762 (face connectivity),
- * aspatial.cpp:50-61 and 97-119 (face centres, ghost centres).
+ * aspatial.cpp:50-61 and 97-119 (face centres, ghost centres), meshpartitioning.cpp:24-159 and
+ * 354-367 (subdomain restriction, trivial partition).
  */
 #ifndef ORC_MESH_HPP
 #define ORC_MESH_HPP
@@ -32,6 +33,8 @@ struct OMesh
 	std::vector<double> rc;            // [nelem+nconnface][2]
 	std::vector<double> gr;            // [naface][2]
 	std::vector<double> rcbp;          // [nbface][2]
+	std::vector<int> connface;         // [nconnface][5] (mesh.hpp:60-70), per-rank meshes
+	std::vector<int> globalElemIndex;  // [nelem], per-rank meshes
 
 	int in(int e, int j) const { return inpoel[static_cast<size_t>(e)*maxnnode+j]; }
 	int gesuel(int e, int j) const { return esuel[static_cast<size_t>(e)*maxnfael+j]; }
@@ -42,6 +45,7 @@ struct OMesh
 	double ny(int f) const { return facemetric[3*f+1]; }
 	double len(int f) const { return facemetric[3*f+2]; }
 	int btag(int f) const { return btags[static_cast<size_t>(f)*nbtag]; }
+	int gconnface(int ic, int k) const { return connface[5*static_cast<size_t>(ic)+k]; }
 };
 
 /// readGmsh2 restated with std::ifstream >> like the reference
@@ -51,6 +55,13 @@ OMesh orc_fromRaw(int npoin, const double* coords, int nelem, int maxnnode, cons
                   const int* nnode, int nbface, int nbtag, const int* bface);
 /// correctBoundaryFaceOrientation + compute_topological + areas + face data + centres
 void orc_preprocess(OMesh& m);
+/// preprocessMesh of one rank's mesh (compute_topological with m.connface, areas, face data, centres;
+/// ghost-row centres left zero)
+void orc_preprocess_rank(OMesh& m);
+/// TrivialReplicatedGlobalMeshPartitioner::compute_partition (meshpartitioning.cpp:354-367)
+std::vector<int> orc_partition_trivial(int nelem, int nranks);
+/// restrictMeshToPartitions (meshpartitioning.cpp:24-159) + preprocessMesh of a preprocessed global mesh
+OMesh orc_restrict(const OMesh& gm, const std::vector<int>& elemdist, int rank);
 
 }
 #endif

@@ -5,6 +5,7 @@
 #include <cstring>
 #include <cmath>
 #include <stdexcept>
+#include <map>
 
 namespace orc {
 
@@ -46,6 +47,17 @@ Spatial::Spatial(const OMesh& mesh, const Config& c)
 				V[4*ie+2*i+j] += w2*dr[i]*dr[j];
 				V[4*je+2*i+j] += w2*dr[i]*dr[j];
 			}
+		}
+		// connectivity faces: the subdomain cell only (agradientschemes.cpp:292-310)
+		for(int f = m.nbface+m.ninface; f < m.naface; f++) {
+			const int ie = m.L(f), je = m.Rt(f);
+			double w2 = 0, dr[2];
+			for(int d = 0; d < 2; d++) {
+				w2 += (rc[2*ie+d]-rc[2*je+d])*(rc[2*ie+d]-rc[2*je+d]);
+				dr[d] = rc[2*ie+d]-rc[2*je+d];
+			}
+			w2 = 1.0/(w2);
+			for(int i = 0; i < 2; i++) for(int j = 0; j < 2; j++) V[4*ie+2*i+j] += w2*dr[i]*dr[j];
 		}
 		// Eigen 2x2 inverse: det = m00*m11 - m10*m01; invdet = 1/det (InverseImpl.h size-2 helper)
 		for(int e = 0; e < N; e++) {
@@ -146,6 +158,22 @@ void Spatial::compute_gradients(const double* u, const double* ug, double* grads
 				}
 			}
 		}
+		// connectivity faces: the subdomain cell only (:173-212)
+		for(int f = m.nbface+m.ninface; f < m.naface; f++) {
+			const int ie = m.L(f), je = m.Rt(f);
+			double md[2]; mid(f, md);
+			double dL = 0, dR = 0;
+			for(int d = 0; d < 2; d++) {
+				dL += (md[d]-rc[2*ie+d])*(md[d]-rc[2*ie+d]);
+				dR += (md[d]-rc[2*je+d])*(md[d]-rc[2*je+d]);
+			}
+			dL = 1.0/std::sqrt(dL); dR = 1.0/std::sqrt(dR);
+			const double a1 = 1.0/m.area[ie];
+			for(int iv = 0; iv < 4; iv++) {
+				const double ut = (u[4*ie+iv]*dL + u[4*je+iv]*dR)/(dL+dR) * m.len(f);
+				for(int d = 0; d < 2; d++) GR(ie,d,iv) += (ut * m.facemetric[3*f+d])*a1;
+			}
+		}
 	}
 	else if(cfg.grad == GRAD_LEASTSQUARES) {                       // :322-440
 		std::vector<double> fr(8*static_cast<size_t>(N), 0.0);   // f(jdim,ivar) at ivar*2+jdim
@@ -181,6 +209,18 @@ void Spatial::compute_gradients(const double* u, const double* ug, double* grads
 				fr[8*je+iv*2+d] += w2*dr[d]*du[iv];
 			}
 		}
+		// connectivity faces: the subdomain cell only (:404-427)
+		for(int f = m.nbface+m.ninface; f < m.naface; f++) {
+			const int ie = m.L(f), je = m.Rt(f);
+			double w2 = 0, dr[2], du[4];
+			for(int d = 0; d < 2; d++) {
+				w2 += (rc[2*ie+d]-rc[2*je+d])*(rc[2*ie+d]-rc[2*je+d]);
+				dr[d] = rc[2*ie+d]-rc[2*je+d];
+			}
+			w2 = 1.0/(w2);
+			for(int iv = 0; iv < 4; iv++) du[iv] = u[4*ie+iv] - u[4*je+iv];
+			for(int iv = 0; iv < 4; iv++) for(int d = 0; d < 2; d++) fr[8*ie+iv*2+d] += w2*dr[d]*du[iv];
+		}
 		// d = V*f (Eigen lazy 2x2 * 2x4 product: d(i,j) = V(i,0) f(0,j) + V(i,1) f(1,j))
 #pragma omp parallel for default(shared)
 		for(int e = 0; e < N; e++) {
@@ -210,6 +250,10 @@ void Spatial::compute_face_values(const double* up, const double* ug, const doub
 	};
 	switch(cfg.recon) {
 	case REC_NONE: {                                               // areconstruction.cpp:51-103
+		for(int f = nb+m.ninface; f < F; f++) {                    // connectivity faces: left only
+			const int ie = m.L(f);
+			for(int i = 0; i < 4; i++) ufl[4*f+i] = linex(up[4*ie+i], G(grads,ie), i, 1.0, gr+2*f, ri+2*ie);
+		}
 #pragma omp parallel for default(shared)
 		for(int f = nb; f < nb+m.ninface; f++) {
 			const int ie = m.L(f), je = m.Rt(f);
@@ -474,6 +518,7 @@ void Spatial::compute_max_timestep(const double* ul, const double* ur, double* d
 // flow_spatial.cpp:636-816 (single domain: no connectivity faces)
 void Spatial::compute_residual(const double* u, double* res, bool gettimesteps, double* dtm) const
 {
+	if(m.nconnface) throw std::invalid_argument("per-rank mesh: use compute_residual_ranks");
 	const int N = m.nelem, nb = m.nbface, F = m.naface;
 	std::vector<double> ul(4*static_cast<size_t>(F), 0.0), ur(4*static_cast<size_t>(F), 0.0);
 	for(int f = 0; f < nb; f++) for(int iv = 0; iv < 4; iv++) ul[4*f+iv] = u[4*m.L(f)+iv];
@@ -728,6 +773,101 @@ std::array<double,3> surface_functionals(const Spatial& s, const double* u, cons
 	}
 	Cdp /= totalarea; Cdf /= totalarea; Cl /= totalarea;
 	return {Cl, Cdp, Cdf};
+}
+
+// flow_spatial.cpp:636-816 on every rank of a partition (per-rank meshes with connectivity faces),
+// with the exchanges the reference makes over MPI in between: the ghost gradients (VecGhostUpdate on
+// gradvec, :711-729 and :784-787) and the face traces (L2TraceVector::updateSharedFaces, :738 and
+// :782, tracevector.cpp:213-340); the ghost rows of u come in filled (the driver's VecGhostUpdate)
+void compute_residual_ranks(const std::vector<const Spatial*>& S, const std::vector<const double*>& u,
+                            const std::vector<double*>& res, bool gettimesteps, const std::vector<double*>& dtm)
+{
+	const size_t P = S.size();
+	const Config& cfg = S[0]->cfg;
+	struct St { std::vector<double> ul, ur, ubcell, up, grads; };
+	std::vector<St> st(P);
+	// owner-local index of a global cell
+	std::map<int, std::pair<int,int>> owner;
+	for(size_t r = 0; r < P; r++)
+		for(int e = 0; e < S[r]->m.nelem; e++) owner[S[r]->m.globalElemIndex[e]] = {static_cast<int>(r), e};
+	auto ghostGradients = [&]() {
+		for(size_t r = 0; r < P; r++) {
+			const OMesh& m = S[r]->m;
+			for(int ic = 0; ic < m.nconnface; ic++) {
+				const auto o = owner.at(m.gconnface(ic,3));
+				for(int k = 0; k < 8; k++)
+					st[r].grads[8*(static_cast<size_t>(m.nelem)+ic)+k] = st[o.first].grads[8*static_cast<size_t>(o.second)+k];
+			}
+		}
+	};
+	for(size_t r = 0; r < P; r++) {
+		const Spatial& s = *S[r];
+		const OMesh& m = s.m;
+		const int N = m.nelem, nb = m.nbface, F = m.naface;
+		St& a = st[r];
+		a.ul.assign(4*static_cast<size_t>(F), 0.0); a.ur.assign(4*static_cast<size_t>(F), 0.0);
+		for(int f = 0; f < nb; f++) for(int iv = 0; iv < 4; iv++) a.ul[4*f+iv] = u[r][4*m.L(f)+iv];
+		a.ubcell.assign(4*static_cast<size_t>(nb), 0.0);
+		if(cfg.order2) {
+			s.compute_boundary_states(a.ul.data(), a.ur.data());
+			a.up.assign(4*static_cast<size_t>(N+m.nconnface), 0.0);
+			for(int f = 0; f < nb; f++) {
+				for(int j = 0; j < 4; j++) a.ubcell[4*f+j] = a.ur[4*f+j];
+				s.phy.primFromCons(&a.ur[4*f], &a.ur[4*f]);
+			}
+			for(int e = 0; e < N+m.nconnface; e++) s.phy.primFromCons(&u[r][4*e], &a.up[4*e]);
+			a.grads.assign(8*static_cast<size_t>(N+m.nconnface), 0.0);
+			s.compute_gradients(a.up.data(), a.ur.data(), a.grads.data());
+		}
+	}
+	if(cfg.order2) {
+		if(cfg.recon == REC_WENO) ghostGradients();
+		for(size_t r = 0; r < P; r++) {
+			const Spatial& s = *S[r];
+			const OMesh& m = s.m;
+			const int nb = m.nbface, F = m.naface, cs = nb + m.ninface;
+			St& a = st[r];
+			std::vector<double> ugcopy(a.ur.begin(), a.ur.begin()+4*nb);
+			s.compute_face_values(a.up.data(), ugcopy.data(), a.grads.data(), a.ul.data(), a.ur.data());
+			for(int f = cs; f < F; f++) s.phy.consFromPrim(&a.ul[4*f], &a.ul[4*f]);
+			for(int f = nb; f < cs; f++) {
+				s.phy.consFromPrim(&a.ul[4*f], &a.ul[4*f]);
+				s.phy.consFromPrim(&a.ur[4*f], &a.ur[4*f]);
+			}
+			for(int f = 0; f < nb; f++) s.phy.consFromPrim(&a.ul[4*f], &a.ul[4*f]);
+		}
+		// trace exchange: a connectivity face's right state is the neighbour's left state of the
+		// same global face
+		for(size_t r = 0; r < P; r++) {
+			const OMesh& m = S[r]->m;
+			const int cs = m.nbface + m.ninface;
+			for(int ic = 0; ic < m.nconnface; ic++) {
+				const int q = m.gconnface(ic,2), gf = m.gconnface(ic,4);
+				const OMesh& mq = S[q]->m;
+				const int csq = mq.nbface + mq.ninface;
+				int jc = 0;
+				while(jc < mq.nconnface && mq.gconnface(jc,4) != gf) jc++;
+				if(jc == mq.nconnface) throw std::logic_error("connectivity face without a partner");
+				for(int iv = 0; iv < 4; iv++) st[r].ur[4*(cs+ic)+iv] = st[q].ul[4*(csq+jc)+iv];
+			}
+		}
+		if(cfg.recon != REC_WENO) ghostGradients();
+	} else {
+		for(size_t r = 0; r < P; r++) {
+			const OMesh& m = S[r]->m;
+			for(int f = m.nbface; f < m.naface; f++) for(int iv = 0; iv < 4; iv++) {
+				st[r].ul[4*f+iv] = u[r][4*m.L(f)+iv]; st[r].ur[4*f+iv] = u[r][4*m.Rt(f)+iv];
+			}
+		}
+	}
+	for(size_t r = 0; r < P; r++) {
+		const Spatial& s = *S[r];
+		St& a = st[r];
+		s.compute_boundary_states(a.ul.data(), a.ur.data());
+		const double* ugpb = cfg.order2 ? a.ubcell.data() : a.ur.data();
+		s.compute_fluxes(u[r], cfg.order2 ? a.grads.data() : nullptr, a.ul.data(), a.ur.data(), ugpb, res[r]);
+		if(gettimesteps) s.compute_max_timestep(a.ul.data(), a.ur.data(), dtm[r]);
+	}
 }
 
 }

@@ -86,6 +86,12 @@ public:
 int steady_forward_euler(const Spatial& s, double* u, double cfl, double tol, int maxiter,
                          double* resratio);
 
+/// FlowFV::compute_residual on every rank of a partition (per-rank meshes from orc_restrict), with
+/// the ghost-gradient and face-trace exchanges in between; u[r] has nelem+nconnface rows (ghost rows
+/// filled as the driver's VecGhostUpdate leaves them)
+void compute_residual_ranks(const std::vector<const Spatial*>& S, const std::vector<const double*>& u,
+                            const std::vector<double*>& res, bool gettimesteps, const std::vector<double*>& dtm);
+
 /// computeSurfaceData (flow_spatial.cpp:130-310): returns {CL, CDp, CDsf} on marker iwbcm
 std::array<double,3> surface_functionals(const Spatial& s, const double* u, const double* grads, int iwbcm);
 

@@ -20,6 +20,10 @@ _SIGS = {
     "orc_mesh_from_raw": (_vp, [ctypes.c_int, _dp, ctypes.c_int, ctypes.c_int, _ip, _ip, ctypes.c_int,
                                 ctypes.c_int, _ip]),
     "orc_mesh_free": (None, [_vp]),
+    "orc_mesh_restrict": (_vp, [_vp, _ip, ctypes.c_int]),
+    "orc_partition_trivial": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, _ip]),
+    "orc_residual_ranks": (ctypes.c_int, [ctypes.c_int, ctypes.POINTER(_vp), ctypes.POINTER(_dp),
+                                          ctypes.POINTER(_dp), ctypes.c_int, ctypes.POINTER(_dp)]),
     "orc_mesh_info": (None, [_vp, _ip]),
     "orc_mesh_get": (ctypes.c_int, [_vp, ctypes.c_char_p, _vp]),
     "orc_spatial_create": (_vp, [_vp, _dp, _ip, _ip, _ip, _dp]),
@@ -81,10 +85,10 @@ class OracleMesh:
         if not h:
             raise RuntimeError(lib().orc_last_error().decode())
         self._h = h
-        info = np.zeros(8, np.int32)
+        info = np.zeros(9, np.int32)
         lib().orc_mesh_info(h, _i(info))
         (self.npoin, self.nelem, self.nbface, self.naface, self.ninface, self.maxnnode, self.maxnfael,
-         self.nbtag) = [int(x) for x in info]
+         self.nbtag, self.nconnface) = [int(x) for x in info]
 
     @classmethod
     def read(cls, path):
@@ -96,12 +100,18 @@ class OracleMesh:
                                            _i(raw["inpoel"]), _i(raw["nnode"]), raw["nbface"], raw["nbtag"],
                                            _i(raw["bface"])))
 
+    def restrict(self, elemdist, rank):
+        """restrictMeshToPartitions + preprocessMesh (meshpartitioning.cpp:24-159) of this global mesh"""
+        d = np.ascontiguousarray(elemdist, np.int32)
+        return OracleMesh(lib().orc_mesh_restrict(self._h, _i(d), int(rank)))
+
     def get(self, name):
-        N, F, nb = self.nelem, self.naface, self.nbface
+        N, F, nb, nc = self.nelem, self.naface, self.nbface, self.nconnface
         shapes = {"coords": ((self.npoin, 2), np.float64), "inpoel": ((N, self.maxnnode), np.int32),
                   "esuel": ((N, self.maxnfael), np.int32), "elemface": ((N, self.maxnfael), np.int32),
                   "intfac": ((F, 4), np.int32), "btags": ((nb, self.nbtag), np.int32),
-                  "facemetric": ((F, 3), np.float64), "area": ((N,), np.float64), "rc": ((N, 2), np.float64),
+                  "facemetric": ((F, 3), np.float64), "area": ((N,), np.float64), "rc": ((N + nc, 2), np.float64),
+                  "connface": ((nc, 5), np.int32), "globalElemIndex": ((N,), np.int32),
                   "gr": ((F, 2), np.float64), "rcbp": ((nb, 2), np.float64)}
         shp, dt = shapes[name]
         a = np.zeros(shp, dt)
@@ -202,6 +212,24 @@ class OracleSpatial:
             lib().orc_spatial_free(self._h)
         except Exception:
             pass
+
+
+def partition_trivial(nelem, nranks):
+    d = np.zeros(nelem, np.int32)
+    _chk(lib().orc_partition_trivial(int(nelem), int(nranks), _i(d)))
+    return d
+
+
+def residual_ranks(spatials, us, rs, gettimesteps=False, dtms=None):
+    """FlowFV::compute_residual on every rank of a partition with the reference's exchanges in between
+    (OracleSpatials over per-rank OracleMeshes; us[r] with nelem+nconnface rows, ghost rows filled)"""
+    n = len(spatials)
+    hs = (_vp * n)(*[sp._h for sp in spatials])
+    up = (_dp * n)(*[_d(u) for u in us])
+    rp = (_dp * n)(*[_d(r) for r in rs])
+    dp = (_dp * n)(*[_d(d) for d in dtms]) if gettimesteps else None
+    _chk(lib().orc_residual_ranks(n, hs, up, rp, int(gettimesteps), dp))
+    return rs
 
 
 def relaxed_update(u, du, gamma, minfactor):
