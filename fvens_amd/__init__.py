@@ -292,6 +292,12 @@ class FlowFV:
                                                    dptr(faces), iptr(nf)))
         return tuple(float(x) for x in funcs), faces[:int(nf[0])]
 
+    def entropy_error_device(self, d_u):
+        """FlowOutput::compute_entropy_cell (aoutput.cpp:28-62): L2 entropy error of the device state"""
+        e = np.zeros(1)
+        check(_ffi.lib().fvhip_entropy_error_device(self._h, ctypes.c_void_p(d_u), dptr(e)))
+        return float(e[0])
+
     def assemble_jacobian(self, u, diag=None, lower=None, upper=None):
         """Spatial::assemble_jacobian (aspatial.cpp:242-340): blocks are ADDED into diag [nelem][4][4],
         lower/upper [ninface][4][4] (A[R][L] += lower, A[L][R] += upper); zeros if not given."""
@@ -470,6 +476,22 @@ def comm_unique_id():
     return bytes(buf.raw)
 
 
+def partition_graph(mesh, nparts):
+    """Graph partition of the cell dual graph (stand-in for the reference's Scotch, absent here)"""
+    part = np.zeros(mesh.nelem, np.int32)
+    check(_ffi.lib().fvhip_partition_graph(ctypes.byref(mesh.view), int(nparts), iptr(part)))
+    return part
+
+
+def partition_edge_cut(mesh, part):
+    """interior faces whose cells lie in different parts"""
+    p = np.ascontiguousarray(part, np.int32)
+    c = _ffi.lib().fvhip_partition_edge_cut(ctypes.byref(mesh.view), iptr(p))
+    if c < 0:
+        raise RuntimeError(_ffi.lib().fvhip_last_error().decode())
+    return int(c)
+
+
 def partition_rcb(mesh, nparts):
     """Recursive coordinate bisection of the cell centres (Scotch is not available here)"""
     part = np.zeros(mesh.nelem, np.int32)
@@ -547,6 +569,11 @@ class FlowFVGroup:
         check(_ffi.lib().fvhip_group_steady_backward_euler_device(self._g, self._ptrs(d_us), ctypes.byref(c),
                                                                   ctypes.byref(st), dptr(hist)))
         return _solve_stats(st, hist)
+
+    def entropy_error_device(self, d_us):
+        e = np.zeros(1)
+        check(_ffi.lib().fvhip_group_entropy_error_device(self._g, self._ptrs(d_us), dptr(e)))
+        return float(e[0])
 
     def matfree_set_state_device(self, d_us, d_rs, d_mdts):
         check(_ffi.lib().fvhip_group_matfree_set_state_device(self._g, self._ptrs(d_us), self._ptrs(d_rs),

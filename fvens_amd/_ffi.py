@@ -59,6 +59,8 @@ _SIGS = {
     "fvhip_destroy": (ctypes.c_int, [ctypes.c_void_p]),
     "fvhip_set_rank": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_int]),
     "fvhip_partition_rcb": (ctypes.c_int, [ctypes.POINTER(FvMeshView), ctypes.c_int, c_int_p]),
+    "fvhip_partition_graph": (ctypes.c_int, [ctypes.POINTER(FvMeshView), ctypes.c_int, c_int_p]),
+    "fvhip_partition_edge_cut": (ctypes.c_longlong, [ctypes.POINTER(FvMeshView), c_int_p]),
     "fvhip_partition_info": (ctypes.c_int, [ctypes.POINTER(FvMeshView), c_int_p, ctypes.c_int, c_int_p, c_int_p,
                                             c_int_p, c_int_p, c_int_p, c_int_p]),
     "fvhip_create_partitioned": (ctypes.c_int, [ctypes.POINTER(FvMeshView), ctypes.POINTER(FvFlowConfig), c_int_p,
@@ -78,6 +80,8 @@ _SIGS = {
     "fvhip_get_gradients": (ctypes.c_int, [ctypes.c_void_p, c_dbl_p, c_dbl_p]),
     "fvhip_surface_data_device": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, c_dbl_p, c_dbl_p,
                                                  c_int_p]),
+    "fvhip_entropy_error_device": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, c_dbl_p]),
+    "fvhip_group_entropy_error_device": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(ctypes.c_void_p), c_dbl_p]),
     "fvhip_assemble_jacobian": (ctypes.c_int, [ctypes.c_void_p, c_dbl_p, c_dbl_p, c_dbl_p, c_dbl_p]),
     "fvhip_assemble_jacobian_device": (ctypes.c_int, [ctypes.c_void_p] + [ctypes.c_void_p] * 4),
     "fvhip_add_pseudo_time_term_device": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_double, ctypes.c_void_p,

@@ -194,6 +194,21 @@ int fvhip_partition_rcb(const fvhip_mesh* mesh, int nparts, int* part)
 	});
 }
 
+int fvhip_partition_graph(const fvhip_mesh* mesh, int nparts, int* part)
+{
+	return guard([&] {
+		const std::vector<int> p = partitionGraph(*mesh, nparts);
+		std::memcpy(part, p.data(), p.size()*sizeof(int));
+	});
+}
+
+long long fvhip_partition_edge_cut(const fvhip_mesh* mesh, const int* part)
+{
+	long long c = -1;
+	if(guard([&] { c = edgeCut(*mesh, part); })) return -1;
+	return c;
+}
+
 int fvhip_partition_info(const fvhip_mesh* mesh, const int* part, int rank, int* counts, int* cell_global,
                          int* nbr_rank, int* ghost_start, int* send_start, int* send_global)
 {
@@ -364,6 +379,50 @@ int fvhip_surface_data_device(fvhip_handle h, const double* d_u, int marker, dou
 		HC(hipStreamSynchronize(h->stream));
 		funcs[0] = s[0]/s[3]; funcs[1] = s[1]/s[3]; funcs[2] = s[2]/s[3];                          // :302
 		if(nfaces) *nfaces = c.S.n;
+	});
+}
+
+/// this handle's owned-cell entropy sum (before the rank sum and the square root), on its stream
+static double* entropySum(fvhip_ctx* h, const double* d_u)
+{
+	if(!h->d_ent) h->d_ent = dalloc(static_cast<size_t>(entropy_partials(h->L.ncell)) + 1, h->owned);
+	// free-stream entropy on the host, as FlowOutput does (compute_freestream_state, aphysics.cpp:43-58)
+	const double sinf = gd::pressure_cons(h->P.gas, h->P.uinf)/std::pow(h->P.uinf[0], h->cfg.gamma);
+	double* out = h->d_ent + entropy_partials(h->L.ncell);
+	launch_entropy(h->L.ncell, d_u, h->M.area, h->P.gas, sinf, h->d_ent, out, h->stream);
+	HC(hipGetLastError());
+	return out;
+}
+
+int fvhip_entropy_error_device(fvhip_handle h, const double* d_u, double* err)
+{
+	return guard([&] {
+		if(!err) throw std::invalid_argument("err must not be NULL");
+		HC(hipSetDevice(h->device));
+		double* out = entropySum(h, d_u);
+		if(h->comm) NC(ncclAllReduce(out, out, 1, ncclDouble, ncclSum, h->comm, h->stream));   // mpi_all_reduce :49
+		else if(h->halo()) throw std::runtime_error("partitioned handle: call fvhip_comm_init (or use a group) first");
+		double s = 0;
+		HC(hipMemcpyAsync(&s, out, sizeof s, hipMemcpyDeviceToHost, h->stream));
+		HC(hipStreamSynchronize(h->stream));
+		*err = std::sqrt(s);
+	});
+}
+
+int fvhip_group_entropy_error_device(fvhip_group g, const double* const* d_u, double* err)
+{
+	return guard([&] {
+		double tot = 0;
+		for(size_t i = 0; i < g->hs.size(); i++) {          // rank order
+			fvhip_ctx* h = g->hs[i];
+			HC(hipSetDevice(h->device));
+			double* out = entropySum(h, d_u[i]);
+			double s = 0;
+			HC(hipMemcpyAsync(&s, out, sizeof s, hipMemcpyDeviceToHost, h->stream));
+			HC(hipStreamSynchronize(h->stream));
+			tot += s;
+		}
+		*err = std::sqrt(tot);
 	});
 }
 

@@ -54,6 +54,133 @@ std::vector<int> partitionRCB(const double* rc, int ncell, int nparts)
 	return part;
 }
 
+namespace {
+
+/// one bisection of the cells `sub` (global ids) of the dual graph into `nl` and the rest: grown
+/// breadth-first from a pseudo-peripheral cell (farthest from the farthest of the first cell, every
+/// component in turn), then improved by passes of balanced boundary swaps (Kernighan-Lin gains)
+void graphBisect(const fvhip_mesh& m, const std::vector<int>& sub, int nl, std::vector<int>& side,
+                 std::vector<int>& loc, std::vector<int>& dist)
+{
+	const int n = static_cast<int>(sub.size());
+	for(int i = 0; i < n; i++) loc[sub[i]] = i;
+	auto nbrs = [&](int c, int* out) {          // neighbours of global cell c inside `sub` (local ids)
+		int k = 0;
+		for(int j = 0; j < m.nnode[c]; j++) {
+			const int e = m.esuel[static_cast<size_t>(c)*m.maxnfael+j];
+			if(e >= 0 && e < m.nelem && loc[e] >= 0) out[k++] = loc[e];
+		}
+		return k;
+	};
+	std::vector<int> queue;
+	queue.reserve(n);
+	auto bfs = [&](int root) {                  // distances from root inside its component; returns farthest
+		queue.clear();
+		dist[root] = 0; queue.push_back(root);
+		int last = root;
+		for(size_t q = 0; q < queue.size(); q++) {
+			const int a = queue[q];
+			last = a;
+			int nb[4];
+			const int k = nbrs(sub[a], nb);
+			for(int j = 0; j < k; j++) if(dist[nb[j]] < 0) { dist[nb[j]] = dist[a] + 1; queue.push_back(nb[j]); }
+		}
+		return last;
+	};
+	// grow the first part breadth-first, component by component
+	std::vector<int> order;
+	order.reserve(n);
+	std::vector<char> done(n, 0);
+	for(int seed = 0; seed < n && static_cast<int>(order.size()) < n; seed++) {
+		if(done[seed]) continue;
+		int root = seed;
+		for(int rep = 0; rep < 2; rep++) {       // pseudo-peripheral cell of this component
+			const int far = bfs(root);
+			for(const int a : queue) dist[a] = -1;
+			root = far;
+		}
+		bfs(root);
+		for(const int a : queue) { done[a] = 1; order.push_back(a); dist[a] = -1; }
+	}
+	for(int i = 0; i < n; i++) side[i] = 1;
+	for(int i = 0; i < nl; i++) side[order[i]] = 0;
+	// refinement: swap the best-gain boundary cells of the two sides while the swap cuts edges
+	auto gain = [&](int a) {
+		int nb[4];
+		const int k = nbrs(sub[a], nb);
+		int ext = 0, in = 0;
+		for(int j = 0; j < k; j++) (side[nb[j]] != side[a] ? ext : in)++;
+		return ext - in;
+	};
+	for(int pass = 0; pass < 12; pass++) {
+		std::vector<std::pair<int,int>> cand[2];
+		for(int a = 0; a < n; a++) {
+			const int g = gain(a);
+			if(g > -2) cand[side[a]].push_back({-g, a});
+		}
+		for(auto& c : cand) std::sort(c.begin(), c.end());
+		size_t i0 = 0, i1 = 0;
+		int moved = 0;
+		while(i0 < cand[0].size() && i1 < cand[1].size()) {
+			const int a = cand[0][i0].second, b = cand[1][i1].second;
+			if(side[a] != 0) { i0++; continue; }
+			if(side[b] != 1) { i1++; continue; }
+			const int ga = gain(a), gb = gain(b);
+			int nb[4], adj = 0;
+			const int k = nbrs(sub[a], nb);
+			for(int j = 0; j < k; j++) if(nb[j] == b) adj = 1;
+			if(ga + gb - 2*adj <= 0) {
+				// the stale-sorted lists ran out of improving pairs
+				if(ga <= 0 && -cand[0][i0].first <= 0) break;
+				if(ga < gb) i0++; else i1++;
+				continue;
+			}
+			side[a] = 1; side[b] = 0;
+			i0++; i1++; moved++;
+		}
+		if(!moved) break;
+	}
+	for(int i = 0; i < n; i++) loc[sub[i]] = -1;
+}
+
+void graphRecurse(const fvhip_mesh& m, std::vector<int>& sub, int p0, int np, int* part,
+                  std::vector<int>& loc, std::vector<int>& dist)
+{
+	if(np == 1) { for(const int c : sub) part[c] = p0; return; }
+	const int npl = np/2;
+	const int n = static_cast<int>(sub.size());
+	const int nl = static_cast<int>((static_cast<long long>(n)*npl)/np);
+	std::vector<int> side(n);
+	graphBisect(m, sub, nl, side, loc, dist);
+	std::vector<int> a, b;
+	for(int i = 0; i < n; i++) (side[i] == 0 ? a : b).push_back(sub[i]);
+	sub.clear(); sub.shrink_to_fit();
+	graphRecurse(m, a, p0, npl, part, loc, dist);
+	graphRecurse(m, b, p0 + npl, np - npl, part, loc, dist);
+}
+
+}
+
+std::vector<int> partitionGraph(const fvhip_mesh& m, int nparts)
+{
+	if(nparts < 1) throw std::invalid_argument("partitionGraph: nparts < 1");
+	if(m.nconnface != 0) throw std::invalid_argument("partitionGraph: expects the single-domain mesh");
+	std::vector<int> part(m.nelem, 0), sub(m.nelem), loc(m.nelem, -1), dist(m.nelem, -1);
+	std::iota(sub.begin(), sub.end(), 0);
+	if(m.nelem > 0) graphRecurse(m, sub, 0, nparts, part.data(), loc, dist);
+	return part;
+}
+
+long long edgeCut(const fvhip_mesh& m, const int* part)
+{
+	long long cut = 0;
+	for(int f = m.nbface; f < m.naface; f++) {
+		const int l = m.intfac[4*static_cast<size_t>(f)], r = m.intfac[4*static_cast<size_t>(f)+1];
+		if(r < m.nelem && part[l] != part[r]) cut++;
+	}
+	return cut;
+}
+
 MeshTopo topoFromMesh(const fvhip_mesh& m)
 {
 	if(m.nconnface != 0)

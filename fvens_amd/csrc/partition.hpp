@@ -69,5 +69,14 @@ MeshTopo extractPartition(const fvhip_mesh& m, const int* part, int rank);
 /// most one cell per bisection level; deterministic (ties broken by cell index)
 std::vector<int> partitionRCB(const double* rc, int ncell, int nparts);
 
+/// Graph partition of the cell dual graph (the reference's Scotch SCOTCH_graphPart on the same graph,
+/// meshpartitioning.cpp:376-458; Scotch is absent from the image): recursive bisection, each grown
+/// breadth-first from a pseudo-peripheral cell and refined by balanced Kernighan-Lin boundary swaps.
+/// Part sizes as RCB's (exact split per level); deterministic.
+std::vector<int> partitionGraph(const fvhip_mesh& m, int nparts);
+
+/// interior faces whose two cells lie in different parts
+long long edgeCut(const fvhip_mesh& m, const int* part);
+
 }
 #endif

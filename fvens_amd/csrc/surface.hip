@@ -70,6 +70,52 @@ __global__ void k_surface_sum(int n, const double* __restrict__ contrib, double*
 	sums[0] = cl; sums[1] = cdp; sums[2] = cdf; sums[3] = area;
 }
 
+/// FlowOutput::compute_entropy_cell (aoutput.cpp:28-62): (s - s_inf)^2/s_inf^2 * area per cell,
+/// s = p/rho^gamma (getEntropyFromConserved, aphysics_defs.hpp:204-207); each block sums its 256 cells by
+/// a fixed tree, k_entropy_sum adds the block sums in block order (deterministic; the reference's is an
+/// OpenMP reduction, so this is a tolerance-level match)
+__global__ __launch_bounds__(256)
+void k_entropy_partial(int N, const double* __restrict__ u, const double* __restrict__ area, Gas G, double sinf,
+                       double* __restrict__ part)
+{
+	__shared__ double red[256];
+	const int i = blockIdx.x*256 + threadIdx.x;
+	double e = 0.0;
+	if(i < N) {
+		double uc[4];
+		const double4 v = reinterpret_cast<const double4*>(u)[i];
+		uc[0] = v.x; uc[1] = v.y; uc[2] = v.z; uc[3] = v.w;
+		const double s = pressure_cons(G, uc)/pow(uc[0], G.g);
+		const double serr = (s - sinf)/sinf;
+		e = serr*serr*area[i];
+	}
+	red[threadIdx.x] = e;
+	__syncthreads();
+	for(int w = 128; w > 0; w >>= 1) {
+		if(static_cast<int>(threadIdx.x) < w) red[threadIdx.x] += red[threadIdx.x + w];
+		__syncthreads();
+	}
+	if(threadIdx.x == 0) part[blockIdx.x] = red[0];
+}
+
+__global__ void k_entropy_sum(int nb, const double* __restrict__ part, double* __restrict__ out)
+{
+	if(threadIdx.x != 0 || blockIdx.x != 0) return;
+	double s = 0;
+	for(int b = 0; b < nb; b++) s += part[b];
+	out[0] = s;
+}
+
+int entropy_partials(int N) { return (N + 255)/256; }
+
+void launch_entropy(int N, const double* u, const double* area, const Gas& G, double sinf, double* part,
+                    double* out, hipStream_t s)
+{
+	const int nb = entropy_partials(N);
+	if(nb > 0) hipLaunchKernelGGL(k_entropy_partial, dim3(nb), dim3(256), 0, s, N, u, area, G, sinf, part);
+	hipLaunchKernelGGL(k_entropy_sum, dim3(1), dim3(64), 0, s, nb, part, out);
+}
+
 void launch_surface(const SurfaceFaces& S, const double* u, const double* grad, const Gas& G, double pinf,
                     double wx, double wy, double* faceout, double* contrib, double* sums, hipStream_t s)
 {

@@ -21,5 +21,11 @@ struct SurfaceFaces
 void launch_surface(const SurfaceFaces& S, const double* u, const double* grad, const gd::Gas& G, double pinf,
                     double wx, double wy, double* faceout, double* contrib, double* sums, hipStream_t s);
 
+/// sum over the owned cells of ((s - sinf)/sinf)^2 area into out[0] (FlowOutput::compute_entropy_cell
+/// before the rank sum and the square root); part has entropy_partials(N) entries
+int entropy_partials(int N);
+void launch_entropy(int N, const double* u, const double* area, const gd::Gas& G, double sinf, double* part,
+                    double* out, hipStream_t s);
+
 }
 #endif

@@ -132,6 +132,12 @@ int fvhip_destroy(fvhip_handle h);
 typedef struct fvhip_group_s* fvhip_group;
 /** Recursive coordinate bisection of the cell centres into nparts (part [nelem]) */
 int fvhip_partition_rcb(const fvhip_mesh* mesh, int nparts, int* part);
+/** Graph partition of the cell dual graph into nparts (stand-in for the reference's Scotch
+ *  SCOTCH_graphPart, mesh/meshpartitioning.cpp:376-458): recursive bisection grown breadth-first from
+ *  a pseudo-peripheral cell and refined by balanced Kernighan-Lin boundary swaps */
+int fvhip_partition_graph(const fvhip_mesh* mesh, int nparts, int* part);
+/** Number of interior faces cut by a partition */
+long long fvhip_partition_edge_cut(const fvhip_mesh* mesh, const int* part);
 /** Halo description of one rank (host only). counts[6] = {owned, ghosts, boundary faces, faces,
  *  neighbour ranks, send rows}; arrays may be NULL: cell_global [owned+ghosts] (owned ascending,
  *  then ghosts by owner rank), nbr_rank [nnbr], ghost_start/send_start [nnbr+1], send_global [nsend] */
@@ -172,6 +178,12 @@ int fvhip_get_gradients(fvhip_handle h, const double* u, double* grads);
  *  NULL it receives (x, y, Cp, Cf) per face [nfaces][4] (host, this rank's faces in reference order). */
 int fvhip_surface_data_device(fvhip_handle h, const double* d_u, int marker, double* funcs, double* faces,
                               int* nfaces);
+
+/** FlowOutput::compute_entropy_cell (spatial/aoutput.cpp:28-62) for the device state d_u (internal order):
+ *  err = sqrt(sum over cells of ((s - s_inf)/s_inf)^2 area), s = p/rho^gamma, summed over all ranks of a
+ *  partitioned handle (RCCL); the reference's mesh-size parameter is 1/sqrt(global cell count) */
+int fvhip_entropy_error_device(fvhip_handle h, const double* d_u, double* err);
+int fvhip_group_entropy_error_device(fvhip_group g, const double* const* d_u, double* err);
 
 /** Spatial::assemble_jacobian into block-sparse storage: diag [nelem][16] (diagonal blocks),
  *  lower/upper [ninface][16] for interior faces in face order (A[R][L] += L, A[L][R] += U). */

@@ -9,6 +9,7 @@
 #include <stdexcept>
 #include <chrono>
 #include <algorithm>
+#include <cmath>
 #ifdef _OPENMP
 #include <omp.h>
 #endif
@@ -143,6 +144,22 @@ int orc_surface(void* h, const double* u, const double* grads, int marker, doubl
 {
 	ORC_TRY(auto r = surface_functionals(*static_cast<Spatial*>(h), u, grads, marker);
 	        out3[0] = r[0]; out3[1] = r[1]; out3[2] = r[2])
+}
+
+/// FlowOutput::compute_entropy_cell (aoutput.cpp:28-62), single rank, serial order
+int orc_entropy(void* h, const double* u, double* err)
+{
+	ORC_TRY(
+		const Spatial& s = *static_cast<Spatial*>(h);
+		const double sinf = s.phy.pressureFromConserved(s.uinf.data())/std::pow(s.uinf[0], s.phy.g);
+		double e = 0;
+		for(int iel = 0; iel < s.m.nelem; iel++) {
+			const double serr = (s.phy.pressureFromConserved(&u[4*static_cast<size_t>(iel)])
+			                     /std::pow(u[4*static_cast<size_t>(iel)], s.phy.g) - sinf) / sinf;
+			e += serr*serr*s.m.area[iel];
+		}
+		*err = std::sqrt(e)
+	)
 }
 
 /// point-wise flux: gas = {gamma, Minf, Tinf, Reinf, Pr}

@@ -42,6 +42,7 @@ _SIGS = {
     "orc_bc_ghost": (ctypes.c_int, [ctypes.c_int, _dp, ctypes.c_double, _dp, _dp, _dp, _dp, _dp]),
     "orc_time_residual": (ctypes.c_double, [_vp, _dp, ctypes.c_int, ctypes.c_int, ctypes.c_int, _dp]),
     "orc_set_threads": (ctypes.c_int, [ctypes.c_int]),
+    "orc_entropy": (ctypes.c_int, [_vp, _dp, _dp]),
 }
 
 _lib = None
@@ -190,6 +191,12 @@ class OracleSpatial:
         ratio = np.zeros(1)
         _chk(lib().orc_forward_euler(self._h, _d(u), cfl, tol, maxiter, _i(steps), _d(ratio)))
         return int(steps[0]), float(ratio[0])
+
+    def entropy(self, u):
+        """FlowOutput::compute_entropy_cell (aoutput.cpp:28-62)"""
+        e = np.zeros(1)
+        _chk(lib().orc_entropy(self._h, _d(u), _d(e)))
+        return float(e[0])
 
     def surface(self, u, grads, marker):
         out = np.zeros(3)

@@ -1,0 +1,83 @@
+"""Order of accuracy, the reference's own entropy-convergence tests (tests/inv-2dcyl/CMakeLists.txt:14-53,
+driver tests/flow_conv.cpp): inviscid flow past a cylinder (inv-cyl-base.ctrl: M 0.38, slip wall 2,
+far field 4) on the reference's nested triangle meshes testcases/2dcylinder/grids/2dcylinder{0..3}.msh,
+solved to steady state by the device pseudo-time drivers (first-order starter, then the second-order
+main solve, casesolvers.cpp:225-314), entropy error by the device FlowOutput::compute_entropy_cell
+(aoutput.cpp:28-62) against the mesh size 1/sqrt(nelem). Pass bar (flow_conv.cpp:77-89): the finest
+pair's slope of log(error) vs log(h) lies in [1.65, 2.1].
+
+Linear solver: the reference's inv_cyl.solverc uses FGMRES (rtol 1e-1, 30 its) with block-Jacobi/ILU(0);
+here device GMRES with block-Jacobi sweeps (same rtol and iteration cap).
+
+Deviation: the implicit main solves run to a 1e-7 residual drop instead of the decks' 1e-5. Stopped at
+1e-5, the device solver's path (block-Jacobi instead of ILU) leaves more algebraic error on the finest
+mesh (measured on MI355X: LS+HLLC finest slope 1.50, GG+HLLC 1.71); converged further, the slopes are
+those of the discretisation itself (LS+HLLC 1.864/1.790/1.656, GG+HLLC 1.934/1.873/1.709, unchanged
+between 1e-8 and 1e-11), which is what the reference's bar is about."""
+import numpy as np
+import pytest
+
+import fvens_amd as fa
+import _oracle as orc
+import cases
+
+pytestmark = pytest.mark.gpu
+
+# (gradient, flux, implicit?, (starter cfl_min, cfl_max, tol, maxit), (main cfl_min, cfl_max, tol, maxit), meshes)
+CASES = {
+    # SpatialFlow_Euler_Cylinder_LeastSquares_HLLC_Tri_EntropyConvergence (inv-cyl-ls-hllc.ctrl)
+    "ls_hllc_implicit": ("LEASTSQUARES", "HLLC", True, (25.0, 500.0, 1e-1, 150), (250.0, 5000.0, 1e-7, 3000), 4),
+    # SpatialFlow_Euler_Cylinder_GreenGauss_HLLC_Tri_EntropyConvergence (inv-cyl-gg-hllc_tri.ctrl)
+    "gg_hllc_implicit": ("GREENGAUSS", "HLLC", True, (25.0, 250.0, 1e-1, 250), (250.0, 1000.0, 1e-7, 3000), 4),
+    # Flow_Explicit_Euler_Cylinder_GreenGauss_Roe_Tri_EntropyConvergence (expl-inv-cyl-gg-roe_tri.ctrl)
+    "gg_roe_explicit": ("GREENGAUSS", "ROE", False, (0.5, 0.7, 1e-1, 15000), (0.25, 0.30, 1e-4, 60000), 3),
+}
+
+
+def solve_entropy(meshname, grad, flux, implicit, init, main):
+    import torch
+    m = fa.UMesh.read_gmsh(cases.fixture_mesh(meshname))
+    p = cases.physics("cyl")
+    n1 = cases.numerics(flux, "NONE", "NONE", order2=False)     # firstorder_spatial_numerics_config
+    n2 = cases.numerics(flux, grad, "NONE")
+    start, sp = fa.FlowFV(m, p, n1), fa.FlowFV(m, p, n2)
+    perm = sp.permutation()
+    u0 = np.tile(cases.freestream(p), (m.nelem, 1))
+    du = torch.tensor(u0[perm], device="cuda")
+    if implicit:
+        lin = dict(lin_rtol=1e-1, lin_maxit=30, restart=30, prec_sweeps=4, min_relax=0.2)
+        st0, _ = start.steady_backward_euler_device(du.data_ptr(), fa.ImplicitConfig(
+            cflinit=init[0], cflfin=init[1], tol=init[2], maxiter=init[3], **lin))
+        st, _ = sp.steady_backward_euler_device(du.data_ptr(), fa.ImplicitConfig(
+            cflinit=main[0], cflfin=main[1], tol=main[2], maxiter=main[3], **lin))
+        converged = st["resratio"] <= 1e-6
+    else:
+        # the explicit solver steps with cfl_min (aodesolver.cpp:194-209)
+        start.steady_forward_euler_device(du.data_ptr(), init[0], init[2], init[3])
+        steps, ratio, _ = sp.steady_forward_euler_device(du.data_ptr(), main[0], main[2], main[3])
+        st, converged = dict(steps=steps, resratio=ratio), ratio <= main[2]
+    err = sp.entropy_error_device(du.data_ptr())
+    u = np.empty_like(u0)
+    u[perm] = du.cpu().numpy()
+    om = orc.OracleMesh.read(cases.fixture_mesh(meshname))
+    err_o = orc.OracleSpatial(om, p, n2).entropy(u)
+    start.close()
+    sp.close()
+    return m.nelem, err, err_o, st, converged
+
+
+@pytest.mark.parametrize("case", list(CASES))
+def test_entropy_convergence(case):
+    grad, flux, implicit, init, main, nmesh = CASES[case]
+    lh, le = [], []
+    for i in range(nmesh):
+        nelem, err, err_o, st, conv = solve_entropy("2dcylinder%d" % i, grad, flux, implicit, init, main)
+        # the device entropy error is the reference's to rounding (a parallel sum; device pow)
+        assert abs(err - err_o) <= 1e-12 * err_o, (err, err_o)
+        assert conv, st
+        lh.append(np.log10(1.0 / np.sqrt(nelem)))
+        le.append(np.log10(err))
+        print(f"{case} mesh {i}: nelem {nelem} log h {lh[-1]:.4f} log err {le[-1]:.6f} {st}")
+    slopes = [(le[i] - le[i - 1]) / (lh[i] - lh[i - 1]) for i in range(1, nmesh)]
+    print(f"{case}: slopes {slopes}")
+    assert 1.65 <= slopes[-1] <= 2.1, slopes
