@@ -7,11 +7,14 @@ Ntheta = 2048, 256 quad + 864 triangle-split layers = 4,063,232 cells, 6,359,040
 Roe flux + weighted-least-squares gradients + MUSCL/Van Albada reconstruction, M 0.8, 1.25 deg.
 One step = one full residual evaluation (primitive conversion, BC ghosts, WLS gradients, fused
 reconstruction/flux/scatter/time-step sweep) with the state resident in HBM.
-Multi-GPU (torchrun, one process per GPU): the mesh is partitioned by recursive coordinate bisection,
-each rank holds its cells plus one ghost layer, and the ghost rows of u and of the gradients are
-exchanged every residual with RCCL ncclSend/ncclRecv over xGMI (the library's own communicator).
---scaling weak (default): the O-grid has N x 2048 cells around, so every GPU owns a C4-size part;
---scaling strong: the C4 mesh itself is split N ways (BASELINE.json config 4).
+Multi-GPU (torchrun, one process per GPU): the mesh is partitioned (--partitioner graph: recursive
+graph bisection of the cell dual graph, the stand-in for the reference's Scotch; or rcb), each rank holds
+its cells plus one ghost layer, and the ghost rows of u and of the gradients are exchanged every
+residual with RCCL ncclSend/ncclRecv over xGMI (the library's own communicator), overlapped with the
+patches that need no halo data.
+--scaling strong (default): the C4 mesh itself is split N ways (BASELINE.json config 4); afterwards every
+rank's owned residual is compared bit for bit with a 1-GPU residual of the whole mesh (halo_parity);
+--scaling weak: the O-grid has N x 2048 cells around, so every GPU owns a C4-size part.
 """
 import argparse
 import json
@@ -189,6 +192,45 @@ def cpu_child(path, threads, nrep):
                       "max_s": float(times.max())}))
 
 
+def halo_parity(fa, torch, dist, mesh, p, n, u, part, rank, world, new_uid):
+    """every rank's owned residual and time steps after one partitioned residual (RCCL halo), compared
+    bit for bit with the 1-GPU residual of the whole mesh that rank 0 computes and broadcasts; returns
+    True only if every owned row on every rank matches"""
+    n.fast_math = False
+    N = mesh.nelem
+    full = torch.zeros((N, 5), dtype=torch.float64, device="cuda")
+    if rank == 0:
+        one = fa.FlowFV(mesh, p, n, device=torch.cuda.current_device())
+        perm = one.permutation()
+        du = torch.tensor(u[perm], device="cuda")
+        dr = torch.zeros((N, 4), dtype=torch.float64, device="cuda")
+        dt = torch.zeros(N, dtype=torch.float64, device="cuda")
+        one.compute_residual_device(du.data_ptr(), dr.data_ptr(), dt.data_ptr(), True, True)
+        one.synchronize()
+        idx = torch.tensor(perm, dtype=torch.int64, device="cuda")
+        full[idx, :4] = dr
+        full[idx, 4] = dt
+        one.close()
+        del du, dr, dt
+    dist.broadcast(full, src=0)
+    sp = fa.FlowFV(mesh, p, n, device=torch.cuda.current_device(), partition=part, rank=rank)
+    sp.comm_init(world, rank, new_uid())
+    owned = np.nonzero(part == rank)[0]
+    gint = owned[sp.permutation()]
+    du = torch.full((sp.nown + sp.nghost, 4), float("nan"), dtype=torch.float64, device="cuda")
+    du[:sp.nown] = torch.tensor(u[gint], device="cuda")
+    dr = torch.zeros((sp.nown, 4), dtype=torch.float64, device="cuda")
+    dt = torch.zeros(sp.nown, dtype=torch.float64, device="cuda")
+    sp.compute_residual_device(du.data_ptr(), dr.data_ptr(), dt.data_ptr(), True, True)
+    sp.synchronize()
+    ref = full[torch.tensor(gint, dtype=torch.int64, device="cuda")]
+    bad = torch.tensor([float((ref[:, :4] != dr).any(dim=1).sum().item() + (ref[:, 4] != dt).sum().item())],
+                       dtype=torch.float64, device="cuda")
+    dist.all_reduce(bad)
+    sp.close()
+    return bool(bad.item() == 0)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -198,7 +240,8 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-sweeps", type=int, default=20, help="timed CPU-baseline sweeps (median)")
     ap.add_argument("--no-fast", action="store_true", help="skip the fast-math mode measurement")
-    ap.add_argument("--scaling", choices=["weak", "strong"], default="weak")
+    ap.add_argument("--scaling", choices=["weak", "strong"], default="strong")
+    ap.add_argument("--partitioner", choices=["graph", "rcb"], default="graph")
     ap.add_argument("--no-pipelined", action="store_true", help="skip the pipelined staged path")
     ap.add_argument("--no-implicit", action="store_true", help="skip the implicit-step figure (1 GPU only)")
     args = ap.parse_args()
@@ -226,8 +269,16 @@ def main():
     u = cases.state(mesh, p, seed=42)
     N, F, Fb = mesh.nelem, mesh.naface, mesh.nbface
     part = None
+    partinfo = None
     if world > 1:
-        part = fa.partition_rcb(mesh, world)
+        tp = time.time()
+        part = fa.partition_graph(mesh, world) if args.partitioner == "graph" else fa.partition_rcb(mesh, world)
+        tp = time.time() - tp
+        partinfo = {"partitioner": args.partitioner + (" (recursive graph bisection, Scotch stand-in)"
+                                                      if args.partitioner == "graph" else " (coordinate bisection)"),
+                    "edge_cut": fa.partition_edge_cut(mesh, part),
+                    "edge_cut_rcb": fa.partition_edge_cut(mesh, fa.partition_rcb(mesh, world)),
+                    "partition_s": round(tp, 2)}
 
     def new_uid():
         """a fresh RCCL unique id for every communicator (an id bootstraps exactly one)"""
@@ -330,6 +381,19 @@ def main():
                                                    / (pms * 1e-3) / 1e9, 1)}
     # the primary measurement: the library's default path for this configuration
     ms_per_step, kernels_ms, stats = measure(False)
+
+    halo = None
+    if world > 1:
+        halo = {"layout_per_rank": None, "halo_parity": None}
+        allstats = [None] * world
+        dist.all_gather_object(allstats, stats)
+        halo["layout_per_rank"] = [{k: st[k] for k in ("cells", "ghosts", "neighbours", "send_rows",
+                                                        "patches", "interior_patches")} for st in allstats]
+        if args.scaling == "strong":
+            try:
+                halo["halo_parity"] = halo_parity(fa, torch, dist, mesh, p, n, u, part, rank, world, new_uid)
+            except Exception as e:          # report, do not lose the measurement
+                halo["halo_parity"] = "error: %s" % e
     sweep_name, sweep_ms = dominant(kernels_ms)
     sweep_name = [sweep_name]
 
@@ -370,7 +434,7 @@ def main():
             "config": {"workload": "C4 mesh, Roe + WLS gradients + MUSCL/Van Albada, 2nd-order residual "
                                    "sweep with local time steps (explicit pseudo-time step)",
                        "cells": N, "faces": F, "boundary_faces": Fb, **dims,
-                       "parallelism": (f"RCB {world}-way partition, RCCL p2p halo (u + gradients)"
+                       "parallelism": (f"{args.partitioner} {world}-way partition, RCCL p2p halo (u + gradients)"
                                        if world > 1 else "single GPU"),
                        "layout": stats, "setup_s": round(t_setup, 2)},
             "roofline": {"bound": "hbm",
@@ -388,6 +452,8 @@ def main():
                          "frac_of_measured_peak": round(achieved / HBM_MEASURED_GBS, 4)},
             "valu_roofline": valu_roofline(tr[2] if tr else None, sweep_ms),
             "kernels_ms": {k: round(v, 5) for k, v in kernels_ms.items()},
+            "multi_gpu": ({**partinfo, **halo} if world > 1 else None),
+            "halo_parity": (halo["halo_parity"] if world > 1 else None),
             "cpu_baseline": cpu,
             "fast_math": fast,
             "staged_path": staged,

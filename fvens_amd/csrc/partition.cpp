@@ -140,6 +140,46 @@ void graphBisect(const fvhip_mesh& m, const std::vector<int>& sub, int nl, std::
 		}
 		if(!moved) break;
 	}
+	// connectivity: a side's small components (cut off by the swaps) join the other side, and the
+	// balance is restored by moving the best-gain boundary cells back
+	std::vector<int> comp(n);
+	for(int round = 0; round < 4; round++) {
+		std::fill(comp.begin(), comp.end(), -1);
+		std::vector<int> csize, cside;
+		for(int a0 = 0; a0 < n; a0++) {
+			if(comp[a0] >= 0) continue;
+			const int id = static_cast<int>(csize.size());
+			queue.clear(); queue.push_back(a0); comp[a0] = id;
+			for(size_t q = 0; q < queue.size(); q++) {
+				int nb[4];
+				const int k = nbrs(sub[queue[q]], nb);
+				for(int j = 0; j < k; j++)
+					if(comp[nb[j]] < 0 && side[nb[j]] == side[a0]) { comp[nb[j]] = id; queue.push_back(nb[j]); }
+			}
+			csize.push_back(static_cast<int>(queue.size())); cside.push_back(side[a0]);
+		}
+		int big[2] = {-1, -1};
+		for(size_t c = 0; c < csize.size(); c++)
+			if(big[cside[c]] < 0 || csize[c] > csize[big[cside[c]]]) big[cside[c]] = static_cast<int>(c);
+		bool flipped = false;
+		for(int a = 0; a < n; a++)
+			if(comp[a] != big[side[a]]) { side[a] = 1 - side[a]; flipped = true; }
+		if(!flipped) break;
+		int n0 = 0;
+		for(int a = 0; a < n; a++) n0 += side[a] == 0;
+		while(n0 != nl) {
+			const int from = n0 > nl ? 0 : 1;
+			int best = -1, bg = -1000;
+			for(int a = 0; a < n; a++) {
+				if(side[a] != from) continue;
+				const int g = gain(a);
+				if(g > bg) { bg = g; best = a; }
+			}
+			if(best < 0) break;
+			side[best] = 1 - from;
+			n0 += from == 0 ? -1 : 1;
+		}
+	}
 	for(int i = 0; i < n; i++) loc[sub[i]] = -1;
 }
 

@@ -171,3 +171,29 @@ def test_subdomains_tile_the_global_mesh():
             # the conn face points out of the subdomain
             assert np.dot(lm.gr[f] - lm.rc[c], lm.facemetric[f, :2]) > 0
     assert (seen[nb:] == 2).all()
+
+
+@pytest.mark.parametrize("nparts", [2, 3, 5, 8])
+def test_graph_partition(nparts):
+    """the Scotch stand-in: complete, exactly balanced per bisection level like RCB, deterministic,
+    parts connected on this O-grid, and a cut of the same order as RCB's"""
+    m = fa.UMesh.naca_ogrid(128, 8, 24)
+    part = fa.partition_graph(m, nparts)
+    counts = np.bincount(part, minlength=nparts)
+    assert counts.min() > 0 and len(counts) == nparts
+    assert counts.max() - counts.min() <= nparts
+    np.testing.assert_array_equal(part, fa.partition_graph(m, nparts))
+    cut = fa.partition_edge_cut(m, part)
+    rcb = fa.partition_edge_cut(m, fa.partition_rcb(m, nparts))
+    assert 0 < cut <= 2 * rcb
+    # connected parts: a BFS over interior faces inside each part reaches all of its cells
+    nb = m.nbface
+    L, R = m.intfac[nb:, 0], m.intfac[nb:, 1]
+    same = part[L] == part[R]
+    import scipy.sparse as sps
+    from scipy.sparse.csgraph import connected_components
+    g = sps.coo_matrix((np.ones(same.sum()), (L[same], R[same])), shape=(m.nelem, m.nelem))
+    ncomp, lab = connected_components(g, directed=False)
+    assert ncomp == nparts
+    # edge cut matches a direct count
+    assert cut == int((part[L] != part[R]).sum())
