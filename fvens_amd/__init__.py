@@ -83,6 +83,8 @@ class ImplicitConfig:
     min_relax: float = 1.0          # nonlinear_update_scheme: >= 1 "full", else "robust_flow" factor
     prec_single: bool = False       # preconditioner blocks stored in fp32 (operator stays fp64)
     prec_gs: bool = False           # multicolour block Gauss-Seidel sweeps instead of block-Jacobi
+    prec_lines: bool = False        # line-implicit (block-tridiagonal along strongly coupled lines)
+    line_threshold: float = 0.0     # strongest/weakest coupling ratio for a cell to join a line (0: 4)
 
     def _struct(self):
         c = _ffi.FvImplicitConfig()
@@ -92,6 +94,8 @@ class ImplicitConfig:
         c.prec_sweeps, c.min_relax = int(self.prec_sweeps), float(self.min_relax)
         c.prec_single = int(self.prec_single)
         c.prec_gs = int(self.prec_gs)
+        c.prec_lines = int(self.prec_lines)
+        c.line_threshold = float(self.line_threshold)
         return c
 
 

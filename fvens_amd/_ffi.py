@@ -39,7 +39,8 @@ class FvImplicitConfig(ctypes.Structure):
                 ("maxiter", ctypes.c_int), ("matrix_free", ctypes.c_int), ("mf_eps", ctypes.c_double),
                 ("lin_rtol", ctypes.c_double), ("lin_maxit", ctypes.c_int), ("restart", ctypes.c_int),
                 ("prec_sweeps", ctypes.c_int), ("min_relax", ctypes.c_double),
-                ("prec_single", ctypes.c_int), ("prec_gs", ctypes.c_int)]
+                ("prec_single", ctypes.c_int), ("prec_gs", ctypes.c_int), ("prec_lines", ctypes.c_int),
+                ("line_threshold", ctypes.c_double)]
 
 
 class FvSolveStats(ctypes.Structure):

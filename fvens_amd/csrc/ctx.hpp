@@ -27,6 +27,9 @@
 #include <stdexcept>
 #include <memory>
 #include <functional>
+#include <array>
+#include <deque>
+#include <numeric>
 
 #include "krylov.hpp"
 
@@ -535,6 +538,97 @@ struct fvhip_ctx
 		std::vector<int> pos(gs_colour_start.begin(), gs_colour_start.end() - 1);
 		for(int c = 0; c < N; c++) cells[pos[col[c]]++] = c;   // ascending within a colour
 		d_gs_cells = upload(cells, owned);
+	}
+
+	/// lines of the line-implicit preconditioner (fvhip_implicit_config::prec_lines), built on first use
+	/// from the mesh: coupling of a cell to a neighbour across an interior face = face length / centre
+	/// distance (what dominates the Jacobian blocks of thin cells). A cell is anisotropic if its
+	/// strongest coupling is at least `thr` times its weakest; lines start at the most anisotropic
+	/// unassigned cell and grow at both ends through the end cell's strongest unassigned owned
+	/// neighbour while that neighbour is anisotropic and the link is one of its own two strongest
+	/// (Mavriplis' line construction); every other cell is a line of one. Lines are sorted by length
+	/// so that a wave's threads walk lines of similar length.
+	LineSet lines{};
+	double lines_thr = -1.0;
+	std::vector<int> h_line_start;
+	void ensureLines(double thr) {
+		if(thr <= 0.0) thr = 4.0;
+		if(lines.start && lines_thr == thr) return;
+		const int N = L.ncell, nb = L.nbface;
+		struct Nb { int c, fi; double w; };
+		std::vector<std::array<Nb,4>> nbr(static_cast<size_t>(N));
+		std::vector<int> nn(static_cast<size_t>(N), 0);
+		std::vector<double> ratio(static_cast<size_t>(N), 1.0);
+		for(int c = 0; c < N; c++) {
+			double wmax = 0, wmin = INFINITY;
+			for(int j = 0; j < 4; j++) {
+				const int code = L.cell_rfaces[4*static_cast<size_t>(c)+j];
+				if(code < 0 || (code >> 1) < nb) continue;           // boundary face
+				const int fi = (code >> 1) - nb;
+				const int o = L.cell_nbr_fo[4*static_cast<size_t>(c)+j];
+				const double dx = L.rc[2*static_cast<size_t>(c)] - L.rc[2*static_cast<size_t>(o)];
+				const double dy = L.rc[2*static_cast<size_t>(c)+1] - L.rc[2*static_cast<size_t>(o)+1];
+				const double w = L.if_len[fi]/std::sqrt(dx*dx + dy*dy);
+				wmax = std::max(wmax, w); wmin = std::min(wmin, w);
+				if(o < N) nbr[c][nn[c]++] = Nb{o, fi, w};
+			}
+			std::sort(nbr[c].begin(), nbr[c].begin() + nn[c], [](const Nb& a, const Nb& b) {
+				return a.w > b.w || (a.w == b.w && a.c < b.c); });
+			if(wmin < INFINITY && wmin > 0) ratio[c] = wmax/wmin;
+		}
+		auto strong2 = [&](int c, int o) {               // o among c's two strongest owned neighbours
+			for(int j = 0; j < std::min(nn[c], 2); j++) if(nbr[c][j].c == o) return true;
+			return false;
+		};
+		std::vector<int> order(static_cast<size_t>(N));
+		std::iota(order.begin(), order.end(), 0);
+		std::stable_sort(order.begin(), order.end(), [&](int a, int b) { return ratio[a] > ratio[b]; });
+		std::vector<char> used(static_cast<size_t>(N), 0);
+		std::vector<std::vector<std::pair<int,int>>> all;   // (cell, face to previous) per line
+		for(const int c0 : order) {
+			if(used[c0]) continue;
+			used[c0] = 1;
+			std::deque<std::pair<int,int>> line{{c0, -1}};
+			if(ratio[c0] >= thr) {
+				for(int dir = 0; dir < 2; dir++) {
+					int e = dir == 0 ? line.back().first : line.front().first;
+					for(;;) {
+						int nxt = -1, fi = -1;
+						for(int j = 0; j < std::min(nn[e], 2); j++) {
+							const Nb& b = nbr[e][j];
+							if(!used[b.c]) { nxt = b.c; fi = b.fi; break; }
+						}
+						if(nxt < 0 || ratio[nxt] < thr || !strong2(nxt, e)) break;
+						used[nxt] = 1;
+						if(dir == 0) line.push_back({nxt, fi});
+						else {                              // prepend: the face now links nxt to e
+							line.front().second = fi;
+							line.push_front({nxt, -1});
+						}
+						e = nxt;
+					}
+				}
+			}
+			all.emplace_back(line.begin(), line.end());
+		}
+		std::stable_sort(all.begin(), all.end(), [](const std::vector<std::pair<int,int>>& a,
+		                                            const std::vector<std::pair<int,int>>& b) { return a.size() > b.size(); });
+		std::vector<int> st(1, 0), cells, faces;
+		for(const auto& ln : all) {
+			for(size_t k = 0; k < ln.size(); k++) {
+				cells.push_back(ln[k].first);
+				if(k == 0) { faces.push_back(-1); continue; }
+				const int fi = ln[k].second, p = ln[k-1].first;
+				faces.push_back((fi << 1) | (L.if_L[fi] == p ? 0 : 1));
+			}
+			st.push_back(static_cast<int>(cells.size()));
+		}
+		lines.nlines = static_cast<int>(all.size());
+		lines.start = upload(st, owned);
+		lines.cell = upload(cells, owned);
+		lines.face = upload(faces, owned);
+		h_line_start = st;
+		lines_thr = thr;
 	}
 
 	/// fp32 copies of the preconditioner blocks (fvhip_implicit_config::prec_single)

@@ -95,6 +95,8 @@ struct LinOp
 	bool matfree = false;
 	bool single = false;                      ///< preconditioner blocks in fp32 (iw.sdinv/slo/sup)
 	bool gs = false;                          ///< multicolour block Gauss-Seidel instead of Jacobi
+	bool lines = false;                       ///< line-implicit (block-tridiagonal along lines)
+	double line_thr = 0.0;
 	int sweeps = 1;
 	std::vector<const double*> D, Lo, Up;     ///< per handle: diagonal / lower / upper blocks
 
@@ -113,6 +115,7 @@ struct LinOp
 	/// alternate between z and aux (both with ghost rows) so that the last one lands in z.
 	void precondition(const ArrayOf& v, const ArrayOf& z) {
 		if(gs) { gaussSeidel(v, z); return; }
+		if(lines) { lineSweeps(v, z); return; }
 		const ArrayOf aux = [&](size_t i) { return S.hs[i]->iw.aux; };
 		auto buf = [&](int k) -> const ArrayOf& { return ((sweeps - 1 - k) % 2 == 0) ? z : aux; };
 		S.each([&](size_t i, fvhip_ctx* h) {
@@ -157,9 +160,31 @@ struct LinOp
 			});
 		}
 	}
-	/// block inverses of the current diagonal blocks
+	/// z = M^-1 v with M the block-tridiagonal line part of A (factorised in setup), then `sweeps` - 1
+	/// corrections z += M^-1 (v - A z) (A with the ghost coupling: block-Jacobi across ranks)
+	void lineSweeps(const ArrayOf& v, const ArrayOf& z) {
+		const ArrayOf aux = [&](size_t i) { return S.hs[i]->iw.aux; };
+		const ArrayOf t = [&](size_t i) { return S.hs[i]->iw.t; };
+		S.each([&](size_t i, fvhip_ctx* h) {
+			h->timed("k_line_solve", [&]{ launch_line_solve(h->lines, h->iw.dinv, Lo[i], Up[i], v(i), z(i), h->stream); });
+		});
+		for(int k = 1; k < sweeps; k++) {
+			blocks(z, t);
+			S.each([&](size_t i, fvhip_ctx* h) {
+				launch_axpby(4LL*h->L.ncell, 1.0, v(i), -1.0, t(i), h->stream);
+				h->timed("k_line_solve", [&]{ launch_line_solve(h->lines, h->iw.dinv, Lo[i], Up[i], t(i), aux(i), h->stream); });
+				launch_add_rows(h->L.ncell, aux(i), z(i), h->stream);
+			});
+		}
+	}
+	/// block inverses of the current diagonal blocks (or the line factorisation)
 	void setup() {
 		S.each([&](size_t i, fvhip_ctx* h) {
+			if(lines) {
+				h->ensureLines(line_thr);
+				h->timed("k_line_factor", [&]{ launch_line_factor(h->lines, D[i], Lo[i], Up[i], h->iw.dinv, h->stream); });
+				return;
+			}
 			h->timed("k_bjac_invert", [&]{ launch_bjac_invert(h->L.ncell, D[i], h->iw.dinv, h->stream); });
 			if(gs) h->ensureColouring();
 			if(single) {
@@ -316,6 +341,9 @@ static void backwardEuler(System& S, const std::vector<double*>& us, const fvhip
 	A.sweeps = c.prec_sweeps;
 	A.single = c.prec_single != 0;
 	A.gs = c.prec_gs != 0;
+	A.lines = c.prec_lines != 0;
+	A.line_thr = c.line_threshold;
+	if(A.lines && (A.gs || A.single)) throw std::invalid_argument("prec_lines does not combine with prec_gs / prec_single");
 	for(fvhip_ctx* h : S.hs) { A.D.push_back(h->iw.jd); A.Lo.push_back(h->iw.jlo); A.Up.push_back(h->iw.jup); }
 	std::vector<const double*> cu(us.begin(), us.end());
 	std::vector<double*> rs, dts;

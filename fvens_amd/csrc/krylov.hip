@@ -49,20 +49,14 @@ __device__ __forceinline__ void blk_mv(const double* __restrict__ B, const doubl
 // -------------------------------------------------------------------------------------------------
 // point-block Jacobi
 // -------------------------------------------------------------------------------------------------
-__global__ __launch_bounds__(256)
-void k_bjac_invert(int n, const double* __restrict__ diag, double* __restrict__ dinv)
+/// b = a^-1 for a 4x4 block (Gauss-Jordan, partial pivoting by selects: static register indices only);
+/// a is destroyed
+__device__ __forceinline__ void inv4(double (&a)[4][4], double (&b)[4][4])
 {
-	const int c = blockIdx.x*blockDim.x + threadIdx.x;
-	if(c >= n) return;
-	double a[4][4], b[4][4];
-	const double4* d4 = reinterpret_cast<const double4*>(diag + 16*static_cast<size_t>(c));
 	#pragma unroll
-	for(int i = 0; i < 4; i++) {
-		const double4 v = d4[i];
-		a[i][0] = v.x; a[i][1] = v.y; a[i][2] = v.z; a[i][3] = v.w;
+	for(int i = 0; i < 4; i++)
 		#pragma unroll
 		for(int j = 0; j < 4; j++) b[i][j] = i == j ? 1.0 : 0.0;
-	}
 	#pragma unroll
 	for(int k = 0; k < 4; k++) {
 		// bring the largest |a[i][k]|, i >= k, to row k with selects (static register indices only)
@@ -87,9 +81,31 @@ void k_bjac_invert(int n, const double* __restrict__ diag, double* __restrict__ 
 			for(int j = 0; j < 4; j++) { a[i][j] -= f*a[k][j]; b[i][j] -= f*b[k][j]; }
 		}
 	}
-	double4* o = reinterpret_cast<double4*>(dinv + 16*static_cast<size_t>(c));
+}
+
+__device__ __forceinline__ void ld16(const double* __restrict__ p, double (&a)[4][4])
+{
+	const double4* d4 = reinterpret_cast<const double4*>(p);
 	#pragma unroll
-	for(int i = 0; i < 4; i++) o[i] = make_double4(b[i][0], b[i][1], b[i][2], b[i][3]);
+	for(int i = 0; i < 4; i++) { const double4 v = d4[i]; a[i][0] = v.x; a[i][1] = v.y; a[i][2] = v.z; a[i][3] = v.w; }
+}
+
+__device__ __forceinline__ void st16(double* __restrict__ p, const double (&a)[4][4])
+{
+	double4* o = reinterpret_cast<double4*>(p);
+	#pragma unroll
+	for(int i = 0; i < 4; i++) o[i] = make_double4(a[i][0], a[i][1], a[i][2], a[i][3]);
+}
+
+__global__ __launch_bounds__(256)
+void k_bjac_invert(int n, const double* __restrict__ diag, double* __restrict__ dinv)
+{
+	const int c = blockIdx.x*blockDim.x + threadIdx.x;
+	if(c >= n) return;
+	double a[4][4], b[4][4];
+	ld16(diag + 16*static_cast<size_t>(c), a);
+	inv4(a, b);
+	st16(dinv + 16*static_cast<size_t>(c), b);
 }
 
 /// y = B x for a row-major fp32 4x4 block, entries widened to fp64
@@ -236,6 +252,125 @@ void k_relaxed_update(int n, gd::Gas G, double minfactor, const double* __restri
 // -------------------------------------------------------------------------------------------------
 // launchers
 // -------------------------------------------------------------------------------------------------
+// -------------------------------------------------------------------------------------------------
+// line-implicit preconditioner: block-tridiagonal solves along lines of strongly coupled cells
+// -------------------------------------------------------------------------------------------------
+/// the coupling blocks between line cells k-1 = p and k = c through interior face code fc = fi<<1 | o:
+/// o = 0: p is the face's L, so A[c][p] = lower[fi] (A[R][L]) and A[p][c] = upper[fi]; o = 1: swapped
+__device__ __forceinline__ const double* blk_cp(int fc, const double* lower, const double* upper) {
+	return ((fc & 1) ? upper : lower) + 16*static_cast<size_t>(fc >> 1);
+}
+__device__ __forceinline__ const double* blk_pc(int fc, const double* lower, const double* upper) {
+	return ((fc & 1) ? lower : upper) + 16*static_cast<size_t>(fc >> 1);
+}
+
+/// block-Thomas factorisation per line (one thread per line): dinvp_k = (D_k - A[k][k-1] dinvp_{k-1} A[k-1][k])^-1
+__global__ __launch_bounds__(64)
+void k_line_factor(int nlines, const int* __restrict__ lstart, const int* __restrict__ lcell, const int* __restrict__ lface,
+                   const double* __restrict__ diag, const double* __restrict__ lower, const double* __restrict__ upper,
+                   double* __restrict__ dinvp)
+{
+	const int l = blockIdx.x*blockDim.x + threadIdx.x;
+	if(l >= nlines) return;
+	const int k0 = lstart[l], k1 = lstart[l+1];
+	double prev[4][4];             // dinvp of the previous line cell
+	for(int k = k0; k < k1; k++) {
+		const int c = lcell[k];
+		double a[4][4], b[4][4];
+		ld16(diag + 16*static_cast<size_t>(c), a);
+		if(k > k0) {
+			const int fc = lface[k];
+			double L[4][4], U[4][4], t[4][4];
+			ld16(blk_cp(fc, lower, upper), L);
+			ld16(blk_pc(fc, lower, upper), U);
+			// t = prev * U ; a -= L * t
+			#pragma unroll
+			for(int i = 0; i < 4; i++)
+				#pragma unroll
+				for(int j = 0; j < 4; j++) t[i][j] = prev[i][0]*U[0][j] + prev[i][1]*U[1][j] + prev[i][2]*U[2][j] + prev[i][3]*U[3][j];
+			#pragma unroll
+			for(int i = 0; i < 4; i++)
+				#pragma unroll
+				for(int j = 0; j < 4; j++) a[i][j] -= L[i][0]*t[0][j] + L[i][1]*t[1][j] + L[i][2]*t[2][j] + L[i][3]*t[3][j];
+		}
+		inv4(a, b);
+		st16(dinvp + 16*static_cast<size_t>(c), b);
+		#pragma unroll
+		for(int i = 0; i < 4; i++)
+			#pragma unroll
+			for(int j = 0; j < 4; j++) prev[i][j] = b[i][j];
+	}
+}
+
+/// z = Lines^-1 v per line (one thread per line): forward g_k = dinvp_k (v_k - A[k][k-1] g_{k-1}) into z,
+/// then backward z_k = g_k - dinvp_k A[k][k+1] z_{k+1}
+__global__ __launch_bounds__(64)
+void k_line_solve(int nlines, const int* __restrict__ lstart, const int* __restrict__ lcell, const int* __restrict__ lface,
+                  const double* __restrict__ dinvp, const double* __restrict__ lower, const double* __restrict__ upper,
+                  const double* __restrict__ v, double* __restrict__ z)
+{
+	const int l = blockIdx.x*blockDim.x + threadIdx.x;
+	if(l >= nlines) return;
+	const int k0 = lstart[l], k1 = lstart[l+1];
+	double4 g = make_double4(0, 0, 0, 0);
+	for(int k = k0; k < k1; k++) {
+		const int c = lcell[k];
+		double4 r = reinterpret_cast<const double4*>(v)[c];
+		if(k > k0) {
+			double t[4];
+			blk_mv(blk_cp(lface[k], lower, upper), g, t);
+			r.x -= t[0]; r.y -= t[1]; r.z -= t[2]; r.w -= t[3];
+		}
+		double y[4];
+		blk_mv(dinvp + 16*static_cast<size_t>(c), r, y);
+		g = make_double4(y[0], y[1], y[2], y[3]);
+		reinterpret_cast<double4*>(z)[c] = g;
+	}
+	double4 x = g;                 // z of the last cell
+	for(int k = k1 - 2; k >= k0; k--) {
+		const int c = lcell[k];
+		double t[4], y[4];
+		blk_mv(blk_pc(lface[k+1], lower, upper), x, t);
+		blk_mv(dinvp + 16*static_cast<size_t>(c), make_double4(t[0], t[1], t[2], t[3]), y);
+		const double4 gk = reinterpret_cast<const double4*>(z)[c];
+		x = make_double4(gk.x - y[0], gk.y - y[1], gk.z - y[2], gk.w - y[3]);
+		reinterpret_cast<double4*>(z)[c] = x;
+	}
+}
+
+/// z += e (4 doubles per cell)
+__global__ __launch_bounds__(256)
+void k_add_rows(int n, const double* __restrict__ e, double* __restrict__ z)
+{
+	const int c = blockIdx.x*blockDim.x + threadIdx.x;
+	if(c >= n) return;
+	const double4 a = reinterpret_cast<const double4*>(e)[c];
+	double4 b = reinterpret_cast<double4*>(z)[c];
+	b.x += a.x; b.y += a.y; b.z += a.z; b.w += a.w;
+	reinterpret_cast<double4*>(z)[c] = b;
+}
+
+void launch_line_factor(const LineSet& Ls, const double* diag, const double* lower, const double* upper, double* dinvp,
+                        hipStream_t s)
+{
+	if(Ls.nlines > 0)
+		hipLaunchKernelGGL(k_line_factor, dim3(nblk(Ls.nlines, 64)), dim3(64), 0, s, Ls.nlines, Ls.start, Ls.cell, Ls.face,
+		                   diag, lower, upper, dinvp);
+}
+
+void launch_line_solve(const LineSet& Ls, const double* dinvp, const double* lower, const double* upper, const double* v,
+                       double* z, hipStream_t s)
+{
+	if(Ls.nlines > 0)
+		hipLaunchKernelGGL(k_line_solve, dim3(nblk(Ls.nlines, 64)), dim3(64), 0, s, Ls.nlines, Ls.start, Ls.cell, Ls.face,
+		                   dinvp, lower, upper, v, z);
+}
+
+void launch_add_rows(int n, const double* e, double* z, hipStream_t s)
+{
+	if(n > 0) hipLaunchKernelGGL(k_add_rows, dim3(nblk(n, 256)), dim3(256), 0, s, n, e, z);
+}
+
 void launch_bjac_invert(int n, const double* diag, double* dinv, hipStream_t s)
 { if(n > 0) k_bjac_invert<<<nblk(n,256), 256, 0, s>>>(n, diag, dinv); }
 void launch_bjac_apply(int n, const double* dinv, const double* x, double* y, hipStream_t s)

@@ -43,6 +43,17 @@ FVHIP_HD double relaxation_factor(const gd::Gas& G, double minfactor, const doub
 }
 
 /// dinv[c] = diag[c]^-1 (Gauss-Jordan with row pivoting), c < ncell
+/// lines of the line-implicit preconditioner (internal cell ids): cells cell[start[l]..start[l+1]) in
+/// line order; face[k] (k > start[l]) = interior face between cells k-1 and k, fi<<1 | (cell k-1 is R)
+struct LineSet { int nlines = 0; const int* start = nullptr; const int* cell = nullptr; const int* face = nullptr; };
+/// block-Thomas factorisation of every line into dinvp [ncell][16]
+void launch_line_factor(const LineSet& Ls, const double* diag, const double* lower, const double* upper, double* dinvp,
+                        hipStream_t s);
+/// z = (block-tridiagonal line part of A)^-1 v
+void launch_line_solve(const LineSet& Ls, const double* dinvp, const double* lower, const double* upper, const double* v,
+                       double* z, hipStream_t s);
+/// z += e over n cells
+void launch_add_rows(int n, const double* e, double* z, hipStream_t s);
 void launch_bjac_invert(int ncell, const double* diag, double* dinv, hipStream_t s);
 /// y[c] = dinv[c] x[c]
 void launch_bjac_apply(int ncell, const double* dinv, const double* x, double* y, hipStream_t s);

@@ -240,6 +240,13 @@ typedef struct fvhip_implicit_config {
 	int prec_gs;              /* 1: multicolour block Gauss-Seidel sweeps (forward/backward colour order on
 	                             alternate sweeps; block-Jacobi across ranks, i.e. PETSc's bjacobi + sor)
 	                             instead of block-Jacobi sweeps */
+	int prec_lines;           /* 1: line-implicit preconditioner: exact block-tridiagonal solves along lines of
+	                             strongly coupled cells (wall-normal in boundary layers; the coupling the
+	                             reference's line ordering, mesh/ameshutils.cpp hybridLineReorder, exploits),
+	                             block-Jacobi between lines and across ranks; prec_sweeps - 1 further
+	                             residual-correction sweeps. Not combined with prec_gs / prec_single. */
+	double line_threshold;    /* a cell joins a line if its strongest coupling (face length / centre distance)
+	                             is at least this many times its weakest (0: 4.0) */
 } fvhip_implicit_config;
 
 typedef struct fvhip_solve_stats {

@@ -99,9 +99,10 @@ def test_gmres_blocks_matches_direct_solve():
     dev.close()
 
 
-@pytest.mark.parametrize("min_relax,single,gs", [(1.0, False, False), (0.2, False, False), (1.0, True, False),
-                                                 (1.0, False, True), (1.0, True, True)])
-def test_one_backward_euler_step_matches_host(min_relax, single, gs):
+@pytest.mark.parametrize("min_relax,single,gs,lines", [(1.0, False, False, False), (0.2, False, False, False),
+                                                       (1.0, True, False, False), (1.0, False, True, False),
+                                                       (1.0, True, True, False), (1.0, False, False, True)])
+def test_one_backward_euler_step_matches_host(min_relax, single, gs, lines):
     m, om = get_mesh("naca_small")
     p = cases.physics("naca")
     n = cases.numerics("ROE", "LEASTSQUARES", "VANALBADA")
@@ -115,7 +116,7 @@ def test_one_backward_euler_step_matches_host(min_relax, single, gs):
     perm = dev.permutation()
     dU = to_device(u0, perm)
     cfg = fa.ImplicitConfig(cflinit=cfl, cflfin=cfl, tol=0.0, maxiter=1, lin_rtol=1e-13, lin_maxit=3000, restart=60,
-                            prec_sweeps=2, min_relax=min_relax, prec_single=single, prec_gs=gs)
+                            prec_sweeps=2, min_relax=min_relax, prec_single=single, prec_gs=gs, prec_lines=lines)
     st, hist = dev.steady_backward_euler_device(dU.data_ptr(), cfg)
     assert st["steps"] == 1 and st["cfl"] == cfl
     u = np.empty_like(u0)
@@ -124,6 +125,30 @@ def test_one_backward_euler_step_matches_host(min_relax, single, gs):
     assert np.all(np.abs(u - u1).max(axis=0) <= 1e-8 * scale), np.abs(u - u1).max(axis=0) / scale
     assert abs(hist[0] - res0) <= 1e-12 * res0
     dev.close()
+
+
+def test_line_preconditioner_cuts_iterations():
+    """the line-implicit preconditioner (prec_lines: block-tridiagonal solves along the wall-normal
+    lines of the O-grid's stretched cells) against point-block Jacobi on the same implicit steps of a
+    wall-resolved mesh (first-cell height 1e-5): far fewer GMRES iterations for one step's linear
+    system at CFL 100, same solution"""
+    m = fa.UMesh.naca_ogrid(128, 16, 24, 20.0, 1e-5)
+    p = cases.physics("naca")
+    n = cases.numerics("ROE", "LEASTSQUARES", "VANALBADA")
+    u0 = cases.state(m, p, 8)
+    out = {}
+    for lines in (False, True):
+        dev = fa.FlowFV(m, p, n)
+        dU = to_device(u0, dev.permutation())
+        cfg = fa.ImplicitConfig(cflinit=100.0, cflfin=100.0, tol=0.0, maxiter=1, lin_rtol=1e-8, lin_maxit=3000,
+                                restart=60, prec_sweeps=1, min_relax=1.0, prec_lines=lines)
+        st, hist = dev.steady_backward_euler_device(dU.data_ptr(), cfg)
+        out[lines] = (st["lin_iters"], dU.cpu().numpy())
+        dev.close()
+    print("GMRES iterations: point-block Jacobi", out[False][0], "lines", out[True][0])
+    assert out[True][0] * 3 <= out[False][0]
+    d = np.abs(out[True][1] - out[False][1]).max(axis=0)
+    assert np.all(d <= 1e-5 * np.abs(u0 - out[False][1]).max(axis=0))
 
 
 def test_matfree_vs_matrix_same_steps():

@@ -46,7 +46,7 @@ def main():
     os.makedirs(out, exist_ok=True)
     shutil.copy(os.path.join(prof, "trace", "run_kernel_stats.csv"), os.path.join(out, "kernel_stats.csv"))
     merged = defaultdict(dict)
-    for sub in ("fetch", "write", "sq", "sq2", "sq3"):
+    for sub in ("fetch", "write", "sq", "sq2", "sq3", "lds"):
         p = os.path.join(prof, sub, "run_counter_collection.csv")
         if not os.path.exists(p):
             continue
