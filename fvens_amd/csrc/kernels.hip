@@ -785,18 +785,18 @@ __device__ __forceinline__ void fused_wls_row(const DevMesh& M, const DevPhys& P
 	double uc[4];
 	ld4(row, 0, uc);
 	const double2 rcc = *reinterpret_cast<const double2*>(row + 12);
-	const int nb[4] = {nb4.x, nb4.y, nb4.z, nb4.w};
 	double f[8] = {0,0,0,0,0,0,0,0};
 	#pragma unroll
 	for(int k = 0; k < 4; k++) {
-		if(nb[k] == -1) break;
+		const int nbk = k == 0 ? nb4.x : (k == 1 ? nb4.y : (k == 2 ? nb4.z : nb4.w));
+		if(nbk == -1) break;
 		double un[4];
 		double2 rn;
-		if(nb[k] >= 0) {
-			ld4(&fz[nb[k]*FZW], 0, un);
-			rn = *reinterpret_cast<const double2*>(&fz[nb[k]*FZW + 12]);
+		if(nbk >= 0) {
+			ld4(&fz[nbk*FZW], 0, un);
+			rn = *reinterpret_cast<const double2*>(&fz[nbk*FZW + 12]);
 		} else {
-			const int bf = -2 - nb[k];
+			const int bf = -2 - nbk;
 			const double4 gp = ghost_prim_of_cell(M, P, B.u, c, bf);
 			un[0] = gp.x; un[1] = gp.y; un[2] = gp.z; un[3] = gp.w;
 			rn = M.bf_rcbp[bf];
@@ -822,65 +822,77 @@ __device__ __forceinline__ void fused_wls_row(const DevMesh& M, const DevPhys& P
 	st8(row + 4, 0, g);
 }
 
-template <int FLUX, int REC, bool DT>
-#ifndef FVHIP_FUSED_WAVES
-#define FVHIP_FUSED_WAVES 4
-#endif
-__global__ void __launch_bounds__(SLOTS_MAX, FVHIP_FUSED_WAVES) k_residual_wls(const DevMesh M, const DevPhys P, const SweepBuffers B)
+/// one patch of the fused residual: uniform (scalar) metadata
+struct FzPatch { int p, s0, s1, c0, c1, nc, e0, nl, ng; const int4* gnbr; };
+/// what one thread loads for its patch before phase 0: its first staged row (state, centre), the
+/// neighbour list and WLS inverse of the gradient it computes first, and the geometry of its face
+struct FzPre { int cf; double ua[4]; double2 rca; int4 nb4a; double4 Va; int2 lrl; double2 nn; double len; };
+
+__device__ __forceinline__ FzPatch fz_patch(const DevMesh& M, const SweepBuffers& B, int pi)
 {
-	extern __shared__ __attribute__((aligned(16))) double fz[];
-	const int np = B.plist ? B.pcount : M.npatch;
-	const int q = (np + 7) >> 3;
-	const int pi = (blockIdx.x & 7) * q + (blockIdx.x >> 3);
-	if(pi >= np) return;
-	const int p = B.plist ? B.plist[pi] : pi;
-	const int s0 = M.patch_slot[p], s1 = M.patch_slot[p+1];
-	const int c0 = M.patch_cell[p], c1 = M.patch_cell[p+1];
-	const int nc = c1 - c0;
-	const int e0 = M.fz_ext_start[p];
-	const int nl = nc + (M.fz_ext_start[p+1] - e0);    // staged rows: patch, ring 1, ring 2
-	const int ng = nc + M.fz_n1[p];                      // rows whose gradients the patch computes
-	const int4* gnbr = M.fz_gnbr + M.fz_g_start[p];
-	const int N = M.ncell;
+	FzPatch q;
+	q.p = B.plist ? B.plist[pi] : pi;
+	q.s0 = M.patch_slot[q.p]; q.s1 = M.patch_slot[q.p+1];
+	q.c0 = M.patch_cell[q.p]; q.c1 = M.patch_cell[q.p+1];
+	q.nc = q.c1 - q.c0;
+	q.e0 = M.fz_ext_start[q.p];
+	q.nl = q.nc + (M.fz_ext_start[q.p+1] - q.e0);    // staged rows: patch, ring 1, ring 2
+	q.ng = q.nc + M.fz_n1[q.p];                       // rows whose gradients the patch computes
+	q.gnbr = M.fz_gnbr + M.fz_g_start[q.p];
+	return q;
+}
+__device__ __forceinline__ int fz_cell(const DevMesh& M, const FzPatch& q, int i)
+{
+	return i < q.nc ? q.c0 + i : M.fz_ext[q.e0 + (i - q.nc)];
+}
+/// the loads of FzPre (a.cf already set): the staged row and the face
+__device__ __forceinline__ void fz_load_rows(const DevMesh& M, const SweepBuffers& B, const FzPatch& q, int t, FzPre& a)
+{
+	a.ua[0] = a.ua[1] = a.ua[2] = a.ua[3] = 0.0;
+	a.rca = make_double2(0, 0);
+	if(t < q.nl) { ld4(B.u, a.cf, a.ua); a.rca = M.rc[a.cf]; }
+	const int s = q.s0 + t;
+	a.lrl = make_int2(0, -1); a.nn = make_double2(0, 0); a.len = 0;
+	if(s < q.s1) { a.lrl = M.fz_slot_lr[s]; a.nn = M.slot_n[s]; a.len = M.slot_len[s]; }
+}
+/// the gradient inputs of the thread's first gradient row
+__device__ __forceinline__ void fz_load_grad(const DevMesh& M, const FzPatch& q, int t, FzPre& a)
+{
+	a.nb4a = make_int4(-1, -1, -1, -1);
+	a.Va = make_double4(0, 0, 0, 0);
+	if(t < q.ng && a.cf < M.nown) { a.nb4a = q.gnbr[t]; a.Va = M.wls_V[a.cf]; }
+}
+
+/// one patch (512 threads): phase 0 stages the primitive states and centres of the patch, ring-1 and
+/// ring-2 cells in LDS; phase 1 computes the WLS gradients of the patch and ring-1 cells; phase 2 one
+/// face per thread (reconstruction, flux, spectral radii); then the fluxes go through LDS and every
+/// cell sums its faces in reference order. hookA runs at the start of phase 1, hookB after the face
+/// work (points at which a caller may issue loads of later work).
+template <int FLUX, int REC, bool DT, typename HA, typename HB>
+__device__ __forceinline__ void fz_body(const DevMesh& M, const DevPhys& P, const SweepBuffers& B, double* fz,
+                                        const FzPatch& q, const FzPre& a, HA&& hookA, HB&& hookB)
+{
 	const Gas& G = P.gas;
 	const int t = static_cast<int>(threadIdx.x);
-	auto cellOf = [&](int i) { return i < nc ? c0 + i : M.fz_ext[e0 + (i - nc)]; };
-
-	// Every load of the patch is issued up front, so the patch waits for one memory round trip:
-	// this thread's first staged row (state, centre), the neighbour list and WLS inverse of the
-	// gradient it computes first, and the geometry of its face (all cells a patch reads are staged)
-	const int s = s0 + t;
-	const int cf = t < nl ? cellOf(t) : 0;
-	double ua[4] = {0, 0, 0, 0};
-	double2 rca = make_double2(0, 0);
-	int4 nb4a = make_int4(-1, -1, -1, -1);
-	double4 Va = make_double4(0, 0, 0, 0);
-	if(t < nl) {
-		ld4(B.u, cf, ua);
-		rca = M.rc[cf];
-		if(t < ng && cf < M.nown) { nb4a = gnbr[t]; Va = M.wls_V[cf]; }
-	}
-	int2 lrl = make_int2(0, -1);
-	double2 nn = make_double2(0, 0);
-	double len = 0;
-	if(s < s1) { lrl = M.fz_slot_lr[s]; nn = M.slot_n[s]; len = M.slot_len[s]; }
+	const int s = q.s0 + t;
 
 	// phase 0: primitive states and centres of the staged cells
-	if(t < nl) stage_row(G, &fz[t*FZW], ua, rca);
-	for(int i = t + SLOTS_MAX; i < nl; i += SLOTS_MAX) {
-		const int c = cellOf(i);
-		double a[4];
-		ld4(B.u, c, a);
-		stage_row(G, &fz[i*FZW], a, M.rc[c]);
+	if(t < q.nl) stage_row(G, &fz[t*FZW], a.ua, a.rca);
+	for(int i = t + SLOTS_MAX; i < q.nl; i += SLOTS_MAX) {
+		const int c = fz_cell(M, q, i);
+		double b[4];
+		ld4(B.u, c, b);
+		stage_row(G, &fz[i*FZW], b, M.rc[c]);
 	}
 	__syncthreads();
 
 	// phase 1: WLS gradients of the patch and ring-1 cells from the staged states
 	// (k_prep_grad_wls arithmetic, neighbours in the same ascending reference face order)
-	if(t < ng) fused_wls_row(M, P, B, fz, &fz[t*FZW], cf, nb4a, Va);
-	for(int i = t + SLOTS_MAX; i < ng; i += SLOTS_MAX) {
-		const int c = cellOf(i);
-		fused_wls_row(M, P, B, fz, &fz[i*FZW], c, c < M.nown ? gnbr[i] : make_int4(-1, -1, -1, -1),
+	hookA();
+	if(t < q.ng) fused_wls_row(M, P, B, fz, &fz[t*FZW], a.cf, a.nb4a, a.Va);
+	for(int i = t + SLOTS_MAX; i < q.ng; i += SLOTS_MAX) {
+		const int c = fz_cell(M, q, i);
+		fused_wls_row(M, P, B, fz, &fz[i*FZW], c, c < M.nown ? q.gnbr[i] : make_int4(-1, -1, -1, -1),
 		              c < M.nown ? M.wls_V[c] : make_double4(0, 0, 0, 0));
 	}
 	__syncthreads();
@@ -888,7 +900,10 @@ __global__ void __launch_bounds__(SLOTS_MAX, FVHIP_FUSED_WAVES) k_residual_wls(c
 	// phase 2: one face per thread (k_sweep arithmetic)
 	double f[4] = {0, 0, 0, 0};
 	double sri = 0, srj = 0;
-	if(s < s1) {
+	if(s < q.s1) {
+		const int2 lrl = a.lrl;
+		const double2 nn = a.nn;
+		const double flen = a.len;
 		const double n[2] = {nn.x, nn.y};
 		const bool bnd = lrl.y < -1;
 		const int bf = -2 - lrl.y;
@@ -964,32 +979,33 @@ __global__ void __launch_bounds__(SLOTS_MAX, FVHIP_FUSED_WAVES) k_residual_wls(c
 		}
 		inviscid_flux<FLUX>(G, ul, ur, n, f);
 		#pragma unroll
-		for(int k = 0; k < 4; k++) f[k] *= len;
+		for(int k = 0; k < 4; k++) f[k] *= flen;
 		if(DT) {
 			const double ci = sound_speed_cons(G, ul), cj = sound_speed_cons(G, ur);
 			const double vni = div_rn(dot2(&ul[1],n), ul[0]);
 			const double vnj = div_rn(dot2(&ur[1],n), ur[0]);
-			sri = (fabs(vni)+ci)*len;
-			srj = (fabs(vnj)+cj)*len;
+			sri = (fabs(vni)+ci)*flen;
+			srj = (fabs(vnj)+cj)*flen;
 		}
 	}
+	hookB();
 	// the cell's face list (and area) are requested before the two barriers of the flux staging,
 	// once the face work no longer holds registers
-	const int c = c0 + t;
+	const int c = q.c0 + t;
 	int4 cs = make_int4(-1, -1, -1, -1);
 	double carea = 0.0;
-	if(c < c1) { cs = M.cell_slots[c]; if(DT) carea = M.area[c]; }
+	if(c < q.c1) { cs = M.cell_slots[c]; if(DT) carea = M.area[c]; }
 	__syncthreads();   // all staged rows read: reuse LDS for the face fluxes
 	double* sf = fz;
 	double* ssr = fz + 4*SLOTS_MAX;
-	if(s < s1) {
+	if(s < q.s1) {
 		sf[0*SLOTS_MAX + t] = f[0]; sf[1*SLOTS_MAX + t] = f[1];
 		sf[2*SLOTS_MAX + t] = f[2]; sf[3*SLOTS_MAX + t] = f[3];
 		if(DT) { ssr[t] = sri; ssr[SLOTS_MAX + t] = srj; }
 	}
 	__syncthreads();
 
-	if(c < c1) {
+	if(c < q.c1) {
 		double r[4];
 		if(B.overwrite) { r[0] = r[1] = r[2] = r[3] = 0.0; }
 		else ld4(B.r, c, r);
@@ -998,7 +1014,7 @@ __global__ void __launch_bounds__(SLOTS_MAX, FVHIP_FUSED_WAVES) k_residual_wls(c
 		#pragma unroll
 		for(int k = 0; k < 4; k++) {
 			if(e[k] < 0) break;
-			const int ls = (e[k] >> 1) - s0;
+			const int ls = (e[k] >> 1) - q.s0;
 			if(e[k] & 1) {
 				r[0] += sf[0*SLOTS_MAX + ls]; r[1] += sf[1*SLOTS_MAX + ls];
 				r[2] += sf[2*SLOTS_MAX + ls]; r[3] += sf[3*SLOTS_MAX + ls];
@@ -1012,7 +1028,27 @@ __global__ void __launch_bounds__(SLOTS_MAX, FVHIP_FUSED_WAVES) k_residual_wls(c
 		st4(B.r, c, r);
 		if(DT) B.dtm[c] = div_rn(carea, integ);
 	}
-	(void)N;
+}
+
+#ifndef FVHIP_FUSED_WAVES
+#define FVHIP_FUSED_WAVES 4
+#endif
+
+template <int FLUX, int REC, bool DT>
+__global__ void __launch_bounds__(SLOTS_MAX, FVHIP_FUSED_WAVES) k_residual_wls(const DevMesh M, const DevPhys P, const SweepBuffers B)
+{
+	extern __shared__ __attribute__((aligned(16))) double fz[];
+	const int np = B.plist ? B.pcount : M.npatch;
+	const int t = static_cast<int>(threadIdx.x);
+	const int q = (np + 7) >> 3;
+	const int pi = (blockIdx.x & 7) * q + (blockIdx.x >> 3);
+	if(pi >= np) return;
+	const FzPatch cur = fz_patch(M, B, pi);
+	FzPre pre;
+	pre.cf = t < cur.nl ? fz_cell(M, cur, t) : 0;
+	fz_load_rows(M, B, cur, t, pre);
+	fz_load_grad(M, cur, t, pre);
+	fz_body<FLUX, REC, DT>(M, P, B, fz, cur, pre, []() {}, []() {});
 }
 
 // ------------------------------------------------------------------------------------------------

@@ -19,10 +19,10 @@
 namespace fvhip {
 
 #ifndef FVHIP_SLOTS
-#define FVHIP_SLOTS 512
+#define FVHIP_SLOTS 256
 #endif
 #ifndef FVHIP_FUSED_ROWS
-#define FVHIP_FUSED_ROWS (FVHIP_SLOTS*11/8)   // 704 x 112 B = 77 KB for 512-slot patches (2 blocks/CU)
+#define FVHIP_FUSED_ROWS (FVHIP_SLOTS*11/8)   // 352 x 112 B = 39 KB for 256-slot patches: 4 blocks = 16 waves per CU, the VGPR-bound occupancy
 #endif
 constexpr int SLOTS_MAX = FVHIP_SLOTS;   ///< faces per patch = threads per sweep workgroup
 constexpr int CELLS_MAX = FVHIP_SLOTS;
