@@ -76,6 +76,10 @@ __device__ __forceinline__ void ghost(const DevPhys& P, int bc, const double* in
 	gs[0] = g.x; gs[1] = g.y; gs[2] = g.z; gs[3] = g.w;
 }
 
+/// an empty register constraint: the value must exist in VGPRs here, so a load producing it cannot be
+/// merged with another load behind a pointer select
+__device__ __forceinline__ void pin_regs(double& x) { asm("" : "+v"(x)); }
+
 // ------------------------------------------------------------------------------------------------
 // preparation
 // ------------------------------------------------------------------------------------------------
@@ -542,17 +546,26 @@ __global__ void __launch_bounds__(SLOTS_MAX) k_sweep(const DevMesh M, const DevP
 	}
 	__syncthreads();
 
-	// cell data from LDS when the cell is in this patch, else from global memory (halo)
+	// cell data from LDS when the cell is in this patch, else from global memory (halo). The LDS row
+	// is read unconditionally (row 0 for a halo cell) and pinned in registers before the global
+	// values may replace it, so the two never merge into one generic (flat) load
 	auto inp = [&](int cell) { return static_cast<unsigned>(cell - c0) < static_cast<unsigned>(nc); };
+	auto lrow = [&](int cell, int off) { return &sbuf[(inp(cell) ? cell - c0 : 0)*W + off]; };
 	auto get4 = [&](int cell, int off, const double* g, double* o) {
-		if(inp(cell)) ld4(&sbuf[(cell - c0)*W + off], 0, o); else ld4(g, cell, o);
+		ld4(lrow(cell, off), 0, o);
+		for(int k = 0; k < 4; k++) pin_regs(o[k]);
+		if(!inp(cell)) ld4(g, cell, o);
 	};
 	auto get8 = [&](int cell, int off, const double* g, double* o) {
-		if(inp(cell)) ld8(&sbuf[(cell - c0)*W + off], 0, o); else ld8(g, cell, o);
+		ld8(lrow(cell, off), 0, o);
+		for(int k = 0; k < 8; k++) pin_regs(o[k]);
+		if(!inp(cell)) ld8(g, cell, o);
 	};
 	auto getrc = [&](int cell) -> double2 {
-		if(inp(cell)) return *reinterpret_cast<const double2*>(&sbuf[(cell - c0)*W + S::RC]);
-		return M.rc[cell];
+		double2 v = *reinterpret_cast<const double2*>(lrow(cell, S::RC));
+		pin_regs(v.x); pin_regs(v.y);
+		if(!inp(cell)) v = M.rc[cell];
+		return v;
 	};
 
 	const int s = s0 + t;
@@ -770,6 +783,28 @@ __device__ __forceinline__ void stage_row(const Gas& G, double* row, const doubl
 	*reinterpret_cast<double2*>(row + 12) = r;
 }
 
+/// FVHIP_FZ_WLSV = 1: the fused residual rebuilds each cell's WLS inverse from the staged centres it
+/// already reads instead of loading the precomputed one (32 B per gradient row less traffic)
+#ifndef FVHIP_FZ_WLSV
+#define FVHIP_FZ_WLSV 1
+#endif
+/// one neighbour's term of the WLS normal matrix, V[2i+j] += w2*dr[i]*dr[j] (agradientschemes.cpp:
+/// 218-317 as restated in layout.cpp: w2*dr[i] first, then times dr[j])
+__device__ __forceinline__ void wls_normal_add(double* vm, double w2, double d0, double d1)
+{
+#if FVHIP_FZ_WLSV
+	const double a = w2*d0, b = w2*d1;
+	vm[0] += a*d0; vm[1] += a*d1; vm[2] += b*d0; vm[3] += b*d1;
+#endif
+}
+/// its inverse, the host's 2x2 inverse arithmetic (layout.cpp, Eigen's inverse for 2x2)
+__device__ __forceinline__ double4 wls_inverse(const double* v)
+{
+	const double det = v[0]*v[3] - v[2]*v[1];
+	const double invdet = div_rn(1.0, det);
+	return make_double4(v[3]*invdet, -v[1]*invdet, -v[2]*invdet, v[0]*invdet);
+}
+
 /// phase 1 of the fused residual: WLS gradient of staged row `row` (cell c) from the staged rows of
 /// its neighbours nb4 (patch-local indices, boundary codes -2-bf, -1 padding), k_prep_grad_wls
 /// arithmetic; a ghost cell takes the gradient received from its owner
@@ -786,16 +821,68 @@ __device__ __forceinline__ void fused_wls_row(const DevMesh& M, const DevPhys& P
 	ld4(row, 0, uc);
 	const double2 rcc = *reinterpret_cast<const double2*>(row + 12);
 	double f[8] = {0,0,0,0,0,0,0,0};
+	double vm[4] = {0, 0, 0, 0};     // WLS normal matrix (FVHIP_FZ_WLSV), same terms and order as the host's
+	if(nb4.x >= 0 && nb4.y >= 0 && nb4.z >= 0 && nb4.w >= -1) {
+		// no boundary neighbour (all but ~0.1 % of the rows): every neighbour is an LDS row. The
+		// first three (every triangle and quad has them) are requested at once and their weights
+		// computed side by side instead of one LDS round trip and one division chain after another;
+		// the fourth (quads) follows
+		const int nb[3] = {nb4.x, nb4.y, nb4.z};
+		double w[3], d0[3], d1[3], un[3][4];
+		#pragma unroll
+		for(int k = 0; k < 3; k++) {
+			const double* nrow = &fz[nb[k]*FZW];
+			const double2 rn = *reinterpret_cast<const double2*>(nrow + 12);
+			ld4(nrow, 0, un[k]);
+			double w2 = 0;
+			w2 += (rcc.x-rn.x)*(rcc.x-rn.x);
+			w2 += (rcc.y-rn.y)*(rcc.y-rn.y);
+			d0[k] = rcc.x-rn.x; d1[k] = rcc.y-rn.y;
+			w[k] = div_rn(1.0, w2);
+		}
+		#pragma unroll
+		for(int k = 0; k < 3; k++) {
+			#pragma unroll
+			for(int iv = 0; iv < 4; iv++) {
+				const double du = uc[iv] - un[k][iv];
+				f[iv*2+0] += w[k]*d0[k]*du;
+				f[iv*2+1] += w[k]*d1[k]*du;
+			}
+			wls_normal_add(vm, w[k], d0[k], d1[k]);
+		}
+		if(nb4.w >= 0) {
+			const double* nrow = &fz[nb4.w*FZW];
+			const double2 rn = *reinterpret_cast<const double2*>(nrow + 12);
+			double u3[4];
+			ld4(nrow, 0, u3);
+			double w2 = 0;
+			w2 += (rcc.x-rn.x)*(rcc.x-rn.x);
+			w2 += (rcc.y-rn.y)*(rcc.y-rn.y);
+			const double e0 = rcc.x-rn.x, e1 = rcc.y-rn.y;
+			w2 = div_rn(1.0, w2);
+			#pragma unroll
+			for(int iv = 0; iv < 4; iv++) {
+				const double du = uc[iv] - u3[iv];
+				f[iv*2+0] += w2*e0*du;
+				f[iv*2+1] += w2*e1*du;
+			}
+			wls_normal_add(vm, w2, e0, e1);
+		}
+	} else
 	#pragma unroll
 	for(int k = 0; k < 4; k++) {
 		const int nbk = k == 0 ? nb4.x : (k == 1 ? nb4.y : (k == 2 ? nb4.z : nb4.w));
 		if(nbk == -1) break;
+		// the LDS row is read unconditionally (row 0 for a boundary code) and pinned in registers
+		// before the boundary values may replace it: otherwise the compiler merges the two loads
+		// into one generic (flat) load of a selected pointer, which waits on every outstanding
+		// global load of the wave
 		double un[4];
-		double2 rn;
-		if(nbk >= 0) {
-			ld4(&fz[nbk*FZW], 0, un);
-			rn = *reinterpret_cast<const double2*>(&fz[nbk*FZW + 12]);
-		} else {
+		const double* nrow = &fz[(nbk >= 0 ? nbk : 0)*FZW];
+		ld4(nrow, 0, un);
+		double2 rn = *reinterpret_cast<const double2*>(nrow + 12);
+		pin_regs(un[0]); pin_regs(un[1]); pin_regs(un[2]); pin_regs(un[3]); pin_regs(rn.x); pin_regs(rn.y);
+		if(nbk < 0) {
 			const int bf = -2 - nbk;
 			const double4 gp = ghost_prim_of_cell(M, P, B.u, c, bf);
 			un[0] = gp.x; un[1] = gp.y; un[2] = gp.z; un[3] = gp.w;
@@ -812,7 +899,11 @@ __device__ __forceinline__ void fused_wls_row(const DevMesh& M, const DevPhys& P
 			f[iv*2+0] += w2*dr0*du;
 			f[iv*2+1] += w2*dr1*du;
 		}
+		wls_normal_add(vm, w2, dr0, dr1);
 	}
+#if FVHIP_FZ_WLSV
+	V = wls_inverse(vm);
+#endif
 	double g[8];
 	#pragma unroll
 	for(int iv = 0; iv < 4; iv++) {
@@ -889,18 +980,24 @@ __device__ __forceinline__ void fz_body(const DevMesh& M, const DevPhys& P, cons
 	// phase 1: WLS gradients of the patch and ring-1 cells from the staged states
 	// (k_prep_grad_wls arithmetic, neighbours in the same ascending reference face order)
 	hookA();
+#ifndef FVHIP_PROBE_NOGRAD
 	if(t < q.ng) fused_wls_row(M, P, B, fz, &fz[t*FZW], a.cf, a.nb4a, a.Va);
 	for(int i = t + SLOTS_MAX; i < q.ng; i += SLOTS_MAX) {
 		const int c = fz_cell(M, q, i);
 		fused_wls_row(M, P, B, fz, &fz[i*FZW], c, c < M.nown ? q.gnbr[i] : make_int4(-1, -1, -1, -1),
-		              c < M.nown ? M.wls_V[c] : make_double4(0, 0, 0, 0));
+		              c < M.nown && !FVHIP_FZ_WLSV ? M.wls_V[c] : make_double4(0, 0, 0, 0));
 	}
+#endif
 	__syncthreads();
 
 	// phase 2: one face per thread (k_sweep arithmetic)
 	double f[4] = {0, 0, 0, 0};
 	double sri = 0, srj = 0;
+#ifdef FVHIP_PROBE_NOFACE
+	if(s < q.s1 && a.len == 12345.0) {
+#else
 	if(s < q.s1) {
+#endif
 		const int2 lrl = a.lrl;
 		const double2 nn = a.nn;
 		const double flen = a.len;

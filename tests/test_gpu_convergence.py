@@ -7,16 +7,19 @@ main solve, casesolvers.cpp:225-314), entropy error by the device FlowOutput::co
 pair's slope of log(error) vs log(h) lies in [1.65, 2.1].
 
 Linear solver: the reference's inv_cyl.solverc uses FGMRES (rtol 1e-1, 30 its) with block-Jacobi/ILU(0);
-here device GMRES (same rtol and iteration cap) with the preconditioner that converges each case: two
-multicolour block Gauss-Seidel sweeps (LS+HLLC) and point-block Jacobi (GG+HLLC).
+here device GMRES (same iteration cap) with the preconditioner that converges each case: two multicolour
+block Gauss-Seidel sweeps and rtol 1e-2 (LS+HLLC), point-block Jacobi and rtol 1e-1 (GG+HLLC).
 
 Deviation, measured on MI355X (tools/conv_probe.py, tools/conv_probe2.py): the implicit main solves run
 towards a 1e-7 residual drop (1500 steps at most) instead of the decks' 1e-5 and must reach the decks'
 1e-5. Stopped at 1e-5 the device path leaves more algebraic error on the finest mesh (LS+HLLC finest
-slope 1.50); converged, the slopes are the discretisation's own: LS+HLLC 1.864/1.790/1.662, GG+HLLC
-1.773/1.973/1.772. These inviscid solves are path-sensitive (four block-Jacobi sweeps stagnate LS+HLLC
-on 2dcylinder3 at 8e-4; other settings stagnate GG+HLLC near 1e-3), which is why the preconditioner is
-chosen per case. The reference's driver does not check convergence at all (flow_conv.cpp only catches
+slope 1.50); converged, the slopes are the discretisation's own: LS+HLLC 1.864/1.790/1.675, GG+HLLC
+1.773/1.973/1.772. These inviscid solves are path-sensitive, and so is where they land: with rtol 1e-1
+two Gauss-Seidel sweeps stagnate LS+HLLC on 2dcylinder3 near 4e-4 in one internal cell order (256-face
+patches) and converge in another (512), point-block Jacobi stagnates on 2dcylinder2 at 3e-3, four
+block-Jacobi sweeps on 2dcylinder3 at 8e-4; with rtol 1e-2 every preconditioner tried converges all
+four meshes, to finest slopes 1.662-1.675 (two solutions of the LS+HLLC discretisation on 2dcylinder3,
+log10 entropy error -2.9245 and -2.9286, both at a 1e-7 residual drop). Hence the per-case choice. The reference's driver does not check convergence at all (flow_conv.cpp only catches
 Numerical_error) and stops at max_timesteps."""
 import numpy as np
 import pytest
@@ -31,7 +34,7 @@ pytestmark = pytest.mark.gpu
 #  meshes, residual drop required of the main solve, preconditioner)
 CASES = {
     # SpatialFlow_Euler_Cylinder_LeastSquares_HLLC_Tri_EntropyConvergence (inv-cyl-ls-hllc.ctrl)
-    "ls_hllc_implicit": ("LEASTSQUARES", "HLLC", True, (25.0, 500.0, 1e-1, 150), (250.0, 5000.0, 1e-7, 1500), 4, 1e-5, dict(prec_sweeps=2, prec_gs=True)),
+    "ls_hllc_implicit": ("LEASTSQUARES", "HLLC", True, (25.0, 500.0, 1e-1, 150), (250.0, 5000.0, 1e-7, 1500), 4, 1e-5, dict(prec_sweeps=2, prec_gs=True, lin_rtol=1e-2)),
     # SpatialFlow_Euler_Cylinder_GreenGauss_HLLC_Tri_EntropyConvergence (inv-cyl-gg-hllc_tri.ctrl)
     "gg_hllc_implicit": ("GREENGAUSS", "HLLC", True, (25.0, 250.0, 1e-1, 250), (250.0, 1000.0, 1e-7, 1500), 4, 1e-5, dict(prec_sweeps=1)),
     # Flow_Explicit_Euler_Cylinder_GreenGauss_Roe_Tri_EntropyConvergence (expl-inv-cyl-gg-roe_tri.ctrl)
@@ -50,7 +53,8 @@ def solve_entropy(meshname, grad, flux, implicit, init, main, drop, prec=None):
     u0 = np.tile(cases.freestream(p), (m.nelem, 1))
     du = torch.tensor(u0[perm], device="cuda")
     if implicit:
-        lin = dict(lin_rtol=1e-1, lin_maxit=30, restart=30, min_relax=0.2, **(prec or {}))
+        lin = dict(lin_rtol=1e-1, lin_maxit=30, restart=30, min_relax=0.2)
+        lin.update(prec or {})
         st0, _ = start.steady_backward_euler_device(du.data_ptr(), fa.ImplicitConfig(
             cflinit=init[0], cflfin=init[1], tol=init[2], maxiter=init[3], **lin))
         st, _ = sp.steady_backward_euler_device(du.data_ptr(), fa.ImplicitConfig(
