@@ -106,7 +106,11 @@ static fvhip_ctx* createCtx(const MeshTopo& T, const fvhip_flow_config* cfg, int
 		M.fz_n1 = upload(L.fz_n1, o);
 		M.fz_g_start = upload(L.fz_g_start, o);
 		M.fz_gnbr = reinterpret_cast<const int4*>(upload(L.fz_gnbr, o));
-		M.fz_slot_lr = reinterpret_cast<const int2*>(upload(L.fz_slot_lr, o));
+		M.fz_slot_lr16 = upload(L.fz_slot_lr16, o);
+		M.fz_gnbr16 = reinterpret_cast<const uint2*>(upload(L.fz_gnbr16, o));
+		M.fz_gbf_start = upload(L.fz_gbf_start, o);
+		M.fz_gbf = upload(L.fz_gbf, o);
+		M.fz_cslot16 = reinterpret_cast<const uint2*>(upload(L.fz_cslot16, o));
 		M.fz_max_cells = L.fz_max_cells;
 	}
 	if(!L.pipe_patch.empty()) h->d_pipe_patch = upload(L.pipe_patch, o);

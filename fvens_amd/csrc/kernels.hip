@@ -914,7 +914,7 @@ __device__ __forceinline__ void fused_wls_row(const DevMesh& M, const DevPhys& P
 }
 
 /// one patch of the fused residual: uniform (scalar) metadata
-struct FzPatch { int p, s0, s1, c0, c1, nc, e0, nl, ng; const int4* gnbr; };
+struct FzPatch { int p, s0, s1, c0, c1, nc, e0, nl, ng; const uint2* gnbr; const int* gbf; };
 /// what one thread loads for its patch before phase 0: its first staged row (state, centre), the
 /// neighbour list and WLS inverse of the gradient it computes first, and the geometry of its face
 struct FzPre { int cf; double ua[4]; double2 rca; int4 nb4a; double4 Va; int2 lrl; double2 nn; double len; };
@@ -929,8 +929,23 @@ __device__ __forceinline__ FzPatch fz_patch(const DevMesh& M, const SweepBuffers
 	q.e0 = M.fz_ext_start[q.p];
 	q.nl = q.nc + (M.fz_ext_start[q.p+1] - q.e0);    // staged rows: patch, ring 1, ring 2
 	q.ng = q.nc + M.fz_n1[q.p];                       // rows whose gradients the patch computes
-	q.gnbr = M.fz_gnbr + M.fz_g_start[q.p];
+	q.gnbr = M.fz_gnbr16 + M.fz_g_start[q.p];
+	q.gbf = M.fz_gbf + M.fz_gbf_start[q.p];
 	return q;
+}
+/// a gradient row's four packed neighbour codes (layout.hpp fz_gnbr16) as patch-local index,
+/// -2-bf (boundary face) or -1 (none)
+__device__ __forceinline__ int fz_nbr_code(unsigned x, const int* gbf)
+{
+	if(x == 0xFFFFu) return -1;
+	if(x & 0x8000u) return -2 - gbf[x & 0x7FFFu];
+	return static_cast<int>(x);
+}
+__device__ __forceinline__ int4 fz_nbrs(const FzPatch& q, int i)
+{
+	const uint2 v = q.gnbr[i];
+	return make_int4(fz_nbr_code(v.x & 0xFFFFu, q.gbf), fz_nbr_code(v.x >> 16, q.gbf),
+	                 fz_nbr_code(v.y & 0xFFFFu, q.gbf), fz_nbr_code(v.y >> 16, q.gbf));
 }
 __device__ __forceinline__ int fz_cell(const DevMesh& M, const FzPatch& q, int i)
 {
@@ -944,14 +959,18 @@ __device__ __forceinline__ void fz_load_rows(const DevMesh& M, const SweepBuffer
 	if(t < q.nl) { ld4(B.u, a.cf, a.ua); a.rca = M.rc[a.cf]; }
 	const int s = q.s0 + t;
 	a.lrl = make_int2(0, -1); a.nn = make_double2(0, 0); a.len = 0;
-	if(s < q.s1) { a.lrl = M.fz_slot_lr[s]; a.nn = M.slot_n[s]; a.len = M.slot_len[s]; }
+	if(s < q.s1) {
+		const unsigned v = M.fz_slot_lr16[s];    // R 0xFFFF: boundary face (bf from slot_LR)
+		a.lrl = make_int2(static_cast<int>(v & 0xFFFFu), (v >> 16) == 0xFFFFu ? -2 : static_cast<int>(v >> 16));
+		a.nn = M.slot_n[s]; a.len = M.slot_len[s];
+	}
 }
 /// the gradient inputs of the thread's first gradient row
 __device__ __forceinline__ void fz_load_grad(const DevMesh& M, const FzPatch& q, int t, FzPre& a)
 {
 	a.nb4a = make_int4(-1, -1, -1, -1);
 	a.Va = make_double4(0, 0, 0, 0);
-	if(t < q.ng && a.cf < M.nown) { a.nb4a = q.gnbr[t]; a.Va = M.wls_V[a.cf]; }
+	if(t < q.ng && a.cf < M.nown) { a.nb4a = fz_nbrs(q, t); if(!FVHIP_FZ_WLSV) a.Va = M.wls_V[a.cf]; }
 }
 
 /// one patch (512 threads): phase 0 stages the primitive states and centres of the patch, ring-1 and
@@ -984,7 +1003,7 @@ __device__ __forceinline__ void fz_body(const DevMesh& M, const DevPhys& P, cons
 	if(t < q.ng) fused_wls_row(M, P, B, fz, &fz[t*FZW], a.cf, a.nb4a, a.Va);
 	for(int i = t + SLOTS_MAX; i < q.ng; i += SLOTS_MAX) {
 		const int c = fz_cell(M, q, i);
-		fused_wls_row(M, P, B, fz, &fz[i*FZW], c, c < M.nown ? q.gnbr[i] : make_int4(-1, -1, -1, -1),
+		fused_wls_row(M, P, B, fz, &fz[i*FZW], c, c < M.nown ? fz_nbrs(q, i) : make_int4(-1, -1, -1, -1),
 		              c < M.nown && !FVHIP_FZ_WLSV ? M.wls_V[c] : make_double4(0, 0, 0, 0));
 	}
 #endif
@@ -1003,7 +1022,8 @@ __device__ __forceinline__ void fz_body(const DevMesh& M, const DevPhys& P, cons
 		const double flen = a.len;
 		const double n[2] = {nn.x, nn.y};
 		const bool bnd = lrl.y < -1;
-		const int bf = -2 - lrl.y;
+		int bf = 0, bcell = 0;          // boundary face: its index and cell from the global slot
+		if(bnd) { const int2 g = M.slot_LR[s]; bf = g.y - M.ncell; bcell = g.x; }
 		double ul[4], ur[4];
 		const double* rowi = &fz[lrl.x*FZW];
 		const double2 ri = *reinterpret_cast<const double2*>(rowi + 12);
@@ -1032,7 +1052,7 @@ __device__ __forceinline__ void fz_body(const DevMesh& M, const DevPhys& P, cons
 				prim2cons(G, ur, ur);
 			} else {
 				// ghost of the cell value (k_prep_grad_wls / k_prep_bfaces arithmetic)
-				const double4 gp = ghost_prim_of_cell(M, P, B.u, M.slot_LR[s].x, bf);
+				const double4 gp = ghost_prim_of_cell(M, P, B.u, bcell, bf);
 				const double uj[4] = {gp.x, gp.y, gp.z, gp.w};
 				const double2 rj = M.bf_rcbp[bf];
 				const double dx = rj.x-ri.x, dy = rj.y-ri.y;
@@ -1089,9 +1109,9 @@ __device__ __forceinline__ void fz_body(const DevMesh& M, const DevPhys& P, cons
 	// the cell's face list (and area) are requested before the two barriers of the flux staging,
 	// once the face work no longer holds registers
 	const int c = q.c0 + t;
-	int4 cs = make_int4(-1, -1, -1, -1);
+	uint2 cs = make_uint2(0xFFFFFFFFu, 0xFFFFFFFFu);
 	double carea = 0.0;
-	if(c < q.c1) { cs = M.cell_slots[c]; if(DT) carea = M.area[c]; }
+	if(c < q.c1) { cs = M.fz_cslot16[c]; if(DT) carea = M.area[c]; }
 	__syncthreads();   // all staged rows read: reuse LDS for the face fluxes
 	double* sf = fz;
 	double* ssr = fz + 4*SLOTS_MAX;
@@ -1107,11 +1127,11 @@ __device__ __forceinline__ void fz_body(const DevMesh& M, const DevPhys& P, cons
 		if(B.overwrite) { r[0] = r[1] = r[2] = r[3] = 0.0; }
 		else ld4(B.r, c, r);
 		double integ = 0.0;
-		const int e[4] = {cs.x, cs.y, cs.z, cs.w};
+		const unsigned e[4] = {cs.x & 0xFFFFu, cs.x >> 16, cs.y & 0xFFFFu, cs.y >> 16};
 		#pragma unroll
 		for(int k = 0; k < 4; k++) {
-			if(e[k] < 0) break;
-			const int ls = (e[k] >> 1) - q.s0;
+			if(e[k] == 0xFFFFu) break;
+			const int ls = static_cast<int>(e[k] >> 1);     // patch-local slot
 			if(e[k] & 1) {
 				r[0] += sf[0*SLOTS_MAX + ls]; r[1] += sf[1*SLOTS_MAX + ls];
 				r[2] += sf[2*SLOTS_MAX + ls]; r[3] += sf[3*SLOTS_MAX + ls];

@@ -45,7 +45,11 @@ struct DevMesh
 	const int* fz_n1;          // [npatch] ring-1 count
 	const int* fz_g_start;     // [npatch+1] first fz_gnbr row of each patch
 	const int4* fz_gnbr;       // neighbour codes of the cells whose gradients a patch computes
-	const int2* fz_slot_lr;    // [S] patch-local L, R
+	const unsigned* fz_slot_lr16;   // [S] patch-local L | R << 16 (R 0xFFFF: boundary face)
+	const uint2* fz_gnbr16;    // per gradient row 4 x 16-bit neighbour codes (layout.hpp)
+	const int* fz_gbf_start;   // [npatch+1]
+	const int* fz_gbf;         // boundary faces of the 0x8000|j codes
+	const uint2* fz_cslot16;   // [nown] 4 x 16-bit (patch-local slot << 1 | isRight)
 	int fz_max_cells;
 };
 

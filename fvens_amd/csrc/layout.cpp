@@ -434,6 +434,10 @@ void buildFused(Layout& Lo)
 	Lo.fz_g_start.assign(1, 0);
 	Lo.fz_gnbr.clear();
 	Lo.fz_slot_lr.assign(2*Lo.slot_L.size(), -1);
+	Lo.fz_slot_lr16.assign(Lo.slot_L.size(), 0xFFFFFFFFu);
+	Lo.fz_gnbr16.clear();
+	Lo.fz_gbf_start.assign(1, 0); Lo.fz_gbf.clear();
+	Lo.fz_cslot16.assign(4*static_cast<size_t>(Lo.ncell), 0xFFFF);
 	Lo.fz_max_cells = 0;
 	Lo.fz_ring2 = 0;
 	std::vector<int> lidx(N, -1);          // patch-local index of a cell while its patch is built
@@ -477,6 +481,30 @@ void buildFused(Layout& Lo)
 			Lo.fz_slot_lr[2*static_cast<size_t>(s)] = code(Lo.slot_L[s]);
 			Lo.fz_slot_lr[2*static_cast<size_t>(s)+1] = code(Lo.slot_R[s]);
 		}
+		// packed forms
+		const size_t gb0 = Lo.fz_gbf.size();
+		for(size_t k = Lo.fz_gnbr.size() - 4*static_cast<size_t>(ng); k < Lo.fz_gnbr.size(); k++) {
+			const int v = Lo.fz_gnbr[k];
+			if(v == -1) { Lo.fz_gnbr16.push_back(0xFFFF); continue; }
+			if(v >= 0) { Lo.fz_gnbr16.push_back(static_cast<uint16_t>(v)); continue; }
+			const size_t j = Lo.fz_gbf.size() - gb0;
+			if(j >= 0x7FFF) throw std::logic_error("fused residual: too many boundary faces in one patch");
+			Lo.fz_gbf.push_back(-2 - v);
+			Lo.fz_gnbr16.push_back(static_cast<uint16_t>(0x8000 | j));
+		}
+		Lo.fz_gbf_start.push_back(static_cast<int>(Lo.fz_gbf.size()));
+		for(int s = Lo.patch_slot[p]; s < Lo.patch_slot[p+1]; s++) {
+			const int l = Lo.fz_slot_lr[2*static_cast<size_t>(s)], r = Lo.fz_slot_lr[2*static_cast<size_t>(s)+1];
+			Lo.fz_slot_lr16[s] = static_cast<uint32_t>(l) | (static_cast<uint32_t>(r >= 0 ? r : 0xFFFF) << 16);
+		}
+		for(int c = c0; c < c1; c++)
+			for(int j = 0; j < MAXF; j++) {
+				const int e = Lo.cell_slots[static_cast<size_t>(c)*MAXF+j];
+				if(e < 0) continue;
+				const int ls = (e >> 1) - Lo.patch_slot[p];
+				if(ls < 0 || ls >= SLOTS_MAX) throw std::logic_error("fused residual: cell face outside its patch");
+				Lo.fz_cslot16[static_cast<size_t>(c)*MAXF+j] = static_cast<uint16_t>((ls << 1) | (e & 1));
+			}
 		Lo.fz_max_cells = std::max(Lo.fz_max_cells, nl);
 		// interior patch: stages no ghost cell, so it needs no halo data and can run while the
 		// exchange is in flight

@@ -91,6 +91,15 @@ struct Layout
 	                                       ///<  -2-bf (boundary face), -1 (none; also every entry of a
 	                                       ///<  ghost ring-1 cell, whose gradient is received)
 	std::vector<int> fz_slot_lr;           ///< [S][2] local L, R (R boundary: -2-bf)
+	// the same, packed for the kernel (16-bit patch-local indices): per slot L | R << 16 with R = 0xFFFF
+	// for a boundary face (its bf then comes from slot_R); per gradient row four neighbour codes
+	// (0xFFFF none, 0x8000|j boundary face fz_gbf[fz_gbf_start[p] + j]); per owned cell its four faces
+	// as (patch-local slot << 1 | isRight), 0xFFFF padded
+	std::vector<uint32_t> fz_slot_lr16;    ///< [S]
+	std::vector<uint16_t> fz_gnbr16;       ///< [rows][4], rows as fz_gnbr
+	std::vector<int> fz_gbf_start;         ///< [npatch+1]
+	std::vector<int> fz_gbf;               ///< boundary faces the gradient rows of each patch read
+	std::vector<uint16_t> fz_cslot16;      ///< [ncell][4]
 	int fz_ring2 = 0;                      ///< ring-2 cells staged over all patches
 	int fz_max_cells = 0;
 	std::vector<int> fz_order;             ///< patches needing no halo data first (fz_ninner), then the rest
@@ -104,6 +113,7 @@ struct Layout
 };
 
 constexpr int FUSED_LDS_CELLS = FVHIP_FUSED_ROWS;   ///< staged cells per patch (rows of 112 B)
+static_assert(FUSED_LDS_CELLS < 0x8000 && 2*SLOTS_MAX < 0xFFFF, "fused codes are 16-bit");
 constexpr int PIPE_CHUNKS = 8;          ///< gradient chunks of the pipelined staged residual
 
 /// whether cfg takes the fused residual kernel (WLS + MUSCL/unlimited linear, inviscid). On a
