@@ -518,8 +518,11 @@ def partition_info(mesh, part, rank):
     sg = np.zeros(max(nsend, 1), np.int32)
     check(_ffi.lib().fvhip_partition_info(ctypes.byref(mesh.view), iptr(part), rank, iptr(counts), iptr(cg),
                                           iptr(nbr), iptr(gs), iptr(ss), iptr(sg)))
+    g1 = np.zeros(max(nnbr, 1), np.int32)
+    s1 = np.zeros(max(nnbr, 1), np.int32)
+    check(_ffi.lib().fvhip_partition_halo_layers(ctypes.byref(mesh.view), iptr(part), rank, iptr(g1), iptr(s1)))
     return dict(owned=nown, ghosts=ngh, bfaces=nb, faces=nf, cell_global=cg, nbr_rank=nbr[:nnbr],
-                ghost_start=gs, send_start=ss, send_global=sg[:nsend])
+                ghost_start=gs, send_start=ss, send_global=sg[:nsend], ghost_l1_end=g1[:nnbr], send_l1_end=s1[:nnbr])
 
 
 LAYOUT_KEYS = ("cells", "faces", "slots", "patches", "max_slots", "bfaces", "ghosts", "neighbours", "send_rows",

@@ -64,6 +64,8 @@ _SIGS = {
     "fvhip_partition_edge_cut": (ctypes.c_longlong, [ctypes.POINTER(FvMeshView), c_int_p]),
     "fvhip_partition_info": (ctypes.c_int, [ctypes.POINTER(FvMeshView), c_int_p, ctypes.c_int, c_int_p, c_int_p,
                                             c_int_p, c_int_p, c_int_p, c_int_p]),
+    "fvhip_partition_halo_layers": (ctypes.c_int, [ctypes.POINTER(FvMeshView), c_int_p, ctypes.c_int, c_int_p,
+                                                   c_int_p]),
     "fvhip_create_partitioned": (ctypes.c_int, [ctypes.POINTER(FvMeshView), ctypes.POINTER(FvFlowConfig), c_int_p,
                                                 ctypes.c_int, ctypes.c_int, ctypes.c_int,
                                                 ctypes.POINTER(ctypes.c_void_p)]),

@@ -311,8 +311,19 @@ struct fvhip_ctx
 		if(!st) st = stream;
 		timed_on(st, "k_pack", [&]{ launch_pack_rows(d_send, nsend, arr, width, d_sendbuf, st); });
 	}
-	/// RCCL point-to-point exchange with every neighbour rank, on stream st (default: the handle's)
-	void exchange_rccl(double* arr, int width, hipStream_t st = nullptr) {
+	/// rows neighbour k sends / receives in an exchange of `layers` halo layers (a one-layer exchange
+	/// of a two-layer halo moves the leading layer-1 part of each block)
+	int sendCount(size_t k, int layers) const {
+		return (layers >= 2 || L.send_l1_end.empty() ? L.send_start[k+1] : L.send_l1_end[k]) - L.send_start[k];
+	}
+	int ghostCount(size_t k, int layers) const {
+		return (layers >= 2 || L.ghost_l1_end.empty() ? L.ghost_start[k+1] : L.ghost_l1_end[k]) - L.ghost_start[k];
+	}
+	/// RCCL point-to-point exchange with every neighbour rank, on stream st (default: the handle's);
+	/// `layers` 2 fills both layers of a two-layer halo (the residual's state), 1 the first (gradients,
+	/// limiter values, Krylov vectors). Both sides derive the counts from the same lists, so a leg
+	/// with nothing to move is skipped on both.
+	void exchange_rccl(double* arr, int width, hipStream_t st = nullptr, int layers = 1) {
 		if(!halo()) return;
 		if(!comm) throw std::runtime_error("partitioned handle: call fvhip_comm_init (or use a group) first");
 		if(!st) st = stream;
@@ -320,12 +331,23 @@ struct fvhip_ctx
 		NC(ncclGroupStart());
 		for(size_t k = 0; k < L.nbr_rank.size(); k++) {
 			const int q = L.nbr_rank[k];
-			const size_t ns = static_cast<size_t>(L.send_start[k+1] - L.send_start[k]);
-			const size_t ng = static_cast<size_t>(L.ghost_start[k+1] - L.ghost_start[k]);
-			NC(ncclSend(d_sendbuf + static_cast<size_t>(width)*L.send_start[k], width*ns, ncclDouble, q, comm, st));
-			NC(ncclRecv(arr + static_cast<size_t>(width)*(L.ncell + L.ghost_start[k]), width*ng, ncclDouble, q, comm, st));
+			const size_t ns = static_cast<size_t>(sendCount(k, layers));
+			const size_t ng = static_cast<size_t>(ghostCount(k, layers));
+			if(ns) NC(ncclSend(d_sendbuf + static_cast<size_t>(width)*L.send_start[k], width*ns, ncclDouble, q, comm, st));
+			if(ng) NC(ncclRecv(arr + static_cast<size_t>(width)*(L.ncell + L.ghost_start[k]), width*ng, ncclDouble, q, comm, st));
 		}
 		NC(ncclGroupEnd());
+	}
+	/// the residual's halo protocol: with a two-layer halo and WLS gradients of an unlimited / MUSCL
+	/// reconstruction, ONE exchange of u (both layers) and the layer-1 ghosts' gradients computed
+	/// locally (k_grad_ghost); otherwise u, then gradients (and limiter data) in further rounds
+	bool singleExchange() const {
+		return halo() && L.halo_layers == 2 && cfg.order2 && cfg.gradientscheme == FVHIP_GRAD_LEASTSQUARES &&
+		       !limited() && cfg.reconstruction != FVHIP_REC_WENO && (L.gg_cells.empty() || !L.gg_V.empty());
+	}
+	void stage_ghost_gradients(const double* u, hipStream_t st = nullptr) {
+		if(!st) st = stream;
+		timed_on(st, "k_grad_ghost", [&]{ KOPS(launch_grad_ghost)(M, P, u, d_grad, st); });
 	}
 
 	/// fused residual of one RCCL rank: the halo exchange (ghost u, border gradients, ghost
@@ -340,9 +362,14 @@ struct fvhip_ctx
 		double* uu = const_cast<double*>(u);
 		HC(hipEventRecord(ev_u, stream));                 // u as the caller left it
 		HC(hipStreamWaitEvent(comm_stream, ev_u, 0));
-		exchange_rccl(uu, 4, comm_stream);
-		stage_border_gradients(u, comm_stream);
-		exchange_rccl(d_grad, 8, comm_stream);
+		if(singleExchange()) {
+			exchange_rccl(uu, 4, comm_stream, 2);
+			stage_ghost_gradients(u, comm_stream);
+		} else {
+			exchange_rccl(uu, 4, comm_stream);
+			stage_border_gradients(u, comm_stream);
+			exchange_rccl(d_grad, 8, comm_stream);
+		}
 		HC(hipEventRecord(ev_halo, comm_stream));
 		stage_fused(u, r, dt, dtm, overwrite, d_fz_order, L.fz_ninner);
 		HC(hipStreamWaitEvent(stream, ev_halo, 0));
@@ -357,17 +384,20 @@ struct fvhip_ctx
 	}
 
 	typedef std::function<double*(size_t)> ArrayOf;
-	typedef std::function<void(const ArrayOf&, int)> GroupExchange;
+	/// (array of each rank, row width, halo layers)
+	typedef std::function<void(const ArrayOf&, int, int)> GroupExchange;
 
+	static bool h0_single(const std::vector<fvhip_ctx*>& hs) { return hs[0]->singleExchange(); }
 	/// The residual as a sequence of stages over one or several handles (several: the ranks of a
 	/// partition held by one process, exchanging through device copies, see fvhip_group_*)
 	static void residual_seq(std::vector<fvhip_ctx*>& hs, const std::vector<const double*>& us,
 	                         const std::vector<double*>& rs, bool dt, const std::vector<double*>& dts,
 	                         bool overwrite, const GroupExchange& exg) {
-		auto exchange = [&](const ArrayOf& arr_of, int width) {
-			if(exg) { exg(arr_of, width); return; }
-			for(size_t i = 0; i < hs.size(); i++) { HC(hipSetDevice(hs[i]->device)); hs[i]->exchange_rccl(arr_of(i), width); }
+		auto exchange = [&](const ArrayOf& arr_of, int width, int layers = 1) {
+			if(exg) { exg(arr_of, width, layers); return; }
+			for(size_t i = 0; i < hs.size(); i++) { HC(hipSetDevice(hs[i]->device)); hs[i]->exchange_rccl(arr_of(i), width, nullptr, layers); }
 		};
+		const bool single = h0_single(hs);
 		// every stage launches on the handle's own device (a group may span devices)
 		auto on = [&](size_t i) -> fvhip_ctx* { HC(hipSetDevice(hs[i]->device)); return hs[i]; };
 		fvhip_ctx* h0 = hs[0];
@@ -382,9 +412,14 @@ struct fvhip_ctx
 				// rows of u and of the gradients of the cells other ranks hold as ghosts, then the rest
 				for(size_t i = 0; i < hs.size(); i++)
 					on(i)->stage_fused(us[i], rs[i], dt, dts[i], overwrite, hs[i]->d_fz_order, hs[i]->L.fz_ninner);
-				exchange([&](size_t i) { return const_cast<double*>(us[i]); }, 4);
-				for(size_t i = 0; i < hs.size(); i++) on(i)->stage_border_gradients(us[i]);
-				exchange([&](size_t i) { return hs[i]->d_grad; }, 8);
+				if(single) {
+					exchange([&](size_t i) { return const_cast<double*>(us[i]); }, 4, 2);
+					for(size_t i = 0; i < hs.size(); i++) on(i)->stage_ghost_gradients(us[i]);
+				} else {
+					exchange([&](size_t i) { return const_cast<double*>(us[i]); }, 4);
+					for(size_t i = 0; i < hs.size(); i++) on(i)->stage_border_gradients(us[i]);
+					exchange([&](size_t i) { return hs[i]->d_grad; }, 8);
+				}
 				for(size_t i = 0; i < hs.size(); i++)
 					on(i)->stage_fused(us[i], rs[i], dt, dts[i], overwrite, hs[i]->d_fz_order + hs[i]->L.fz_ninner,
 					                   static_cast<int>(hs[i]->L.fz_order.size()) - hs[i]->L.fz_ninner);
@@ -393,10 +428,11 @@ struct fvhip_ctx
 			for(size_t i = 0; i < hs.size(); i++) on(i)->stage_fused(us[i], rs[i], dt, dts[i], overwrite);
 			return;
 		}
-		exchange([&](size_t i) { return const_cast<double*>(us[i]); }, 4);
+		exchange([&](size_t i) { return const_cast<double*>(us[i]); }, 4, h0->L.halo_layers);
 		if(h0->recKind() != SR_FIRST) {
 			for(size_t i = 0; i < hs.size(); i++) on(i)->stage_gradients(us[i]);
-			exchange([&](size_t i) { return hs[i]->d_grad; }, 8);
+			if(single) { for(size_t i = 0; i < hs.size(); i++) on(i)->stage_ghost_gradients(us[i]); }
+			else exchange([&](size_t i) { return hs[i]->d_grad; }, 8);
 			if(h0->limited()) {
 				for(size_t i = 0; i < hs.size(); i++) on(i)->stage_limiter();
 				exchange([&](size_t i) { return hs[i]->d_phi; }, 4);

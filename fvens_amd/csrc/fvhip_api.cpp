@@ -12,7 +12,7 @@ namespace fvhip_detail {
 fvhip_ctx::GroupExchange groupExchange(const fvhip_group_s* g)
 {
 	// in-process exchange: pack everywhere, then copy each neighbour's packed rows into the ghost block
-	return [g](const fvhip_ctx::ArrayOf& arr_of, int width) {
+	return [g](const fvhip_ctx::ArrayOf& arr_of, int width, int layers) {
 		const std::vector<fvhip_ctx*>& hs = g->hs;
 		const size_t n = hs.size();
 		std::vector<fvhip_ctx*> byrank(n);
@@ -28,8 +28,9 @@ fvhip_ctx::GroupExchange groupExchange(const fvhip_group_s* g)
 				size_t kk = 0;
 				while(kk < Q.nbr_rank.size() && Q.nbr_rank[kk] != h->rank) kk++;
 				if(kk == Q.nbr_rank.size()) throw std::logic_error("halo lists are not symmetric");
-				const int cnt = L.ghost_start[k+1] - L.ghost_start[k];
-				if(cnt != Q.send_start[kk+1] - Q.send_start[kk]) throw std::logic_error("halo sizes differ");
+				const int cnt = h->ghostCount(k, layers);
+				if(cnt != q->sendCount(kk, layers)) throw std::logic_error("halo sizes differ");
+				if(cnt == 0) continue;
 				HC(hipMemcpyAsync(arr_of(i) + static_cast<size_t>(width)*(L.ncell + L.ghost_start[k]),
 				                  q->d_sendbuf + static_cast<size_t>(width)*Q.send_start[kk],
 				                  sizeof(double)*width*static_cast<size_t>(cnt), hipMemcpyDeviceToDevice, h->stream));
@@ -113,6 +114,13 @@ static fvhip_ctx* createCtx(const MeshTopo& T, const fvhip_flow_config* cfg, int
 		M.fz_cslot16 = reinterpret_cast<const uint2*>(upload(L.fz_cslot16, o));
 		M.fz_max_cells = L.fz_max_cells;
 	}
+	M.gg_n = static_cast<int>(L.gg_cells.size());
+	M.gg_cells = upload(L.gg_cells, o);
+	M.gg_nbr = reinterpret_cast<const int4*>(upload(L.gg_nbr, o));
+	M.gg_V = reinterpret_cast<const double4*>(upload(L.gg_V, o));
+	M.xb_bc = upload(L.xb_bc, o);
+	M.xb_n = reinterpret_cast<const double2*>(upload(L.xb_n, o));
+	M.xb_rcbp = reinterpret_cast<const double2*>(upload(L.xb_rcbp, o));
 	if(!L.pipe_patch.empty()) h->d_pipe_patch = upload(L.pipe_patch, o);
 	if(L.nghost > 0 && !L.fz_order.empty()) h->d_fz_order = upload(L.fz_order, o);
 	h->d_perm = upload(L.perm, o);
@@ -226,6 +234,18 @@ int fvhip_partition_info(const fvhip_mesh* mesh, const int* part, int rank, int*
 		if(ghost_start) for(int k = 0; k <= nnbr; k++) ghost_start[k] = nnbr ? T.ghost_start[k] : 0;
 		if(send_start) for(int k = 0; k <= nnbr; k++) send_start[k] = T.send_start[k];
 		if(send_global) for(size_t i = 0; i < T.send_cells.size(); i++) send_global[i] = T.cell_global[T.send_cells[i]];
+	});
+}
+
+int fvhip_partition_halo_layers(const fvhip_mesh* mesh, const int* part, int rank, int* ghost_l1_end,
+                                int* send_l1_end)
+{
+	return guard([&] {
+		const MeshTopo T = extractPartition(*mesh, part, rank);
+		for(size_t k = 0; k < T.nbr_rank.size(); k++) {
+			if(ghost_l1_end) ghost_l1_end[k] = T.ghost_l1_end[k];
+			if(send_l1_end) send_l1_end[k] = T.send_l1_end[k];
+		}
 	});
 }
 

@@ -37,7 +37,7 @@ struct System
 	}
 	void exchange(const fvhip_ctx::ArrayOf& arr, int width) {
 		if(!halo()) return;
-		if(exg) { exg(arr, width); return; }
+		if(exg) { exg(arr, width, 1); return; }
 		each([&](size_t i, fvhip_ctx* h) { h->exchange_rccl(arr(i), width); });
 	}
 	/// global sums of the k values every handle left in its iw.red: returned on the host and, if

@@ -366,6 +366,65 @@ __global__ void __launch_bounds__(256) k_grad_wls_list(DevMesh M, DevPhys P, con
 	st8(grad, c, g);
 }
 
+/// WLS gradients of the layer-1 ghosts of a two-layer halo, from the received layer-1 and layer-2
+/// states: the arithmetic of k_grad_wls_list on the ghost's own neighbour list (ascending global face
+/// order; extra boundary faces for the physical faces no owned cell touches), so each value is the
+/// owner's bit for bit and needs no exchange
+__global__ void __launch_bounds__(256) k_grad_ghost(DevMesh M, DevPhys P, const double* __restrict__ u,
+                                                    double* __restrict__ grad)
+{
+	const int i = blockIdx.x*blockDim.x + threadIdx.x;
+	if(i >= M.gg_n) return;
+	const int c = M.gg_cells[i];
+	const Gas& G = P.gas;
+	const int4 nb4 = M.gg_nbr[i];
+	const int nb[4] = {nb4.x, nb4.y, nb4.z, nb4.w};
+	double ucons[4], uc[4];
+	ld4(u, c, ucons);
+	cons2prim(G, ucons, uc);
+	const double2 rcc = M.rc[c];
+	double f[8] = {0,0,0,0,0,0,0,0};
+	#pragma unroll
+	for(int k = 0; k < 4; k++) {
+		if(nb[k] == -1) break;
+		double un[4];
+		double2 rn;
+		if(nb[k] < 0) {
+			const int x = -2 - nb[k];
+			const double2 nn = M.xb_n[x];
+			const double n[2] = {nn.x, nn.y};
+			double gs[4];
+			ghost(P, M.xb_bc[x], ucons, n, gs);
+			cons2prim(G, gs, un);
+			rn = M.xb_rcbp[x];
+		} else {
+			double t4[4];
+			ld4(u, nb[k], t4);
+			cons2prim(G, t4, un);
+			rn = M.rc[nb[k]];
+		}
+		double w2 = 0;
+		w2 += (rcc.x-rn.x)*(rcc.x-rn.x);
+		w2 += (rcc.y-rn.y)*(rcc.y-rn.y);
+		const double dr0 = rcc.x-rn.x, dr1 = rcc.y-rn.y;
+		w2 = div_rn(1.0, w2);
+		#pragma unroll
+		for(int iv = 0; iv < 4; iv++) {
+			const double du = uc[iv] - un[iv];
+			f[iv*2+0] += w2*dr0*du;
+			f[iv*2+1] += w2*dr1*du;
+		}
+	}
+	const double4 V = M.gg_V[i];
+	double g[8];
+	#pragma unroll
+	for(int iv = 0; iv < 4; iv++) {
+		g[iv*2+0] = V.x*f[iv*2+0] + V.y*f[iv*2+1];
+		g[iv*2+1] = V.z*f[iv*2+0] + V.w*f[iv*2+1];
+	}
+	st8(grad, c, g);
+}
+
 __global__ void __launch_bounds__(256) k_grad_gg(DevMesh M, const double* __restrict__ up,
                                                  const double* __restrict__ ug, double* __restrict__ grad)
 {
@@ -705,8 +764,9 @@ __global__ void __launch_bounds__(SLOTS_MAX) k_sweep(const DevMesh M, const DevP
 				const double aj = div_rn(4.0, 3*ur[0]), bj = div_rn(G.g, ur[0]);
 				const double coi = (ai < bi) ? bi : ai;          // std::max
 				const double coj = (aj < bj) ? bj : aj;
-				sri += div_rn(div_rn(coi*mui, G.Pr) * len*len, M.area[lr.x]);
-				if(!bnd) srj += div_rn(div_rn(coj*muj, G.Pr) * len*len, M.area[lr.y]);
+				// a ghost cell's spectral radius is never summed (and its area is not stored)
+				if(lr.x < M.nown) sri += div_rn(div_rn(coi*mui, G.Pr) * len*len, M.area[lr.x]);
+				if(!bnd && lr.y < M.nown) srj += div_rn(div_rn(coj*muj, G.Pr) * len*len, M.area[lr.y]);
 			}
 		}
 	}
@@ -1230,6 +1290,12 @@ void launch_limiter(const DevMesh& M, const DevPhys& P, int venk, const double* 
 	if(M.nown <= 0) return;
 	if(venk) k_limiter<true><<<nblk(M.nown,256), 256, 0, s>>>(M, up, ug, grad, phi);
 	else     k_limiter<false><<<nblk(M.nown,256), 256, 0, s>>>(M, up, ug, grad, phi);
+}
+
+void launch_grad_ghost(const DevMesh& M, const DevPhys& P, const double* u, double* grad, hipStream_t s)
+{
+	if(M.gg_n <= 0) return;
+	k_grad_ghost<<<(M.gg_n + 255)/256, 256, 0, s>>>(M, P, u, grad);
 }
 void launch_weno(const DevMesh& M, const DevPhys& P, const double* grad, double* lgrad, hipStream_t s)
 { if(M.nown > 0) k_weno<<<nblk(M.nown,256), 256, 0, s>>>(M, P.limiter_param, grad, lgrad); }

@@ -51,6 +51,14 @@ struct DevMesh
 	const int* fz_gbf;         // boundary faces of the 0x8000|j codes
 	const uint2* fz_cslot16;   // [nown] 4 x 16-bit (patch-local slot << 1 | isRight)
 	int fz_max_cells;
+	// layer-1 ghosts of a two-layer halo (layout.hpp gg_*, xb_*)
+	int gg_n;
+	const int* gg_cells;
+	const int4* gg_nbr;
+	const double4* gg_V;
+	const int* xb_bc;
+	const double2* xb_n;
+	const double2* xb_rcbp;
 };
 
 struct DevPhys
@@ -90,6 +98,7 @@ void launch_prep_grad_wls(const DevMesh& M, const DevPhys& P, const double* u, d
                           int lim = 0, double* phi = nullptr); \
 void launch_grad_wls_list(const DevMesh& M, const DevPhys& P, const double* u, const int* list, int n, \
                           double* grad, hipStream_t s); \
+void launch_grad_ghost(const DevMesh& M, const DevPhys& P, const double* u, double* grad, hipStream_t s); \
 void launch_grad_gg(const DevMesh& M, const double* up, const double* ug, double* grad, hipStream_t s); \
 void launch_limiter(const DevMesh& M, const DevPhys& P, int venk, const double* up, const double* ug, \
                     const double* grad, double* phi, hipStream_t s); \

@@ -293,7 +293,14 @@ Layout buildLayout(const MeshTopo& T, const fvhip_flow_config& cfg, bool renumbe
 	Lo.send_start = T.send_start;
 	Lo.send_cells.resize(T.send_cells.size());
 	for(size_t i = 0; i < T.send_cells.size(); i++) Lo.send_cells[i] = Lo.iperm[T.send_cells[i]];
-	Lo.border_cells = Lo.send_cells;
+	Lo.halo_layers = T.halo_layers;
+	Lo.ghost_l1_end = T.ghost_l1_end;
+	Lo.send_l1_end = T.send_l1_end;
+	Lo.border_cells.clear();
+	for(size_t k = 0; k + 1 < Lo.send_start.size(); k++) {
+		const int e = k < Lo.send_l1_end.size() ? Lo.send_l1_end[k] : Lo.send_start[k+1];
+		for(int i = Lo.send_start[k]; i < e; i++) Lo.border_cells.push_back(Lo.send_cells[i]);
+	}
 	std::sort(Lo.border_cells.begin(), Lo.border_cells.end());
 	Lo.border_cells.erase(std::unique(Lo.border_cells.begin(), Lo.border_cells.end()), Lo.border_cells.end());
 	Lo.cell_global.resize(NT);
@@ -314,6 +321,43 @@ Layout buildLayout(const MeshTopo& T, const fvhip_flow_config& cfg, bool renumbe
 		Lo.bf_rcbp[2*f] = T.rcbp[2*f]; Lo.bf_rcbp[2*f+1] = T.rcbp[2*f+1];
 		Lo.bf_tag[f] = tag;
 		Lo.bf_gr[2*f] = T.gr[2*static_cast<size_t>(f)]; Lo.bf_gr[2*f+1] = T.gr[2*static_cast<size_t>(f)+1];
+	}
+	// --- layer-1 ghosts of a two-layer halo: neighbour lists, extra boundary faces, WLS inverses ---
+	Lo.gg_cells = T.g1_cells;               // ghosts keep their local ids
+	Lo.gg_nbr.resize(T.g1_nbr.size());
+	for(size_t k = 0; k < T.g1_nbr.size(); k++) Lo.gg_nbr[k] = T.g1_nbr[k] >= 0 ? toInt(T.g1_nbr[k]) : T.g1_nbr[k];
+	Lo.xb_bc.resize(T.xb_btag.size());
+	for(size_t x = 0; x < T.xb_btag.size(); x++) {
+		int bi = -1;
+		for(int i = 0; i < cfg.nbc; i++) if(cfg.bc_tag[i] == T.xb_btag[x]) bi = i;
+		if(bi < 0) throw std::runtime_error("no boundary condition for marker " + std::to_string(T.xb_btag[x]));
+		Lo.xb_bc[x] = bi;
+	}
+	Lo.xb_n = T.xb_n; Lo.xb_rcbp = T.xb_rcbp;
+	if(cfg.gradientscheme == FVHIP_GRAD_LEASTSQUARES) {
+		// the host WLS normal matrix below, cell by cell: faces in ascending global order, the ghost's
+		// centre minus the other centre (the face loop's dr up to a sign that cancels in each term)
+		Lo.gg_V.resize(4*Lo.gg_cells.size());
+		for(size_t i = 0; i < Lo.gg_cells.size(); i++) {
+			const int g = Lo.gg_cells[i];
+			double v[4] = {0, 0, 0, 0};
+			for(int j = 0; j < MAXF; j++) {
+				const int nbk = Lo.gg_nbr[4*i+j];
+				if(nbk == -1) break;
+				const double* rn = nbk >= 0 ? &Lo.rc[2*static_cast<size_t>(nbk)] : &Lo.xb_rcbp[2*static_cast<size_t>(-2 - nbk)];
+				double w2 = 0, dr[2];
+				for(int d = 0; d < 2; d++) {
+					w2 += (Lo.rc[2*static_cast<size_t>(g)+d]-rn[d])*(Lo.rc[2*static_cast<size_t>(g)+d]-rn[d]);
+					dr[d] = Lo.rc[2*static_cast<size_t>(g)+d]-rn[d];
+				}
+				w2 = 1.0/(w2);
+				for(int a = 0; a < 2; a++) for(int b = 0; b < 2; b++) v[2*a+b] += w2*dr[a]*dr[b];
+			}
+			const double det = v[0]*v[3] - v[2]*v[1];
+			const double invdet = 1.0/det;
+			double* o = &Lo.gg_V[4*i];
+			o[0] = v[3]*invdet; o[2] = -v[2]*invdet; o[1] = -v[1]*invdet; o[3] = v[0]*invdet;
+		}
 	}
 	// --- interior faces (reference order) ---
 	Lo.if_L.resize(F-nb); Lo.if_R.resize(F-nb); Lo.if_slot.assign(F-nb, -1);

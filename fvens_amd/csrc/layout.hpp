@@ -76,7 +76,15 @@ struct Layout
 	// halo (partitioned meshes): ghosts from nbr_rank[k] are internal cells
 	// ncell+ghost_start[k] .. ncell+ghost_start[k+1]-1; send_cells[send_start[k]..] go to nbr_rank[k]
 	std::vector<int> nbr_rank, ghost_start, send_start, send_cells;
-	std::vector<int> border_cells;         ///< unique send cells (their gradients are computed first)
+	std::vector<int> border_cells;         ///< unique layer-1 send cells (their gradients are computed first)
+	// two-layer halo (partition.hpp MeshTopo): layer-1 then layer-2 rows in each neighbour's block
+	int halo_layers = 1;
+	std::vector<int> ghost_l1_end, send_l1_end;   ///< [nnbr]
+	std::vector<int> gg_cells;             ///< layer-1 ghosts whose gradients this rank computes
+	std::vector<int> gg_nbr;               ///< [n1][4] internal neighbour, -2-j extra boundary face, -1
+	std::vector<double> gg_V;              ///< [n1][4] their WLS inverses (as wls_V)
+	std::vector<int> xb_bc;                ///< extra boundary faces: BC index,
+	std::vector<double> xb_n, xb_rcbp;     ///<  normal [2], ghost centre [2]
 	std::vector<int> cell_global;          ///< [ncell+nghost] global cell of each internal cell
 	// fused residual (k_residual_wls): per patch, the ring-1 cells (far side of its cut faces) whose
 	// primitive states and gradients it recomputes, and the ring-2 cells (the other neighbours of the

@@ -4,6 +4,7 @@
 #include "partition.hpp"
 #include <algorithm>
 #include <cmath>
+#include <map>
 #include <numeric>
 #include <stdexcept>
 
@@ -332,19 +333,22 @@ MeshTopo topoFromRankMesh(const fvhip_mesh& m)
 	return T;
 }
 
-MeshTopo extractPartition(const fvhip_mesh& m, const int* part, int rank)
+MeshTopo extractPartition(const fvhip_mesh& m, const int* part, int rank, int layers)
 {
 	if(m.nconnface != 0) throw std::runtime_error("extractPartition: expects the single-domain mesh");
 	if(m.maxnfael > 4) throw std::runtime_error("cells with more than 4 faces are not supported");
+	if(layers != 1 && layers != 2) throw std::invalid_argument("extractPartition: layers must be 1 or 2");
 	const int N = m.nelem, nb = m.nbface, F = m.naface;
 	auto Lg = [&](int f) { return m.intfac[4*static_cast<size_t>(f)]; };
 	auto Rg = [&](int f) { return m.intfac[4*static_cast<size_t>(f)+1]; };
+	auto esuel = [&](int e, int j) { return m.esuel[static_cast<size_t>(e)*m.maxnfael+j]; };
 	MeshTopo T;
+	T.halo_layers = layers;
 	std::vector<int> loc(N, -1);
 	for(int e = 0; e < N; e++) if(part[e] == rank) { loc[e] = T.nown++; T.cell_global.push_back(e); }
 	if(T.nown == 0) throw std::runtime_error("extractPartition: rank owns no cells");
 
-	// faces touching owned cells, ascending global index; ghosts across interior faces
+	// faces touching owned cells, ascending global index; layer-1 ghosts across interior faces
 	std::vector<int> ghosts;
 	for(int f = 0; f < F; f++) {
 		const int l = Lg(f), r = Rg(f);
@@ -357,20 +361,42 @@ MeshTopo extractPartition(const fvhip_mesh& m, const int* part, int rank)
 		if(!ro) ghosts.push_back(r);
 	}
 	T.naface = static_cast<int>(T.face_global.size());
-	std::sort(ghosts.begin(), ghosts.end(), [&](int a, int b) { return part[a] < part[b] || (part[a] == part[b] && a < b); });
+	std::sort(ghosts.begin(), ghosts.end());
 	ghosts.erase(std::unique(ghosts.begin(), ghosts.end()), ghosts.end());
+	std::vector<char> layer(N, 0);                 // 1, 2: halo layer of a cell of this rank
+	for(const int g : ghosts) layer[g] = 1;
+	if(layers == 2) {
+		const size_t n1 = ghosts.size();
+		for(size_t i = 0; i < n1; i++)
+			for(int j = 0; j < m.nnode[ghosts[i]]; j++) {
+				const int e = esuel(ghosts[i], j);
+				if(e < 0 || e >= N || part[e] == rank || layer[e]) continue;
+				layer[e] = 2; ghosts.push_back(e);
+			}
+	}
+	// grouped by owner rank, layer 1 before layer 2, ascending global id
+	std::sort(ghosts.begin(), ghosts.end(), [&](int a, int b) {
+		return part[a] < part[b] || (part[a] == part[b] && (layer[a] < layer[b] || (layer[a] == layer[b] && a < b))); });
 	T.nghost = static_cast<int>(ghosts.size());
-	T.ghost_start.push_back(0);
+	// neighbour ranks: the owners of the ghosts. The relation is symmetric (a cell within two faces of
+	// another rank's cell sees that rank's cell within two faces), so they are also the ranks this one
+	// sends to
 	for(int i = 0; i < T.nghost; i++) {
 		const int g = ghosts[i];
 		loc[g] = T.nown + i;
 		T.cell_global.push_back(g);
 		if(T.nbr_rank.empty() || T.nbr_rank.back() != part[g]) {
 			if(!T.nbr_rank.empty()) T.ghost_start.push_back(i);
+			else T.ghost_start.push_back(0);
 			T.nbr_rank.push_back(part[g]);
 		}
+		if(layer[g] == 1) {
+			if(T.ghost_l1_end.size() < T.nbr_rank.size()) T.ghost_l1_end.push_back(i + 1);
+			else T.ghost_l1_end.back() = i + 1;
+		} else if(T.ghost_l1_end.size() < T.nbr_rank.size()) T.ghost_l1_end.push_back(i);
 	}
-	if(!T.nbr_rank.empty()) T.ghost_start.push_back(T.nghost);
+	if(T.nbr_rank.empty()) T.ghost_start.push_back(0);
+	else T.ghost_start.push_back(T.nghost);
 	const int NT = T.ncell();
 
 	// faces
@@ -410,28 +436,97 @@ MeshTopo extractPartition(const fvhip_mesh& m, const int* part, int rank)
 		for(int j = 0; j < m.nnode[e]; j++) {
 			const int f = m.elemface[static_cast<size_t>(e)*m.maxnfael+j];
 			T.cell_faces[4*static_cast<size_t>(c)+j] = floc[f];
-			const int nbr = m.esuel[static_cast<size_t>(e)*m.maxnfael+j];
+			const int nbr = esuel(e, j);
 			T.cell_esuel[4*static_cast<size_t>(c)+j] = nbr >= N ? NT + floc[f] : loc[nbr];
 		}
 	}
 
-	// send lists: owned cells adjacent to a cell of each neighbour rank, ascending global id
+	// layer-1 ghosts: neighbour lists in ascending global face order for their local gradients;
+	// physical boundary faces that touch no owned cell become "extra" boundary faces
+	if(layers == 2) {
+		std::vector<int> xbloc;
+		std::map<int,int> xbof;
+		for(int i = 0; i < T.nghost; i++) {
+			const int g = ghosts[i];
+			if(layer[g] != 1) continue;
+			T.g1_cells.push_back(T.nown + i);
+			int fs[4];
+			const int k = m.nnode[g];
+			for(int j = 0; j < k; j++) fs[j] = m.elemface[static_cast<size_t>(g)*m.maxnfael+j];
+			std::sort(fs, fs + k);
+			for(int j = 0; j < 4; j++) {
+				if(j >= k) { T.g1_nbr.push_back(-1); continue; }
+				const int f = fs[j];
+				if(f < nb) {
+					auto it = xbof.find(f);
+					int x;
+					if(it != xbof.end()) x = it->second;
+					else {
+						x = static_cast<int>(T.xb_btag.size());
+						xbof[f] = x;
+						T.xb_btag.push_back(m.btags[static_cast<size_t>(f)*m.nbtag]);
+						T.xb_n.push_back(m.facemetric[3*static_cast<size_t>(f)]);
+						T.xb_n.push_back(m.facemetric[3*static_cast<size_t>(f)+1]);
+						T.xb_rcbp.push_back(m.rcbp[2*static_cast<size_t>(f)]);
+						T.xb_rcbp.push_back(m.rcbp[2*static_cast<size_t>(f)+1]);
+					}
+					T.g1_nbr.push_back(-2 - x);
+					continue;
+				}
+				const int other = Lg(f) != g ? Lg(f) : Rg(f);
+				if(loc[other] < 0) throw std::logic_error("extractPartition: layer-2 halo incomplete");
+				T.g1_nbr.push_back(loc[other]);
+			}
+		}
+	}
+
+	// send lists: per neighbour rank q, the owned cells q holds as ghosts, in q's order (layer, global
+	// id); the layer of an owned cell for q is its face distance (1 or 2) to q's cells
+	std::vector<std::vector<std::pair<int,int>>> sends(T.nbr_rank.size());
+	std::vector<int> kof;
+	{
+		int maxr = 0;
+		for(const int q : T.nbr_rank) maxr = std::max(maxr, q);
+		kof.assign(maxr + 1, -1);
+		for(size_t k = 0; k < T.nbr_rank.size(); k++) kof[T.nbr_rank[k]] = static_cast<int>(k);
+	}
+	std::vector<int> dq;                             // (rank, distance) seen from one owned cell
+	for(int c = 0; c < T.nown; c++) {
+		const int e = T.cell_global[c];
+		dq.clear();
+		for(int j = 0; j < m.nnode[e]; j++) {
+			const int a = esuel(e, j);
+			if(a < 0 || a >= N) continue;
+			if(part[a] != rank) { dq.push_back(part[a]); dq.push_back(1); }
+			if(layers < 2) continue;
+			for(int jj = 0; jj < m.nnode[a]; jj++) {
+				const int b = esuel(a, jj);
+				if(b < 0 || b >= N || part[b] == rank) continue;
+				dq.push_back(part[b]); dq.push_back(2);
+			}
+		}
+		for(size_t i = 0; i < dq.size(); i += 2) {
+			const int q = dq[i];
+			int d = dq[i+1];
+			bool first = true;
+			for(size_t i2 = 0; i2 < dq.size(); i2 += 2) {
+				if(dq[i2] != q) continue;
+				if(dq[i2+1] < d || (dq[i2+1] == d && i2 < i)) { first = false; break; }
+			}
+			if(!first) continue;
+			if(q >= static_cast<int>(kof.size()) || kof[q] < 0) throw std::logic_error("extractPartition: halo not symmetric");
+			sends[kof[q]].push_back({d, e});
+		}
+	}
 	T.send_start.push_back(0);
 	for(size_t k = 0; k < T.nbr_rank.size(); k++) {
-		const int q = T.nbr_rank[k];
-		std::vector<int> s;
-		for(int i = 0; i < T.naface; i++) {
-			const int f = T.face_global[i];
-			if(f < nb) continue;
-			const int l = Lg(f), r = Rg(f);
-			if(part[l] == rank && part[r] == q) s.push_back(l);
-			if(part[r] == rank && part[l] == q) s.push_back(r);
-		}
-		std::sort(s.begin(), s.end());
-		s.erase(std::unique(s.begin(), s.end()), s.end());
-		for(int g : s) T.send_cells.push_back(loc[g]);
+		std::sort(sends[k].begin(), sends[k].end());
+		int n1 = 0;
+		for(const auto& s : sends[k]) { T.send_cells.push_back(loc[s.second]); n1 += s.first == 1; }
+		T.send_l1_end.push_back(T.send_start.back() + n1);
 		T.send_start.push_back(static_cast<int>(T.send_cells.size()));
 	}
+	if(layers == 1) { T.ghost_l1_end.assign(T.ghost_start.begin() + 1, T.ghost_start.end()); }
 	return T;
 }
 

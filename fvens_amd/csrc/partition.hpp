@@ -46,6 +46,19 @@ struct MeshTopo
 	std::vector<int> send_start;       ///< [nnbr+1] ranges into send_cells
 	std::vector<int> send_cells;       ///< local owned cells each neighbour holds as ghosts (ascending global id)
 	std::vector<int> ghost_row;        ///< [nghost] per-rank meshes: reference row (nelem+icface) of each ghost
+	// two-layer halo (extractPartition): each neighbour's ghost block and send block hold its layer-1
+	// cells (across a face of an owned cell) first, then its layer-2 cells (across a face of a layer-1
+	// ghost); one exchange of u fills both, and the layer-1 ghosts' gradients are then computed
+	// locally from the g1_* lists instead of being exchanged
+	int halo_layers = 1;
+	std::vector<int> ghost_l1_end;     ///< [nnbr] end of neighbour k's layer-1 ghosts (same base as ghost_start)
+	std::vector<int> send_l1_end;      ///< [nnbr] end of neighbour k's layer-1 sends (same base as send_start)
+	std::vector<int> g1_cells;         ///< local ids of the layer-1 ghosts
+	std::vector<int> g1_nbr;           ///< [n1][4] their neighbours in ascending GLOBAL face order: local
+	                                   ///<  cell, -2-j (extra boundary face j), -1 none
+	std::vector<int> xb_btag;          ///< extra boundary faces (touching a layer-1 ghost only): marker,
+	std::vector<double> xb_n;          ///<  unit normal [2] (facemetric),
+	std::vector<double> xb_rcbp;       ///<  ghost-cell centre [2]
 };
 
 /// Whole mesh as one rank (no ghosts)
@@ -62,8 +75,9 @@ MeshTopo topoFromMesh(const fvhip_mesh& m);
 /// and accumulation order are the subdomain's own.
 MeshTopo topoFromRankMesh(const fvhip_mesh& m);
 
-/// Rank `rank`'s piece of a single-domain mesh partitioned by `part` (part[cell] in [0,nparts))
-MeshTopo extractPartition(const fvhip_mesh& m, const int* part, int rank);
+/// Rank `rank`'s piece of a single-domain mesh partitioned by `part` (part[cell] in [0,nparts)),
+/// with a two-layer halo (layers = 2, the default) or the one-layer halo of round 1 (layers = 1)
+MeshTopo extractPartition(const fvhip_mesh& m, const int* part, int rank, int layers = 2);
 
 /// Recursive coordinate bisection of cell centres into nparts parts with sizes differing by at
 /// most one cell per bisection level; deterministic (ties broken by cell index)

@@ -143,6 +143,14 @@ long long fvhip_partition_edge_cut(const fvhip_mesh* mesh, const int* part);
  *  then ghosts by owner rank), nbr_rank [nnbr], ghost_start/send_start [nnbr+1], send_global [nsend] */
 int fvhip_partition_info(const fvhip_mesh* mesh, const int* part, int rank, int* counts, int* cell_global,
                          int* nbr_rank, int* ghost_start, int* send_start, int* send_global);
+/** The two halo layers inside those lists (host only): each neighbour's ghost block and send block
+ *  hold its layer-1 cells (across a face of an owned cell) first, then its layer-2 cells (across a
+ *  face of a layer-1 ghost); ghost_l1_end / send_l1_end [nnbr] are where layer 1 ends (same base as
+ *  ghost_start / send_start). One exchange of u fills both layers and the layer-1 ghosts' WLS
+ *  gradients are then computed locally: the reference's two exchanges (state, then ghost gradients,
+ *  flow_spatial.cpp:636-816) become one. */
+int fvhip_partition_halo_layers(const fvhip_mesh* mesh, const int* part, int rank, int* ghost_l1_end,
+                                int* send_l1_end);
 /** The rank's handle; host u/r/dtm then hold the owned cells in ascending global order, device
  *  u has owned+ghost rows (fvhip_layout_stats[6] = ghosts) and the ghost rows are filled by it */
 int fvhip_create_partitioned(const fvhip_mesh* mesh, const fvhip_flow_config* cfg, const int* part, int nparts,

@@ -41,10 +41,18 @@ def test_halo_lists_consistent(nparts):
         own = inf["cell_global"][:inf["owned"]]
         assert np.all(part[own] == r) and np.all(np.diff(own) > 0)
         ghosts = inf["cell_global"][inf["owned"]:]
-        # ghosts are exactly the off-rank cells across interior faces of owned cells
+        # layer 1: exactly the off-rank cells across interior faces of owned cells; layer 2: the
+        # off-rank cells across interior faces of layer-1 cells that are not layer 1 themselves
         Li, Ri = L[nb:], R[nb:]
-        exp = set(Ri[(part[Li] == r) & (part[Ri] != r)]) | set(Li[(part[Ri] == r) & (part[Li] != r)])
-        assert set(ghosts.tolist()) == exp and len(ghosts) == len(exp)
+        exp1 = set(Ri[(part[Li] == r) & (part[Ri] != r)]) | set(Li[(part[Ri] == r) & (part[Li] != r)])
+        in1 = np.zeros(m.nelem, bool)
+        in1[list(exp1)] = True
+        exp2 = set(Ri[in1[Li] & (part[Ri] != r) & ~in1[Ri]]) | set(Li[in1[Ri] & (part[Li] != r) & ~in1[Li]])
+        g1 = np.concatenate([ghosts[inf["ghost_start"][k]:inf["ghost_l1_end"][k]] for k in range(len(inf["nbr_rank"]))] or [[]])
+        g2 = np.concatenate([ghosts[inf["ghost_l1_end"][k]:inf["ghost_start"][k + 1]] for k in range(len(inf["nbr_rank"]))] or [[]])
+        assert set(g1.tolist()) == exp1 and len(g1) == len(exp1)
+        assert set(g2.tolist()) == exp2 and len(g2) == len(exp2)
+        assert len(ghosts) == len(exp1) + len(exp2)
         # every face touching an owned cell, boundary faces = those of owned cells
         touching = np.count_nonzero((part[Li] == r) | (part[Ri] == r))
         bnd = np.count_nonzero(part[L[:nb]] == r)
@@ -57,6 +65,12 @@ def test_halo_lists_consistent(nparts):
             kk = list(other["nbr_rank"]).index(r)
             sent = other["send_global"][other["send_start"][kk]:other["send_start"][kk + 1]]
             np.testing.assert_array_equal(mine, sent)
+            # the layer-1 parts agree too (a one-layer exchange moves just those)
+            n1 = inf["ghost_l1_end"][k] - inf["ghost_start"][k]
+            assert n1 == other["send_l1_end"][kk] - other["send_start"][kk]
+            # owner rank, then layer, then ascending global id
+            assert np.all(part[mine] == q)
+            assert np.all(np.diff(mine[:n1]) > 0) and np.all(np.diff(mine[n1:]) > 0)
     cut = np.count_nonzero(part[L[nb:]] != part[R[nb:]])
     assert faces_total == m.naface + cut
 
