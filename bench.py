@@ -9,9 +9,9 @@ One step = one full residual evaluation (primitive conversion, BC ghosts, WLS gr
 reconstruction/flux/scatter/time-step sweep) with the state resident in HBM.
 Multi-GPU (torchrun, one process per GPU): the mesh is partitioned (--partitioner graph: recursive
 graph bisection of the cell dual graph, the stand-in for the reference's Scotch; or rcb), each rank holds
-its cells plus one ghost layer, and the ghost rows of u and of the gradients are exchanged every
-residual with RCCL ncclSend/ncclRecv over xGMI (the library's own communicator), overlapped with the
-patches that need no halo data.
+its cells plus a two-layer halo: ONE exchange of u per residual (both layers, RCCL ncclSend/ncclRecv
+over xGMI with the library's own communicator) after which each rank computes its layer-1 ghosts'
+gradients itself, overlapped with the patches that need no halo data.
 --scaling strong (default): the C4 mesh itself is split N ways (BASELINE.json config 4); afterwards every
 rank's owned residual is compared bit for bit with a 1-GPU residual of the whole mesh (halo_parity);
 --scaling weak: the O-grid has N x 2048 cells around, so every GPU owns a C4-size part.
@@ -31,11 +31,15 @@ sys.path.insert(0, os.path.join(ROOT, "tests"))
 HBM_PEAK_GBS = 8000.0   # MI355X HBM3E spec (MI355X_MICROARCH.md)
 
 
-def c4_mesh(fa, scale, mult=1):
+C4_WALL_SPACING = 1e-5
+
+
+def c4_mesh(fa, scale, mult=1, wall=None):
     nt = 2048 * mult // scale
     nq = 256 // scale
     ntri = 864 // scale
-    return fa.UMesh.naca_ogrid(nt, nq, ntri, 20.0, 1e-5), dict(ntheta=nt, nquad=nq, ntri=ntri)
+    ws = C4_WALL_SPACING if wall is None else wall
+    return fa.UMesh.naca_ogrid(nt, nq, ntri, 20.0, ws), dict(ntheta=nt, nquad=nq, ntri=ntri, wall_spacing=ws)
 
 
 def sweep_algorithmic_bytes(N, F, Fb):
@@ -51,11 +55,12 @@ def sweep_bytes_area_dt(N, F, Fb):
 
 
 def residual_algorithmic_bytes(N, F, Fb):
-    """Compulsory bytes of the one-launch residual k_residual_wls (gradients computed in LDS, never
-    stored): 32 B/face (L,R 8 + nx,ny,len 24) + 128 B/cell (conserved state 32 + centre 16 + WLS
-    inverse 32 + area 8 read; residual 32 + time step 8 written) + 16 B/boundary face (ghost centre;
-    the ghost state is computed in registers)."""
-    return 32 * F + 128 * N + 16 * Fb
+    """Compulsory bytes of the one-launch residual k_residual_wls (gradients and WLS inverses computed
+    in LDS / registers, never stored): 32 B/face (L,R 8 + nx,ny,len 24) + 96 B/cell (conserved state
+    32 + centre 16 + area 8 read; residual 32 + time step 8 written) + 16 B/boundary face (ghost
+    centre; the ghost state is computed in registers). Index data (packed 16-bit neighbour, slot and
+    face codes) and the ring-1/ring-2 re-reads come on top and show in the PMC traffic."""
+    return 32 * F + 96 * N + 16 * Fb
 
 
 def prep_algorithmic_bytes(N, F, Fb):
@@ -384,7 +389,11 @@ def main():
 
     halo = None
     if world > 1:
-        halo = {"layout_per_rank": None, "halo_parity": None}
+        halo = {"layout_per_rank": None, "halo_parity": None, "halo_layers": 2,
+                "exchange_rounds_per_residual": 1,
+                "exchange": "one RCCL ncclSend/ncclRecv round of u rows (layer-1 + layer-2 ghosts); layer-1 "
+                            "ghost gradients computed locally (k_grad_ghost), on a comm stream overlapped "
+                            "with the interior patches"}
         allstats = [None] * world
         dist.all_gather_object(allstats, stats)
         halo["layout_per_rank"] = [{k: st[k] for k in ("cells", "ghosts", "neighbours", "send_rows",

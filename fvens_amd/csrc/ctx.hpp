@@ -142,6 +142,8 @@ struct fvhip_ctx
 	int* d_fz_order = nullptr;
 	hipStream_t comm_stream = nullptr;
 	hipEvent_t ev_u = nullptr, ev_halo = nullptr;
+	hipEvent_t ev_packed = nullptr, ev_copied = nullptr;   ///< in-process overlapped transport (groups)
+	bool copied_recorded = false;
 	int* d_send = nullptr;
 	int* d_border = nullptr;
 	int nborder = 0;
@@ -163,6 +165,8 @@ struct fvhip_ctx
 		if(stream2) (void)hipStreamDestroy(stream2);
 		if(ev_u) (void)hipEventDestroy(ev_u);
 		if(ev_halo) (void)hipEventDestroy(ev_halo);
+		if(ev_packed) (void)hipEventDestroy(ev_packed);
+		if(ev_copied) (void)hipEventDestroy(ev_copied);
 		if(comm_stream) (void)hipStreamDestroy(comm_stream);
 		for(void* p : owned) (void)hipFree(p);
 		for(void* p : owned_host) (void)hipHostFree(p);
@@ -350,15 +354,82 @@ struct fvhip_ctx
 		timed_on(st, "k_grad_ghost", [&]{ KOPS(launch_grad_ghost)(M, P, u, d_grad, st); });
 	}
 
+	/// the second stream and events of the overlapped fused residual
+	void ensureOverlap() {
+		if(comm_stream) return;
+		HC(hipStreamCreateWithFlags(&comm_stream, hipStreamNonBlocking));
+		for(hipEvent_t* e : {&ev_u, &ev_halo, &ev_packed, &ev_copied}) HC(hipEventCreateWithFlags(e, hipEventDisableTiming));
+	}
+
+	/// The overlapped fused residual of a group held by one process (fvhip_group_*): the schedule of
+	/// residual_fused_overlapped with the in-process transport placed on each handle's comm stream --
+	/// pack, device copies that wait on the sender's pack, ghost gradients, halo event -- while the
+	/// interior patches run on the handle's stream and the border patches wait for the halo event.
+	/// The stream/event ordering and the send-buffer reuse of the RCCL path therefore run (and are
+	/// checked bitwise against one GPU) with several ranks on one device, where RCCL cannot.
+	static void residual_group_overlapped(std::vector<fvhip_ctx*>& hs, const std::vector<const double*>& us,
+	                                      const std::vector<double*>& rs, bool dt, const std::vector<double*>& dts,
+	                                      bool overwrite) {
+		const size_t n = hs.size();
+		std::vector<fvhip_ctx*> byrank(n, nullptr);
+		for(fvhip_ctx* h : hs) {
+			if(h->rank < 0 || h->rank >= static_cast<int>(n)) throw std::logic_error("group: ranks are not 0..n-1");
+			byrank[h->rank] = h;
+		}
+		auto on = [&](size_t i) -> fvhip_ctx* { HC(hipSetDevice(hs[i]->device)); return hs[i]; };
+		// 1. the comm stream takes u as the caller left it; a send buffer is refilled only after every
+		//    receiver has copied the previous exchange out of it
+		for(size_t i = 0; i < n; i++) {
+			fvhip_ctx* h = on(i);
+			h->ensureOverlap();
+			HC(hipEventRecord(h->ev_u, h->stream));
+			HC(hipStreamWaitEvent(h->comm_stream, h->ev_u, 0));
+			for(fvhip_ctx* q : hs) if(q->copied_recorded) HC(hipStreamWaitEvent(h->comm_stream, q->ev_copied, 0));
+			h->pack(us[i], 4, h->comm_stream);
+			HC(hipEventRecord(h->ev_packed, h->comm_stream));
+		}
+		// 2. the patches that read no halo data
+		for(size_t i = 0; i < n; i++)
+			on(i)->stage_fused(us[i], rs[i], dt, dts[i], overwrite, hs[i]->d_fz_order, hs[i]->L.fz_ninner);
+		// 3. receive both halo layers (copies wait on the sender's pack), layer-1 ghost gradients
+		for(size_t i = 0; i < n; i++) {
+			fvhip_ctx* h = on(i);
+			const Layout& L = h->L;
+			for(size_t k = 0; k < L.nbr_rank.size(); k++) {
+				fvhip_ctx* q = byrank[L.nbr_rank[k]];
+				const Layout& Q = q->L;
+				size_t kk = 0;
+				while(kk < Q.nbr_rank.size() && Q.nbr_rank[kk] != h->rank) kk++;
+				if(kk == Q.nbr_rank.size()) throw std::logic_error("halo lists are not symmetric");
+				const int cnt = h->ghostCount(k, 2);
+				if(cnt != q->sendCount(kk, 2)) throw std::logic_error("halo sizes differ");
+				if(cnt == 0) continue;
+				HC(hipStreamWaitEvent(h->comm_stream, q->ev_packed, 0));
+				HC(hipMemcpyAsync(const_cast<double*>(us[i]) + 4*static_cast<size_t>(L.ncell + L.ghost_start[k]),
+				                  q->d_sendbuf + 4*static_cast<size_t>(Q.send_start[kk]),
+				                  sizeof(double)*4*static_cast<size_t>(cnt), hipMemcpyDeviceToDevice, h->comm_stream));
+			}
+			h->stage_ghost_gradients(us[i], h->comm_stream);
+			HC(hipEventRecord(h->ev_copied, h->comm_stream));
+			HC(hipEventRecord(h->ev_halo, h->comm_stream));
+		}
+		for(fvhip_ctx* h : hs) h->copied_recorded = true;
+		// 4. the border patches once the halo is in place; later work on a handle's stream (the next
+		//    pack of a synchronous exchange included) also follows every copy out of its send buffer
+		for(size_t i = 0; i < n; i++) {
+			fvhip_ctx* h = on(i);
+			HC(hipStreamWaitEvent(h->stream, h->ev_halo, 0));
+			for(fvhip_ctx* q : hs) HC(hipStreamWaitEvent(h->stream, q->ev_copied, 0));
+			h->stage_fused(us[i], rs[i], dt, dts[i], overwrite, h->d_fz_order + h->L.fz_ninner,
+			               static_cast<int>(h->L.fz_order.size()) - h->L.fz_ninner);
+		}
+	}
+
 	/// fused residual of one RCCL rank: the halo exchange (ghost u, border gradients, ghost
 	/// gradients) runs on comm_stream while the interior patches run on `stream`; the border
 	/// patches follow once the halo has arrived
 	void residual_fused_overlapped(const double* u, double* r, bool dt, double* dtm, bool overwrite) {
-		if(!comm_stream) {
-			HC(hipStreamCreateWithFlags(&comm_stream, hipStreamNonBlocking));
-			HC(hipEventCreateWithFlags(&ev_u, hipEventDisableTiming));
-			HC(hipEventCreateWithFlags(&ev_halo, hipEventDisableTiming));
-		}
+		ensureOverlap();
 		double* uu = const_cast<double*>(u);
 		HC(hipEventRecord(ev_u, stream));                 // u as the caller left it
 		HC(hipStreamWaitEvent(comm_stream, ev_u, 0));
@@ -408,6 +479,7 @@ struct fvhip_ctx
 		if(h0->fused()) {
 			if(h0->halo()) {
 				if(hs.size() == 1 && !exg) { h0->residual_fused_overlapped(us[0], rs[0], dt, dts[0], overwrite); return; }
+				if(single && exg) { residual_group_overlapped(hs, us, rs, dt, dts, overwrite); return; }
 				// interior patches need no halo data: they run first, then the exchange of the ghost
 				// rows of u and of the gradients of the cells other ranks hold as ghosts, then the rest
 				for(size_t i = 0; i < hs.size(); i++)

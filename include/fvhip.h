@@ -125,9 +125,11 @@ int fvhip_destroy(fvhip_handle h);
  * Multi-GPU (one rank per GPU). Replaces the reference's partitioned mesh (meshpartitioning.cpp:
  * 24-159, Scotch :376-458) and ghost scatters (alinalg.cpp:17-29, tracevector.cpp:213-340).
  * Every rank passes the single-domain mesh and the same partition vector; the handle holds the
- * rank's owned cells plus one ghost layer, faces in global order with global orientation, so the
- * residual of every owned cell is bitwise the single-GPU one. Ghost rows of u, gradients and
- * limiter data are exchanged with RCCL ncclSend/ncclRecv on the handle's stream.
+ * rank's owned cells plus a two-layer halo, faces in global order with global orientation, so the
+ * residual of every owned cell is bitwise the single-GPU one. For WLS gradients with an unlimited or
+ * MUSCL reconstruction one RCCL ncclSend/ncclRecv round of u per residual fills both halo layers
+ * and the layer-1 ghosts' gradients are computed locally; other schemes exchange u, gradients and
+ * limiter data in turn (one-layer exchanges).
  * -------------------------------------------------------------------------------------------- */
 typedef struct fvhip_group_s* fvhip_group;
 /** Recursive coordinate bisection of the cell centres into nparts (part [nelem]) */

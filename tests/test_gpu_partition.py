@@ -92,3 +92,49 @@ def test_partitioned_fast_math_within_tolerance():
     scale = np.abs(r1).max(axis=0)
     assert np.all(np.abs(r - r1).max(axis=0) <= 1e-11 * scale)
     np.testing.assert_allclose(dt, dt1, rtol=1e-12, atol=0)
+
+
+@pytest.mark.parametrize("nparts", [3, 8])
+def test_overlapped_group_repeated_residuals(nparts):
+    """the group's overlapped schedule (pack and halo copies on each rank's comm stream, interior
+    patches concurrent, border patches behind the halo event; ONE exchange of the two-layer halo):
+    five residuals back to back on different states, each compared bit for bit with one GPU -- a
+    send buffer refilled before a receiver copied it, or a border patch ahead of its ghost gradients,
+    would show up as a mismatch"""
+    import torch
+    m, _ = get_mesh("naca_small")
+    p = cases.physics("naca")
+    n = cases.numerics("ROE", "LEASTSQUARES", "VANALBADA")
+    one = fa.FlowFV(m, p, n)
+    part = fa.partition_rcb(m, nparts)
+    sps = [fa.FlowFV(m, p, n, partition=part, rank=k) for k in range(nparts)]
+    grp = fa.FlowFVGroup(sps)
+    gl = [np.nonzero(part == k)[0][sp.permutation()] for k, sp in enumerate(sps)]
+    dus = [torch.full((sp.nown + sp.nghost, 4), float("nan"), dtype=torch.float64, device="cuda") for sp in sps]
+    drs = [torch.zeros((sp.nown, 4), dtype=torch.float64, device="cuda") for sp in sps]
+    dts = [torch.zeros(sp.nown, dtype=torch.float64, device="cuda") for sp in sps]
+    results = []
+    for it in range(5):
+        u = cases.state(m, p, seed=100 + it)
+        for k in range(nparts):
+            dus[k][:sps[k].nown] = torch.tensor(u[gl[k]], device="cuda")
+        torch.cuda.synchronize()         # torch's stream and the library's streams
+        grp.compute_residual_device([d.data_ptr() for d in dus], [d.data_ptr() for d in drs],
+                                    [d.data_ptr() for d in dts], True, True)
+        torch.cuda.synchronize()
+        r = np.full((m.nelem, 4), np.nan)
+        dt = np.full(m.nelem, np.nan)
+        for k in range(nparts):
+            r[gl[k]] = drs[k].cpu().numpy()
+            dt[gl[k]] = dts[k].cpu().numpy()
+        r1 = np.zeros((m.nelem, 4))
+        dt1 = np.zeros(m.nelem)
+        one.compute_residual(u, r1, True, dt1)
+        results.append((r, dt, r1, dt1))
+    grp.close()
+    for sp in sps:
+        sp.close()
+    one.close()
+    for r, dt, r1, dt1 in results:
+        np.testing.assert_array_equal(r, r1)
+        np.testing.assert_array_equal(dt, dt1)
