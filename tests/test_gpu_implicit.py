@@ -331,7 +331,11 @@ def test_naca0012_implicit_functional_regression():
     main = HLLC + least squares + Van Albada (CFL 500-5000, tol 1e-7), robust_flow update (0.2),
     Jacobian 'consistent' (HLLC), -ksp_rtol 1e-1, -ksp_max_it 30. The reference preconditions with
     SOR; block-Jacobi sweeps here, so its step count may differ (max_timesteps raised 170 -> 600).
-    Bars: CL (the reference's 1e-6) and CDp (1e-6) relative to regr-MUSCL_LeastSquares_HLLC.txt."""
+    Bars: CL (the reference's 1e-6) and CDp 1e-7 relative to regr-MUSCL_LeastSquares_HLLC.txt (the
+    reference: 1e-8). Measured on MI355X (tools/regr_probe.py): 136 steps to the 1e-7 drop, CL 8.2e-8 /
+    CDp 3.3e-8; converged on to a 1e-11 drop, CL 9.07e-8 / CDp 4.65e-8 -- the gap of the file's own
+    values to the converged discrete solution, so 1e-8 holds only along the reference's solver path.
+    The second solve below converges to the 1e-11 drop and checks that gap."""
     m = fa.UMesh.read_gmsh(cases.fixture_mesh("naca0012luo"))
     om = orc.OracleMesh.read(cases.fixture_mesh("naca0012luo"))
     p = cases.physics("naca")
@@ -356,6 +360,15 @@ def test_naca0012_implicit_functional_regression():
     assert dcl == cl and dcdp == cdp
     assert st["converged"], st
     assert abs(cl - 0.154112792928976) / 0.154112792928976 <= 1e-6
-    assert abs(cdp - 0.0115814414408097) / 0.0115814414408097 <= 1e-6
+    assert abs(cdp - 0.0115814414408097) / 0.0115814414408097 <= 1e-7
+    # converged to a 1e-11 drop: the discrete solution's own functionals
+    st2, _ = main.steady_backward_euler_device(dU.data_ptr(), fa.ImplicitConfig(cflinit=500.0, cflfin=5000.0,
+                                                                               tol=1e-4, maxiter=600, **lin))
+    (ccl, ccdp, _), _ = main.surface_data_device(dU.data_ptr(), 2)
+    print(f"converged further {st2} CL rel {abs(ccl - 0.154112792928976) / 0.154112792928976:.3e} "
+          f"CDp rel {abs(ccdp - 0.0115814414408097) / 0.0115814414408097:.3e}")
+    assert st2["converged"], st2
+    assert abs(ccl - 0.154112792928976) / 0.154112792928976 <= 2e-7
+    assert abs(ccdp - 0.0115814414408097) / 0.0115814414408097 <= 1e-7
     start.close()
     main.close()
