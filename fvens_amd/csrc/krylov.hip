@@ -338,6 +338,140 @@ void k_line_solve(int nlines, const int* __restrict__ lstart, const int* __restr
 	}
 }
 
+/// Wave-per-line forms of the two kernels above (one 64-lane workgroup per line): the lanes stage 64
+/// cells' blocks of the line in LDS with independent loads, then one lane runs the recurrence over them
+/// from LDS and the lanes write the results back. The recurrence is the same arithmetic in the same
+/// order, so the results are bitwise those of the one-thread-per-line kernels; what goes is the global
+/// load latency inside the sequential chain (a line of a few hundred cells walked by one thread paid
+/// one memory round trip per cell).
+constexpr int LCH = 64;
+
+__global__ __launch_bounds__(64)
+void k_line_factor_w(int nlines, const int* __restrict__ lstart, const int* __restrict__ lcell, const int* __restrict__ lface,
+                     const double* __restrict__ diag, const double* __restrict__ lower, const double* __restrict__ upper,
+                     double* __restrict__ dinvp)
+{
+	__shared__ __attribute__((aligned(32))) double sD[LCH][16], sL[LCH][16], sU[LCH][16];
+	__shared__ int sc[LCH];
+	const int l = blockIdx.x, j = threadIdx.x;
+	if(l >= nlines) return;
+	const int k0 = lstart[l], k1 = lstart[l+1];
+	double prev[4][4];
+	for(int base = k0; base < k1; base += LCH) {
+		const int n = min(LCH, k1 - base);
+		__syncthreads();                         // the previous chunk is written back
+		if(j < n) {
+			const int k = base + j, c = lcell[k];
+			sc[j] = c;
+			for(int e = 0; e < 16; e++) sD[j][e] = diag[16*static_cast<size_t>(c) + e];
+			if(k > k0) {
+				const double* L = blk_cp(lface[k], lower, upper);
+				const double* U = blk_pc(lface[k], lower, upper);
+				for(int e = 0; e < 16; e++) { sL[j][e] = L[e]; sU[j][e] = U[e]; }
+			}
+		}
+		__syncthreads();
+		if(j == 0) {
+			for(int i = 0; i < n; i++) {
+				double a[4][4], b[4][4];
+				#pragma unroll
+				for(int r = 0; r < 4; r++)
+					#pragma unroll
+					for(int q = 0; q < 4; q++) a[r][q] = sD[i][4*r+q];
+				if(base + i > k0) {
+					double t[4][4];
+					#pragma unroll
+					for(int r = 0; r < 4; r++)
+						#pragma unroll
+						for(int q = 0; q < 4; q++)
+							t[r][q] = prev[r][0]*sU[i][q] + prev[r][1]*sU[i][4+q] + prev[r][2]*sU[i][8+q] + prev[r][3]*sU[i][12+q];
+					#pragma unroll
+					for(int r = 0; r < 4; r++)
+						#pragma unroll
+						for(int q = 0; q < 4; q++)
+							a[r][q] -= sL[i][4*r]*t[0][q] + sL[i][4*r+1]*t[1][q] + sL[i][4*r+2]*t[2][q] + sL[i][4*r+3]*t[3][q];
+				}
+				inv4(a, b);
+				#pragma unroll
+				for(int r = 0; r < 4; r++)
+					#pragma unroll
+					for(int q = 0; q < 4; q++) { sD[i][4*r+q] = b[r][q]; prev[r][q] = b[r][q]; }
+			}
+		}
+		__syncthreads();
+		if(j < n) for(int e = 0; e < 16; e++) dinvp[16*static_cast<size_t>(sc[j]) + e] = sD[j][e];
+	}
+}
+
+__global__ __launch_bounds__(64)
+void k_line_solve_w(int nlines, const int* __restrict__ lstart, const int* __restrict__ lcell, const int* __restrict__ lface,
+                    const double* __restrict__ dinvp, const double* __restrict__ lower, const double* __restrict__ upper,
+                    const double* __restrict__ v, double* __restrict__ z)
+{
+	__shared__ __attribute__((aligned(32))) double sD[LCH][16], sB[LCH][16], sv[LCH][4];
+	__shared__ int sc[LCH];
+	const int l = blockIdx.x, j = threadIdx.x;
+	if(l >= nlines) return;
+	const int k0 = lstart[l], k1 = lstart[l+1];
+	double4 g = make_double4(0, 0, 0, 0);
+	// forward: g_k = dinvp_k (v_k - A[k][k-1] g_{k-1})
+	for(int base = k0; base < k1; base += LCH) {
+		const int n = min(LCH, k1 - base);
+		__syncthreads();
+		if(j < n) {
+			const int k = base + j, c = lcell[k];
+			sc[j] = c;
+			for(int e = 0; e < 16; e++) sD[j][e] = dinvp[16*static_cast<size_t>(c) + e];
+			for(int e = 0; e < 4; e++) sv[j][e] = v[4*static_cast<size_t>(c) + e];
+			if(k > k0) { const double* L = blk_cp(lface[k], lower, upper); for(int e = 0; e < 16; e++) sB[j][e] = L[e]; }
+		}
+		__syncthreads();
+		if(j == 0) {
+			for(int i = 0; i < n; i++) {
+				double4 r = make_double4(sv[i][0], sv[i][1], sv[i][2], sv[i][3]);
+				if(base + i > k0) {
+					double t[4];
+					blk_mv(sB[i], g, t);
+					r.x -= t[0]; r.y -= t[1]; r.z -= t[2]; r.w -= t[3];
+				}
+				double y[4];
+				blk_mv(sD[i], r, y);
+				g = make_double4(y[0], y[1], y[2], y[3]);
+				sv[i][0] = y[0]; sv[i][1] = y[1]; sv[i][2] = y[2]; sv[i][3] = y[3];
+			}
+		}
+		__syncthreads();
+		if(j < n) for(int e = 0; e < 4; e++) z[4*static_cast<size_t>(sc[j]) + e] = sv[j][e];
+	}
+	// backward: z_k = g_k - dinvp_k A[k][k+1] z_{k+1}, chunks from the end (the last cell keeps g)
+	double4 x = g;
+	const int kl = k1 - 2;                      // last cell the backward pass updates
+	for(int top = kl; top >= k0; top -= LCH) {
+		const int n = min(LCH, top - k0 + 1);   // cells top, top-1, ..., top-n+1
+		__syncthreads();
+		if(j < n) {
+			const int k = top - j, c = lcell[k];
+			sc[j] = c;
+			for(int e = 0; e < 16; e++) sD[j][e] = dinvp[16*static_cast<size_t>(c) + e];
+			for(int e = 0; e < 4; e++) sv[j][e] = z[4*static_cast<size_t>(c) + e];
+			const double* U = blk_pc(lface[k+1], lower, upper);
+			for(int e = 0; e < 16; e++) sB[j][e] = U[e];
+		}
+		__syncthreads();
+		if(j == 0) {
+			for(int i = 0; i < n; i++) {
+				double t[4], y[4];
+				blk_mv(sB[i], x, t);
+				blk_mv(sD[i], make_double4(t[0], t[1], t[2], t[3]), y);
+				x = make_double4(sv[i][0] - y[0], sv[i][1] - y[1], sv[i][2] - y[2], sv[i][3] - y[3]);
+				sv[i][0] = x.x; sv[i][1] = x.y; sv[i][2] = x.z; sv[i][3] = x.w;
+			}
+		}
+		__syncthreads();
+		if(j < n) for(int e = 0; e < 4; e++) z[4*static_cast<size_t>(sc[j]) + e] = sv[j][e];
+	}
+}
+
 /// z += e (4 doubles per cell)
 __global__ __launch_bounds__(256)
 void k_add_rows(int n, const double* __restrict__ e, double* __restrict__ z)
@@ -354,7 +488,7 @@ void launch_line_factor(const LineSet& Ls, const double* diag, const double* low
                         hipStream_t s)
 {
 	if(Ls.nlines > 0)
-		hipLaunchKernelGGL(k_line_factor, dim3(nblk(Ls.nlines, 64)), dim3(64), 0, s, Ls.nlines, Ls.start, Ls.cell, Ls.face,
+		hipLaunchKernelGGL(k_line_factor_w, dim3(Ls.nlines), dim3(64), 0, s, Ls.nlines, Ls.start, Ls.cell, Ls.face,
 		                   diag, lower, upper, dinvp);
 }
 
@@ -362,7 +496,7 @@ void launch_line_solve(const LineSet& Ls, const double* dinvp, const double* low
                        double* z, hipStream_t s)
 {
 	if(Ls.nlines > 0)
-		hipLaunchKernelGGL(k_line_solve, dim3(nblk(Ls.nlines, 64)), dim3(64), 0, s, Ls.nlines, Ls.start, Ls.cell, Ls.face,
+		hipLaunchKernelGGL(k_line_solve_w, dim3(Ls.nlines), dim3(64), 0, s, Ls.nlines, Ls.start, Ls.cell, Ls.face,
 		                   dinvp, lower, upper, v, z);
 }
 
