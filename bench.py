@@ -443,7 +443,8 @@ def main():
             "config": {"workload": "C4 mesh, Roe + WLS gradients + MUSCL/Van Albada, 2nd-order residual "
                                    "sweep with local time steps (explicit pseudo-time step)",
                        "cells": N, "faces": F, "boundary_faces": Fb, **dims,
-                       "parallelism": (f"{args.partitioner} {world}-way partition, RCCL p2p halo (u + gradients)"
+                       "parallelism": (f"dp{world}: {args.partitioner} {world}-way partition, two-layer halo, one RCCL "
+                                       f"p2p exchange of u per residual"
                                        if world > 1 else "single GPU"),
                        "layout": stats, "setup_s": round(t_setup, 2)},
             "roofline": {"bound": "hbm",
