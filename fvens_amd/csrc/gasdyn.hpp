@@ -28,7 +28,29 @@ struct Gas {
 	double g, Minf, Tinf, Reinf, Pr, sC;
 };
 
-FVHIP_HD double dot2(const double* a, const double* b) { double d = 0; d += a[0]*b[0]; d += a[1]*b[1]; return d; }
+/// `0 + a*b`: the first term of a sum the reference accumulates from zero. On the device this is
+/// fma(a, b, +0) -- one instruction instead of a multiply and an add. fma rounds a*b once and adds
+/// +0, which is bitwise 0 + RN(a*b) for all a, b (a zero product of either sign gives +0 both ways)
+/// except a nonzero product below half the smallest subnormal (|a*b| < 2^-1075), where fma keeps the
+/// product's sign on the zero.
+FVHIP_HD double mul0(double a, double b) {
+#if defined(__HIP_DEVICE_COMPILE__) && !defined(FVHIP_FAST)
+	return __builtin_fma(a, b, 0.0);
+#else
+	double d = 0; d += a*b; return d;
+#endif
+}
+/// `2*a - b` as fma(a, 2, -b): 2a is exact, so the single rounding is the same (bitwise, short of
+/// 2a overflowing)
+FVHIP_HD double twice_minus(double a, double b) {
+#if defined(__HIP_DEVICE_COMPILE__) && !defined(FVHIP_FAST)
+	return __builtin_fma(a, 2.0, -b);
+#else
+	return 2.0*a - b;
+#endif
+}
+
+FVHIP_HD double dot2(const double* a, const double* b) { double d = mul0(a[0], b[0]); d += a[1]*b[1]; return d; }
 
 /// a/b and sqrt(x), correctly rounded, for the parity kernels. On the device these are the compiler's
 /// own f64 sequences -- division: v_rcp, two Newton steps, Markstein's correction; square root:
@@ -275,10 +297,18 @@ FVHIP_HD void flux_roe(const Gas& G, const double* ul, const double* ur, const d
 	if(l1 < delta) l1 = div_rn(l1*l1 + delta*delta, 2.0*delta);
 	if(l3 < delta) l3 = div_rn(l3*l3 + delta*delta, 2.0*delta);
 	const double devn = vnj-vni, dep = pj-pi, derho = ur[0]-ul[0];
-	const double a0 = div_rn(l0*(dep-a.rho*a.c*devn), 2.0*a.c*a.c);
-	const double a1 = l1*(derho - div_rn(dep, a.c*a.c));
+	// 2*c*c = (c*c) + (c*c) exactly; on the device the two divisions by it are taken as halves of
+	// divisions by c*c, sharing a1's reciprocal (div_rn is correctly rounded, and halving is exact)
+	const double cc = a.c*a.c;
+	const double a1 = l1*(derho - div_rn(dep, cc));
 	const double a2 = l1*a.rho;
-	const double a3 = div_rn(l3*(dep+a.rho*a.c*devn), 2.0*a.c*a.c);
+#if defined(__HIP_DEVICE_COMPILE__) && !defined(FVHIP_FAST)
+	const double a0 = 0.5*div_rn(l0*(dep-a.rho*a.c*devn), cc);
+	const double a3 = 0.5*div_rn(l3*(dep+a.rho*a.c*devn), cc);
+#else
+	const double a0 = div_rn(l0*(dep-a.rho*a.c*devn), cc + cc);
+	const double a3 = div_rn(l3*(dep+a.rho*a.c*devn), cc + cc);
+#endif
 	double d0 = a0, d1 = a0*(a.v[0]-a.c*n[0]), d2 = a0*(a.v[1]-a.c*n[1]), d3 = a0*(a.H-a.c*a.vn);
 	d0 += a1;
 	d1 += a1*a.v[0] +      a2*(vj[0]-vi[0] - devn*n[0]);

@@ -657,11 +657,11 @@ __global__ void __launch_bounds__(SLOTS_MAX) k_sweep(const DevMesh M, const DevP
 				const double dx = rj.x-ri.x, dy = rj.y-ri.y;
 				#pragma unroll
 				for(int i = 0; i < 4; i++) {
-					double dl = 0; dl += gi[i*2]*dx; dl += gi[i*2+1]*dy;
-					double dr = 0; dr += gj[i*2]*dx; dr += gj[i*2+1]*dy;
+					double dl = mul0(gi[i*2], dx); dl += gi[i*2+1]*dy;
+					double dr = mul0(gj[i*2], dx); dr += gj[i*2+1]*dy;
 					const double du = uj[i] - ui[i];
-					const double dm = 2.0*dl - du;
-					const double dp = 2.0*dr - du;
+					const double dm = twice_minus(dl, du);
+					const double dp = twice_minus(dr, du);
 					ul[i] = muscl_left(ui[i], uj[i], dm, muscl_phi(dm, du));
 					ur[i] = muscl_right(ui[i], uj[i], dp, muscl_phi(dp, du));
 				}
@@ -674,9 +674,9 @@ __global__ void __launch_bounds__(SLOTS_MAX) k_sweep(const DevMesh M, const DevP
 				const double dx = rj.x-ri.x, dy = rj.y-ri.y;
 				#pragma unroll
 				for(int i = 0; i < 4; i++) {
-					double dl = 0; dl += gi[i*2]*dx; dl += gi[i*2+1]*dy;
+					double dl = mul0(gi[i*2], dx); dl += gi[i*2+1]*dy;
 					const double du = uj[i] - ui[i];
-					const double dm = 2.0*dl - du;
+					const double dm = twice_minus(dl, du);
 					ul[i] = muscl_left(ui[i], uj[i], dm, muscl_phi(dm, du));
 				}
 				prim2cons(G, ul, ul);
@@ -857,6 +857,14 @@ __device__ __forceinline__ void wls_normal_add(double* vm, double w2, double d0,
 	vm[0] += a*d0; vm[1] += a*d1; vm[2] += b*d0; vm[3] += b*d1;
 #endif
 }
+/// the first neighbour's term, 0 + w2*dr[i]*dr[j] (mul0)
+__device__ __forceinline__ void wls_normal_first(double* vm, double w2, double d0, double d1)
+{
+#if FVHIP_FZ_WLSV
+	const double a = w2*d0, b = w2*d1;
+	vm[0] = mul0(a, d0); vm[1] = mul0(a, d1); vm[2] = mul0(b, d0); vm[3] = mul0(b, d1);
+#endif
+}
 /// its inverse, the host's 2x2 inverse arithmetic (layout.cpp, Eigen's inverse for 2x2)
 __device__ __forceinline__ double4 wls_inverse(const double* v)
 {
@@ -894,14 +902,21 @@ __device__ __forceinline__ void fused_wls_row(const DevMesh& M, const DevPhys& P
 			const double* nrow = &fz[nb[k]*FZW];
 			const double2 rn = *reinterpret_cast<const double2*>(nrow + 12);
 			ld4(nrow, 0, un[k]);
-			double w2 = 0;
-			w2 += (rcc.x-rn.x)*(rcc.x-rn.x);
+			double w2 = mul0(rcc.x-rn.x, rcc.x-rn.x);
 			w2 += (rcc.y-rn.y)*(rcc.y-rn.y);
 			d0[k] = rcc.x-rn.x; d1[k] = rcc.y-rn.y;
 			w[k] = div_rn(1.0, w2);
 		}
+		// the sums start from zero: the first neighbour's terms are 0 + a*b (mul0)
 		#pragma unroll
-		for(int k = 0; k < 3; k++) {
+		for(int iv = 0; iv < 4; iv++) {
+			const double du = uc[iv] - un[0][iv];
+			f[iv*2+0] = mul0(w[0]*d0[0], du);
+			f[iv*2+1] = mul0(w[0]*d1[0], du);
+		}
+		wls_normal_first(vm, w[0], d0[0], d1[0]);
+		#pragma unroll
+		for(int k = 1; k < 3; k++) {
 			#pragma unroll
 			for(int iv = 0; iv < 4; iv++) {
 				const double du = uc[iv] - un[k][iv];
@@ -915,8 +930,7 @@ __device__ __forceinline__ void fused_wls_row(const DevMesh& M, const DevPhys& P
 			const double2 rn = *reinterpret_cast<const double2*>(nrow + 12);
 			double u3[4];
 			ld4(nrow, 0, u3);
-			double w2 = 0;
-			w2 += (rcc.x-rn.x)*(rcc.x-rn.x);
+			double w2 = mul0(rcc.x-rn.x, rcc.x-rn.x);
 			w2 += (rcc.y-rn.y)*(rcc.y-rn.y);
 			const double e0 = rcc.x-rn.x, e1 = rcc.y-rn.y;
 			w2 = div_rn(1.0, w2);
@@ -1100,11 +1114,11 @@ __device__ __forceinline__ void fz_body(const DevMesh& M, const DevPhys& P, cons
 				const double dx = rj.x-ri.x, dy = rj.y-ri.y;
 				#pragma unroll
 				for(int i = 0; i < 4; i++) {
-					double dl = 0; dl += gi[i*2]*dx; dl += gi[i*2+1]*dy;
-					double dr = 0; dr += gj[i*2]*dx; dr += gj[i*2+1]*dy;
+					double dl = mul0(gi[i*2], dx); dl += gi[i*2+1]*dy;
+					double dr = mul0(gj[i*2], dx); dr += gj[i*2+1]*dy;
 					const double du = uj[i] - ui[i];
-					const double dm = 2.0*dl - du;
-					const double dp = 2.0*dr - du;
+					const double dm = twice_minus(dl, du);
+					const double dp = twice_minus(dr, du);
 					ul[i] = muscl_left(ui[i], uj[i], dm, muscl_phi(dm, du));
 					ur[i] = muscl_right(ui[i], uj[i], dp, muscl_phi(dp, du));
 				}
@@ -1118,9 +1132,9 @@ __device__ __forceinline__ void fz_body(const DevMesh& M, const DevPhys& P, cons
 				const double dx = rj.x-ri.x, dy = rj.y-ri.y;
 				#pragma unroll
 				for(int i = 0; i < 4; i++) {
-					double dl = 0; dl += gi[i*2]*dx; dl += gi[i*2+1]*dy;
+					double dl = mul0(gi[i*2], dx); dl += gi[i*2+1]*dy;
 					const double du = uj[i] - ui[i];
-					const double dm = 2.0*dl - du;
+					const double dm = twice_minus(dl, du);
 					ul[i] = muscl_left(ui[i], uj[i], dm, muscl_phi(dm, du));
 				}
 				prim2cons(G, ul, ul);
