@@ -32,14 +32,20 @@ HBM_PEAK_GBS = 8000.0   # MI355X HBM3E spec (MI355X_MICROARCH.md)
 
 
 C4_WALL_SPACING = 1e-5
+# far-field angles uniform in the surface parameter (generateNacaOgrid farmap 1): with the mid-chord
+# direction map (0) the cosine-clustered trailing-edge points crowd the far field at angle 0, leaving
+# sliver triangles (aspect ratio ~1e3) along the wake line where second-order solves blow up
+C4_FARMAP = 1
 
 
-def c4_mesh(fa, scale, mult=1, wall=None):
+def c4_mesh(fa, scale, mult=1, wall=None, farmap=None):
     nt = 2048 * mult // scale
     nq = 256 // scale
     ntri = 864 // scale
     ws = C4_WALL_SPACING if wall is None else wall
-    return fa.UMesh.naca_ogrid(nt, nq, ntri, 20.0, ws), dict(ntheta=nt, nquad=nq, ntri=ntri, wall_spacing=ws)
+    fm = C4_FARMAP if farmap is None else farmap
+    return (fa.UMesh.naca_ogrid(nt, nq, ntri, 20.0, ws, farmap=fm),
+            dict(ntheta=nt, nquad=nq, ntri=ntri, wall_spacing=ws, farmap=fm))
 
 
 def sweep_algorithmic_bytes(N, F, Fb):

@@ -146,9 +146,11 @@ class UMesh:
         return cls(h.value)
 
     @classmethod
-    def naca_ogrid(cls, ntheta, nquad, ntri, rfar=20.0, wallspacing=1e-4):
+    def naca_ogrid(cls, ntheta, nquad, ntri, rfar=20.0, wallspacing=1e-4, farmap=0):
+        """farmap 0: far-field points in the direction of the surface point from mid-chord; 1: far-field
+        angles uniform in the surface parameter (mesh.cpp generateNacaOgrid)"""
         h = ctypes.c_void_p()
-        check(_ffi.lib().fvmesh_generate(0, ntheta, nquad, ntri, rfar, wallspacing, 0.0, ctypes.byref(h)))
+        check(_ffi.lib().fvmesh_generate(0, ntheta, nquad, ntri, rfar, wallspacing, float(farmap), ctypes.byref(h)))
         return cls(h.value)
 
     @classmethod

@@ -784,7 +784,7 @@ int fvmesh_generate(int kind, int a, int b, int c, double x, double y, double z,
 {
 	return guard([&] {
 		std::unique_ptr<fvmesh_s> m(new fvmesh_s());
-		if(kind == 0) m->raw = generateNacaOgrid(a, b, c, x, y);
+		if(kind == 0) m->raw = generateNacaOgrid(a, b, c, x, y, static_cast<int>(z));
 		else if(kind == 1) m->raw = generateCylinderOgrid(a, b, x, y);
 		else if(kind == 2) m->raw = generateFlatPlate(a, b, x, y, z);
 		else throw std::invalid_argument("unknown mesh kind");

@@ -616,7 +616,7 @@ void finishOgrid(MeshData& m, int ntheta, int nl, int wallmarker, int farmarker)
 
 }
 
-MeshData generateNacaOgrid(int ntheta, int nquad, int ntri, double rfar, double wallspacing)
+MeshData generateNacaOgrid(int ntheta, int nquad, int ntri, double rfar, double wallspacing, int farmap)
 {
 	if(ntheta < 8 || ntheta % 2) throw std::invalid_argument("ntheta must be even and >= 8");
 	MeshData m;
@@ -640,8 +640,12 @@ MeshData generateNacaOgrid(int ntheta, int nquad, int ntri, double rfar, double 
 			y = naca0012(x);
 		}
 		sx[i] = x; sy[i] = y;
-		// matching far-field point: same direction from the mid-chord centre
+		// matching far-field point. farmap 0: the direction of the surface point from the mid-chord
+		// centre (cosine-clustered surface points crowd the far field fore and aft: the grid lines
+		// above and below mid-chord fan out to ~1 degree per cell at ntheta 2048); farmap 1: far-field
+		// angles uniform in the surface parameter (lower surface TE -> LE: 0 -> -pi, upper: pi -> 0)
 		double ang = std::atan2(y, x - 0.5);
+		if(farmap == 1) ang = i <= half ? -PI*static_cast<double>(i)/half : PI - PI*static_cast<double>(i-half)/half;
 		if(i == 0) ang = 0.0;
 		if(i == half) ang = PI;
 		fx[i] = 0.5 + rfar*std::cos(ang); fy[i] = rfar*std::sin(ang);

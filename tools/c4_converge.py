@@ -21,7 +21,8 @@ import numpy as np
 
 
 def converge(scale=1, wall=None, init_flux="ROE", init_steps=600, init_cfl=(5.0, 200.0), main_cfl=(5.0, 200.0),
-             main_tol=1e-6, main_steps=3000, rec="VANALBADA", lin_maxit=40, sweeps=1, min_relax=0.2, verbose=True):
+             main_tol=1e-6, main_steps=3000, rec="VANALBADA", lin_maxit=40, sweeps=1, min_relax=0.2, verbose=True,
+             lines=False, init_tol=0.0, lin_rtol=1e-2):
     import torch
     import fvens_amd as fa
     import cases
@@ -34,9 +35,12 @@ def converge(scale=1, wall=None, init_flux="ROE", init_steps=600, init_cfl=(5.0,
     sp1, sp2 = fa.FlowFV(mesh, p, n1, device=dev), fa.FlowFV(mesh, p, n2, device=dev)
     perm = sp2.permutation()
     du = torch.tensor(np.tile(cases.freestream(p), (mesh.nelem, 1))[perm], device="cuda")
-    lin = dict(lin_rtol=1e-2, lin_maxit=lin_maxit, restart=lin_maxit, prec_sweeps=sweeps, min_relax=min_relax)
+    lin = dict(lin_rtol=lin_rtol, lin_maxit=lin_maxit, restart=lin_maxit, prec_sweeps=sweeps, min_relax=min_relax,
+               prec_lines=lines)
     out = {"cells": mesh.nelem, "dims": dims, "wall_spacing": wall, "stages": []}
-    for name, sp, cfl, tol, nit in (("init", sp1, init_cfl, 0.0, init_steps), ("main", sp2, main_cfl, main_tol, main_steps)):
+    for name, sp, cfl, tol, nit in (("init", sp1, init_cfl, init_tol, init_steps), ("main", sp2, main_cfl, main_tol, main_steps)):
+        if nit <= 0:
+            continue
         torch.cuda.synchronize()
         t0 = time.perf_counter()
         st, hist = sp.steady_backward_euler_device(du.data_ptr(), fa.ImplicitConfig(
@@ -71,11 +75,16 @@ def main():
     ap.add_argument("--init-cfl", type=float, nargs=2, default=(5.0, 200.0))
     ap.add_argument("--rec", default="VANALBADA")
     ap.add_argument("--sweeps", type=int, default=1)
+    ap.add_argument("--lines", action="store_true", help="line-implicit preconditioner")
+    ap.add_argument("--lin-maxit", type=int, default=40)
+    ap.add_argument("--lin-rtol", type=float, default=1e-2)
+    ap.add_argument("--init-tol", type=float, default=0.0, help="stop the first-order stage at this residual ratio")
     args = ap.parse_args()
     import torch
     torch.cuda.set_device(0)
     r = converge(args.scale, args.wall, args.init_flux, args.init_steps, tuple(args.init_cfl), tuple(args.main_cfl),
-                 1e-6, args.main_steps, args.rec, sweeps=args.sweeps)
+                 1e-6, args.main_steps, args.rec, lin_maxit=args.lin_maxit, sweeps=args.sweeps, lines=args.lines,
+                 init_tol=args.init_tol, lin_rtol=args.lin_rtol)
     print(json.dumps(r), flush=True)
 
 
