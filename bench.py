@@ -417,14 +417,24 @@ def main():
     value = F / (ms_per_step * 1e-3) / 1e6       # every face of the (global) mesh once per step
 
     # secondary figure, one GPU: the device implicit pseudo-time step on the same
-    # mesh -- residual, analytic Jacobian, GMRES(30) with 4 block-Jacobi sweeps in fp32, update
+    # mesh -- residual, analytic Jacobian, GMRES(30) with point-block Jacobi (fp32 blocks), update; and the committed C4 convergence run
     implicit = None
     if world == 1 and not args.no_implicit:
         sys.path.insert(0, os.path.join(ROOT, "tools"))
         from bench_implicit import implicit_steps
-        implicit = next(implicit_steps(mesh, "naca", steps=3, warmup=1, init_steps=5, sweeps=4, single=True,
+        implicit = next(implicit_steps(mesh, "naca", steps=3, warmup=1, init_steps=5, sweeps=1, single=True,
                                        operators=(False,)))
         implicit.pop("faces", None)
+        # the committed full-size convergence run of the same device solver (not re-run here: ~10 min)
+        conv = os.path.join(ROOT, "profiles", "r02", "c4_first_order_converged.log")
+        if os.path.exists(conv):
+            last = json.loads(open(conv).read().strip().splitlines()[-1])
+            st = last["stages"][0]
+            implicit["c4_converged_run"] = {
+                "source": os.path.relpath(conv, ROOT), "cells": last["cells"], "mesh": last["dims"],
+                "stage": "first-order Roe, point-block Jacobi, GMRES(40), expResidualRamp CFL 5 -> 200",
+                "steps": st["steps"], "seconds": st["seconds"], "ms_per_step": st["ms_per_step"],
+                "drop_from_peak": st["drop_from_peak"], "drop_from_first": st["drop_from_first"]}
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:

@@ -26,6 +26,7 @@ namespace gd {
 /// Gas constants (IdealGasPhysics members, aphysics.hpp; sC = 110.5, aphysics.cpp:19)
 struct Gas {
 	double g, Minf, Tinf, Reinf, Pr, sC;
+	double rgm1;     ///< 1/(g-1) correctly rounded (host division), for div_rcp by g-1 on the device
 };
 
 /// `0 + a*b`: the first term of a sum the reference accumulates from zero. On the device this is
@@ -113,7 +114,19 @@ FVHIP_HD double pressure_cons(const Gas& G, const double* uc) {
 FVHIP_HD double sound_speed(const Gas& G, double rho, double p) { return sqrt_rn(div_rn(G.g * p, rho)); }
 FVHIP_HD double sound_speed_cons(const Gas& G, const double* uc) { return sound_speed(G, uc[0], pressure_cons(G, uc)); }
 FVHIP_HD double temperature(const Gas& G, double rho, double p) { return div_rn(p, rho) * G.g*G.Minf*G.Minf; }
-FVHIP_HD double energy_from_pressure(const Gas& G, double p, double d, double vm2) { return div_rn(p, G.g-1.0) + 0.5*d*vm2; }
+/// a/b given r = RN(1/b): Markstein's correction alone (q = RN(a r), e = a - b q exact by fma,
+/// RN(q + e r) is a/b correctly rounded when r is the correctly rounded reciprocal) -- for divisions by
+/// a run-time constant, whose reciprocal the host computes once
+FVHIP_HD double div_rcp(double a, double b, double r) {
+#if defined(__HIP_DEVICE_COMPILE__) && !defined(FVHIP_FAST)
+	const double q = a*r;
+	const double e = fma(-b, q, a);
+	return fma(e, r, q);
+#else
+	return a/b;
+#endif
+}
+FVHIP_HD double energy_from_pressure(const Gas& G, double p, double d, double vm2) { return div_rcp(p, G.g-1.0, G.rgm1) + 0.5*d*vm2; }
 FVHIP_HD double energy_from_temperature(const Gas& G, double T, double d, double vm2) {
 	return d * (div_rn(T, G.g*(G.g-1.0)*G.Minf*G.Minf) + 0.5*vm2);
 }

@@ -43,6 +43,8 @@ def main():
     t_start = time.perf_counter()
     summary = []
     for name, sp, nmax in (("init", sp1, args.init_steps), ("main", sp2, args.main_steps)):
+        if nmax <= 0:
+            continue
         cfl = args.cfl[0]
         hist_all = []
         t0 = time.perf_counter()
