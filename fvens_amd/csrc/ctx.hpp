@@ -305,7 +305,7 @@ struct fvhip_ctx
 		if(plist && pcount == 0) return;
 		B.grad = d_grad;     // received gradients of ghost cells (partitioned meshes)
 		const char* nm = nullptr;
-		timed("k_residual_wls", [&]{ nm = KOPS(launch_residual_wls)(M, P, B, cfg.conv_numflux, recKind(), dt, stream); });
+		timed("k_residual_wls", [&]{ nm = KOPS(launch_residual_wls)(M, P, B, cfg.conv_numflux, recKind(), viscKind(), dt, stream); });
 		if(prof && !recs.empty() && recs.back().name == "k_residual_wls" && nm) recs.back().name = nm;
 		HC(hipGetLastError());
 	}

@@ -1052,7 +1052,7 @@ __device__ __forceinline__ void fz_load_grad(const DevMesh& M, const FzPatch& q,
 /// face per thread (reconstruction, flux, spectral radii); then the fluxes go through LDS and every
 /// cell sums its faces in reference order. hookA runs at the start of phase 1, hookB after the face
 /// work (points at which a caller may issue loads of later work).
-template <int FLUX, int REC, bool DT, typename HA, typename HB>
+template <int FLUX, int REC, bool DT, int VISC, typename HA, typename HB>
 __device__ __forceinline__ void fz_body(const DevMesh& M, const DevPhys& P, const SweepBuffers& B, double* fz,
                                         const FzPatch& q, const FzPre& a, HA&& hookA, HB&& hookB)
 {
@@ -1171,12 +1171,50 @@ __device__ __forceinline__ void fz_body(const DevMesh& M, const DevPhys& P, cons
 		inviscid_flux<FLUX>(G, ul, ur, n, f);
 		#pragma unroll
 		for(int k = 0; k < 4; k++) f[k] *= flen;
+		if(VISC != SV_NONE) {
+			// modified-average viscous flux, k_sweep's arithmetic, from the staged primitive states,
+			// gradients and centres; a boundary face takes its cell's ghost primitive state (B.ug of
+			// the staged path) and the cell's own gradient
+			double pl[4], gl[8], pr[4], grr[8];
+			ld4(rowi, 0, pl);
+			ld8(rowi + 4, 0, gl);
+			double2 rr;
+			if(bnd) {
+				const double4 g4 = ghost_prim_of_cell(M, P, B.u, bcell, bf);
+				pr[0] = g4.x; pr[1] = g4.y; pr[2] = g4.z; pr[3] = g4.w;
+				#pragma unroll
+				for(int k = 0; k < 8; k++) grr[k] = gl[k];
+				rr = M.bf_rcbp[bf];
+			} else {
+				const double* rowj = &fz[lrl.y*FZW];
+				ld4(rowj, 0, pr);
+				ld8(rowj + 4, 0, grr);
+				rr = *reinterpret_cast<const double2*>(rowj + 12);
+			}
+			const double rcl[2] = {ri.x, ri.y}, rcr[2] = {rr.x, rr.y};
+			double vf[4];
+			viscous_flux<true, VISC == SV_CONST>(G, n, rcl, rcr, pl, pr, gl, grr, ul, ur, vf);
+			#pragma unroll
+			for(int k = 0; k < 4; k++) f[k] += vf[k]*flen;
+		}
 		if(DT) {
 			const double ci = sound_speed_cons(G, ul), cj = sound_speed_cons(G, ur);
 			const double vni = div_rn(dot2(&ul[1],n), ul[0]);
 			const double vnj = div_rn(dot2(&ur[1],n), ur[0]);
 			sri = (fabs(vni)+ci)*flen;
 			srj = (fabs(vnj)+cj)*flen;
+			if(VISC != SV_NONE) {
+				const double mui = VISC == SV_CONST ? 1.0/G.Reinf : sutherland(G, ul);
+				const double muj = VISC == SV_CONST ? 1.0/G.Reinf : sutherland(G, ur);
+				const double ai = div_rn(4.0, 3*ul[0]), bi = div_rn(G.g, ul[0]);
+				const double aj = div_rn(4.0, 3*ur[0]), bj = div_rn(G.g, ur[0]);
+				const double coi = (ai < bi) ? bi : ai;          // std::max
+				const double coj = (aj < bj) ? bj : aj;
+				// a ghost cell's spectral radius is never summed (and its area is not stored)
+				const int2 g = M.slot_LR[s];
+				if(g.x < M.nown) sri += div_rn(div_rn(coi*mui, G.Pr) * flen*flen, M.area[g.x]);
+				if(!bnd && g.y < M.nown) srj += div_rn(div_rn(coj*muj, G.Pr) * flen*flen, M.area[g.y]);
+			}
 		}
 	}
 	hookB();
@@ -1224,9 +1262,14 @@ __device__ __forceinline__ void fz_body(const DevMesh& M, const DevPhys& P, cons
 #ifndef FVHIP_FUSED_WAVES
 #define FVHIP_FUSED_WAVES 4
 #endif
+#ifndef FVHIP_FUSED_WAVES_VISC
+// viscous instantiations: 3 waves per SIMD (168 VGPRs, no spill; 4 waves spill 144 B per lane and run
+// 2.1x slower: Roe + MUSCL + Sutherland on C4 0.370 vs 0.768 ms, staged path 0.511 ms)
+#define FVHIP_FUSED_WAVES_VISC 3
+#endif
 
-template <int FLUX, int REC, bool DT>
-__global__ void __launch_bounds__(SLOTS_MAX, FVHIP_FUSED_WAVES) k_residual_wls(const DevMesh M, const DevPhys P, const SweepBuffers B)
+template <int FLUX, int REC, bool DT, int VISC>
+__global__ void __launch_bounds__(SLOTS_MAX, VISC != SV_NONE ? FVHIP_FUSED_WAVES_VISC : FVHIP_FUSED_WAVES) k_residual_wls(const DevMesh M, const DevPhys P, const SweepBuffers B)
 {
 	extern __shared__ __attribute__((aligned(16))) double fz[];
 	const int np = B.plist ? B.pcount : M.npatch;
@@ -1239,7 +1282,7 @@ __global__ void __launch_bounds__(SLOTS_MAX, FVHIP_FUSED_WAVES) k_residual_wls(c
 	pre.cf = t < cur.nl ? fz_cell(M, cur, t) : 0;
 	fz_load_rows(M, B, cur, t, pre);
 	fz_load_grad(M, cur, t, pre);
-	fz_body<FLUX, REC, DT>(M, P, B, fz, cur, pre, []() {}, []() {});
+	fz_body<FLUX, REC, DT, VISC>(M, P, B, fz, cur, pre, []() {}, []() {});
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -1379,10 +1422,16 @@ const char* launch_sweep(const DevMesh& M, const DevPhys& P, const SweepBuffers&
 
 // fused residual dispatch
 typedef void (*FusedFn)(const DevMesh, const DevPhys, const SweepBuffers);
+template <int FLUX, int VISC>
+static FusedFn pickFused3(int rec, bool dt) {
+	if(rec == SR_MUSCL) return dt ? k_residual_wls<FLUX,SR_MUSCL,true,VISC> : k_residual_wls<FLUX,SR_MUSCL,false,VISC>;
+	return dt ? k_residual_wls<FLUX,SR_LINEAR,true,VISC> : k_residual_wls<FLUX,SR_LINEAR,false,VISC>;
+}
 template <int FLUX>
-static FusedFn pickFused(int rec, bool dt) {
-	if(rec == SR_MUSCL) return dt ? k_residual_wls<FLUX,SR_MUSCL,true> : k_residual_wls<FLUX,SR_MUSCL,false>;
-	return dt ? k_residual_wls<FLUX,SR_LINEAR,true> : k_residual_wls<FLUX,SR_LINEAR,false>;
+static FusedFn pickFused(int rec, int visc, bool dt) {
+	if(visc == SV_SUTHERLAND) return pickFused3<FLUX,SV_SUTHERLAND>(rec, dt);
+	if(visc == SV_CONST) return pickFused3<FLUX,SV_CONST>(rec, dt);
+	return pickFused3<FLUX,SV_NONE>(rec, dt);
 }
 
 #ifdef FVHIP_FAST
@@ -1395,17 +1444,17 @@ static const char* kFusedNames[7] = {"k_residual_wls<LLF>", "k_residual_wls<VANL
 #endif
 
 const char* launch_residual_wls(const DevMesh& M, const DevPhys& P, const SweepBuffers& B, int flux, int rec,
-                                bool dt, hipStream_t s)
+                                int visc, bool dt, hipStream_t s)
 {
 	FusedFn fn;
 	switch(flux) {
-		case 0: fn = pickFused<0>(rec, dt); break;
-		case 1: fn = pickFused<1>(rec, dt); break;
-		case 2: fn = pickFused<2>(rec, dt); break;
-		case 3: fn = pickFused<3>(rec, dt); break;
-		case 4: fn = pickFused<4>(rec, dt); break;
-		case 5: fn = pickFused<5>(rec, dt); break;
-		default: fn = pickFused<6>(rec, dt); break;
+		case 0: fn = pickFused<0>(rec, visc, dt); break;
+		case 1: fn = pickFused<1>(rec, visc, dt); break;
+		case 2: fn = pickFused<2>(rec, visc, dt); break;
+		case 3: fn = pickFused<3>(rec, visc, dt); break;
+		case 4: fn = pickFused<4>(rec, visc, dt); break;
+		case 5: fn = pickFused<5>(rec, visc, dt); break;
+		default: fn = pickFused<6>(rec, visc, dt); break;
 	}
 	const size_t lds = std::max(static_cast<size_t>(M.fz_max_cells)*FZW, static_cast<size_t>(6*SLOTS_MAX))*sizeof(double);
 	// raise the dynamic-LDS limit once per instantiation and device to the largest patch the layout

@@ -466,7 +466,7 @@ void buildPipeline(Layout& Lo, int chunks)
 
 bool fusedEligible(const fvhip_flow_config& cfg)
 {
-	return cfg.order2 && cfg.gradientscheme == FVHIP_GRAD_LEASTSQUARES && !cfg.viscous_sim &&
+	return cfg.order2 && cfg.gradientscheme == FVHIP_GRAD_LEASTSQUARES &&
 	       (cfg.reconstruction == FVHIP_REC_VANALBADA || cfg.reconstruction == FVHIP_REC_NONE);
 }
 

@@ -124,7 +124,7 @@ constexpr int FUSED_LDS_CELLS = FVHIP_FUSED_ROWS;   ///< staged cells per patch 
 static_assert(FUSED_LDS_CELLS < 0x8000 && 2*SLOTS_MAX < 0xFFFF, "fused codes are 16-bit");
 constexpr int PIPE_CHUNKS = 8;          ///< gradient chunks of the pipelined staged residual
 
-/// whether cfg takes the fused residual kernel (WLS + MUSCL/unlimited linear, inviscid). On a
+/// whether cfg takes the fused residual kernel (WLS + MUSCL/unlimited linear, inviscid or viscous). On a
 /// partitioned mesh, ghost cells in a patch's ring 1 take their received gradients.
 bool fusedEligible(const fvhip_flow_config& cfg);
 /// builds the fz_* arrays (owned-only meshes)

@@ -39,6 +39,7 @@ def main():
     ap.add_argument("--steps", type=int, default=100)
     ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--only", default=None, help="comma-separated case names")
+    ap.add_argument("--staged", action="store_true", help="force the staged (gradient + sweep) path")
     args = ap.parse_args()
 
     import torch
@@ -68,7 +69,7 @@ def main():
         ddt = torch.empty(mesh.nelem, dtype=torch.float64, device="cuda")
 
         def step():
-            sp.compute_residual_device(du.data_ptr(), dr.data_ptr(), ddt.data_ptr(), True, True)
+            sp.compute_residual_device(du.data_ptr(), dr.data_ptr(), ddt.data_ptr(), True, True, staged=args.staged)
         for _ in range(args.warmup):
             step()
         sp.synchronize()
@@ -83,7 +84,7 @@ def main():
         kt = sp.kernel_times()
         sp.profile(False)
         sp.close()
-        print(json.dumps({"case": name, "cells": mesh.nelem, "faces": mesh.naface, "dims": dims,
+        print(json.dumps({"case": name, "path": "staged" if args.staged else "default", "cells": mesh.nelem, "faces": mesh.naface, "dims": dims,
                           "ms_per_residual": round(ms, 4), "gfaces_per_s": round(mesh.naface / (ms * 1e-3) / 1e9, 2),
                           "kernels_ms": {k: round(v[0] / args.steps, 4) for k, v in kt.items()}}), flush=True)
 
