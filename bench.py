@@ -426,7 +426,7 @@ def main():
                                        operators=(False,)))
         implicit.pop("faces", None)
         # the committed full-size convergence run of the same device solver (not re-run here: ~10 min)
-        conv = os.path.join(ROOT, "profiles", "r02", "c4_first_order_converged.log")
+        conv = os.path.join(ROOT, "profiles", "r02", "c4_first_order_converged.txt")
         if os.path.exists(conv):
             last = json.loads(open(conv).read().strip().splitlines()[-1])
             st = last["stages"][0]
