@@ -305,7 +305,9 @@ struct fvhip_ctx
 		if(plist && pcount == 0) return;
 		B.grad = d_grad;     // received gradients of ghost cells (partitioned meshes)
 		const char* nm = nullptr;
-		timed("k_residual_wls", [&]{ nm = KOPS(launch_residual_wls)(M, P, B, cfg.conv_numflux, recKind(), viscKind(), dt, stream); });
+		timed("k_residual_wls", [&]{ nm = KOPS(launch_residual_wls)(M, P, B, cfg.conv_numflux, recKind(), viscKind(),
+		                                                                limited() ? (cfg.reconstruction == FVHIP_REC_VENKATAKRISHNAN ? 2 : 1) : 0,
+		                                                                dt, stream); });
 		if(prof && !recs.empty() && recs.back().name == "k_residual_wls" && nm) recs.back().name = nm;
 		HC(hipGetLastError());
 	}

@@ -876,8 +876,23 @@ __device__ __forceinline__ double4 wls_inverse(const double* v)
 /// phase 1 of the fused residual: WLS gradient of staged row `row` (cell c) from the staged rows of
 /// its neighbours nb4 (patch-local indices, boundary codes -2-bf, -1 padding), k_prep_grad_wls
 /// arithmetic; a ghost cell takes the gradient received from its owner
+/// the centres of cell c's faces in ascending reference face order (k_prep_grad_wls<LIM>'s source:
+/// cell_slots -> slot_gr); padding entries (0, 0)
+__device__ __forceinline__ void fz_face_centres(const DevMesh& M, int c, double2* gp)
+{
+	const int4 cs = M.cell_slots[c];
+	const int sl[4] = {cs.x, cs.y, cs.z, cs.w};
+	#pragma unroll
+	for(int k = 0; k < 4; k++) gp[k] = sl[k] >= 0 ? M.slot_gr[sl[k] >> 1] : make_double2(0, 0);
+}
+template <int LIM>
+__device__ __forceinline__ void fused_limit_row(const DevMesh& M, const DevPhys& P, const SweepBuffers& B,
+                                                const double* fz, const double* row, int c, int4 nb4,
+                                                const double2* gp, double eps2, double* g);
+template <int LIM>
 __device__ __forceinline__ void fused_wls_row(const DevMesh& M, const DevPhys& P, const SweepBuffers& B,
-                                              const double* fz, double* row, int c, int4 nb4, double4 V)
+                                              const double* fz, double* row, int c, int4 nb4, double4 V,
+                                              const double2* gp = nullptr, double eps2 = 0.0)
 {
 	if(c >= M.nown) {
 		double g[8];
@@ -984,14 +999,51 @@ __device__ __forceinline__ void fused_wls_row(const DevMesh& M, const DevPhys& P
 		g[iv*2+0] = V.x*f[iv*2+0] + V.y*f[iv*2+1];
 		g[iv*2+1] = V.z*f[iv*2+0] + V.w*f[iv*2+1];
 	}
+	if(LIM) fused_limit_row<LIM>(M, P, B, fz, row, c, nb4, gp, eps2, g);
 	st8(row + 4, 0, g);
+}
+
+/// limited reconstructions in the fused residual: the row's Barth-Jespersen / Venkatakrishnan limiter
+/// values from the staged neighbour states (boundary: the ghost primitive state, as the staged path)
+/// and its face centres, k_prep_grad_wls<LIM>'s arithmetic; the staged row then holds lim*g, which is
+/// the product linearExtrapolate forms first ((lim*grad)*(gp - rc), reconstruction_utils.hpp:28-30)
+template <int LIM>
+__device__ __forceinline__ void fused_limit_row(const DevMesh& M, const DevPhys& P, const SweepBuffers& B,
+                                                const double* fz, const double* row, int c, int4 nb4,
+                                                const double2* gpre, double eps2, double* g)
+{
+	double uc[4];
+	ld4(row, 0, uc);
+	const double2 rcc = *reinterpret_cast<const double2*>(row + 12);
+	double2 gp[4];
+	if(gpre) { gp[0] = gpre[0]; gp[1] = gpre[1]; gp[2] = gpre[2]; gp[3] = gpre[3]; }
+	else { fz_face_centres(M, c, gp); eps2 = LIM == 2 ? M.venk_eps2[c] : 0.0; }
+	const int nb[4] = {nb4.x, nb4.y, nb4.z, nb4.w};
+	double un[4][4];
+	bool has[4];
+	#pragma unroll
+	for(int k = 0; k < 4; k++) {
+		has[k] = nb[k] != -1;
+		un[k][0] = un[k][1] = un[k][2] = un[k][3] = 0.0;
+		if(!has[k]) continue;
+		if(nb[k] >= 0) ld4(&fz[nb[k]*FZW], 0, un[k]);
+		else {
+			const double4 q = ghost_prim_of_cell(M, P, B.u, c, -2 - nb[k]);
+			un[k][0] = q.x; un[k][1] = q.y; un[k][2] = q.z; un[k][3] = q.w;
+		}
+	}
+	double lim[4];
+	cell_limiter<LIM == 2>(uc, g, un, gp, has, rcc, eps2, lim);
+	#pragma unroll
+	for(int iv = 0; iv < 4; iv++) { g[iv*2+0] = lim[iv]*g[iv*2+0]; g[iv*2+1] = lim[iv]*g[iv*2+1]; }
 }
 
 /// one patch of the fused residual: uniform (scalar) metadata
 struct FzPatch { int p, s0, s1, c0, c1, nc, e0, nl, ng; const uint2* gnbr; const int* gbf; };
 /// what one thread loads for its patch before phase 0: its first staged row (state, centre), the
 /// neighbour list and WLS inverse of the gradient it computes first, and the geometry of its face
-struct FzPre { int cf; double ua[4]; double2 rca; int4 nb4a; double4 Va; int2 lrl; double2 nn; double len; };
+struct FzPre { int cf; double ua[4]; double2 rca; int4 nb4a; double4 Va; int2 lrl; double2 nn; double len;
+               double2 gpa[4]; double eps2a; };     // gpa, eps2a: limited reconstructions' first-row inputs
 
 __device__ __forceinline__ FzPatch fz_patch(const DevMesh& M, const SweepBuffers& B, int pi)
 {
@@ -1052,7 +1104,7 @@ __device__ __forceinline__ void fz_load_grad(const DevMesh& M, const FzPatch& q,
 /// face per thread (reconstruction, flux, spectral radii); then the fluxes go through LDS and every
 /// cell sums its faces in reference order. hookA runs at the start of phase 1, hookB after the face
 /// work (points at which a caller may issue loads of later work).
-template <int FLUX, int REC, bool DT, int VISC, typename HA, typename HB>
+template <int FLUX, int REC, bool DT, int VISC, int LIM, typename HA, typename HB>
 __device__ __forceinline__ void fz_body(const DevMesh& M, const DevPhys& P, const SweepBuffers& B, double* fz,
                                         const FzPatch& q, const FzPre& a, HA&& hookA, HB&& hookB)
 {
@@ -1074,10 +1126,10 @@ __device__ __forceinline__ void fz_body(const DevMesh& M, const DevPhys& P, cons
 	// (k_prep_grad_wls arithmetic, neighbours in the same ascending reference face order)
 	hookA();
 #ifndef FVHIP_PROBE_NOGRAD
-	if(t < q.ng) fused_wls_row(M, P, B, fz, &fz[t*FZW], a.cf, a.nb4a, a.Va);
+	if(t < q.ng) fused_wls_row<LIM>(M, P, B, fz, &fz[t*FZW], a.cf, a.nb4a, a.Va, LIM ? a.gpa : nullptr, a.eps2a);
 	for(int i = t + SLOTS_MAX; i < q.ng; i += SLOTS_MAX) {
 		const int c = fz_cell(M, q, i);
-		fused_wls_row(M, P, B, fz, &fz[i*FZW], c, c < M.nown ? fz_nbrs(q, i) : make_int4(-1, -1, -1, -1),
+		fused_wls_row<LIM>(M, P, B, fz, &fz[i*FZW], c, c < M.nown ? fz_nbrs(q, i) : make_int4(-1, -1, -1, -1),
 		              c < M.nown && !FVHIP_FZ_WLSV ? M.wls_V[c] : make_double4(0, 0, 0, 0));
 	}
 #endif
@@ -1263,13 +1315,14 @@ __device__ __forceinline__ void fz_body(const DevMesh& M, const DevPhys& P, cons
 #define FVHIP_FUSED_WAVES 4
 #endif
 #ifndef FVHIP_FUSED_WAVES_VISC
-// viscous instantiations: 3 waves per SIMD (168 VGPRs, no spill; 4 waves spill 144 B per lane and run
-// 2.1x slower: Roe + MUSCL + Sutherland on C4 0.370 vs 0.768 ms, staged path 0.511 ms)
+// viscous and limited instantiations: 3 waves per SIMD (168 VGPRs, no spill; at 4 waves the viscous ones
+// spill 144 B per lane and run 2.1x slower: Roe + MUSCL + Sutherland on C4 0.370 vs 0.768 ms, staged
+// path 0.511 ms; the limited ones spill 160 B)
 #define FVHIP_FUSED_WAVES_VISC 3
 #endif
 
-template <int FLUX, int REC, bool DT, int VISC>
-__global__ void __launch_bounds__(SLOTS_MAX, VISC != SV_NONE ? FVHIP_FUSED_WAVES_VISC : FVHIP_FUSED_WAVES) k_residual_wls(const DevMesh M, const DevPhys P, const SweepBuffers B)
+template <int FLUX, int REC, bool DT, int VISC, int LIM>
+__global__ void __launch_bounds__(SLOTS_MAX, (VISC != SV_NONE || LIM) ? FVHIP_FUSED_WAVES_VISC : FVHIP_FUSED_WAVES) k_residual_wls(const DevMesh M, const DevPhys P, const SweepBuffers B)
 {
 	extern __shared__ __attribute__((aligned(16))) double fz[];
 	const int np = B.plist ? B.pcount : M.npatch;
@@ -1282,7 +1335,12 @@ __global__ void __launch_bounds__(SLOTS_MAX, VISC != SV_NONE ? FVHIP_FUSED_WAVES
 	pre.cf = t < cur.nl ? fz_cell(M, cur, t) : 0;
 	fz_load_rows(M, B, cur, t, pre);
 	fz_load_grad(M, cur, t, pre);
-	fz_body<FLUX, REC, DT, VISC>(M, P, B, fz, cur, pre, []() {}, []() {});
+	pre.eps2a = 0.0;
+	if(LIM) {   // the first row's face centres and eps^2, requested before the staging barrier
+		fz_face_centres(M, pre.cf, pre.gpa);
+		if(LIM == 2) pre.eps2a = M.venk_eps2[pre.cf];
+	}
+	fz_body<FLUX, REC, DT, VISC, LIM>(M, P, B, fz, cur, pre, []() {}, []() {});
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -1424,11 +1482,14 @@ const char* launch_sweep(const DevMesh& M, const DevPhys& P, const SweepBuffers&
 typedef void (*FusedFn)(const DevMesh, const DevPhys, const SweepBuffers);
 template <int FLUX, int VISC>
 static FusedFn pickFused3(int rec, bool dt) {
-	if(rec == SR_MUSCL) return dt ? k_residual_wls<FLUX,SR_MUSCL,true,VISC> : k_residual_wls<FLUX,SR_MUSCL,false,VISC>;
-	return dt ? k_residual_wls<FLUX,SR_LINEAR,true,VISC> : k_residual_wls<FLUX,SR_LINEAR,false,VISC>;
+	if(rec == SR_MUSCL) return dt ? k_residual_wls<FLUX,SR_MUSCL,true,VISC,0> : k_residual_wls<FLUX,SR_MUSCL,false,VISC,0>;
+	return dt ? k_residual_wls<FLUX,SR_LINEAR,true,VISC,0> : k_residual_wls<FLUX,SR_LINEAR,false,VISC,0>;
 }
+/// lim: 0 none, 1 Barth-Jespersen, 2 Venkatakrishnan (inviscid; linear reconstruction of lim*g)
 template <int FLUX>
-static FusedFn pickFused(int rec, int visc, bool dt) {
+static FusedFn pickFused(int rec, int visc, int lim, bool dt) {
+	if(lim == 1) return dt ? k_residual_wls<FLUX,SR_LINEAR,true,SV_NONE,1> : k_residual_wls<FLUX,SR_LINEAR,false,SV_NONE,1>;
+	if(lim == 2) return dt ? k_residual_wls<FLUX,SR_LINEAR,true,SV_NONE,2> : k_residual_wls<FLUX,SR_LINEAR,false,SV_NONE,2>;
 	if(visc == SV_SUTHERLAND) return pickFused3<FLUX,SV_SUTHERLAND>(rec, dt);
 	if(visc == SV_CONST) return pickFused3<FLUX,SV_CONST>(rec, dt);
 	return pickFused3<FLUX,SV_NONE>(rec, dt);
@@ -1444,17 +1505,17 @@ static const char* kFusedNames[7] = {"k_residual_wls<LLF>", "k_residual_wls<VANL
 #endif
 
 const char* launch_residual_wls(const DevMesh& M, const DevPhys& P, const SweepBuffers& B, int flux, int rec,
-                                int visc, bool dt, hipStream_t s)
+                                int visc, int lim, bool dt, hipStream_t s)
 {
 	FusedFn fn;
 	switch(flux) {
-		case 0: fn = pickFused<0>(rec, visc, dt); break;
-		case 1: fn = pickFused<1>(rec, visc, dt); break;
-		case 2: fn = pickFused<2>(rec, visc, dt); break;
-		case 3: fn = pickFused<3>(rec, visc, dt); break;
-		case 4: fn = pickFused<4>(rec, visc, dt); break;
-		case 5: fn = pickFused<5>(rec, visc, dt); break;
-		default: fn = pickFused<6>(rec, visc, dt); break;
+		case 0: fn = pickFused<0>(rec, visc, lim, dt); break;
+		case 1: fn = pickFused<1>(rec, visc, lim, dt); break;
+		case 2: fn = pickFused<2>(rec, visc, lim, dt); break;
+		case 3: fn = pickFused<3>(rec, visc, lim, dt); break;
+		case 4: fn = pickFused<4>(rec, visc, lim, dt); break;
+		case 5: fn = pickFused<5>(rec, visc, lim, dt); break;
+		default: fn = pickFused<6>(rec, visc, lim, dt); break;
 	}
 	const size_t lds = std::max(static_cast<size_t>(M.fz_max_cells)*FZW, static_cast<size_t>(6*SLOTS_MAX))*sizeof(double);
 	// raise the dynamic-LDS limit once per instantiation and device to the largest patch the layout

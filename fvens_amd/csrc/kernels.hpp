@@ -107,7 +107,7 @@ void launch_weno(const DevMesh& M, const DevPhys& P, const double* grad, double*
 const char* launch_sweep(const DevMesh& M, const DevPhys& P, const SweepBuffers& B, int flux, int rec, \
                          int visc, bool dt, hipStream_t s); \
 const char* launch_residual_wls(const DevMesh& M, const DevPhys& P, const SweepBuffers& B, int flux, int rec, \
-                                int visc, bool dt, hipStream_t s); \
+                                int visc, int lim, bool dt, hipStream_t s); \
 void launch_fill(double* p, double v, long long n, hipStream_t s); \
 void launch_local_flux(int flux, const gd::Gas& G, int nf, const double* ul, const double* ur, \
                        const double* n, double* f, hipStream_t s); \

@@ -167,7 +167,10 @@ Layout buildLayout(const MeshTopo& T, const fvhip_flow_config& cfg, bool renumbe
 		Lo.patch_cell.push_back(N);
 	}
 	// fused residual path: also cap the patch cells + ring-1 + ring-2 cells the patch stages in LDS
-	const bool fused = fusedEligible(cfg);
+	// limited reconstructions (Barth-Jespersen / Venkatakrishnan) take the fused kernel on single-domain
+	// meshes only: a ghost cell's limiter values would have to be exchanged as well
+	const bool limitedRec = cfg.reconstruction == FVHIP_REC_BARTHJESPERSEN || cfg.reconstruction == FVHIP_REC_VENKATAKRISHNAN;
+	const bool fused = fusedEligible(cfg) && (!limitedRec || T.nghost == 0);
 	if(fused) {
 		std::vector<int> ranges, mark2(NT, -1), r1;
 		int stamp = 0;
@@ -466,8 +469,10 @@ void buildPipeline(Layout& Lo, int chunks)
 
 bool fusedEligible(const fvhip_flow_config& cfg)
 {
+	const bool limited = cfg.reconstruction == FVHIP_REC_BARTHJESPERSEN || cfg.reconstruction == FVHIP_REC_VENKATAKRISHNAN;
 	return cfg.order2 && cfg.gradientscheme == FVHIP_GRAD_LEASTSQUARES &&
-	       (cfg.reconstruction == FVHIP_REC_VANALBADA || cfg.reconstruction == FVHIP_REC_NONE);
+	       (cfg.reconstruction == FVHIP_REC_VANALBADA || cfg.reconstruction == FVHIP_REC_NONE ||
+	        (limited && !cfg.viscous_sim));
 }
 
 void buildFused(Layout& Lo)

@@ -249,11 +249,12 @@ def test_fast_math_within_tolerance(meshkey, kind, flux, grad, rec):
 
 
 # ------------------------------------------------------------------------------------------------
-# one-launch fused residual (WLS + MUSCL / unlimited linear, inviscid or viscous) vs the staged kernels
+# one-launch fused residual (WLS + MUSCL / unlimited linear, inviscid or viscous; Barth-Jespersen /
+# Venkatakrishnan inviscid) vs the staged kernels
 # (same device arithmetic, Sutherland's T*sqrt(T) included: bitwise)
 # ------------------------------------------------------------------------------------------------
 @pytest.mark.parametrize("flux", ["ROE", "HLLC", "LLF", "AUSMPLUS"])
-@pytest.mark.parametrize("rec", ["VANALBADA", "NONE"])
+@pytest.mark.parametrize("rec", ["VANALBADA", "NONE", "VENKATAKRISHNAN", "BARTHJESPERSEN"])
 @pytest.mark.parametrize("meshkey,kind", [("naca_small", "naca"), ("2dcylinderhybrid.msh", "cyl"),
                                           ("plate_small", "plate_inviscid"), ("naca_c2", "naca"),
                                           ("naca_small", "visc"), ("naca_small", "viscconst"),

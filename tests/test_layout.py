@@ -23,7 +23,7 @@ def test_fused_layout_stages_ring_two():
 
 def test_staged_layout_has_no_fused_rows():
     m = fa.UMesh.naca_ogrid(128, 8, 24, 20.0, 1e-5)
-    st = _probe(m, rec="VENKATAKRISHNAN")      # staged path: no fused staging lists
+    st = _probe(m, rec="WENO")      # staged path (WENO gradients): no fused staging lists
     assert st["ring1_cells"] == 0 and st["ring2_cells"] == 0 and st["max_staged_cells"] == 0
 
 
