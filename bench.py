@@ -88,7 +88,7 @@ def kernel_bytes(label, N, F, Fb):
 def kernel_symbol(label):
     """profiling label -> rocprofv3 kernel symbol suffix of the Roe/MUSCL/dt instantiation"""
     if label.startswith("k_residual_wls"):
-        return "k_residual_wls<4, 1, true>"
+        return "k_residual_wls<4, 1, true, 0, 0>"
     return "k_sweep<4, 1, 0, true, false>"
 
 
