@@ -25,6 +25,7 @@ CASES = {   # physics, flux, gradients, reconstruction
     "naca": ("naca", "ROE", "LEASTSQUARES", "VANALBADA"),
     "naca-venkat": ("naca", "ROE", "LEASTSQUARES", "VENKATAKRISHNAN"),
     "plate": ("plate", "HLLC", "LEASTSQUARES", "NONE"),
+    "visc-c5": ("visc", "ROE", "LEASTSQUARES", "VANALBADA"),
 }
 
 
@@ -32,7 +33,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--case", default="naca", choices=sorted(CASES),
                     help="naca: bench.py's C4 workload; naca-venkat: BASELINE config 3 numerics on it; "
-                         "plate: config 2, laminar flat plate, ~1M quads")
+                         "plate: config 2, laminar flat plate, ~1M quads; visc-c5: config 5, laminar NACA0012, 8.1M cells")
     ap.add_argument("--scale", type=int, default=1, help="divide the mesh dimensions by this")
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
@@ -43,6 +44,7 @@ def main():
     ap.add_argument("--sweeps", type=int, default=4)
     ap.add_argument("--prec-single", action="store_true", help="preconditioner blocks in fp32")
     ap.add_argument("--gs", action="store_true", help="multicolour block Gauss-Seidel sweeps")
+    ap.add_argument("--lines", action="store_true", help="line-implicit preconditioner")
     args = ap.parse_args()
 
     import torch
@@ -54,17 +56,21 @@ def main():
     if kind == "plate":
         nx = ny = 1024 // args.scale
         mesh, dims = fa.UMesh.flat_plate(nx, ny), dict(nx=nx, ny=ny)
+    elif args.case == "visc-c5":    # BASELINE config 5: laminar NACA0012, 8,126,464 cells, 1e-5 wall spacing
+        nt = 4096 // args.scale
+        mesh = fa.UMesh.naca_ogrid(nt, 256 // args.scale, 864 // args.scale, 20.0, 1e-5, farmap=1)
+        dims = dict(ntheta=nt, nquad=256 // args.scale, ntri=864 // args.scale, wall_spacing=1e-5, farmap=1)
     else:
         mesh, dims = c4_mesh(fa, args.scale)
     for out in implicit_steps(mesh, args.case, steps=args.steps, warmup=args.warmup, init_steps=args.init_steps,
                               cfl=args.cfl, restart=args.restart, lin_maxit=args.lin_maxit, sweeps=args.sweeps,
-                              single=args.prec_single, gs=args.gs):
+                              single=args.prec_single, gs=args.gs, lines=args.lines):
         out["dims"] = dims
         print(json.dumps(out), flush=True)
 
 
 def implicit_steps(mesh, case="naca", steps=5, warmup=2, init_steps=10, cfl=25.0, restart=30, lin_maxit=30,
-                   sweeps=4, single=False, gs=False, operators=(False, True)):
+                   sweeps=4, single=False, gs=False, operators=(False, True), lines=False):
     """time `steps` second-order backward-Euler steps per operator kind (False: assembled, True:
     matrix-free) after a first-order start; yields one dict per operator"""
     import torch
@@ -84,7 +90,7 @@ def implicit_steps(mesh, case="naca", steps=5, warmup=2, init_steps=10, cfl=25.0
     # second-order main solve. Its CFL ramps (25/50 -> 500) blow up on this O-grid's 1e-5 wall cells
     # during the start-up transient (measured), so the CFL is held fixed
     lin = dict(lin_rtol=1e-2, lin_maxit=lin_maxit, restart=restart, prec_sweeps=sweeps, prec_single=single,
-               prec_gs=gs)
+               prec_gs=gs, prec_lines=lines)
     dinit = torch.tensor(u0, dtype=torch.float64, device="cuda")
     st0, _ = sp1.steady_backward_euler_device(dinit.data_ptr(), fa.ImplicitConfig(
         cflinit=cfl, cflfin=cfl, tol=0.0, maxiter=init_steps, **lin))
@@ -107,7 +113,7 @@ def implicit_steps(mesh, case="naca", steps=5, warmup=2, init_steps=10, cfl=25.0
                "lin_iters_per_step": round(st["lin_iters"] / k, 2),
                "ms_per_lin_iter": round(dt * 1e3 / max(st["lin_iters"], 1), 4),
                "resratio": st["resratio"], "cells": mesh.nelem, "faces": mesh.naface,
-               "restart": restart, "prec_sweeps": sweeps, "prec_single": single, "prec_gs": gs, "cfl": cfl,
+               "restart": restart, "prec_sweeps": sweeps, "prec_single": single, "prec_gs": gs, "prec_lines": lines, "cfl": cfl,
                "init": {"steps": st0["steps"], "resratio": st0["resratio"]}}
     sp.close()
 
