@@ -719,7 +719,15 @@ struct fvhip_ctx
 					}
 				}
 			}
-			all.emplace_back(line.begin(), line.end());
+			// lines longer than LINE_MAX_CELLS are cut into pieces: the recurrence along a line is
+			// sequential, so one line of thousands of cells (circumferential lines of the outer O-grid
+			// layers) would set the whole sweep's time
+			for(size_t b = 0; b < line.size(); b += LINE_MAX_CELLS) {
+				const size_t e = std::min(line.size(), b + static_cast<size_t>(LINE_MAX_CELLS));
+				std::vector<std::pair<int,int>> piece(line.begin() + b, line.begin() + e);
+				piece[0].second = -1;
+				all.push_back(std::move(piece));
+			}
 		}
 		std::stable_sort(all.begin(), all.end(), [](const std::vector<std::pair<int,int>>& a,
 		                                            const std::vector<std::pair<int,int>>& b) { return a.size() > b.size(); });
@@ -734,6 +742,8 @@ struct fvhip_ctx
 			st.push_back(static_cast<int>(cells.size()));
 		}
 		lines.nlines = static_cast<int>(all.size());
+		lines.nlong = 0;
+		while(lines.nlong < lines.nlines && static_cast<int>(all[lines.nlong].size()) >= LINE_WAVE_MIN) lines.nlong++;
 		lines.start = upload(st, owned);
 		lines.cell = upload(cells, owned);
 		lines.face = upload(faces, owned);

@@ -268,9 +268,9 @@ __device__ __forceinline__ const double* blk_pc(int fc, const double* lower, con
 __global__ __launch_bounds__(64)
 void k_line_factor(int nlines, const int* __restrict__ lstart, const int* __restrict__ lcell, const int* __restrict__ lface,
                    const double* __restrict__ diag, const double* __restrict__ lower, const double* __restrict__ upper,
-                   double* __restrict__ dinvp)
+                   double* __restrict__ dinvp, int first)
 {
-	const int l = blockIdx.x*blockDim.x + threadIdx.x;
+	const int l = first + static_cast<int>(blockIdx.x*blockDim.x + threadIdx.x);
 	if(l >= nlines) return;
 	const int k0 = lstart[l], k1 = lstart[l+1];
 	double prev[4][4];             // dinvp of the previous line cell
@@ -307,9 +307,9 @@ void k_line_factor(int nlines, const int* __restrict__ lstart, const int* __rest
 __global__ __launch_bounds__(64)
 void k_line_solve(int nlines, const int* __restrict__ lstart, const int* __restrict__ lcell, const int* __restrict__ lface,
                   const double* __restrict__ dinvp, const double* __restrict__ lower, const double* __restrict__ upper,
-                  const double* __restrict__ v, double* __restrict__ z)
+                  const double* __restrict__ v, double* __restrict__ z, int first)
 {
-	const int l = blockIdx.x*blockDim.x + threadIdx.x;
+	const int l = first + static_cast<int>(blockIdx.x*blockDim.x + threadIdx.x);
 	if(l >= nlines) return;
 	const int k0 = lstart[l], k1 = lstart[l+1];
 	double4 g = make_double4(0, 0, 0, 0);
@@ -487,17 +487,24 @@ void k_add_rows(int n, const double* __restrict__ e, double* __restrict__ z)
 void launch_line_factor(const LineSet& Ls, const double* diag, const double* lower, const double* upper, double* dinvp,
                         hipStream_t s)
 {
-	if(Ls.nlines > 0)
-		hipLaunchKernelGGL(k_line_factor_w, dim3(Ls.nlines), dim3(64), 0, s, Ls.nlines, Ls.start, Ls.cell, Ls.face,
+	// long lines: a workgroup each; the short rest (same arithmetic, bitwise the same): a thread each
+	if(Ls.nlong > 0)
+		hipLaunchKernelGGL(k_line_factor_w, dim3(Ls.nlong), dim3(64), 0, s, Ls.nlines, Ls.start, Ls.cell, Ls.face,
 		                   diag, lower, upper, dinvp);
+	if(Ls.nlines > Ls.nlong)
+		hipLaunchKernelGGL(k_line_factor, dim3(nblk(Ls.nlines - Ls.nlong, 64)), dim3(64), 0, s, Ls.nlines, Ls.start,
+		                   Ls.cell, Ls.face, diag, lower, upper, dinvp, Ls.nlong);
 }
 
 void launch_line_solve(const LineSet& Ls, const double* dinvp, const double* lower, const double* upper, const double* v,
                        double* z, hipStream_t s)
 {
-	if(Ls.nlines > 0)
-		hipLaunchKernelGGL(k_line_solve_w, dim3(Ls.nlines), dim3(64), 0, s, Ls.nlines, Ls.start, Ls.cell, Ls.face,
+	if(Ls.nlong > 0)
+		hipLaunchKernelGGL(k_line_solve_w, dim3(Ls.nlong), dim3(64), 0, s, Ls.nlines, Ls.start, Ls.cell, Ls.face,
 		                   dinvp, lower, upper, v, z);
+	if(Ls.nlines > Ls.nlong)
+		hipLaunchKernelGGL(k_line_solve, dim3(nblk(Ls.nlines - Ls.nlong, 64)), dim3(64), 0, s, Ls.nlines, Ls.start,
+		                   Ls.cell, Ls.face, dinvp, lower, upper, v, z, Ls.nlong);
 }
 
 void launch_add_rows(int n, const double* e, double* z, hipStream_t s)

@@ -45,7 +45,14 @@ FVHIP_HD double relaxation_factor(const gd::Gas& G, double minfactor, const doub
 /// dinv[c] = diag[c]^-1 (Gauss-Jordan with row pivoting), c < ncell
 /// lines of the line-implicit preconditioner (internal cell ids): cells cell[start[l]..start[l+1]) in
 /// line order; face[k] (k > start[l]) = interior face between cells k-1 and k, fi<<1 | (cell k-1 is R)
-struct LineSet { int nlines = 0; const int* start = nullptr; const int* cell = nullptr; const int* face = nullptr; };
+/// lines sorted by length, longest first; lines [0, nlong) have at least LINE_WAVE_MIN cells and take
+/// the wave-per-line kernels, the short rest (most of them single cells) the thread-per-line ones
+struct LineSet { int nlines = 0; const int* start = nullptr; const int* cell = nullptr; const int* face = nullptr; int nlong = 0; };
+constexpr int LINE_WAVE_MIN = 8;
+#ifndef FVHIP_LINE_MAX
+#define FVHIP_LINE_MAX 256
+#endif
+constexpr int LINE_MAX_CELLS = FVHIP_LINE_MAX;   ///< longest line piece (ctx.hpp ensureLines)
 /// block-Thomas factorisation of every line into dinvp [ncell][16]
 void launch_line_factor(const LineSet& Ls, const double* diag, const double* lower, const double* upper, double* dinvp,
                         hipStream_t s);
