@@ -336,7 +336,8 @@ int fvhip_local_flux_jacobian(int flux_type, const double* gas5, int nf, const d
  * ------------------------------------------------------------------------------------------- */
 typedef struct fvmesh_s* fvmesh_handle;
 int fvmesh_read_gmsh(const char* path, fvmesh_handle* out);
-/** kind: 0 = NACA0012 hybrid O-grid (a=ntheta, b=nquad, c=ntri, x=rfar, y=wall spacing)
+/** kind: 0 = NACA0012 hybrid O-grid (a=ntheta, b=nquad, c=ntri, x=rfar, y=wall spacing, z=far-field map:
+ *            0 = direction of the surface point from mid-chord, 1 = angles uniform in the surface parameter)
  *        1 = cylinder triangle O-grid (a=ntheta, b=nr, x=r0, y=r1)
  *        2 = flat plate quads (a=nx, b=ny, x=lead length, y=height, z=wall spacing) */
 int fvmesh_generate(int kind, int a, int b, int c, double x, double y, double z, fvmesh_handle* out);

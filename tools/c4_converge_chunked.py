@@ -27,6 +27,7 @@ def main():
     ap.add_argument("--cfl", type=float, nargs=2, default=(5.0, 200.0))
     ap.add_argument("--rec", default="VANALBADA")
     ap.add_argument("--seconds", type=float, default=800.0, help="wall-time budget")
+    ap.add_argument("--lines", action="store_true", help="line-implicit preconditioner")
     args = ap.parse_args()
     import torch
     torch.cuda.set_device(0)
@@ -38,7 +39,7 @@ def main():
     sp1 = fa.FlowFV(mesh, p, cases.numerics(args.init_flux, "NONE", "NONE", order2=False))
     sp2 = fa.FlowFV(mesh, p, cases.numerics("ROE", "LEASTSQUARES", args.rec))
     du = torch.tensor(np.tile(cases.freestream(p), (mesh.nelem, 1))[sp2.permutation()], device="cuda")
-    lin = dict(lin_rtol=1e-2, lin_maxit=40, restart=40, prec_sweeps=1, min_relax=0.2)
+    lin = dict(lin_rtol=1e-2, lin_maxit=40, restart=40, prec_sweeps=1, min_relax=0.2, prec_lines=args.lines)
     print("cells", mesh.nelem, dims, flush=True)
     t_start = time.perf_counter()
     summary = []
