@@ -426,14 +426,19 @@ def main():
                                        operators=(False,)))
         implicit.pop("faces", None)
         # the committed full-size convergence run of the same device solver (not re-run here: ~10 min)
-        conv = os.path.join(ROOT, "profiles", "r02", "c4_first_order_converged.txt")
-        if os.path.exists(conv):
+        runs = (("c4_first_order_converged_bench_mesh.txt",
+                 "first-order LLF, line-implicit preconditioner, GMRES(40), expResidualRamp CFL 5 -> 1000"),
+                ("c4_first_order_converged.txt",
+                 "first-order Roe, point-block Jacobi, GMRES(40), expResidualRamp CFL 5 -> 200"))
+        for key, (fname, stage) in zip(("c4_converged_run", "c4_converged_run_wall1e-3"), runs):
+            conv = os.path.join(ROOT, "profiles", "r02", fname)
+            if not os.path.exists(conv):
+                continue
             last = json.loads(open(conv).read().strip().splitlines()[-1])
             st = last["stages"][0]
-            implicit["c4_converged_run"] = {
+            implicit[key] = {
                 "source": os.path.relpath(conv, ROOT), "cells": last["cells"], "mesh": last["dims"],
-                "stage": "first-order Roe, point-block Jacobi, GMRES(40), expResidualRamp CFL 5 -> 200",
-                "steps": st["steps"], "seconds": st["seconds"], "ms_per_step": st["ms_per_step"],
+                "stage": stage, "steps": st["steps"], "seconds": st["seconds"], "ms_per_step": st["ms_per_step"],
                 "drop_from_peak": st["drop_from_peak"], "drop_from_first": st["drop_from_first"]}
 
     cpu = None
