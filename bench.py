@@ -417,12 +417,12 @@ def main():
     value = F / (ms_per_step * 1e-3) / 1e6       # every face of the (global) mesh once per step
 
     # secondary figure, one GPU: the device implicit pseudo-time step on the same
-    # mesh -- residual, analytic Jacobian, GMRES(30) with point-block Jacobi (fp32 blocks), update; and the committed C4 convergence run
+    # mesh -- residual, analytic Jacobian, GMRES(30) with the line-implicit preconditioner, update; and the committed C4 convergence runs
     implicit = None
     if world == 1 and not args.no_implicit:
         sys.path.insert(0, os.path.join(ROOT, "tools"))
         from bench_implicit import implicit_steps
-        implicit = next(implicit_steps(mesh, "naca", steps=3, warmup=1, init_steps=5, sweeps=1, single=True,
+        implicit = next(implicit_steps(mesh, "naca", steps=3, warmup=1, init_steps=5, sweeps=1, lines=True,
                                        operators=(False,)))
         implicit.pop("faces", None)
         # the committed full-size convergence run of the same device solver (not re-run here: ~10 min)
