@@ -76,20 +76,30 @@ def prep_algorithmic_bytes(N, F, Fb):
     return (32 + 16 + 32 + 16 + 32 + 64) * N + 96 * Fb
 
 
-def kernel_bytes(label, N, F, Fb):
+def config4_algorithmic_bytes(N, F, Fb):
+    """SURVEY.md 8(d), Roe + linear/Venkatakrishnan: the face centres are read too (48 B/face instead of
+    32); + 8 B/cell time step. The limiter pass's own bytes (clength, phi), which the fused kernel never
+    moves, are not counted (a lower figure than SURVEY's '+ limiter pass')"""
+    return 48 * F + 144 * N + 48 * Fb + 8 * N
+
+
+def kernel_bytes(label, N, F, Fb, numerics="headline"):
     """algorithmic bytes of one launch of the residual kernel `label` (profiling name): SURVEY.md 8(d)'s
     per-face figure for the second-order sweep (124.0 B/face on C4) plus the time-step bytes, the same
     for the one-launch residual and for the staged sweep -- they perform the same operation; the
     one-launch kernel's own compulsory traffic is lower (residual_algorithmic_bytes: gradients stay
     in LDS), which is why it is faster, not a different amount of algorithmic work"""
+    if numerics == "config4":
+        return config4_algorithmic_bytes(N, F, Fb)
     return sweep_algorithmic_bytes(N, F, Fb)
 
 
-def kernel_symbol(label):
-    """profiling label -> rocprofv3 kernel symbol suffix of the Roe/MUSCL/dt instantiation"""
+def kernel_symbol(label, numerics="headline"):
+    """profiling label -> rocprofv3 kernel symbol suffix of the Roe/MUSCL/dt (headline) or
+    Roe/linear/Venkatakrishnan/dt (config4) instantiation"""
     if label.startswith("k_residual_wls"):
-        return "k_residual_wls<4, 1, true, 0, 0>"
-    return "k_sweep<4, 1, 0, true, false>"
+        return "k_residual_wls<4, 1, true, 0, 0>" if numerics == "headline" else "k_residual_wls<4, 2, true, 0, 2>"
+    return "k_sweep<4, 1, 0, true, false>" if numerics == "headline" else "k_sweep<4, 2, 0, true, true>"
 
 
 def pmc_traffic(kernel_symbol, workload_cells):
@@ -106,9 +116,24 @@ def pmc_traffic(kernel_symbol, workload_cells):
         if str(workload_cells) not in d.get("workload", "").replace(",", ""):
             continue
         for k, v in d.get("kernels", {}).items():
-            if k.endswith(kernel_symbol):
-                best = (v["hbm_bytes_corrected"], os.path.relpath(f, ROOT), v.get("SQ_INSTS_VALU"))
+            if k.endswith(kernel_symbol) and "hbm_bytes_corrected" in v:
+                best = (v["hbm_bytes_corrected"], os.path.relpath(f, ROOT), v.get("SQ_INSTS_VALU"), v)
     return best
+
+
+NUM_SIMDS = 256 * 4
+
+
+def counter_bound(counters, kernel_ms):
+    """which resource bounds the kernel, from its committed PMC counters: the fraction of time the
+    vector ALUs issue (SQ_ACTIVE_INST_VALU quad-cycles x 4 over 1,024 SIMDs x the kernel's cycles,
+    GRBM_GUI_ACTIVE / 8 XCDs) against the HBM fraction (PMC bytes / kernel time / 8 TB/s)"""
+    if not counters or not counters.get("SQ_ACTIVE_INST_VALU") or not counters.get("GRBM_GUI_ACTIVE"):
+        return None
+    cycles = counters["GRBM_GUI_ACTIVE"] / 8.0
+    valu = counters["SQ_ACTIVE_INST_VALU"] * 4.0 / (NUM_SIMDS * cycles)
+    hbm = counters["hbm_bytes_corrected"] / (kernel_ms * 1e-3) / 1e9 / HBM_PEAK_GBS
+    return {"bound": "valu" if valu > hbm else "hbm", "valu_busy": round(valu, 3), "hbm_busy": round(hbm, 3)}
 
 
 HBM_MEASURED_GBS = 6290.0          # MI355X_MICROARCH.md: float4 copy, 79 % of the spec
@@ -155,7 +180,7 @@ def host_cpu_info():
             "affinity_cpus": aff, "cgroup_cpu_quota": quota, "physical_cores_used": cores}
 
 
-def cpu_baseline(mesh, u, nrep):
+def cpu_baseline(mesh, u, nrep, rec="VANALBADA"):
     """BASELINE.md's CPU baseline: the oracle's OpenMP restatement (the reference's omp parallel for /
     omp atomic structure) on this host's physical cores, in a child process so that OMP_PROC_BIND /
     OMP_PLACES take effect (torch has already loaded the OpenMP runtime here); median of `nrep` sweeps
@@ -173,7 +198,7 @@ def cpu_baseline(mesh, u, nrep):
         for threads, reps in ((nt, nrep), (1, max(3, nrep // 4))):
             env = dict(os.environ, OMP_NUM_THREADS=str(threads), OMP_PROC_BIND="close", OMP_PLACES="cores")
             out = subprocess.run([sys.executable, os.path.abspath(__file__), "--cpu-child", path, str(threads),
-                                  str(reps)], env=env, capture_output=True, text=True, timeout=900)
+                                  str(reps), rec], env=env, capture_output=True, text=True, timeout=900)
             if out.returncode != 0:
                 raise RuntimeError("cpu baseline child failed: " + out.stderr[-2000:])
             res[threads] = json.loads(out.stdout.strip().splitlines()[-1])
@@ -190,14 +215,14 @@ def cpu_baseline(mesh, u, nrep):
                       f"{med_1:.3f} s"}
 
 
-def cpu_child(path, threads, nrep):
+def cpu_child(path, threads, nrep, rec="VANALBADA"):
     """child of cpu_baseline: builds the oracle from the saved mesh and times it (prints one JSON line)"""
     import _oracle as orc
     import cases
     d = np.load(path)
     raw = {k: (int(d[k]) if d[k].ndim == 0 else d[k]) for k in d.files if k != "u"}
     om = orc.OracleMesh.from_raw(raw)
-    ref = orc.OracleSpatial(om, cases.physics("naca"), cases.numerics("ROE", "LEASTSQUARES", "VANALBADA"))
+    ref = orc.OracleSpatial(om, cases.physics("naca"), cases.numerics("ROE", "LEASTSQUARES", rec))
     med, times = ref.time_residual(np.ascontiguousarray(d["u"]), nrep, True, threads=threads, nwarm=3)
     print(json.dumps({"median_s": med, "nrep": nrep, "threads": threads, "min_s": float(times.min()),
                       "max_s": float(times.max())}))
@@ -255,6 +280,12 @@ def main():
     ap.add_argument("--partitioner", choices=["graph", "rcb"], default="graph")
     ap.add_argument("--no-pipelined", action="store_true", help="skip the pipelined staged path")
     ap.add_argument("--no-implicit", action="store_true", help="skip the implicit-step figure (1 GPU only)")
+    ap.add_argument("--preheat-ms", type=float, default=400.0,
+                    help="untimed steps for this long (wall clock) after the warm-up steps of the primary path, "
+                         "so the timed steps run at the clock the GPU holds under this load (reported)")
+    ap.add_argument("--numerics", choices=["headline", "config4"], default="headline",
+                    help="headline: Roe + WLS + MUSCL/Van Albada (north_star's sweep); config4: BASELINE config 4's "
+                         "Roe + WLS + Venkatakrishnan (K = 20)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -276,7 +307,8 @@ def main():
     mult = world if (world > 1 and args.scaling == "weak") else 1
     mesh, dims = c4_mesh(fa, args.scale, mult)
     p = cases.physics("naca")
-    n = cases.numerics("ROE", "LEASTSQUARES", "VANALBADA")
+    rec = "VANALBADA" if args.numerics == "headline" else "VENKATAKRISHNAN"
+    n = cases.numerics("ROE", "LEASTSQUARES", rec)
     u = cases.state(mesh, p, seed=42)
     N, F, Fb = mesh.nelem, mesh.naface, mesh.nbface
     part = None
@@ -303,8 +335,10 @@ def main():
         torch.cuda.synchronize()
         sp.synchronize()
 
-    def measure(fast, path="default"):
-        """ms per step (timed region bracketed by barrier + sync, max over ranks) and per-kernel ms"""
+    def measure(fast, path="default", preheat_ms=0.0):
+        """ms per step (timed region bracketed by barrier + sync, max over ranks) and per-kernel ms;
+        preheat_ms: after the warm-up steps, further untimed steps for that long (all ranks run the
+        same count), outside the timed region"""
         n.fast_math = fast
         if world > 1:
             sp = fa.FlowFV(mesh, p, n, device=torch.cuda.current_device(), partition=part, rank=rank)
@@ -327,6 +361,23 @@ def main():
         for _ in range(args.warmup):
             step()
         barrier(sp)
+        pre = {"ms": 0.0, "steps": 0}
+        if preheat_ms > 0:
+            # step time from a short burst, then one batch of steps covering preheat_ms
+            tb = time.perf_counter()
+            for _ in range(10):
+                step()
+            sp.synchronize()
+            est = max((time.perf_counter() - tb) / 10, 1e-5)
+            k = int(preheat_ms * 1e-3 / est)
+            if dist is not None:           # every rank the same count (the exchange pairs them)
+                kt_ = torch.tensor([k], dtype=torch.int64, device="cuda")
+                dist.all_reduce(kt_, op=dist.ReduceOp.MAX)
+                k = int(kt_.item())
+            for _ in range(k):
+                step()
+            barrier(sp)
+            pre = {"ms": round((time.perf_counter() - tb) * 1e3, 1), "steps": k + 10}
         t1 = time.perf_counter()
         for _ in range(args.steps):
             step()
@@ -349,6 +400,7 @@ def main():
             dist.barrier()
         sp.close()
         # per step: a kernel launched several times per step (gradient chunks, sweep groups) is summed
+        measure.preheat = pre
         return 1e3 * elapsed / args.steps, {k: v[0] / args.steps for k, v in kt.items()}, stats
 
     t_setup = time.time() - t0
@@ -365,8 +417,8 @@ def main():
         fms, fk, stats = measure(True)
         cnt = (stats["cells"], stats["faces"], stats["bfaces"])
         fname, fsms = dominant(fk)
-        fab = kernel_bytes(fname, *cnt) / (fsms * 1e-3) / 1e9
-        ftr = pmc_traffic("fast::" + kernel_symbol(fname), N) if world == 1 else None
+        fab = kernel_bytes(fname, *cnt, args.numerics) / (fsms * 1e-3) / 1e9
+        ftr = pmc_traffic("fast::" + kernel_symbol(fname, args.numerics), N) if world == 1 else None
         fast = {"value": round(F / (fms * 1e-3) / 1e6, 3), "ms_per_step": round(fms, 5),
                 "traffic": int(ftr[0]) if ftr else None,
                 "kernels_ms": {k: round(v, 5) for k, v in fk.items()},
@@ -390,8 +442,11 @@ def main():
                      "kernels_ms_summed_over_chunks": {k: round(v, 5) for k, v in pk.items()},
                      "hbm_GBs_both_kernels": round((sweep_algorithmic_bytes(*cnt) + prep_algorithmic_bytes(*cnt))
                                                    / (pms * 1e-3) / 1e9, 1)}
-    # the primary measurement: the library's default path for this configuration
-    ms_per_step, kernels_ms, stats = measure(False)
+    # the primary measurement: the library's default path for this configuration, after a wall-clock
+    # pre-heat (untimed, reported): layout set-up between the secondary measurements leaves the GPU
+    # idle for ~1 s, and a 20-step timed region (~6 ms) would otherwise run while the clocks ramp
+    ms_per_step, kernels_ms, stats = measure(False, preheat_ms=args.preheat_ms)
+    preheat = measure.preheat
 
     halo = None
     if world > 1:
@@ -412,7 +467,7 @@ def main():
     sweep_name, sweep_ms = dominant(kernels_ms)
     sweep_name = [sweep_name]
 
-    ab = kernel_bytes(sweep_name[0], *cnt)
+    ab = kernel_bytes(sweep_name[0], *cnt, args.numerics)
     achieved = ab / (sweep_ms * 1e-3) / 1e9
     value = F / (ms_per_step * 1e-3) / 1e6       # every face of the (global) mesh once per step
 
@@ -425,7 +480,11 @@ def main():
         implicit = next(implicit_steps(mesh, "naca", steps=3, warmup=1, init_steps=5, sweeps=1, lines=True,
                                        operators=(False,)))
         implicit.pop("faces", None)
-        # the committed full-size convergence run of the same device solver (not re-run here: ~10 min)
+    # recorded (NOT measured by this run): the committed full-size convergence runs of the same
+    # device solver (~10 min each), kept apart from the measured figures
+    recorded = None
+    if world == 1 and not args.no_implicit:
+        recorded = {"note": "read from committed profiles, not re-run here"}
         runs = (("c4_first_order_converged_bench_mesh.txt",
                  "first-order LLF, line-implicit preconditioner, GMRES(40), expResidualRamp CFL 5 -> 1000"),
                 ("c4_first_order_converged.txt",
@@ -436,18 +495,22 @@ def main():
                 continue
             last = json.loads(open(conv).read().strip().splitlines()[-1])
             st = last["stages"][0]
-            implicit[key] = {
+            recorded[key] = {
                 "source": os.path.relpath(conv, ROOT), "cells": last["cells"], "mesh": last["dims"],
                 "stage": stage, "steps": st["steps"], "seconds": st["seconds"], "ms_per_step": st["ms_per_step"],
                 "drop_from_peak": st["drop_from_peak"], "drop_from_first": st["drop_from_first"]}
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        cpu = cpu_baseline(mesh, u, args.cpu_sweeps)
+        cpu = cpu_baseline(mesh, u, args.cpu_sweeps, rec)
 
     if rank == 0:
-        # template of the timed sweep: k_sweep<FLUX=ROE(4), REC=MUSCL(1), VISC=none(0), DT, no PHI>
-        tr = pmc_traffic("exact::" + kernel_symbol(sweep_name[0]), N) if world == 1 else None
+        # template of the timed sweep: k_residual_wls<FLUX=ROE(4), REC=MUSCL(1), DT, VISC=none(0), LIM=0>
+        # (config4: REC=linear(2), LIM=Venkatakrishnan(2))
+        tr = pmc_traffic("exact::" + kernel_symbol(sweep_name[0], args.numerics), N) if world == 1 else None
+        cb = counter_bound(tr[3] if tr else None, sweep_ms)
+        wl = ("Roe + WLS gradients + MUSCL/Van Albada" if args.numerics == "headline" else
+              "Roe + WLS gradients + Venkatakrishnan (K = 20), BASELINE config 4's numerics")
         out = {
             "metric": "Mfaces/s (flux+residual sweep) + achieved HBM GB/s, 1/2/4/8 MI355X",
             "value": round(value, 3),
@@ -457,26 +520,33 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": round(ms_per_step, 5),
             "higher_is_better": True,
-            "scaling": args.scaling if world > 1 else "weak",
+            # N = 1 is the first point of the same (default strong) series the multi-GPU runs extend
+            "scaling": args.scaling,
             "vs_baseline": None,
             "dtype": "f64",
             "data": "synthetic (generated C4 NACA0012 hybrid O-grid; seeded perturbed free stream)",
-            "config": {"workload": "C4 mesh, Roe + WLS gradients + MUSCL/Van Albada, 2nd-order residual "
-                                   "sweep with local time steps (explicit pseudo-time step)",
+            "config": {"workload": f"C4 mesh, {wl}, 2nd-order residual sweep with local time steps "
+                                   "(explicit pseudo-time step)",
                        "cells": N, "faces": F, "boundary_faces": Fb, **dims,
                        "parallelism": (f"dp{world}: {args.partitioner} {world}-way partition, two-layer halo, one RCCL "
                                        f"p2p exchange of u per residual"
                                        if world > 1 else "single GPU"),
                        "layout": stats, "setup_s": round(t_setup, 2)},
-            "roofline": {"bound": "hbm",
-                         "limiter": "FP64 VALU issue and barrier latency between the kernel's phases, not HBM "
-                                    "bandwidth (PMC: valu_roofline below; DESIGN.md section 5)", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "preheat": {**preheat, "note": "untimed steps of the primary path after its warm-up, outside the "
+                                           "timed region (--preheat-ms)"},
+            "roofline": {"bound": cb["bound"] if cb else None,
+                         "bound_basis": ({**cb, "source": tr[1], "rule": "valu if SQ_ACTIVE_INST_VALU x 4 / "
+                                          "(1024 SIMDs x GRBM_GUI_ACTIVE / 8) exceeds PMC bytes / time / 8 TB/s"}
+                                         if cb else "no committed PMC profile of this kernel on this workload"),
+                         "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 4),
                          "traffic": int(tr[0]) if tr else None,
                          "traffic_source": tr[1] if tr else None,
                          "kernel": sweep_name[0] if sweep_name else None,
                          "kernel_ms": round(sweep_ms, 5), "algorithmic_bytes": ab,
-                         "bytes_basis": "SURVEY.md 8(d) 32F + 144N + 48Fb (124.0 B/face on C4) + 8N time step",
+                         "bytes_basis": ("SURVEY.md 8(d) 32F + 144N + 48Fb (124.0 B/face on C4) + 8N time step"
+                                         if args.numerics == "headline" else
+                                         "SURVEY.md 8(d) Roe + linear/Venkatakrishnan: 48F + 144N + 48Fb + 8N time step"),
                          "frac_area_dt_basis": round(sweep_bytes_area_dt(*cnt) / (sweep_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
                          "area_dt_basis": "same + 8N (time step as area read 8 + dtm write 8 = 16 B/cell)",
                          "compulsory_bytes_one_launch": residual_algorithmic_bytes(*cnt),
@@ -490,6 +560,7 @@ def main():
             "staged_path": staged,
             "pipelined_path": pipelined,
             "implicit_step": implicit,
+            "recorded": recorded,
         }
         print(json.dumps(out))
     if dist is not None:
@@ -497,7 +568,7 @@ def main():
 
 
 if __name__ == "__main__":
-    if len(sys.argv) == 5 and sys.argv[1] == "--cpu-child":
-        cpu_child(sys.argv[2], int(sys.argv[3]), int(sys.argv[4]))
+    if len(sys.argv) == 6 and sys.argv[1] == "--cpu-child":
+        cpu_child(sys.argv[2], int(sys.argv[3]), int(sys.argv[4]), sys.argv[5])
     else:
         main()

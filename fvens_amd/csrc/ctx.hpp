@@ -19,6 +19,8 @@
 #include <rccl/rccl.h>
 #include <hip/hip_runtime.h>
 #include <cstring>
+#include <cstdio>
+#include <cstdlib>
 #include <algorithm>
 #include <cmath>
 #include <string>
@@ -155,8 +157,23 @@ struct fvhip_ctx
 	std::vector<Rec> recs;
 	std::map<std::string, std::pair<double,int>> acc;
 
+#ifdef FVHIP_PROBE_PHASES
+	unsigned long long* d_probe = nullptr;
+	/// diagnostic build: the phase stamps of the last fused launch to $FVHIP_PROBE_OUT (raw u64 [blocks][8])
+	void dumpProbe() {
+		const char* path = getenv("FVHIP_PROBE_OUT");
+		if(!d_probe || !path) return;
+		std::vector<unsigned long long> h(8*(L.patch_cell.size() + 16));
+		(void)hipStreamSynchronize(stream);
+		(void)hipMemcpy(h.data(), d_probe, h.size()*sizeof(unsigned long long), hipMemcpyDeviceToHost);
+		if(FILE* f = fopen(path, "wb")) { fwrite(h.data(), sizeof(unsigned long long), h.size(), f); fclose(f); }
+	}
+#endif
 	~fvhip_ctx() {
 		(void)hipSetDevice(device);
+#ifdef FVHIP_PROBE_PHASES
+		dumpProbe();
+#endif
 		if(comm) (void)ncclCommDestroy(comm);
 		for(auto& r : recs) { (void)hipEventDestroy(r.a); (void)hipEventDestroy(r.b); }
 		for(hipEvent_t e : pipe_ev) (void)hipEventDestroy(e);
@@ -304,6 +321,11 @@ struct fvhip_ctx
 		B.plist = plist; B.pcount = pcount;
 		if(plist && pcount == 0) return;
 		B.grad = d_grad;     // received gradients of ghost cells (partitioned meshes)
+		if(limited()) B.phi = d_phi;   // layer-1 ghosts' limiter values (two-layer halo)
+#ifdef FVHIP_PROBE_PHASES
+		if(!d_probe) d_probe = static_cast<unsigned long long*>(static_cast<void*>(dalloc(8*(static_cast<size_t>(L.patch_cell.size()) + 16), owned)));
+		B.probe = d_probe;
+#endif
 		const char* nm = nullptr;
 		timed("k_residual_wls", [&]{ nm = KOPS(launch_residual_wls)(M, P, B, cfg.conv_numflux, recKind(), viscKind(),
 		                                                                limited() ? (cfg.reconstruction == FVHIP_REC_VENKATAKRISHNAN ? 2 : 1) : 0,
@@ -344,16 +366,18 @@ struct fvhip_ctx
 		}
 		NC(ncclGroupEnd());
 	}
-	/// the residual's halo protocol: with a two-layer halo and WLS gradients of an unlimited / MUSCL
-	/// reconstruction, ONE exchange of u (both layers) and the layer-1 ghosts' gradients computed
-	/// locally (k_grad_ghost); otherwise u, then gradients (and limiter data) in further rounds
+	/// the residual's halo protocol: with a two-layer halo and WLS gradients of an unlimited, MUSCL,
+	/// Barth-Jespersen or Venkatakrishnan reconstruction, ONE exchange of u (both layers) and the
+	/// layer-1 ghosts' gradients (and limiter values) computed locally (k_grad_ghost); otherwise u,
+	/// then gradients (and limiter data) in further rounds
 	bool singleExchange() const {
 		return halo() && L.halo_layers == 2 && cfg.order2 && cfg.gradientscheme == FVHIP_GRAD_LEASTSQUARES &&
-		       !limited() && cfg.reconstruction != FVHIP_REC_WENO && (L.gg_cells.empty() || !L.gg_V.empty());
+		       cfg.reconstruction != FVHIP_REC_WENO && (L.gg_cells.empty() || !L.gg_V.empty());
 	}
+	int limKind() const { return limited() ? (cfg.reconstruction == FVHIP_REC_VENKATAKRISHNAN ? 2 : 1) : 0; }
 	void stage_ghost_gradients(const double* u, hipStream_t st = nullptr) {
 		if(!st) st = stream;
-		timed_on(st, "k_grad_ghost", [&]{ KOPS(launch_grad_ghost)(M, P, u, d_grad, st); });
+		timed_on(st, "k_grad_ghost", [&]{ KOPS(launch_grad_ghost)(M, P, u, d_grad, st, limKind(), d_phi); });
 	}
 
 	/// the second stream and events of the overlapped fused residual
@@ -507,7 +531,7 @@ struct fvhip_ctx
 			for(size_t i = 0; i < hs.size(); i++) on(i)->stage_gradients(us[i]);
 			if(single) { for(size_t i = 0; i < hs.size(); i++) on(i)->stage_ghost_gradients(us[i]); }
 			else exchange([&](size_t i) { return hs[i]->d_grad; }, 8);
-			if(h0->limited()) {
+			if(h0->limited() && !single) {      // single exchange: the ghosts' limiter values are local
 				for(size_t i = 0; i < hs.size(); i++) on(i)->stage_limiter();
 				exchange([&](size_t i) { return hs[i]->d_phi; }, 4);
 			}

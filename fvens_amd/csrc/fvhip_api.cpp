@@ -118,6 +118,8 @@ static fvhip_ctx* createCtx(const MeshTopo& T, const fvhip_flow_config* cfg, int
 	M.gg_cells = upload(L.gg_cells, o);
 	M.gg_nbr = reinterpret_cast<const int4*>(upload(L.gg_nbr, o));
 	M.gg_V = reinterpret_cast<const double4*>(upload(L.gg_V, o));
+	M.gg_gp = reinterpret_cast<const double2*>(upload(L.gg_gp, o));
+	M.gg_eps2 = upload(L.gg_eps2, o);
 	M.xb_bc = upload(L.xb_bc, o);
 	M.xb_n = reinterpret_cast<const double2*>(upload(L.xb_n, o));
 	M.xb_rcbp = reinterpret_cast<const double2*>(upload(L.xb_rcbp, o));

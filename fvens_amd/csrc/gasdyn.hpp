@@ -507,10 +507,31 @@ FVHIP_HD void ghost_state(const Gas& G, const BCDev& bc, const double* uinf, con
 // stages them already, bit for bit what getPrimitive2StatesAndGradients derives from the conserved
 // states; first order: pl, pr are the conserved states (converted here with cons2prim2).
 // ---------------------------------------------------------------------------------------------
+/// the face-state inputs of the viscous flux: the averaged viscosity (flow_spatial.cpp:379-383) and
+/// the averaged velocity of the energy term (viscousphysics.cpp:108-111); split out so a caller can
+/// form them while the face states are live and drop those states before the gradient terms
+template <bool CONSTVISC>
+FVHIP_HD void viscous_face_terms(const Gas& G, const double* ul, const double* ur, double& muRe, double* va) {
+	muRe = CONSTVISC ? 1.0/G.Reinf : 0.5*( sutherland(G, ul) + sutherland(G, ur) );
+	va[0] = 0.5*( div_rn(ul[1], ul[0]) + div_rn(ur[1], ur[0]) );
+	va[1] = 0.5*( div_rn(ul[2], ul[0]) + div_rn(ur[2], ur[0]) );
+}
+template <bool ORDER2>
+FVHIP_HD void viscous_flux_core(const Gas& G, const double* n, const double* rcl, const double* rcr,
+                                const double* pl, const double* pr, const double* gl, const double* grr,
+                                double muRe, const double* va, double* vf);
 template <bool ORDER2, bool CONSTVISC>
 FVHIP_HD void viscous_flux(const Gas& G, const double* n, const double* rcl, const double* rcr,
                            const double* pl, const double* pr, const double* gl, const double* grr,
                            const double* ul, const double* ur, double* vf) {
+	double muRe, va[2];
+	viscous_face_terms<CONSTVISC>(G, ul, ur, muRe, va);
+	viscous_flux_core<ORDER2>(G, n, rcl, rcr, pl, pr, gl, grr, muRe, va, vf);
+}
+template <bool ORDER2>
+FVHIP_HD void viscous_flux_core(const Gas& G, const double* n, const double* rcl, const double* rcr,
+                                const double* pl, const double* pr, const double* gl, const double* grr,
+                                double muRe, const double* va, double* vf) {
 	double tl[4], tr[4], gL[8], gR[8];          // gL[dim*4 + var]
 	if(ORDER2) {
 		for(int i = 0; i < 2; i++) for(int j = 0; j < 4; j++) { gL[i*4+j] = gl[j*2+i]; gR[i*4+j] = grr[j*2+i]; }
@@ -543,7 +564,6 @@ FVHIP_HD void viscous_flux(const Gas& G, const double* n, const double* rcl, con
 			grad[1][i] = davg[1] - ddr*dr[1] + corr*dr[1];
 		}
 	}
-	const double muRe = CONSTVISC ? 1.0/G.Reinf : 0.5*( sutherland(G, ul) + sutherland(G, ur) );
 	const double kd = div_rn(muRe, G.Minf*G.Minf*(G.g-1.0)*G.Pr);
 	double ldiv = 0;
 	ldiv += grad[0][1]; ldiv += grad[1][2];
@@ -555,9 +575,6 @@ FVHIP_HD void viscous_flux(const Gas& G, const double* n, const double* rcl, con
 	s[1][1] -= ldiv;
 	vf[0] = 0;
 	for(int i = 0; i < 2; i++) { double t = 0; t -= s[i][0]*n[0]; t -= s[i][1]*n[1]; vf[i+1] = t; }
-	double va[2];
-	va[0] = 0.5*( div_rn(ul[1], ul[0]) + div_rn(ur[1], ur[0]) );
-	va[1] = 0.5*( div_rn(ul[2], ul[0]) + div_rn(ur[2], ur[0]) );
 	double e = 0;
 	for(int i = 0; i < 2; i++) {
 		double comp = 0;

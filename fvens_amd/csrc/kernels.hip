@@ -369,9 +369,13 @@ __global__ void __launch_bounds__(256) k_grad_wls_list(DevMesh M, DevPhys P, con
 /// WLS gradients of the layer-1 ghosts of a two-layer halo, from the received layer-1 and layer-2
 /// states: the arithmetic of k_grad_wls_list on the ghost's own neighbour list (ascending global face
 /// order; extra boundary faces for the physical faces no owned cell touches), so each value is the
-/// owner's bit for bit and needs no exchange
+/// owner's bit for bit and needs no exchange. LIM (1 Barth-Jespersen, 2 Venkatakrishnan): the ghost's
+/// limiter values too, k_prep_grad_wls<LIM>'s cell_limiter on the same neighbour states (boundary:
+/// the ghost primitive state) and the ghost's face centres -- the owner's values, since min / max over
+/// the faces do not depend on their order (limitedlinearreconstruction.cpp:107-268)
+template <int LIM>
 __global__ void __launch_bounds__(256) k_grad_ghost(DevMesh M, DevPhys P, const double* __restrict__ u,
-                                                    double* __restrict__ grad)
+                                                    double* __restrict__ grad, double* __restrict__ phi)
 {
 	const int i = blockIdx.x*blockDim.x + threadIdx.x;
 	if(i >= M.gg_n) return;
@@ -384,10 +388,10 @@ __global__ void __launch_bounds__(256) k_grad_ghost(DevMesh M, DevPhys P, const 
 	cons2prim(G, ucons, uc);
 	const double2 rcc = M.rc[c];
 	double f[8] = {0,0,0,0,0,0,0,0};
+	double un[4][4];
 	#pragma unroll
 	for(int k = 0; k < 4; k++) {
 		if(nb[k] == -1) break;
-		double un[4];
 		double2 rn;
 		if(nb[k] < 0) {
 			const int x = -2 - nb[k];
@@ -395,12 +399,12 @@ __global__ void __launch_bounds__(256) k_grad_ghost(DevMesh M, DevPhys P, const 
 			const double n[2] = {nn.x, nn.y};
 			double gs[4];
 			ghost(P, M.xb_bc[x], ucons, n, gs);
-			cons2prim(G, gs, un);
+			cons2prim(G, gs, un[k]);
 			rn = M.xb_rcbp[x];
 		} else {
 			double t4[4];
 			ld4(u, nb[k], t4);
-			cons2prim(G, t4, un);
+			cons2prim(G, t4, un[k]);
 			rn = M.rc[nb[k]];
 		}
 		double w2 = 0;
@@ -410,7 +414,7 @@ __global__ void __launch_bounds__(256) k_grad_ghost(DevMesh M, DevPhys P, const 
 		w2 = div_rn(1.0, w2);
 		#pragma unroll
 		for(int iv = 0; iv < 4; iv++) {
-			const double du = uc[iv] - un[iv];
+			const double du = uc[iv] - un[k][iv];
 			f[iv*2+0] += w2*dr0*du;
 			f[iv*2+1] += w2*dr1*du;
 		}
@@ -423,6 +427,18 @@ __global__ void __launch_bounds__(256) k_grad_ghost(DevMesh M, DevPhys P, const 
 		g[iv*2+1] = V.z*f[iv*2+0] + V.w*f[iv*2+1];
 	}
 	st8(grad, c, g);
+	if(LIM) {
+		double2 gp[4];
+		bool has[4];
+		#pragma unroll
+		for(int k = 0; k < 4; k++) {
+			has[k] = nb[k] != -1;
+			gp[k] = M.gg_gp[4*i + k];
+		}
+		double out[4];
+		cell_limiter<LIM == 2>(uc, g, un, gp, has, rcc, LIM == 2 ? M.gg_eps2[i] : 0.0, out);
+		st4(phi, c, out);
+	}
 }
 
 __global__ void __launch_bounds__(256) k_grad_gg(DevMesh M, const double* __restrict__ up,
@@ -897,6 +913,14 @@ __device__ __forceinline__ void fused_wls_row(const DevMesh& M, const DevPhys& P
 	if(c >= M.nown) {
 		double g[8];
 		ld8(B.grad, c, g);
+		if(LIM) {
+			// layer-1 ghost of a two-layer halo: its limiter values were computed locally
+			// (k_grad_ghost<LIM>); lim*g as fused_limit_row forms it
+			double lim[4];
+			ld4(B.phi, c, lim);
+			#pragma unroll
+			for(int iv = 0; iv < 4; iv++) { g[iv*2+0] = lim[iv]*g[iv*2+0]; g[iv*2+1] = lim[iv]*g[iv*2+1]; }
+		}
 		st8(row + 4, 0, g);
 		return;
 	}
@@ -1038,6 +1062,23 @@ __device__ __forceinline__ void fused_limit_row(const DevMesh& M, const DevPhys&
 	for(int iv = 0; iv < 4; iv++) { g[iv*2+0] = lim[iv]*g[iv*2+0]; g[iv*2+1] = lim[iv]*g[iv*2+1]; }
 }
 
+/// diagnostic build (-DFVHIP_PROBE_PHASES): thread 0 of each block records the 100 MHz real-time
+/// counter at the phase boundaries of the fused residual (probe[8*block + k]) and the shader clock at
+/// its start and end, to see where a block's lifetime goes
+#ifdef FVHIP_PROBE_PHASES
+#define FZ_STAMP(B, k) do { if(threadIdx.x == 0 && (B).probe) (B).probe[8*blockIdx.x + (k)] = __builtin_amdgcn_s_memrealtime(); } while(0)
+#define FZ_CLOCK(B, k) do { if(threadIdx.x == 0 && (B).probe) (B).probe[8*blockIdx.x + (k)] = __builtin_amdgcn_s_memtime(); } while(0)
+#else
+#define FZ_STAMP(B, k) do {} while(0)
+#define FZ_CLOCK(B, k) do {} while(0)
+#endif
+
+#ifndef FVHIP_FZ_VISC_FENCE
+#define FVHIP_FZ_VISC_FENCE 1
+#endif
+#ifndef FVHIP_FZ_LIM_PREFETCH
+#define FVHIP_FZ_LIM_PREFETCH 1
+#endif
 /// one patch of the fused residual: uniform (scalar) metadata
 struct FzPatch { int p, s0, s1, c0, c1, nc, e0, nl, ng; const uint2* gnbr; const int* gbf; };
 /// what one thread loads for its patch before phase 0: its first staged row (state, centre), the
@@ -1121,12 +1162,13 @@ __device__ __forceinline__ void fz_body(const DevMesh& M, const DevPhys& P, cons
 		stage_row(G, &fz[i*FZW], b, M.rc[c]);
 	}
 	__syncthreads();
+	FZ_STAMP(B, 1);
 
 	// phase 1: WLS gradients of the patch and ring-1 cells from the staged states
 	// (k_prep_grad_wls arithmetic, neighbours in the same ascending reference face order)
 	hookA();
 #ifndef FVHIP_PROBE_NOGRAD
-	if(t < q.ng) fused_wls_row<LIM>(M, P, B, fz, &fz[t*FZW], a.cf, a.nb4a, a.Va, LIM ? a.gpa : nullptr, a.eps2a);
+	if(t < q.ng) fused_wls_row<LIM>(M, P, B, fz, &fz[t*FZW], a.cf, a.nb4a, a.Va, LIM && FVHIP_FZ_LIM_PREFETCH ? a.gpa : nullptr, a.eps2a);
 	for(int i = t + SLOTS_MAX; i < q.ng; i += SLOTS_MAX) {
 		const int c = fz_cell(M, q, i);
 		fused_wls_row<LIM>(M, P, B, fz, &fz[i*FZW], c, c < M.nown ? fz_nbrs(q, i) : make_int4(-1, -1, -1, -1),
@@ -1134,6 +1176,7 @@ __device__ __forceinline__ void fz_body(const DevMesh& M, const DevPhys& P, cons
 	}
 #endif
 	__syncthreads();
+	FZ_STAMP(B, 2);
 
 	// phase 2: one face per thread (k_sweep arithmetic)
 	double f[4] = {0, 0, 0, 0};
@@ -1223,32 +1266,6 @@ __device__ __forceinline__ void fz_body(const DevMesh& M, const DevPhys& P, cons
 		inviscid_flux<FLUX>(G, ul, ur, n, f);
 		#pragma unroll
 		for(int k = 0; k < 4; k++) f[k] *= flen;
-		if(VISC != SV_NONE) {
-			// modified-average viscous flux, k_sweep's arithmetic, from the staged primitive states,
-			// gradients and centres; a boundary face takes its cell's ghost primitive state (B.ug of
-			// the staged path) and the cell's own gradient
-			double pl[4], gl[8], pr[4], grr[8];
-			ld4(rowi, 0, pl);
-			ld8(rowi + 4, 0, gl);
-			double2 rr;
-			if(bnd) {
-				const double4 g4 = ghost_prim_of_cell(M, P, B.u, bcell, bf);
-				pr[0] = g4.x; pr[1] = g4.y; pr[2] = g4.z; pr[3] = g4.w;
-				#pragma unroll
-				for(int k = 0; k < 8; k++) grr[k] = gl[k];
-				rr = M.bf_rcbp[bf];
-			} else {
-				const double* rowj = &fz[lrl.y*FZW];
-				ld4(rowj, 0, pr);
-				ld8(rowj + 4, 0, grr);
-				rr = *reinterpret_cast<const double2*>(rowj + 12);
-			}
-			const double rcl[2] = {ri.x, ri.y}, rcr[2] = {rr.x, rr.y};
-			double vf[4];
-			viscous_flux<true, VISC == SV_CONST>(G, n, rcl, rcr, pl, pr, gl, grr, ul, ur, vf);
-			#pragma unroll
-			for(int k = 0; k < 4; k++) f[k] += vf[k]*flen;
-		}
 		if(DT) {
 			const double ci = sound_speed_cons(G, ul), cj = sound_speed_cons(G, ur);
 			const double vni = div_rn(dot2(&ul[1],n), ul[0]);
@@ -1268,8 +1285,43 @@ __device__ __forceinline__ void fz_body(const DevMesh& M, const DevPhys& P, cons
 				if(!bnd && g.y < M.nown) srj += div_rn(div_rn(coj*muj, G.Pr) * flen*flen, M.area[g.y]);
 			}
 		}
+		if(VISC != SV_NONE) {
+			// modified-average viscous flux, k_sweep's arithmetic, from the staged primitive states,
+			// gradients and centres; a boundary face takes its cell's ghost primitive state (B.ug of
+			// the staged path) and the cell's own gradient. Register pressure: the face states enter
+			// only through the averaged viscosity and velocity, formed first (the time step above has
+			// used the face states too), and the fence makes the cell rows fresh LDS reads instead of
+			// the reconstruction's copies kept live through the inviscid flux -- 4 waves per SIMD
+			double muRe, va[2];
+			viscous_face_terms<VISC == SV_CONST>(G, ul, ur, muRe, va);
+#if FVHIP_FZ_VISC_FENCE
+			__asm__ volatile("" ::: "memory");
+#endif
+			double pl[4], gl[8], pr[4], grr[8];
+			ld4(rowi, 0, pl);
+			ld8(rowi + 4, 0, gl);
+			double2 rr;
+			if(bnd) {
+				const double4 g4 = ghost_prim_of_cell(M, P, B.u, bcell, bf);
+				pr[0] = g4.x; pr[1] = g4.y; pr[2] = g4.z; pr[3] = g4.w;
+				#pragma unroll
+				for(int k = 0; k < 8; k++) grr[k] = gl[k];
+				rr = M.bf_rcbp[bf];
+			} else {
+				const double* rowj = &fz[lrl.y*FZW];
+				ld4(rowj, 0, pr);
+				ld8(rowj + 4, 0, grr);
+				rr = *reinterpret_cast<const double2*>(rowj + 12);
+			}
+			const double rcl[2] = {ri.x, ri.y}, rcr[2] = {rr.x, rr.y};
+			double vf[4];
+			viscous_flux_core<true>(G, n, rcl, rcr, pl, pr, gl, grr, muRe, va, vf);
+			#pragma unroll
+			for(int k = 0; k < 4; k++) f[k] += vf[k]*flen;
+		}
 	}
 	hookB();
+	FZ_STAMP(B, 3);
 	// the cell's face list (and area) are requested before the two barriers of the flux staging,
 	// once the face work no longer holds registers
 	const int c = q.c0 + t;
@@ -1285,6 +1337,7 @@ __device__ __forceinline__ void fz_body(const DevMesh& M, const DevPhys& P, cons
 		if(DT) { ssr[t] = sri; ssr[SLOTS_MAX + t] = srj; }
 	}
 	__syncthreads();
+	FZ_STAMP(B, 4);
 
 	if(c < q.c1) {
 		double r[4];
@@ -1309,6 +1362,8 @@ __device__ __forceinline__ void fz_body(const DevMesh& M, const DevPhys& P, cons
 		st4(B.r, c, r);
 		if(DT) B.dtm[c] = div_rn(carea, integ);
 	}
+	FZ_STAMP(B, 5);
+	FZ_CLOCK(B, 7);
 }
 
 #ifndef FVHIP_FUSED_WAVES
@@ -1330,15 +1385,19 @@ __global__ void __launch_bounds__(SLOTS_MAX, (VISC != SV_NONE || LIM) ? FVHIP_FU
 	const int q = (np + 7) >> 3;
 	const int pi = (blockIdx.x & 7) * q + (blockIdx.x >> 3);
 	if(pi >= np) return;
+	FZ_STAMP(B, 0);
+	FZ_CLOCK(B, 6);
 	const FzPatch cur = fz_patch(M, B, pi);
 	FzPre pre;
 	pre.cf = t < cur.nl ? fz_cell(M, cur, t) : 0;
 	fz_load_rows(M, B, cur, t, pre);
 	fz_load_grad(M, cur, t, pre);
 	pre.eps2a = 0.0;
-	if(LIM) {   // the first row's face centres and eps^2, requested before the staging barrier
-		fz_face_centres(M, pre.cf, pre.gpa);
-		if(LIM == 2) pre.eps2a = M.venk_eps2[pre.cf];
+	if(LIM && FVHIP_FZ_LIM_PREFETCH) {   // the first row's face centres and eps^2, requested before the staging barrier
+		// (owned gradient rows only: a ghost row's limiter values come with its gradient)
+		const bool own = t < cur.ng && pre.cf < M.nown;
+		fz_face_centres(M, own ? pre.cf : 0, pre.gpa);
+		if(LIM == 2) pre.eps2a = M.venk_eps2[own ? pre.cf : 0];
 	}
 	fz_body<FLUX, REC, DT, VISC, LIM>(M, P, B, fz, cur, pre, []() {}, []() {});
 }
@@ -1407,10 +1466,16 @@ void launch_limiter(const DevMesh& M, const DevPhys& P, int venk, const double* 
 	else     k_limiter<false><<<nblk(M.nown,256), 256, 0, s>>>(M, up, ug, grad, phi);
 }
 
-void launch_grad_ghost(const DevMesh& M, const DevPhys& P, const double* u, double* grad, hipStream_t s)
+void launch_grad_ghost(const DevMesh& M, const DevPhys& P, const double* u, double* grad, hipStream_t s, int lim, double* phi)
 {
 	if(M.gg_n <= 0) return;
-	k_grad_ghost<<<(M.gg_n + 255)/256, 256, 0, s>>>(M, P, u, grad);
+	if(lim && !phi) throw std::invalid_argument("launch_grad_ghost: limiter values need a phi buffer");
+	if(lim == 2 && !M.gg_eps2) throw std::invalid_argument("launch_grad_ghost: Venkatakrishnan eps^2 of the ghosts missing");
+	if(lim && !M.gg_gp) throw std::invalid_argument("launch_grad_ghost: ghost face centres missing");
+	const int nb = (M.gg_n + 255)/256;
+	if(lim == 2) k_grad_ghost<2><<<nb, 256, 0, s>>>(M, P, u, grad, phi);
+	else if(lim == 1) k_grad_ghost<1><<<nb, 256, 0, s>>>(M, P, u, grad, phi);
+	else k_grad_ghost<0><<<nb, 256, 0, s>>>(M, P, u, grad, phi);
 }
 void launch_weno(const DevMesh& M, const DevPhys& P, const double* grad, double* lgrad, hipStream_t s)
 { if(M.nown > 0) k_weno<<<nblk(M.nown,256), 256, 0, s>>>(M, P.limiter_param, grad, lgrad); }
@@ -1464,6 +1529,11 @@ const char* launch_sweep(const DevMesh& M, const DevPhys& P, const SweepBuffers&
 {
 	const bool phi = B.phi != nullptr;
 	SweepFn fn;
+#ifdef FVHIP_EXPERIMENT_FLUX
+	// ISA experiments: one flux instantiated (every request takes it; results of others are wrong)
+	fn = pick2<FVHIP_EXPERIMENT_FLUX>(rec, visc, dt, phi);
+	(void)flux;
+#else
 	switch(flux) {
 		case 0: fn = pick2<0>(rec, visc, dt, phi); break;
 		case 1: fn = pick2<1>(rec, visc, dt, phi); break;
@@ -1473,6 +1543,7 @@ const char* launch_sweep(const DevMesh& M, const DevPhys& P, const SweepBuffers&
 		case 5: fn = pick2<5>(rec, visc, dt, phi); break;
 		default: fn = pick2<6>(rec, visc, dt, phi); break;
 	}
+#endif
 	const int np = B.plist ? B.pcount : M.npatch;
 	if(np > 0) hipLaunchKernelGGL(fn, dim3(8*((np + 7)/8)), dim3(SLOTS_MAX), 0, s, M, P, B);
 	return kSweepNames[flux < 0 || flux > 6 ? 6 : flux];
@@ -1508,6 +1579,11 @@ const char* launch_residual_wls(const DevMesh& M, const DevPhys& P, const SweepB
                                 int visc, int lim, bool dt, hipStream_t s)
 {
 	FusedFn fn;
+#ifdef FVHIP_EXPERIMENT_FLUX
+	// ISA experiments: one flux instantiated (every request takes it; results of others are wrong)
+	fn = pickFused<FVHIP_EXPERIMENT_FLUX>(rec, visc, lim, dt);
+	(void)flux;
+#else
 	switch(flux) {
 		case 0: fn = pickFused<0>(rec, visc, lim, dt); break;
 		case 1: fn = pickFused<1>(rec, visc, lim, dt); break;
@@ -1517,6 +1593,7 @@ const char* launch_residual_wls(const DevMesh& M, const DevPhys& P, const SweepB
 		case 5: fn = pickFused<5>(rec, visc, lim, dt); break;
 		default: fn = pickFused<6>(rec, visc, lim, dt); break;
 	}
+#endif
 	const size_t lds = std::max(static_cast<size_t>(M.fz_max_cells)*FZW, static_cast<size_t>(6*SLOTS_MAX))*sizeof(double);
 	// raise the dynamic-LDS limit once per instantiation and device to the largest patch the layout
 	// allows (hipFuncSetAttribute is a host-side runtime call: not on every launch)

@@ -56,6 +56,8 @@ struct DevMesh
 	const int* gg_cells;
 	const int4* gg_nbr;
 	const double4* gg_V;
+	const double2* gg_gp;      // [n1][4] face centres (limited reconstructions)
+	const double* gg_eps2;     // [n1] Venkatakrishnan eps^2
 	const int* xb_bc;
 	const double2* xb_n;
 	const double2* xb_rcbp;
@@ -84,6 +86,7 @@ struct SweepBuffers
 	int overwrite;
 	const int* plist;     // patches to sweep (pcount of them), or null: all patches
 	int pcount;
+	unsigned long long* probe;   // diagnostic builds (-DFVHIP_PROBE_PHASES) only: per-block phase stamps
 };
 
 // Host launchers (all asynchronous on stream). kernels.hip is compiled twice: namespace `exact`
@@ -98,7 +101,8 @@ void launch_prep_grad_wls(const DevMesh& M, const DevPhys& P, const double* u, d
                           int lim = 0, double* phi = nullptr); \
 void launch_grad_wls_list(const DevMesh& M, const DevPhys& P, const double* u, const int* list, int n, \
                           double* grad, hipStream_t s); \
-void launch_grad_ghost(const DevMesh& M, const DevPhys& P, const double* u, double* grad, hipStream_t s); \
+void launch_grad_ghost(const DevMesh& M, const DevPhys& P, const double* u, double* grad, hipStream_t s, \
+                       int lim = 0, double* phi = nullptr); \
 void launch_grad_gg(const DevMesh& M, const double* up, const double* ug, double* grad, hipStream_t s); \
 void launch_limiter(const DevMesh& M, const DevPhys& P, int venk, const double* up, const double* ug, \
                     const double* grad, double* phi, hipStream_t s); \

@@ -168,9 +168,10 @@ Layout buildLayout(const MeshTopo& T, const fvhip_flow_config& cfg, bool renumbe
 	}
 	// fused residual path: also cap the patch cells + ring-1 + ring-2 cells the patch stages in LDS
 	// limited reconstructions (Barth-Jespersen / Venkatakrishnan) take the fused kernel on single-domain
-	// meshes only: a ghost cell's limiter values would have to be exchanged as well
+	// meshes and on two-layer halos, whose layer-1 ghosts' limiter values are computed locally
+	// (k_grad_ghost<LIM>); with the one-layer halo they would have to be exchanged as well
 	const bool limitedRec = cfg.reconstruction == FVHIP_REC_BARTHJESPERSEN || cfg.reconstruction == FVHIP_REC_VENKATAKRISHNAN;
-	const bool fused = fusedEligible(cfg) && (!limitedRec || T.nghost == 0);
+	const bool fused = fusedEligible(cfg) && (!limitedRec || T.nghost == 0 || T.halo_layers == 2);
 	if(fused) {
 		std::vector<int> ranges, mark2(NT, -1), r1;
 		int stamp = 0;
@@ -337,6 +338,11 @@ Layout buildLayout(const MeshTopo& T, const fvhip_flow_config& cfg, bool renumbe
 		Lo.xb_bc[x] = bi;
 	}
 	Lo.xb_n = T.xb_n; Lo.xb_rcbp = T.xb_rcbp;
+	Lo.gg_gp = T.g1_gr;
+	if(cfg.reconstruction == FVHIP_REC_VENKATAKRISHNAN) {
+		Lo.gg_eps2.resize(T.g1_clength.size());
+		for(size_t i = 0; i < T.g1_clength.size(); i++) Lo.gg_eps2[i] = std::pow(cfg.limiter_param*T.g1_clength[i], 3);
+	}
 	if(cfg.gradientscheme == FVHIP_GRAD_LEASTSQUARES) {
 		// the host WLS normal matrix below, cell by cell: faces in ascending global order, the ghost's
 		// centre minus the other centre (the face loop's dr up to a sign that cancels in each term)

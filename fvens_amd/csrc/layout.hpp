@@ -83,6 +83,9 @@ struct Layout
 	std::vector<int> gg_cells;             ///< layer-1 ghosts whose gradients this rank computes
 	std::vector<int> gg_nbr;               ///< [n1][4] internal neighbour, -2-j extra boundary face, -1
 	std::vector<double> gg_V;              ///< [n1][4] their WLS inverses (as wls_V)
+	std::vector<double> gg_gp;             ///< [n1][4][2] their face centres in gg_nbr order (limited
+	                                       ///<  reconstructions: the ghosts' limiter values are local too)
+	std::vector<double> gg_eps2;           ///< [n1] Venkatakrishnan (K*clength)^3 of each
 	std::vector<int> xb_bc;                ///< extra boundary faces: BC index,
 	std::vector<double> xb_n, xb_rcbp;     ///<  normal [2], ghost centre [2]
 	std::vector<int> cell_global;          ///< [ncell+nghost] global cell of each internal cell

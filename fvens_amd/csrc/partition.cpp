@@ -7,6 +7,7 @@
 #include <map>
 #include <numeric>
 #include <stdexcept>
+#include <string>
 
 namespace fvhip {
 
@@ -24,6 +25,18 @@ double cellLength(const fvhip_mesh& m, int ref)
 		if(cl < llen) cl = llen;
 	}
 	return std::sqrt(cl);
+}
+
+/// the hot path's cells are linear triangles and quads, whose node count is their face count (every
+/// loop here takes nnode as the number of faces): reject anything else (quadratic gmsh elements,
+/// nnode 6/8/9, which the reader accepts) before an esuel row or a 4-entry buffer is overrun
+void checkLinearCells(const fvhip_mesh& m, const char* who)
+{
+	if(m.maxnfael > 4 || m.maxnfael < 3) throw std::runtime_error(std::string(who) + ": cells with more than 4 faces are not supported");
+	for(int e = 0; e < m.nelem; e++)
+		if(m.nnode[e] < 3 || m.nnode[e] > m.maxnfael)
+			throw std::runtime_error(std::string(who) + ": cell " + std::to_string(e) + " has " + std::to_string(m.nnode[e]) +
+			                         " nodes; only linear triangles and quadrangles are supported");
 }
 
 void rcbRecurse(const double* rc, int* idx, int n, int p0, int np, int* part)
@@ -206,6 +219,7 @@ std::vector<int> partitionGraph(const fvhip_mesh& m, int nparts)
 {
 	if(nparts < 1) throw std::invalid_argument("partitionGraph: nparts < 1");
 	if(m.nconnface != 0) throw std::invalid_argument("partitionGraph: expects the single-domain mesh");
+	checkLinearCells(m, "partitionGraph");
 	std::vector<int> part(m.nelem, 0), sub(m.nelem), loc(m.nelem, -1), dist(m.nelem, -1);
 	std::iota(sub.begin(), sub.end(), 0);
 	if(m.nelem > 0) graphRecurse(m, sub, 0, nparts, part.data(), loc, dist);
@@ -226,7 +240,7 @@ MeshTopo topoFromMesh(const fvhip_mesh& m)
 {
 	if(m.nconnface != 0)
 		throw std::runtime_error("mesh with connectivity faces: pass the global mesh and a partition instead");
-	if(m.maxnfael > 4) throw std::runtime_error("cells with more than 4 faces are not supported");
+	checkLinearCells(m, "fvhip_create");
 	MeshTopo T;
 	const int N = m.nelem, nb = m.nbface, F = m.naface;
 	T.nown = N; T.nghost = 0; T.nbface = nb; T.naface = F;
@@ -262,7 +276,7 @@ MeshTopo topoFromRankMesh(const fvhip_mesh& m)
 {
 	const int N = m.nelem, nb = m.nbface, F = m.naface, nc = m.nconnface;
 	if(nc <= 0 || !m.connface) throw std::invalid_argument("per-rank mesh: connface missing");
-	if(m.maxnfael > 4) throw std::runtime_error("cells with more than 4 faces are not supported");
+	checkLinearCells(m, "per-rank mesh");
 	const int cs = F - nc;                                  // gConnBFaceStart
 	auto C = [&](int ic, int k) { return m.connface[5*static_cast<size_t>(ic)+k]; };
 	std::vector<int> order(nc);
@@ -336,7 +350,7 @@ MeshTopo topoFromRankMesh(const fvhip_mesh& m)
 MeshTopo extractPartition(const fvhip_mesh& m, const int* part, int rank, int layers)
 {
 	if(m.nconnface != 0) throw std::runtime_error("extractPartition: expects the single-domain mesh");
-	if(m.maxnfael > 4) throw std::runtime_error("cells with more than 4 faces are not supported");
+	checkLinearCells(m, "extractPartition");
 	if(layers != 1 && layers != 2) throw std::invalid_argument("extractPartition: layers must be 1 or 2");
 	const int N = m.nelem, nb = m.nbface, F = m.naface;
 	auto Lg = [&](int f) { return m.intfac[4*static_cast<size_t>(f)]; };
@@ -477,6 +491,9 @@ MeshTopo extractPartition(const fvhip_mesh& m, const int* part, int rank, int la
 				if(loc[other] < 0) throw std::logic_error("extractPartition: layer-2 halo incomplete");
 				T.g1_nbr.push_back(loc[other]);
 			}
+			for(int j = 0; j < 4; j++)
+				for(int d = 0; d < 2; d++) T.g1_gr.push_back(j < k ? m.gr[2*static_cast<size_t>(fs[j])+d] : 0.0);
+			T.g1_clength.push_back(cellLength(m, g));
 		}
 	}
 

@@ -56,7 +56,10 @@ struct MeshTopo
 	std::vector<int> g1_cells;         ///< local ids of the layer-1 ghosts
 	std::vector<int> g1_nbr;           ///< [n1][4] their neighbours in ascending GLOBAL face order: local
 	                                   ///<  cell, -2-j (extra boundary face j), -1 none
-	std::vector<int> xb_btag;          ///< extra boundary faces (touching a layer-1 ghost only): marker,
+	std::vector<double> g1_gr;         ///< [n1][4][2] centres of those faces (same order; 0 padding), for
+	                                   ///<  the layer-1 ghosts' limiter values (limited reconstructions)
+	std::vector<double> g1_clength;    ///< [n1] their longest edges (Venkatakrishnan's eps)
+	std::vector<int> xb_btag;         ///< extra boundary faces (touching a layer-1 ghost only): marker,
 	std::vector<double> xb_n;          ///<  unit normal [2] (facemetric),
 	std::vector<double> xb_rcbp;       ///<  ghost-cell centre [2]
 };

@@ -15,13 +15,16 @@ CONFIGS = [("naca_small", "naca", "ROE", "LEASTSQUARES", "VANALBADA", True),
            ("naca_small", "naca", "LLF", "NONE", "NONE", False),
            ("2dcylinderhybrid.msh", "cyl", "HLLC", "GREENGAUSS", "VENKATAKRISHNAN", True),
            ("naca_small", "naca", "ROE", "LEASTSQUARES", "BARTHJESPERSEN", True),
+           ("naca_small", "naca", "ROE", "LEASTSQUARES", "VENKATAKRISHNAN", True),
            ("naca_small", "naca", "AUSM", "GREENGAUSS", "WENO", True),
            ("naca_small", "viscconst", "ROE", "LEASTSQUARES", "VANALBADA", True),
            ("plate_small", "plate", "HLLC", "LEASTSQUARES", "NONE", True),
-           ("naca_c2", "naca", "ROE", "LEASTSQUARES", "VANALBADA", True)]
+           ("naca_c2", "naca", "ROE", "LEASTSQUARES", "VANALBADA", True),
+           # BASELINE config 4's numerics: Roe + WLS + Venkatakrishnan (K = 20)
+           ("naca_c2", "naca", "ROE", "LEASTSQUARES", "VENKATAKRISHNAN", True)]
 
 
-def run_partitioned(meshkey, kind, flux, grad, rec, order2, nparts, fast=False):
+def run_partitioned(meshkey, kind, flux, grad, rec, order2, nparts, fast=False, partitioner="rcb"):
     import torch
     m, _ = get_mesh(meshkey)
     p = cases.physics(kind)
@@ -34,7 +37,7 @@ def run_partitioned(meshkey, kind, flux, grad, rec, order2, nparts, fast=False):
     dt1 = np.zeros(m.nelem)
     one.compute_residual(u, r1, True, dt1)
     one.close()
-    part = fa.partition_rcb(m, nparts)
+    part = fa.partition_rcb(m, nparts) if partitioner == "rcb" else fa.partition_graph(m, nparts)
     sps = [fa.FlowFV(m, p, n, partition=part, rank=k) for k in range(nparts)]
     glob = []
     dus, drs, dts = [], [], []
@@ -64,7 +67,7 @@ def run_partitioned(meshkey, kind, flux, grad, rec, order2, nparts, fast=False):
 
 
 @pytest.mark.parametrize("nparts", [2, 3, 8])
-@pytest.mark.parametrize("cfg", CONFIGS[:7], ids=lambda c: f"{c[0]}-{c[2]}-{c[3]}-{c[4]}")
+@pytest.mark.parametrize("cfg", CONFIGS[:8], ids=lambda c: f"{c[0]}-{c[2]}-{c[3]}-{c[4]}")
 def test_partitioned_residual_bitwise(cfg, nparts):
     r, dt, r1, dt1, stats = run_partitioned(*cfg, nparts)
     assert sum(s["ghosts"] for s in stats) > 0
@@ -76,11 +79,25 @@ def test_partitioned_residual_bitwise(cfg, nparts):
 
 
 def test_partitioned_c2_eight_ranks():
-    r, dt, r1, dt1, stats = run_partitioned(*CONFIGS[7], 8)
+    r, dt, r1, dt1, stats = run_partitioned(*CONFIGS[8], 8)
     np.testing.assert_array_equal(r, r1)
     np.testing.assert_array_equal(dt, dt1)
     # the fused residual runs most patches before the halo arrives (overlapped with the exchange)
     for s in stats:
+        assert 0 < s["interior_patches"] < s["patches"]
+        assert s["interior_patches"] >= 0.7 * s["patches"], s
+
+
+@pytest.mark.parametrize("partitioner", ["rcb", "graph"])
+def test_partitioned_c2_eight_ranks_venkatakrishnan(partitioner):
+    """config 4's numerics on the partitioned path: ONE exchange of the two-layer halo, the layer-1
+    ghosts' gradients AND Venkatakrishnan limiter values computed locally, the fused kernel with
+    interior patches ahead of the halo -- every owned row bitwise the single-GPU residual"""
+    r, dt, r1, dt1, stats = run_partitioned(*CONFIGS[9], 8, partitioner=partitioner)
+    np.testing.assert_array_equal(r, r1)
+    np.testing.assert_array_equal(dt, dt1)
+    for s in stats:
+        assert s["patches"] > 0, s                      # the fused (one-launch) residual
         assert 0 < s["interior_patches"] < s["patches"]
         assert s["interior_patches"] >= 0.7 * s["patches"], s
 

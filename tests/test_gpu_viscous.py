@@ -20,7 +20,7 @@ the reference's viscous functional regression.
     discretisation. Bars here: CDp and CDsf within 1e-6 relative of regr-LeastSquares_Roe.txt, CL
     within 2 % of it (the reference's own files span 0.7 %). Preconditioner: line-implicit (block-
     tridiagonal along the wall-normal lines) with 3 sweeps, GMRES(60) rtol 1e-1. Measured on MI355X
-    (tools/visc_probe.py): assembled, 93 steps to the deck's 1e-6 drop, CDp 6.5e-8 / CDsf 4.0e-8 /
+    (tools/experiments/visc_probe.py): assembled, 93 steps to the deck's 1e-6 drop, CDp 6.5e-8 / CDsf 4.0e-8 /
     CL 3.2e-4 relative to the file; the matrix-free Newton path reaches 1e-6 in 30 steps but there
     sits 1.3e-6 / 3.1e-6 off in CDp / CDsf, so it runs on to a 1e-8 drop.
 """
@@ -148,3 +148,48 @@ def test_c3_implicit_matrix_free():
     assert st["steps"] == 60 and np.all(np.isfinite(du.cpu().numpy()))
     assert h[-1] <= 0.5 * h.max(), (h[-1], h.max())
     main.close()
+
+
+def test_flatplate_cdsf_convergence(tmp_path):
+    """The reference's C3 known answer, SpatialFlow_NS_FlatPlate_LeastSquares_Roe_Struct_CDConvergence
+    (tests/visc-flatplate/CMakeLists.txt:32-39): flatplate.ctrl (Roe + WLS, unlimited, Sutherland;
+    M 0.2, Re 8.7e5, T 290.19 K, Pr 0.708; slip wall 3, adiabatic plate 2, far field 4, inflow-outflow
+    5) on the three structured stretched meshes of flatplatestructstretched.geo (restated in
+    tests/flatplate_meshes.py), solved by the device implicit driver with the deck's schedule
+    (first-order starter: CFL 20 -> 2000, 1e-1, 50 steps; main: CFL 100 -> 4000, 1e-5, 500 steps;
+    robust_flow update, minimum factor 0.2; Jacobian 'consistent' = Roe). Bar (flow_clcd_conv.cpp:
+    103-146): the skin-friction drag error against exact_clcd_flatplate.dat's CDsf = 1.423765e-3 falls
+    with slope in [0.95, 1.5] between the two finest meshes, h = 1/sqrt(nelem) (casesolvers.cpp:96).
+    The reference preconditions with ILU(0) (flatplate.solverc); here line-implicit, GMRES(30), rtol 1e-1."""
+    import torch
+    from flatplate_meshes import write_flatplate_msh
+    exact = [float(x) for x in open(os.path.join(os.path.dirname(cases.MESHDIR), "exact_clcd_flatplate.dat"))
+             .read().split()[:3]]
+    p = cases.physics("plate")
+    n1 = cases.numerics("ROE", "NONE", "NONE", order2=False)
+    n2 = cases.numerics("ROE", "LEASTSQUARES", "NONE")
+    lin = dict(lin_rtol=1e-1, lin_maxit=30, restart=30, prec_lines=True, prec_sweeps=2, min_relax=0.2)
+    lh, err, cdsfs = [], [], []
+    for level in range(3):
+        path = str(tmp_path / f"flatplatestructstretched{level}.msh")
+        nel = write_flatplate_msh(path, level)
+        m = fa.UMesh.read_gmsh(path)
+        assert m.nelem == nel
+        start, main = fa.FlowFV(m, p, n1), fa.FlowFV(m, p, n2)
+        perm = main.permutation()
+        du = torch.tensor(np.tile(cases.freestream(p), (m.nelem, 1))[perm], device="cuda")
+        st0, _ = start.steady_backward_euler_device(du.data_ptr(), fa.ImplicitConfig(
+            cflinit=20.0, cflfin=2000.0, tol=1e-1, maxiter=50, **lin))
+        st, _ = main.steady_backward_euler_device(du.data_ptr(), fa.ImplicitConfig(
+            cflinit=100.0, cflfin=4000.0, tol=1e-5, maxiter=500, **lin))
+        (cl, cdp, cdsf), _ = main.surface_data_device(du.data_ptr(), 2)
+        print(f"mesh {level}: {m.nelem} cells, starter {st0}, main {st}, CL {cl} CDp {cdp} CDsf {cdsf}")
+        assert st["converged"], st
+        lh.append(np.log10(1.0 / np.sqrt(m.nelem)))
+        err.append(np.log10(abs(abs(cdsf) - exact[2])))
+        cdsfs.append(cdsf)
+        start.close()
+        main.close()
+    slopes = [(err[i] - err[i - 1]) / (lh[i] - lh[i - 1]) for i in (1, 2)]
+    print("CDsf", cdsfs, "exact", exact[2], "slopes", slopes)
+    assert 0.95 <= slopes[-1] <= 1.5, slopes

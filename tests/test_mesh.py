@@ -95,3 +95,23 @@ def test_gmsh_roundtrip(tmp_path):
     m2 = fa.UMesh.read_gmsh(p)
     assert np.array_equal(m.intfac, m2.intfac)
     assert np.array_equal(m.facemetric, m2.facemetric)
+
+
+def test_flatplate_struct_stretched_meshes(tmp_path):
+    """tests/flatplate_meshes.py restates flatplatestructstretched.geo: 28 x 19 quads on mesh 0, each
+    RefineMesh quadruples them; the domain [-0.5, 1] x [0, 1] is covered; markers 2 (plate) / 3 / 4 / 5
+    on the right boundary pieces; first wall-normal spacing (1.4 progression, 20 points) halves per level"""
+    from flatplate_meshes import write_flatplate_msh, flatplate_points
+    for level, cells in enumerate((532, 2128, 8512)):
+        path = str(tmp_path / f"fp{level}.msh")
+        assert write_flatplate_msh(path, level) == cells
+        m = fa.UMesh.read_gmsh(path)
+        assert m.nelem == cells
+        assert abs(m.area.sum() - 1.5) < 1e-12
+        x, y = flatplate_points(level)
+        assert abs(y[1] - 0.4 / (1.4 ** 19 - 1.0) / 2 ** level) < 1e-15
+        tags = m.btags.reshape(m.nbface, -1)[:, 0]
+        fm = m.facemetric.reshape(-1, 3)[:m.nbface]
+        lens = {t: fm[tags == t, 2].sum() for t in (2, 3, 4, 5)}
+        assert abs(lens[2] - 1.0) < 1e-12 and abs(lens[3] - 0.5) < 1e-12
+        assert abs(lens[4] - 2.5) < 1e-12 and abs(lens[5] - 1.0) < 1e-12
