@@ -561,6 +561,7 @@ def main():
             "pipelined_path": pipelined,
             "implicit_step": implicit,
             "recorded": recorded,
+            "build": fa._ffi.build_info(),
         }
         print(json.dumps(out))
     if dist is not None:

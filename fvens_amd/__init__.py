@@ -271,6 +271,11 @@ class FlowFV:
         buf = ctypes.create_string_buffer(bytes(uid), 128)
         check(_ffi.lib().fvhip_comm_init(self._h, nranks, rank, buf))
 
+    def trace_exchange_device(self, d_left, d_right, width=4):
+        """L2TraceVector::updateSharedFaces (tracevector.cpp:213-340) of this RCCL rank's per-rank mesh"""
+        check(_ffi.lib().fvhip_trace_exchange_device(self._h, ctypes.c_void_p(d_left), ctypes.c_void_p(d_right),
+                                                     int(width)))
+
     # --- reference-ordered host interface -----------------------------------------------------
     def compute_residual(self, u, r, gettimesteps=False, dtm=None):
         """Adds -r(u) into r (flow_spatial.hpp:73-87); fills dtm if gettimesteps."""
@@ -578,6 +583,12 @@ class FlowFVGroup:
         check(_ffi.lib().fvhip_group_steady_backward_euler_device(self._g, self._ptrs(d_us), ctypes.byref(c),
                                                                   ctypes.byref(st), dptr(hist)))
         return _solve_stats(st, hist)
+
+    def trace_exchange_device(self, d_lefts, d_rights, width=4):
+        """L2TraceVector::updateSharedFaces (tracevector.cpp:213-340) over the per-rank meshes of the
+        group: d_lefts[r] [nconnface][width] -> each neighbour's d_rights (device arrays)"""
+        check(_ffi.lib().fvhip_group_trace_exchange_device(self._g, self._ptrs(d_lefts), self._ptrs(d_rights),
+                                                           int(width)))
 
     def entropy_error_device(self, d_us):
         e = np.zeros(1)

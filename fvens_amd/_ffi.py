@@ -74,6 +74,11 @@ _SIGS = {
     "fvhip_group_create": (ctypes.c_int, [ctypes.POINTER(ctypes.c_void_p), ctypes.c_int,
                                           ctypes.POINTER(ctypes.c_void_p)]),
     "fvhip_group_destroy": (ctypes.c_int, [ctypes.c_void_p]),
+    "fvhip_build_info": (ctypes.c_char_p, []),
+    "fvhip_divsqrt_probe": (ctypes.c_int, [ctypes.c_int, c_dbl_p, c_dbl_p, c_dbl_p]),
+    "fvhip_trace_exchange_device": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int]),
+    "fvhip_group_trace_exchange_device": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(ctypes.c_void_p),
+                                                         ctypes.POINTER(ctypes.c_void_p), ctypes.c_int]),
     "fvhip_group_compute_residual_device": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(ctypes.c_void_p),
                                                            ctypes.POINTER(ctypes.c_void_p), ctypes.c_int,
                                                            ctypes.POINTER(ctypes.c_void_p), ctypes.c_int]),
@@ -166,6 +171,33 @@ def lib():
             f.argtypes = args
         _lib = L
     return _lib
+
+
+def source_hash():
+    """sha256 (first 16 hex digits) over the library's sources, in the Makefile's order (SRCHASH):
+    sorted csrc/*.hip, *.cpp, *.hpp, then include/fvhip.h"""
+    import glob
+    import hashlib
+    here = os.path.dirname(os.path.abspath(__file__))
+    names = sorted(os.path.relpath(p, here) for ext in ("hip", "cpp", "hpp")
+                   for p in glob.glob(os.path.join(here, "csrc", "*." + ext)))
+    h = hashlib.sha256()
+    for n in names:
+        with open(os.path.join(here, n), "rb") as f:
+            h.update(f.read())
+    with open(os.path.join(os.path.dirname(here), "include", "fvhip.h"), "rb") as f:
+        h.update(f.read())
+    return h.hexdigest()[:16]
+
+
+def build_info():
+    """{"library": path, "lib_src_hash": hash the loaded library was built from, "tree_src_hash": hash
+    of the sources in this tree, "fresh": whether they agree}"""
+    info = lib().fvhip_build_info().decode()
+    kv = dict(x.split("=", 1) for x in info.split() if "=" in x)
+    tree = source_hash()
+    return {"library": LIB_PATH, "lib_src_hash": kv.get("src_sha256_16"), "tree_src_hash": tree,
+            "fresh": kv.get("src_sha256_16") == tree, "extra": kv.get("extra", "")}
 
 
 def check(rc):

@@ -150,6 +150,8 @@ struct fvhip_ctx
 	int* d_border = nullptr;
 	int nborder = 0;
 	double* d_sendbuf = nullptr;
+	int* d_trace_conn = nullptr;     ///< per-rank meshes: Layout::trace_conn on the device
+	double* d_tracebuf = nullptr;    ///< [nghost][4] received face traces before the unpack
 	int nsend = 0;
 	// profiling
 	bool prof = false;
@@ -346,6 +348,32 @@ struct fvhip_ctx
 	}
 	int ghostCount(size_t k, int layers) const {
 		return (layers >= 2 || L.ghost_l1_end.empty() ? L.ghost_start[k+1] : L.ghost_l1_end[k]) - L.ghost_start[k];
+	}
+	/// L2TraceVector::updateSharedFacesBegin/End (tracevector.cpp:213-340) on a per-rank mesh: left
+	/// [nconnface][width] holds this rank's face values of its connectivity faces (icface order); each
+	/// neighbour's values of the same faces land in right[icface]. Packed in the exchange order (per
+	/// neighbour rank, ascending global face), sent with RCCL, unpacked by face. width <= 4.
+	void trace_pack(const double* left, int width, hipStream_t st) {
+		if(L.trace_conn.empty()) throw std::logic_error("face-trace exchange: not a per-rank mesh (no connectivity faces)");
+		if(width < 1 || width > 4) throw std::invalid_argument("face-trace exchange: width must be 1..4");
+		timed_on(st, "k_pack", [&]{ launch_pack_rows(d_trace_conn, nsend, left, width, d_sendbuf, st); });
+	}
+	void trace_unpack(double* right, int width, hipStream_t st) {
+		timed_on(st, "k_unpack", [&]{ launch_unpack_rows(d_trace_conn, L.nghost, d_tracebuf, width, right, st); });
+	}
+	void trace_exchange_rccl(const double* left, double* right, int width) {
+		if(!comm) throw std::runtime_error("face-trace exchange: call fvhip_comm_init (or use a group) first");
+		trace_pack(left, width, stream);
+		NC(ncclGroupStart());
+		for(size_t k = 0; k < L.nbr_rank.size(); k++) {
+			const int q = L.nbr_rank[k];
+			const size_t ns = static_cast<size_t>(L.send_start[k+1] - L.send_start[k]);
+			const size_t ng = static_cast<size_t>(L.ghost_start[k+1] - L.ghost_start[k]);
+			if(ns) NC(ncclSend(d_sendbuf + static_cast<size_t>(width)*L.send_start[k], width*ns, ncclDouble, q, comm, stream));
+			if(ng) NC(ncclRecv(d_tracebuf + static_cast<size_t>(width)*L.ghost_start[k], width*ng, ncclDouble, q, comm, stream));
+		}
+		NC(ncclGroupEnd());
+		trace_unpack(right, width, stream);
 	}
 	/// RCCL point-to-point exchange with every neighbour rank, on stream st (default: the handle's);
 	/// `layers` 2 fills both layers of a two-layer halo (the residual's state), 1 the first (gradients,

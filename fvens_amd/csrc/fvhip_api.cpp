@@ -133,6 +133,11 @@ static fvhip_ctx* createCtx(const MeshTopo& T, const fvhip_flow_config* cfg, int
 		h->d_send = upload(L.send_cells, o);
 		h->d_sendbuf = dalloc(8*static_cast<size_t>(h->nsend), o);
 	}
+	if(!L.trace_conn.empty()) {
+		if(static_cast<int>(L.trace_conn.size()) != h->nsend) throw std::logic_error("per-rank mesh: trace lists differ");
+		h->d_trace_conn = upload(L.trace_conn, o);
+		h->d_tracebuf = dalloc(4*static_cast<size_t>(L.nghost), o);
+	}
 
 	DevPhys& P = h->P;
 	P.gas = gd::Gas{cfg->gamma, cfg->Minf, cfg->Tinf, cfg->Reinf, cfg->Pr, 110.5, 1.0/(cfg->gamma - 1.0)};
@@ -301,6 +306,47 @@ int fvhip_group_compute_residual_device(fvhip_group g, const double* const* d_u,
 		fvhip_ctx::residual_seq(g->hs, us, rs, gettimesteps != 0, dts, (flags & FVHIP_RES_OVERWRITE) != 0,
 		                        groupExchange(g));
 		for(size_t i = 0; i < n; i++) HC(hipStreamSynchronize(g->hs[i]->stream));
+	});
+}
+
+int fvhip_trace_exchange_device(fvhip_handle h, const double* d_left, double* d_right, int width)
+{
+	return guard([&] {
+		HC(hipSetDevice(h->device));
+		h->trace_exchange_rccl(d_left, d_right, width);
+		HC(hipStreamSynchronize(h->stream));
+	});
+}
+
+int fvhip_group_trace_exchange_device(fvhip_group g, const double* const* d_left, double* const* d_right, int width)
+{
+	return guard([&] {
+		const std::vector<fvhip_ctx*>& hs = g->hs;
+		const size_t n = hs.size();
+		std::vector<fvhip_ctx*> byrank(n);
+		for(fvhip_ctx* h : hs) byrank[h->rank] = h;
+		for(size_t i = 0; i < n; i++) { HC(hipSetDevice(hs[i]->device)); hs[i]->trace_pack(d_left[i], width, hs[i]->stream); }
+		for(size_t i = 0; i < n; i++) HC(hipStreamSynchronize(hs[i]->stream));
+		for(size_t i = 0; i < n; i++) {
+			fvhip_ctx* h = hs[i];
+			const Layout& L = h->L;
+			HC(hipSetDevice(h->device));
+			for(size_t k = 0; k < L.nbr_rank.size(); k++) {
+				fvhip_ctx* q = byrank[L.nbr_rank[k]];
+				const Layout& Q = q->L;
+				size_t kk = 0;
+				while(kk < Q.nbr_rank.size() && Q.nbr_rank[kk] != h->rank) kk++;
+				if(kk == Q.nbr_rank.size()) throw std::logic_error("halo lists are not symmetric");
+				const int cnt = L.ghost_start[k+1] - L.ghost_start[k];
+				if(cnt != Q.send_start[kk+1] - Q.send_start[kk]) throw std::logic_error("halo sizes differ");
+				if(cnt == 0) continue;
+				HC(hipMemcpyAsync(h->d_tracebuf + static_cast<size_t>(width)*L.ghost_start[k],
+				                  q->d_sendbuf + static_cast<size_t>(width)*Q.send_start[kk],
+				                  sizeof(double)*width*static_cast<size_t>(cnt), hipMemcpyDeviceToDevice, h->stream));
+			}
+			h->trace_unpack(d_right[i], width, h->stream);
+		}
+		for(size_t i = 0; i < n; i++) HC(hipStreamSynchronize(hs[i]->stream));
 	});
 }
 
@@ -741,6 +787,21 @@ int fvhip_local_flux(int flux_type, const double* gas5, int nf, const double* ul
 		HC(hipGetLastError());
 		HC(hipMemcpy(flux, d, 4*sizeof(double)*nf, hipMemcpyDeviceToHost));
 		(void)hipFree(a); (void)hipFree(b); (void)hipFree(c); (void)hipFree(d);
+	});
+}
+
+int fvhip_divsqrt_probe(int n, const double* a, const double* b, double* out)
+{
+	return guard([&] {
+		double *da, *db, *dout;
+		HC(hipMalloc(&da, sizeof(double)*n + 8)); HC(hipMalloc(&db, sizeof(double)*n + 8));
+		HC(hipMalloc(&dout, 4*sizeof(double)*n + 8));
+		HC(hipMemcpy(da, a, sizeof(double)*n, hipMemcpyHostToDevice));
+		HC(hipMemcpy(db, b, sizeof(double)*n, hipMemcpyHostToDevice));
+		exact::launch_divsqrt_probe(n, da, db, dout, nullptr);
+		HC(hipGetLastError());
+		HC(hipMemcpy(out, dout, 4*sizeof(double)*n, hipMemcpyDeviceToHost));
+		(void)hipFree(da); (void)hipFree(db); (void)hipFree(dout);
 	});
 }
 

@@ -56,11 +56,14 @@ FVHIP_HD double dot2(const double* a, const double* b) { double d = mul0(a[0], b
 /// a/b and sqrt(x), correctly rounded, for the parity kernels. On the device these are the compiler's
 /// own f64 sequences -- division: v_rcp, two Newton steps, Markstein's correction; square root:
 /// v_rsq and Goldschmidt steps -- without their range scaling and special-value fix-ups
-/// (v_div_scale / v_div_fmas / v_div_fixup; ldexp and class selects). For operands whose result is
-/// a normal number, which every division and root of the sweep has (densities, pressures, sound
-/// speeds, eps-shifted limiter denominators, face lengths), they execute the same instructions on the
-/// same values, i.e. they return bitwise a/b and sqrt(x), in 8 instead of 11 and 10 instead of 19
-/// instructions (the sweep is FP64-issue bound). Host builds and the fast-math kernels use / and sqrt.
+/// (v_div_scale / v_div_fmas / v_div_fixup; ldexp and class selects). Inside their domain -- |a|, |b|
+/// and |a/b| in [2^-1000, 2^1000] for the division, x in [2^-766, 2^1000] for the root (below 2^-767
+/// the IEEE root first scales x by 2^256; sqrt_rn may then be one ulp off) -- they execute the same
+/// instructions on the same values, i.e. return bitwise a/b and sqrt(x) (tests/test_gpu_edge.py
+/// test_div_sqrt_rn_domain), in 8 instead of 11 and 10 instead of 19 instructions (the sweep is FP64-
+/// issue bound). Every division and root of the sweep lies far inside (densities, pressures, sound
+/// speeds, eps-shifted limiter sums, squared distances: 1e-12..1e12); an overflowing quotient gives NaN
+/// instead of inf. Host builds and the fast-math kernels use / and sqrt.
 FVHIP_HD double div_rn(double a, double b) {
 #if defined(__HIP_DEVICE_COMPILE__) && !defined(FVHIP_FAST)
 	double r = __builtin_amdgcn_rcp(b);
@@ -432,22 +435,11 @@ FVHIP_HD void inviscid_flux_rt(int type, const Gas& G, const double* ul, const d
 // ---------------------------------------------------------------------------------------------
 struct BCDev { int type; double v0, v1; };
 
+FVHIP_HD void ghost_state_common(const Gas& G, const BCDev& bc, const double* uinf, const double* ins,
+                                 const double* n, double* gs);
 FVHIP_HD void ghost_state(const Gas& G, const BCDev& bc, const double* uinf, const double* ins,
                           const double* n, double* gs) {
 	switch(bc.type) {
-	case 2: {  // INFLOW_OUTFLOW (abc.cpp:46-81)
-		const double vni = div_rn(dot2(&ins[1],n), ins[0]);
-		const double ci = sound_speed_cons(G, ins);
-		const double Mni = div_rn(vni, ci);
-		if(Mni <= 0) { gs[0] = uinf[0]; gs[1] = uinf[1]; gs[2] = uinf[2]; gs[3] = uinf[3]; }
-		else if(Mni < 1) {
-			const double pinf = freestream_pressure(G);
-			const double e = energy_from_pressure(G, pinf, ins[0], div_rn(dot2(&ins[1],&ins[1]), ins[0]*ins[0]));
-			gs[0] = ins[0]; gs[1] = ins[1]; gs[2] = ins[2]; gs[3] = e;
-		}
-		else { gs[0] = ins[0]; gs[1] = ins[1]; gs[2] = ins[2]; gs[3] = ins[3]; }
-		break;
-	}
 	case 3: {  // SUBSONIC_INFLOW (abc.cpp:145-175)
 		const double g = G.g, ptotal = bc.v0, ttotal = bc.v1;
 		const double ci = sound_speed_cons(G, ins);
@@ -462,6 +454,43 @@ FVHIP_HD void ghost_state(const Gas& G, const BCDev& bc, const double* uinf, con
 		const double vx = vm*1.0*n[0], vy = vm*1.0*n[1];
 		gs[0] = rho; gs[1] = rho*vx; gs[2] = rho*vy;
 		gs[3] = energy_from_pressure(G, pg, rho, vm*vm);
+		break;
+	}
+	case 6: {  // ISOTHERMAL_WALL (abc.cpp:349-366)
+		const double p = pressure_cons(G, ins);
+		const double gtemp = 2.0*bc.v1 - temperature(G, ins[0], p);
+		const double r = ins[0];
+		const double m0 = r*( 2.0*bc.v0*n[1] - div_rn(ins[1], ins[0]));
+		const double m1 = r*(-2.0*bc.v0*n[0] - div_rn(ins[2], ins[0]));
+		double mm[2] = {m0, m1};
+		const double vm2 = div_rn(dot2(mm,mm), r*r);
+		gs[0] = r; gs[1] = m0; gs[2] = m1; gs[3] = energy_from_temperature(G, gtemp, r, vm2);
+		break;
+	}
+	default:
+		ghost_state_common(G, bc, uinf, ins, n, gs);
+		break;
+	}
+}
+
+/// ghost_state for the common boundary conditions only (slip wall, far field, inflow-outflow,
+/// adiabatic wall, extrapolation): the kernels inline this form when a configuration uses no other
+/// BC type (the subsonic-inflow and isothermal-wall states are long, register-hungry sequences that
+/// stay out of line)
+FVHIP_HD void ghost_state_common(const Gas& G, const BCDev& bc, const double* uinf, const double* ins,
+                          const double* n, double* gs) {
+	switch(bc.type) {
+	case 2: {  // INFLOW_OUTFLOW (abc.cpp:46-81)
+		const double vni = div_rn(dot2(&ins[1],n), ins[0]);
+		const double ci = sound_speed_cons(G, ins);
+		const double Mni = div_rn(vni, ci);
+		if(Mni <= 0) { gs[0] = uinf[0]; gs[1] = uinf[1]; gs[2] = uinf[2]; gs[3] = uinf[3]; }
+		else if(Mni < 1) {
+			const double pinf = freestream_pressure(G);
+			const double e = energy_from_pressure(G, pinf, ins[0], div_rn(dot2(&ins[1],&ins[1]), ins[0]*ins[0]));
+			gs[0] = ins[0]; gs[1] = ins[1]; gs[2] = ins[2]; gs[3] = e;
+		}
+		else { gs[0] = ins[0]; gs[1] = ins[1]; gs[2] = ins[2]; gs[3] = ins[3]; }
 		break;
 	}
 	case 1:    // FARFIELD
@@ -481,17 +510,6 @@ FVHIP_HD void ghost_state(const Gas& G, const BCDev& bc, const double* uinf, con
 		const double m0 =  2.0*tm*n[1] - ins[1];
 		const double m1 = -2.0*tm*n[0] - ins[2];
 		gs[0] = r; gs[1] = m0; gs[2] = m1; gs[3] = e;
-		break;
-	}
-	case 6: {  // ISOTHERMAL_WALL (abc.cpp:349-366)
-		const double p = pressure_cons(G, ins);
-		const double gtemp = 2.0*bc.v1 - temperature(G, ins[0], p);
-		const double r = ins[0];
-		const double m0 = r*( 2.0*bc.v0*n[1] - div_rn(ins[1], ins[0]));
-		const double m1 = r*(-2.0*bc.v0*n[0] - div_rn(ins[2], ins[0]));
-		double mm[2] = {m0, m1};
-		const double vm2 = div_rn(dot2(mm,mm), r*r);
-		gs[0] = r; gs[1] = m0; gs[2] = m1; gs[3] = energy_from_temperature(G, gtemp, r, vm2);
 		break;
 	}
 	default:   // EXTRAPOLATION (and anything else, rejected at setup)

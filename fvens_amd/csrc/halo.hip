@@ -31,6 +31,21 @@ __global__ void __launch_bounds__(256) k_cons2prim_rows(gd::Gas G, const double*
 	reinterpret_cast<double4*>(up)[c] = make_double4(b[0], b[1], b[2], b[3]);
 }
 
+__global__ void __launch_bounds__(256) k_unpack_rows(const int* __restrict__ idx, int n, const double* __restrict__ src,
+                                                     int width, double* __restrict__ dst)
+{
+	const long long i = static_cast<long long>(blockIdx.x)*blockDim.x + threadIdx.x;
+	if(i >= static_cast<long long>(n)*width) return;
+	const int r = static_cast<int>(i / width), k = static_cast<int>(i % width);
+	dst[static_cast<size_t>(idx[r])*width + k] = src[i];
+}
+
+void launch_unpack_rows(const int* idx, int n, const double* src, int width, double* dst, hipStream_t s)
+{
+	const long long tot = static_cast<long long>(n)*width;
+	if(tot > 0) k_unpack_rows<<<static_cast<int>((tot + 255)/256), 256, 0, s>>>(idx, n, src, width, dst);
+}
+
 void launch_pack_rows(const int* idx, int n, const double* src, int width, double* dst, hipStream_t s)
 {
 	const long long tot = static_cast<long long>(n)*width;

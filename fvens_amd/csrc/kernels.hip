@@ -839,13 +839,23 @@ __global__ void __launch_bounds__(SLOTS_MAX) k_sweep(const DevMesh M, const DevP
 constexpr int FZW = 14;
 
 /// primitive ghost state of a cell's value across boundary face bf (k_prep_bfaces arithmetic)
+/// the fused residual's ghost states: the common BC types' ghost_state (gasdyn.hpp ghost_state_common)
+/// inlined -- fusedEligible admits only configurations whose BCs are all of those types (the others
+/// take the staged path). An out-of-line call in this kernel (ghost_ool: 82 VGPRs of its own, and the
+/// caller's values kept live across the call) costs 28 VGPRs on every path: 118 instead of 90 for the
+/// inviscid kernel, i.e. 4 instead of 5 waves per SIMD; 162 instead of 124 for the limited ones
+__device__ __forceinline__ void ghost_c(const DevPhys& P, int bc, const double* ins, const double* n, double* gs)
+{
+	const double ui[4] = {P.uinf[0], P.uinf[1], P.uinf[2], P.uinf[3]};
+	ghost_state_common(P.gas, P.bc[bc], ui, ins, n, gs);
+}
 __device__ __forceinline__ double4 ghost_prim_of_cell(const DevMesh& M, const DevPhys& P, const double* u, int cell, int bf)
 {
 	const double2 nn = M.bf_n[bf];
 	const double n[2] = {nn.x, nn.y};
 	double ucons[4], gs[4], gp[4];
 	ld4(u, cell, ucons);
-	ghost(P, M.bf_bc[bf], ucons, n, gs);
+	ghost_c(P, M.bf_bc[bf], ucons, n, gs);
 	cons2prim(P.gas, gs, gp);
 	return make_double4(gp[0], gp[1], gp[2], gp[3]);
 }
@@ -1233,7 +1243,7 @@ __device__ __forceinline__ void fz_body(const DevMesh& M, const DevPhys& P, cons
 					ul[i] = muscl_left(ui[i], uj[i], dm, muscl_phi(dm, du));
 				}
 				prim2cons(G, ul, ul);
-				ghost(P, M.bf_bc[bf], ul, n, ur);
+				ghost_c(P, M.bf_bc[bf], ul, n, ur);
 			}
 		} else {  // unlimited linear
 			const double2 gp = M.slot_gr[s];
@@ -1260,7 +1270,7 @@ __device__ __forceinline__ void fz_body(const DevMesh& M, const DevPhys& P, cons
 				}
 				prim2cons(G, ur, ur);
 			} else {
-				ghost(P, M.bf_bc[bf], ul, n, ur);
+				ghost_c(P, M.bf_bc[bf], ul, n, ur);
 			}
 		}
 		inviscid_flux<FLUX>(G, ul, ur, n, f);
@@ -1366,18 +1376,20 @@ __device__ __forceinline__ void fz_body(const DevMesh& M, const DevPhys& P, cons
 	FZ_CLOCK(B, 7);
 }
 
+// waves per SIMD the fused instantiations are compiled for (VGPR budgets 96 / 128 / 168); the layout
+// caps the staged rows to match (layout.cpp fusedRowCap: 5 blocks of 32 KB LDS per CU)
 #ifndef FVHIP_FUSED_WAVES
-#define FVHIP_FUSED_WAVES 4
+#define FVHIP_FUSED_WAVES 5          // inviscid, unlimited: 90 VGPRs
+#endif
+#ifndef FVHIP_FUSED_WAVES_LIM
+#define FVHIP_FUSED_WAVES_LIM 4      // Barth-Jespersen / Venkatakrishnan: 124-126 VGPRs
 #endif
 #ifndef FVHIP_FUSED_WAVES_VISC
-// viscous and limited instantiations: 3 waves per SIMD (168 VGPRs, no spill; at 4 waves the viscous ones
-// spill 144 B per lane and run 2.1x slower: Roe + MUSCL + Sutherland on C4 0.370 vs 0.768 ms, staged
-// path 0.511 ms; the limited ones spill 160 B)
-#define FVHIP_FUSED_WAVES_VISC 3
+#define FVHIP_FUSED_WAVES_VISC 3     // viscous: 144-156 VGPRs (at 4 waves 20-48 spilled)
 #endif
 
 template <int FLUX, int REC, bool DT, int VISC, int LIM>
-__global__ void __launch_bounds__(SLOTS_MAX, (VISC != SV_NONE || LIM) ? FVHIP_FUSED_WAVES_VISC : FVHIP_FUSED_WAVES) k_residual_wls(const DevMesh M, const DevPhys P, const SweepBuffers B)
+__global__ void __launch_bounds__(SLOTS_MAX, VISC != SV_NONE ? FVHIP_FUSED_WAVES_VISC : (LIM ? FVHIP_FUSED_WAVES_LIM : FVHIP_FUSED_WAVES)) k_residual_wls(const DevMesh M, const DevPhys P, const SweepBuffers B)
 {
 	extern __shared__ __attribute__((aligned(16))) double fz[];
 	const int np = B.plist ? B.pcount : M.npatch;
@@ -1484,6 +1496,21 @@ void launch_fill(double* p, double v, long long n, hipStream_t s)
 void launch_local_flux(int flux, const Gas& G, int nf, const double* ul, const double* ur,
                        const double* n, double* f, hipStream_t s)
 { if(nf > 0) k_local_flux<<<nblk(nf,256), 256, 0, s>>>(flux, G, nf, ul, ur, n, f); }
+/// parity-mode division and square root against the device's IEEE a/b and sqrt(a): out[i] =
+/// {div_rn(a,b), a/b, sqrt_rn(a), sqrt(a)} (the check of gasdyn.hpp's bitwise claim)
+__global__ void k_divsqrt_probe(int n, const double* __restrict__ a, const double* __restrict__ b, double* __restrict__ out)
+{
+	const int i = blockIdx.x*blockDim.x + threadIdx.x;
+	if(i >= n) return;
+	const double x = a[i], y = b[i];
+	out[4*i+0] = div_rn(x, y);
+	out[4*i+1] = x / y;
+	out[4*i+2] = sqrt_rn(x);
+	out[4*i+3] = sqrt(x);
+}
+void launch_divsqrt_probe(int n, const double* a, const double* b, double* out, hipStream_t s)
+{ if(n > 0) k_divsqrt_probe<<<nblk(n,256), 256, 0, s>>>(n, a, b, out); }
+
 void launch_gather_cells(const int* perm, const double* src, double* dst, int n, int width, hipStream_t s)
 { if(n > 0) k_gather<<<nblk(static_cast<long long>(n)*width,256), 256, 0, s>>>(perm, src, dst, n, width); }
 

@@ -172,6 +172,8 @@ Layout buildLayout(const MeshTopo& T, const fvhip_flow_config& cfg, bool renumbe
 	// (k_grad_ghost<LIM>); with the one-layer halo they would have to be exchanged as well
 	const bool limitedRec = cfg.reconstruction == FVHIP_REC_BARTHJESPERSEN || cfg.reconstruction == FVHIP_REC_VENKATAKRISHNAN;
 	const bool fused = fusedEligible(cfg) && (!limitedRec || T.nghost == 0 || T.halo_layers == 2);
+	const int rowcap = fusedRowCap(cfg);
+	Lo.fz_row_cap = rowcap;
 	if(fused) {
 		std::vector<int> ranges, mark2(NT, -1), r1;
 		int stamp = 0;
@@ -208,7 +210,7 @@ Layout buildLayout(const MeshTopo& T, const fvhip_flow_config& cfg, bool renumbe
 			std::vector<std::pair<int,int>> done;
 			while(!stack.empty()) {
 				const auto r = stack.back(); stack.pop_back();
-				if(r.second - r.first > 1 && (r.second - r.first) + ring1(r.first, r.second) > FUSED_LDS_CELLS) {
+				if(r.second - r.first > 1 && (r.second - r.first) + ring1(r.first, r.second) > rowcap) {
 					const int mid = (r.first + r.second)/2;
 					stack.push_back({mid, r.second}); stack.push_back({r.first, mid});
 				} else done.push_back(r);
@@ -310,6 +312,8 @@ Layout buildLayout(const MeshTopo& T, const fvhip_flow_config& cfg, bool renumbe
 	Lo.cell_global.resize(NT);
 	for(int c = 0; c < N; c++) Lo.cell_global[c] = T.cell_global[Lo.perm[c]];
 	for(int c = N; c < NT; c++) Lo.cell_global[c] = T.cell_global[c];
+	Lo.trace_conn.clear();
+	for(const int row : T.ghost_row) Lo.trace_conn.push_back(row - N);
 
 	// --- boundary faces ---
 	Lo.bf_L.resize(nb); Lo.bf_bc.resize(nb); Lo.bf_n.resize(2*static_cast<size_t>(nb)); Lo.bf_rcbp.resize(2*static_cast<size_t>(nb));
@@ -476,9 +480,19 @@ void buildPipeline(Layout& Lo, int chunks)
 bool fusedEligible(const fvhip_flow_config& cfg)
 {
 	const bool limited = cfg.reconstruction == FVHIP_REC_BARTHJESPERSEN || cfg.reconstruction == FVHIP_REC_VENKATAKRISHNAN;
+	// the fused kernel inlines the common BC types' ghost states (kernels.hip ghost_c); subsonic inflow
+	// and isothermal walls take the staged path, whose kernels call the full ghost state out of line
+	for(int i = 0; i < cfg.nbc; i++)
+		if(cfg.bc_type[i] == FVHIP_BC_SUBSONIC_INFLOW || cfg.bc_type[i] == FVHIP_BC_ISOTHERMAL_WALL) return false;
 	return cfg.order2 && cfg.gradientscheme == FVHIP_GRAD_LEASTSQUARES &&
 	       (cfg.reconstruction == FVHIP_REC_VANALBADA || cfg.reconstruction == FVHIP_REC_NONE ||
 	        (limited && !cfg.viscous_sim));
+}
+
+int fusedRowCap(const fvhip_flow_config& cfg)
+{
+	const bool limited = cfg.reconstruction == FVHIP_REC_BARTHJESPERSEN || cfg.reconstruction == FVHIP_REC_VENKATAKRISHNAN;
+	return (!cfg.viscous_sim && !limited) ? FUSED_LDS_CELLS_5W : FUSED_LDS_CELLS;
 }
 
 void buildFused(Layout& Lo)
@@ -515,7 +529,7 @@ void buildFused(Layout& Lo)
 			if(c >= Lo.ncell) continue;
 			for(int j = 0; j < MAXF; j++) add(Lo.cell_nbr_fo[static_cast<size_t>(c)*MAXF+j]);
 		}
-		if(nl > FUSED_LDS_CELLS) throw std::logic_error("fused residual: patch exceeds its LDS budget");
+		if(nl > Lo.fz_row_cap) throw std::logic_error("fused residual: patch exceeds its LDS budget");
 		Lo.fz_n1[p] = ng - nc;
 		Lo.fz_ring2 += nl - ng;
 		Lo.fz_ext_start.push_back(static_cast<int>(Lo.fz_ext.size()));

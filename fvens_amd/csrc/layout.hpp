@@ -89,6 +89,9 @@ struct Layout
 	std::vector<int> xb_bc;                ///< extra boundary faces: BC index,
 	std::vector<double> xb_n, xb_rcbp;     ///<  normal [2], ghost centre [2]
 	std::vector<int> cell_global;          ///< [ncell+nghost] global cell of each internal cell
+	std::vector<int> trace_conn;           ///< per-rank meshes: [nghost] the connectivity face (icface) of
+	                                       ///<  each ghost entry = of each send entry (same order), for the
+	                                       ///<  face-trace exchange (L2TraceVector)
 	// fused residual (k_residual_wls): per patch, the ring-1 cells (far side of its cut faces) whose
 	// primitive states and gradients it recomputes, and the ring-2 cells (the other neighbours of the
 	// owned ring-1 cells) whose primitive states those gradients read; every cell a patch reads is
@@ -113,6 +116,7 @@ struct Layout
 	std::vector<uint16_t> fz_cslot16;      ///< [ncell][4]
 	int fz_ring2 = 0;                      ///< ring-2 cells staged over all patches
 	int fz_max_cells = 0;
+	int fz_row_cap = 0;                    ///< fusedRowCap of the configuration
 	std::vector<int> fz_order;             ///< patches needing no halo data first (fz_ninner), then the rest
 	int fz_ninner = 0;
 	// pipelined staged residual (single domain, WLS): the gradient kernel runs in chunks of cells on
@@ -123,7 +127,11 @@ struct Layout
 	std::vector<int> pipe_group_start;     ///< [K+1] ranges into pipe_patch
 };
 
-constexpr int FUSED_LDS_CELLS = FVHIP_FUSED_ROWS;   ///< staged cells per patch (rows of 112 B)
+constexpr int FUSED_LDS_CELLS = FVHIP_FUSED_ROWS;   ///< staged cells per patch (rows of 112 B), at most
+constexpr int FUSED_LDS_CELLS_5W = 284;              ///< ... for the 5-wave inviscid kernel: 284 x 112 B = 31,808 B, five blocks within 160 KB at a 1,280-B allocation granule
+/// the fused kernel's staged-row cap for cfg: 5 blocks of 32 KB per CU for the inviscid unlimited
+/// instantiations (compiled for 5 waves per SIMD), else FUSED_LDS_CELLS (4 blocks of 39 KB)
+int fusedRowCap(const fvhip_flow_config& cfg);
 static_assert(FUSED_LDS_CELLS < 0x8000 && 2*SLOTS_MAX < 0xFFFF, "fused codes are 16-bit");
 constexpr int PIPE_CHUNKS = 8;          ///< gradient chunks of the pipelined staged residual
 

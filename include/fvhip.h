@@ -105,6 +105,9 @@ typedef struct fvhip_ctx* fvhip_handle;
 const char* fvhip_last_error(void);
 /** Library version string */
 const char* fvhip_version(void);
+/** build provenance: "src_sha256_16=<first 16 hex digits of sha256 over the sorted fvens_amd/csrc
+ *  .hip, .cpp and .hpp files and include/fvhip.h> arch=gfx950 extra=<experiment defines>" */
+const char* fvhip_build_info(void);
 /** Number of visible HIP devices (0 if none; never fails) */
 int fvhip_device_count(void);
 
@@ -162,6 +165,12 @@ int fvhip_comm_unique_id(void* id128);
 int fvhip_comm_init(fvhip_handle h, int nranks, int rank, const void* id128);
 /** All ranks of a partition in ONE process (e.g. on one device): exchange by device copies */
 int fvhip_group_create(fvhip_handle* handles, int n, fvhip_group* out);
+/** L2TraceVector::updateSharedFacesBegin + End (linalg/tracevector.cpp:213-340) on a per-rank mesh
+ *  (nconnface > 0): d_left [nconnface][width] (device, the mesh's connectivity-face order) holds this
+ *  rank's face values; on return d_right[icface] holds the neighbour rank's value of the same face
+ *  (its left). width 1..4. RCCL ranks (fvhip_comm_init) / all ranks of a group in one process. */
+int fvhip_trace_exchange_device(fvhip_handle h, const double* d_left, double* d_right, int width);
+int fvhip_group_trace_exchange_device(fvhip_group g, const double* const* d_left, double* const* d_right, int width);
 int fvhip_group_destroy(fvhip_group g);
 int fvhip_group_compute_residual_device(fvhip_group g, const double* const* d_u, double* const* d_r,
                                         int gettimesteps, double* const* d_dtm, int flags);
@@ -326,6 +335,10 @@ int fvhip_layout_probe(const fvhip_mesh* mesh, const fvhip_flow_config* cfg, lon
 /** Point-wise numerical flux on the device (get_flux) for nf faces: ul, ur [nf][4], n [nf][2] */
 int fvhip_local_flux(int flux_type, const double* gas5, int nf, const double* ul, const double* ur,
                      const double* n, double* flux);
+/** Diagnostics of the parity-mode arithmetic (not a reference interface): on the device, out[i] =
+ *  {div_rn(a,b), a/b, sqrt_rn(a), sqrt(a)} -- the shortened correctly rounded division and square
+ *  root of the residual kernels next to the device's full IEEE operations (gasdyn.hpp) */
+int fvhip_divsqrt_probe(int n, const double* a, const double* b, double* out);
 /** Point-wise flux Jacobians (get_jacobian) on the device: dfdl, dfdr [nf][16] */
 int fvhip_local_flux_jacobian(int flux_type, const double* gas5, int nf, const double* ul,
                               const double* ur, const double* n, double* dfdl, double* dfdr);

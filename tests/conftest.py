@@ -13,9 +13,23 @@ def pytest_configure(config):
 
 
 def _ensure_built():
+    """build when a library is missing, and rebuild when the library was built from other sources than
+    this tree holds (fvhip_build_info's source hash): the tests never run a stale binary"""
     lib = os.path.join(ROOT, "fvens_amd", "libfvhip.so")
     orc = os.path.join(ROOT, "oracle", "liboracle.so")
     if not (os.path.exists(lib) and os.path.exists(orc)):
+        import __graft_entry__
+        __graft_entry__.build()
+        return
+    if os.environ.get("FVHIP_LIB"):
+        return
+    import subprocess
+    import fvens_amd._ffi as ffi
+    probe = subprocess.run([sys.executable, "-c", "import sys; sys.path.insert(0, %r); import fvens_amd._ffi as f; "
+                            "print(f.lib().fvhip_build_info().decode())" % ROOT], capture_output=True, text=True)
+    built = dict(x.split("=", 1) for x in probe.stdout.split() if "=" in x).get("src_sha256_16")
+    if built != ffi.source_hash():
+        sys.stderr.write("libfvhip.so was built from other sources (%s, tree %s): rebuilding\n" % (built, ffi.source_hash()))
         import __graft_entry__
         __graft_entry__.build()
 
