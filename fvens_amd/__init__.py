@@ -395,14 +395,15 @@ class FlowFV:
         check(_ffi.lib().fvhip_matfree_apply_device(self._h, ctypes.c_void_p(d_x), ctypes.c_void_p(d_y)))
 
     def compute_residual_device(self, d_u, d_r, d_dtm=None, gettimesteps=False, overwrite=True, staged=False,
-                                pipelined=False):
+                                pipelined=False, halo_ready=False):
         """staged=True forces the gradient + sweep kernels one after the other, pipelined=True the
         gradient chunks overlapped with the sweep groups (FVHIP_RES_STAGED / FVHIP_RES_PIPELINED);
-        every path gives the same bits"""
+        every path gives the same bits. halo_ready=True (partitioned handles): the ghost rows of d_u
+        are current, no exchange runs (FVHIP_RES_HALO_READY)"""
         check(_ffi.lib().fvhip_compute_residual_device(self._h, ctypes.c_void_p(d_u), ctypes.c_void_p(d_r),
                                                        int(gettimesteps), ctypes.c_void_p(d_dtm or 0),
                                                        (1 if overwrite else 0) | (2 if staged else 0) |
-                                                       (4 if pipelined else 0)))
+                                                       (4 if pipelined else 0) | (8 if halo_ready else 0)))
 
     def permutation(self):
         p = np.zeros(self.nown, np.int32)

@@ -317,7 +317,8 @@ struct fvhip_ctx
 		HC(hipStreamWaitEvent(stream, pipe_done, 0));   // the residual completes on `stream`
 	}
 	void stage_fused(const double* u, double* r, bool dt, double* dtm, bool overwrite,
-	                 const int* plist = nullptr, int pcount = 0) {
+	                 const int* plist = nullptr, int pcount = 0, hipStream_t st = nullptr) {
+		if(!st) st = stream;
 		SweepBuffers B{};
 		B.u = u; B.r = r; B.dtm = dtm; B.overwrite = overwrite ? 1 : 0;
 		B.plist = plist; B.pcount = pcount;
@@ -329,9 +330,8 @@ struct fvhip_ctx
 		B.probe = d_probe;
 #endif
 		const char* nm = nullptr;
-		timed("k_residual_wls", [&]{ nm = KOPS(launch_residual_wls)(M, P, B, cfg.conv_numflux, recKind(), viscKind(),
-		                                                                limited() ? (cfg.reconstruction == FVHIP_REC_VENKATAKRISHNAN ? 2 : 1) : 0,
-		                                                                dt, stream); });
+		timed_on(st, "k_residual_wls", [&]{ nm = KOPS(launch_residual_wls)(M, P, B, cfg.conv_numflux, recKind(), viscKind(),
+		                                                                       limKind(), dt, st); });
 		if(prof && !recs.empty() && recs.back().name == "k_residual_wls" && nm) recs.back().name = nm;
 		HC(hipGetLastError());
 	}
@@ -465,27 +465,31 @@ struct fvhip_ctx
 			}
 			h->stage_ghost_gradients(us[i], h->comm_stream);
 			HC(hipEventRecord(h->ev_copied, h->comm_stream));
+			// 4. the border patches on the comm stream right behind the halo (concurrent with the
+			//    interior launch's tail, as in residual_fused_overlapped)
+			h->stage_fused(us[i], rs[i], dt, dts[i], overwrite, h->d_fz_order + h->L.fz_ninner,
+			               static_cast<int>(h->L.fz_order.size()) - h->L.fz_ninner, h->comm_stream);
 			HC(hipEventRecord(h->ev_halo, h->comm_stream));
 		}
 		for(fvhip_ctx* h : hs) h->copied_recorded = true;
-		// 4. the border patches once the halo is in place; later work on a handle's stream (the next
-		//    pack of a synchronous exchange included) also follows every copy out of its send buffer
+		// 5. the residual completes on each handle's stream; later work there (the next pack of a
+		//    synchronous exchange included) also follows every copy out of its send buffer
 		for(size_t i = 0; i < n; i++) {
 			fvhip_ctx* h = on(i);
 			HC(hipStreamWaitEvent(h->stream, h->ev_halo, 0));
 			for(fvhip_ctx* q : hs) HC(hipStreamWaitEvent(h->stream, q->ev_copied, 0));
-			h->stage_fused(us[i], rs[i], dt, dts[i], overwrite, h->d_fz_order + h->L.fz_ninner,
-			               static_cast<int>(h->L.fz_order.size()) - h->L.fz_ninner);
 		}
 	}
 
 	/// fused residual of one RCCL rank: the halo exchange (ghost u, border gradients, ghost
-	/// gradients) runs on comm_stream while the interior patches run on `stream`; the border
-	/// patches follow once the halo has arrived
+	/// gradients) runs on comm_stream while the interior patches run on `stream`; the border patches
+	/// are launched on comm_stream right behind the halo, so their blocks fill the interior launch's
+	/// last partial wave instead of forming a fraction-of-a-wave launch after it. The two launches
+	/// write disjoint cells; `stream` joins the comm stream before the residual is complete.
 	void residual_fused_overlapped(const double* u, double* r, bool dt, double* dtm, bool overwrite) {
 		ensureOverlap();
 		double* uu = const_cast<double*>(u);
-		HC(hipEventRecord(ev_u, stream));                 // u as the caller left it
+		HC(hipEventRecord(ev_u, stream));                 // u as the caller left it (and r, dtm free)
 		HC(hipStreamWaitEvent(comm_stream, ev_u, 0));
 		if(singleExchange()) {
 			exchange_rccl(uu, 4, comm_stream, 2);
@@ -495,10 +499,22 @@ struct fvhip_ctx
 			stage_border_gradients(u, comm_stream);
 			exchange_rccl(d_grad, 8, comm_stream);
 		}
-		HC(hipEventRecord(ev_halo, comm_stream));
 		stage_fused(u, r, dt, dtm, overwrite, d_fz_order, L.fz_ninner);
+		stage_fused(u, r, dt, dtm, overwrite, d_fz_order + L.fz_ninner, static_cast<int>(L.fz_order.size()) - L.fz_ninner,
+		            comm_stream);
+		HC(hipEventRecord(ev_halo, comm_stream));
 		HC(hipStreamWaitEvent(stream, ev_halo, 0));
-		stage_fused(u, r, dt, dtm, overwrite, d_fz_order + L.fz_ninner, static_cast<int>(L.fz_order.size()) - L.fz_ninner);
+	}
+
+	/// the residual with the ghost rows of u already current (FVHIP_RES_HALO_READY): layer-1 ghost
+	/// gradients (and limiter values), then every patch on the handle's stream
+	void residual_halo_ready(const double* u, double* r, bool dt, double* dtm, bool overwrite) {
+		if(!halo()) { residual(u, r, dt, dtm, overwrite); return; }
+		if(!fused() || !singleExchange())
+			throw std::runtime_error("FVHIP_RES_HALO_READY: only the fused single-exchange configurations (two-layer "
+			                         "halo, WLS + MUSCL / linear / Barth-Jespersen / Venkatakrishnan)");
+		stage_ghost_gradients(u);
+		stage_fused(u, r, dt, dtm, overwrite, d_fz_order, static_cast<int>(L.fz_order.size()));
 	}
 
 	/// the device sweep: -r(u) added (or written) into r, time steps into dtm. On a partitioned
@@ -714,8 +730,13 @@ struct fvhip_ctx
 	double lines_thr = -1.0;
 	std::vector<int> h_line_start;
 	void ensureLines(double thr) {
-		if(thr <= 0.0) thr = 4.0;
+		if(!(thr >= 0.0) || !std::isfinite(thr)) throw std::invalid_argument("line_threshold must be finite and >= 0 (0: 4)");
+		if(thr == 0.0) thr = 4.0;
 		if(lines.start && lines_thr == thr) return;
+		// a rebuild (another threshold) releases the previous line set's device arrays
+		for(const void* p : {static_cast<const void*>(lines.start), static_cast<const void*>(lines.cell),
+		                     static_cast<const void*>(lines.face)}) release(p);
+		lines = LineSet{};
 		const int N = L.ncell, nb = L.nbface;
 		struct Nb { int c, fi; double w; };
 		std::vector<std::array<Nb,4>> nbr(static_cast<size_t>(N));
@@ -801,6 +822,15 @@ struct fvhip_ctx
 		lines.face = upload(faces, owned);
 		h_line_start = st;
 		lines_thr = thr;
+	}
+
+	/// frees one device array of `owned` before the handle's destruction
+	void release(const void* p) {
+		if(!p) return;
+		auto it = std::find(owned.begin(), owned.end(), p);
+		if(it == owned.end()) throw std::logic_error("release: not a buffer of this handle");
+		(void)hipFree(*it);
+		owned.erase(it);
 	}
 
 	/// fp32 copies of the preconditioner blocks (fvhip_implicit_config::prec_single)

@@ -140,7 +140,7 @@ static fvhip_ctx* createCtx(const MeshTopo& T, const fvhip_flow_config* cfg, int
 	}
 
 	DevPhys& P = h->P;
-	P.gas = gd::Gas{cfg->gamma, cfg->Minf, cfg->Tinf, cfg->Reinf, cfg->Pr, 110.5, 1.0/(cfg->gamma - 1.0)};
+	P.gas = gd::make_gas(cfg->gamma, cfg->Minf, cfg->Tinf, cfg->Reinf, cfg->Pr);
 	// free stream, aphysics.cpp:43-58 (sideslip 0)
 	const double beta = 0;
 	P.uinf[0] = 1.0;
@@ -359,7 +359,8 @@ int fvhip_compute_residual_device(fvhip_handle h, const double* d_u, double* d_r
 		HC(hipSetDevice(h->device));
 		h->use_staged = (flags & FVHIP_RES_STAGED) != 0;
 		h->use_pipe = (flags & FVHIP_RES_PIPELINED) != 0;
-		h->residual(d_u, d_r, gettimesteps != 0, d_dtm, (flags & FVHIP_RES_OVERWRITE) != 0);
+		if(flags & FVHIP_RES_HALO_READY) h->residual_halo_ready(d_u, d_r, gettimesteps != 0, d_dtm, (flags & FVHIP_RES_OVERWRITE) != 0);
+		else h->residual(d_u, d_r, gettimesteps != 0, d_dtm, (flags & FVHIP_RES_OVERWRITE) != 0);
 		h->use_staged = h->use_pipe = false;
 	});
 }
@@ -776,7 +777,7 @@ int fvhip_local_flux(int flux_type, const double* gas5, int nf, const double* ul
                      const double* n, double* flux)
 {
 	return guard([&] {
-		gd::Gas G{gas5[0], gas5[1], gas5[2], gas5[3], gas5[4], 110.5, 1.0/(gas5[0] - 1.0)};
+		const gd::Gas G = gd::make_gas(gas5[0], gas5[1], gas5[2], gas5[3], gas5[4]);
 		double *a, *b, *c, *d;
 		HC(hipMalloc(&a, 4*sizeof(double)*nf + 8)); HC(hipMalloc(&b, 4*sizeof(double)*nf + 8));
 		HC(hipMalloc(&c, 2*sizeof(double)*nf + 8)); HC(hipMalloc(&d, 4*sizeof(double)*nf + 8));
@@ -812,7 +813,7 @@ int fvhip_local_flux_jacobian(int flux_type, const double* gas5, int nf, const d
 		if(flux_type == FVHIP_FLUX_VANLEER) throw std::runtime_error(" ! VanLeerFlux: Not implemented!");
 		if(flux_type == FVHIP_FLUX_AUSMPLUS) throw std::runtime_error(" ! AUSMPlusFlux: Not implemented!");
 		if(flux_type < 0 || flux_type > 6) throw std::invalid_argument("unknown flux");
-		gd::Gas G{gas5[0], gas5[1], gas5[2], gas5[3], gas5[4], 110.5, 1.0/(gas5[0] - 1.0)};
+		const gd::Gas G = gd::make_gas(gas5[0], gas5[1], gas5[2], gas5[3], gas5[4]);
 		double *a, *b, *c, *d, *e;
 		HC(hipMalloc(&a, 4*sizeof(double)*nf + 8)); HC(hipMalloc(&b, 4*sizeof(double)*nf + 8));
 		HC(hipMalloc(&c, 2*sizeof(double)*nf + 8)); HC(hipMalloc(&d, 16*sizeof(double)*nf + 8));

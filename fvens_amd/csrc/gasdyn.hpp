@@ -23,11 +23,31 @@
 namespace fvhip {
 namespace gd {
 
-/// Gas constants (IdealGasPhysics members, aphysics.hpp; sC = 110.5, aphysics.cpp:19)
+/// Gas constants (IdealGasPhysics members, aphysics.hpp; sC = 110.5, aphysics.cpp:19), and run-time
+/// constants of the viscous terms the host forms once, each with the reference's arithmetic, so that a
+/// division by a constant becomes div_rcp (Markstein's correction with the correctly rounded
+/// reciprocal: the same bits as the division, 3 instead of 8 instructions) -- build with make_gas
 struct Gas {
 	double g, Minf, Tinf, Reinf, Pr, sC;
 	double rgm1;     ///< 1/(g-1) correctly rounded (host division), for div_rcp by g-1 on the device
+	double sCT;      ///< sC/Tinf (getViscosityCoeffFromTemperature, aphysics_defs.hpp:411)
+	double sCT1;     ///< 1.0 + sC/Tinf
+	double rReinf;   ///< 1/Reinf (also the constant viscosity, aphysics_defs.hpp:444)
+	double kden;     ///< Minf*Minf*(g-1.0)*Pr (getThermalConductivityFromViscosity, :449)
+	double rkden;    ///< 1/kden
+	double rPr;      ///< 1/Pr
 };
+/// Gas with its derived constants (host IEEE arithmetic in the reference's association order)
+inline Gas make_gas(double g, double Minf, double Tinf, double Reinf, double Pr) {
+	Gas G{g, Minf, Tinf, Reinf, Pr, 110.5, 1.0/(g - 1.0), 0, 0, 0, 0, 0, 0};
+	G.sCT = G.sC/G.Tinf;
+	G.sCT1 = 1.0 + G.sCT;
+	G.rReinf = 1.0/G.Reinf;
+	G.kden = G.Minf*G.Minf*(G.g-1.0)*G.Pr;
+	G.rkden = 1.0/G.kden;
+	G.rPr = 1.0/G.Pr;
+	return G;
+}
 
 /// `0 + a*b`: the first term of a sum the reference accumulates from zero. On the device this is
 /// fma(a, b, +0) -- one instruction instead of a multiply and an add. fma rounds a*b once and adds
@@ -170,7 +190,7 @@ FVHIP_HD double pow15(double T) {
 }
 FVHIP_HD double sutherland(const Gas& G, const double* uc) {
 	const double T = temperature(G, uc[0], pressure_cons(G, uc));
-	return div_rn(div_rn(1.0+div_rn(G.sC, G.Tinf), T+div_rn(G.sC, G.Tinf)) * pow15(T), G.Reinf);
+	return div_rcp(div_rn(G.sCT1, T+G.sCT) * pow15(T), G.Reinf, G.rReinf);
 }
 
 /// Roe averages (anumericalflux.hpp:175-189)
@@ -530,7 +550,7 @@ FVHIP_HD void ghost_state_common(const Gas& G, const BCDev& bc, const double* ui
 /// form them while the face states are live and drop those states before the gradient terms
 template <bool CONSTVISC>
 FVHIP_HD void viscous_face_terms(const Gas& G, const double* ul, const double* ur, double& muRe, double* va) {
-	muRe = CONSTVISC ? 1.0/G.Reinf : 0.5*( sutherland(G, ul) + sutherland(G, ur) );
+	muRe = CONSTVISC ? G.rReinf : 0.5*( sutherland(G, ul) + sutherland(G, ur) );
 	va[0] = 0.5*( div_rn(ul[1], ul[0]) + div_rn(ur[1], ur[0]) );
 	va[1] = 0.5*( div_rn(ul[2], ul[0]) + div_rn(ur[2], ur[0]) );
 }
@@ -582,7 +602,7 @@ FVHIP_HD void viscous_flux_core(const Gas& G, const double* n, const double* rcl
 			grad[1][i] = davg[1] - ddr*dr[1] + corr*dr[1];
 		}
 	}
-	const double kd = div_rn(muRe, G.Minf*G.Minf*(G.g-1.0)*G.Pr);
+	const double kd = div_rcp(muRe, G.kden, G.rkden);
 	double ldiv = 0;
 	ldiv += grad[0][1]; ldiv += grad[1][2];
 	ldiv *= 2.0/3.0*muRe;

@@ -327,6 +327,8 @@ static void checkImplicit(const fvhip_implicit_config& c)
 	if(c.prec_sweeps < 1) throw std::invalid_argument("prec_sweeps must be >= 1");
 	if(!(c.min_relax > 0.0)) throw std::domain_error("Minimum relaxation factor is invalid!");  // nonlinearrelaxation.cpp:20-21
 	if(c.matrix_free && !(c.mf_eps > 0.0)) throw std::invalid_argument("matrix-free difference step must be positive");
+	if(!(c.line_threshold >= 0.0) || !std::isfinite(c.line_threshold))
+		throw std::invalid_argument("line_threshold must be finite and >= 0 (0: the default 4)");
 }
 
 /// SteadyBackwardEulerSolver::solve (aodesolver.cpp:363-638) on device states us (internal order,

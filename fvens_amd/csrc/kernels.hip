@@ -774,15 +774,15 @@ __global__ void __launch_bounds__(SLOTS_MAX) k_sweep(const DevMesh M, const DevP
 			sri = (fabs(vni)+ci)*len;
 			srj = (fabs(vnj)+cj)*len;
 			if(VISC != SV_NONE) {
-				const double mui = VISC == SV_CONST ? 1.0/G.Reinf : sutherland(G, ul);
-				const double muj = VISC == SV_CONST ? 1.0/G.Reinf : sutherland(G, ur);
+				const double mui = VISC == SV_CONST ? G.rReinf : sutherland(G, ul);
+				const double muj = VISC == SV_CONST ? G.rReinf : sutherland(G, ur);
 				const double ai = div_rn(4.0, 3*ul[0]), bi = div_rn(G.g, ul[0]);
 				const double aj = div_rn(4.0, 3*ur[0]), bj = div_rn(G.g, ur[0]);
 				const double coi = (ai < bi) ? bi : ai;          // std::max
 				const double coj = (aj < bj) ? bj : aj;
 				// a ghost cell's spectral radius is never summed (and its area is not stored)
-				if(lr.x < M.nown) sri += div_rn(div_rn(coi*mui, G.Pr) * len*len, M.area[lr.x]);
-				if(!bnd && lr.y < M.nown) srj += div_rn(div_rn(coj*muj, G.Pr) * len*len, M.area[lr.y]);
+				if(lr.x < M.nown) sri += div_rn(div_rcp(coi*mui, G.Pr, G.rPr) * len*len, M.area[lr.x]);
+				if(!bnd && lr.y < M.nown) srj += div_rn(div_rcp(coj*muj, G.Pr, G.rPr) * len*len, M.area[lr.y]);
 			}
 		}
 	}
@@ -1089,6 +1089,75 @@ __device__ __forceinline__ void fused_limit_row(const DevMesh& M, const DevPhys&
 #ifndef FVHIP_FZ_LIM_PREFETCH
 #define FVHIP_FZ_LIM_PREFETCH 1
 #endif
+/// the modified-average viscous flux of one face in the fused residual (gasdyn.hpp viscous_flux_core's
+/// arithmetic, same operations in the same order, so bitwise its result), streamed from the staged LDS
+/// rows variable by variable: first the temperature terms (density and pressure values and gradients),
+/// then the velocity terms, each group read after a compiler fence, so only one group's LDS values are
+/// live at a time instead of both cells' full rows (24 doubles) -- register pressure. The density
+/// face gradient (unused by the flux) is not formed. Boundary face: rowj = nullptr, the right state is
+/// the ghost primitive state gpr and the right gradient the cell's own.
+__device__ __forceinline__ void fz_viscous(const Gas& G, const double* rowi, const double* rowj, const double* gpr,
+                                           double2 ri, double2 rr, const double* n, double muRe, const double* va,
+                                           double* vf)
+{
+	const double* gsrc = rowj ? rowj : rowi;          // right gradient: the boundary cell's own
+	double dr[2], dist = 0;
+	dr[0] = rr.x-ri.x; dist += dr[0]*dr[0];
+	dr[1] = rr.y-ri.y; dist += dr[1]*dr[1];
+	dist = sqrt_rn(dist);
+	dr[0] = div_rn(dr[0], dist); dr[1] = div_rn(dr[1], dist);
+	double grad[2][4];
+	{   // temperature: T = temperature(rho, p), dT from the density and pressure gradients
+		__asm__ volatile("" ::: "memory");
+		const double rl = rowi[0], pl = rowi[3];
+		const double rrr = rowj ? rowj[0] : gpr[0], prr = rowj ? rowj[3] : gpr[3];
+		double gL[2], gR[2];
+		for(int j = 0; j < 2; j++) {
+			gL[j] = grad_temperature(G, rl, rowi[4 + 0*2 + j], pl, rowi[4 + 3*2 + j]);
+			gR[j] = grad_temperature(G, rrr, gsrc[4 + 0*2 + j], prr, gsrc[4 + 3*2 + j]);
+		}
+		const double tl = temperature(G, rl, pl), tr = temperature(G, rrr, prr);
+		double davg[2];
+		davg[0] = 0.5*(gL[0] + gR[0]);
+		davg[1] = 0.5*(gL[1] + gR[1]);
+		const double corr = div_rn(tr-tl, dist);
+		const double ddr = dot2(davg,dr);
+		grad[0][3] = davg[0] - ddr*dr[0] + corr*dr[0];
+		grad[1][3] = davg[1] - ddr*dr[1] + corr*dr[1];
+	}
+	#pragma unroll
+	for(int i = 1; i < 3; i++) {   // velocity components
+		__asm__ volatile("" ::: "memory");
+		const double tl = rowi[i], tr = rowj ? rowj[i] : gpr[i];
+		double davg[2];
+		davg[0] = 0.5*(rowi[4 + i*2 + 0] + gsrc[4 + i*2 + 0]);
+		davg[1] = 0.5*(rowi[4 + i*2 + 1] + gsrc[4 + i*2 + 1]);
+		const double corr = div_rn(tr-tl, dist);
+		const double ddr = dot2(davg,dr);
+		grad[0][i] = davg[0] - ddr*dr[0] + corr*dr[0];
+		grad[1][i] = davg[1] - ddr*dr[1] + corr*dr[1];
+	}
+	const double kd = div_rcp(muRe, G.kden, G.rkden);
+	double ldiv = 0;
+	ldiv += grad[0][1]; ldiv += grad[1][2];
+	ldiv *= 2.0/3.0*muRe;
+	double s[2][2];
+	s[0][0] = muRe*(grad[0][1] + grad[0][1]); s[0][1] = muRe*(grad[0][2] + grad[1][1]);
+	s[0][0] -= ldiv;
+	s[1][0] = muRe*(grad[1][1] + grad[0][2]); s[1][1] = muRe*(grad[1][2] + grad[1][2]);
+	s[1][1] -= ldiv;
+	vf[0] = 0;
+	for(int i = 0; i < 2; i++) { double t = 0; t -= s[i][0]*n[0]; t -= s[i][1]*n[1]; vf[i+1] = t; }
+	double e = 0;
+	for(int i = 0; i < 2; i++) {
+		double comp = 0;
+		comp += s[i][0]*va[0]; comp += s[i][1]*va[1];
+		comp += kd*grad[i][3];
+		e -= comp * n[i];
+	}
+	vf[3] = e;
+}
+
 /// one patch of the fused residual: uniform (scalar) metadata
 struct FzPatch { int p, s0, s1, c0, c1, nc, e0, nl, ng; const uint2* gnbr; const int* gbf; };
 /// what one thread loads for its patch before phase 0: its first staged row (state, centre), the
@@ -1283,16 +1352,16 @@ __device__ __forceinline__ void fz_body(const DevMesh& M, const DevPhys& P, cons
 			sri = (fabs(vni)+ci)*flen;
 			srj = (fabs(vnj)+cj)*flen;
 			if(VISC != SV_NONE) {
-				const double mui = VISC == SV_CONST ? 1.0/G.Reinf : sutherland(G, ul);
-				const double muj = VISC == SV_CONST ? 1.0/G.Reinf : sutherland(G, ur);
+				const double mui = VISC == SV_CONST ? G.rReinf : sutherland(G, ul);
+				const double muj = VISC == SV_CONST ? G.rReinf : sutherland(G, ur);
 				const double ai = div_rn(4.0, 3*ul[0]), bi = div_rn(G.g, ul[0]);
 				const double aj = div_rn(4.0, 3*ur[0]), bj = div_rn(G.g, ur[0]);
 				const double coi = (ai < bi) ? bi : ai;          // std::max
 				const double coj = (aj < bj) ? bj : aj;
 				// a ghost cell's spectral radius is never summed (and its area is not stored)
 				const int2 g = M.slot_LR[s];
-				if(g.x < M.nown) sri += div_rn(div_rn(coi*mui, G.Pr) * flen*flen, M.area[g.x]);
-				if(!bnd && g.y < M.nown) srj += div_rn(div_rn(coj*muj, G.Pr) * flen*flen, M.area[g.y]);
+				if(g.x < M.nown) sri += div_rn(div_rcp(coi*mui, G.Pr, G.rPr) * flen*flen, M.area[g.x]);
+				if(!bnd && g.y < M.nown) srj += div_rn(div_rcp(coj*muj, G.Pr, G.rPr) * flen*flen, M.area[g.y]);
 			}
 		}
 		if(VISC != SV_NONE) {
@@ -1304,28 +1373,19 @@ __device__ __forceinline__ void fz_body(const DevMesh& M, const DevPhys& P, cons
 			// the reconstruction's copies kept live through the inviscid flux -- 4 waves per SIMD
 			double muRe, va[2];
 			viscous_face_terms<VISC == SV_CONST>(G, ul, ur, muRe, va);
-#if FVHIP_FZ_VISC_FENCE
-			__asm__ volatile("" ::: "memory");
-#endif
-			double pl[4], gl[8], pr[4], grr[8];
-			ld4(rowi, 0, pl);
-			ld8(rowi + 4, 0, gl);
+			double gpr[4] = {0, 0, 0, 0};
+			const double* rowj = nullptr;
 			double2 rr;
 			if(bnd) {
 				const double4 g4 = ghost_prim_of_cell(M, P, B.u, bcell, bf);
-				pr[0] = g4.x; pr[1] = g4.y; pr[2] = g4.z; pr[3] = g4.w;
-				#pragma unroll
-				for(int k = 0; k < 8; k++) grr[k] = gl[k];
+				gpr[0] = g4.x; gpr[1] = g4.y; gpr[2] = g4.z; gpr[3] = g4.w;
 				rr = M.bf_rcbp[bf];
 			} else {
-				const double* rowj = &fz[lrl.y*FZW];
-				ld4(rowj, 0, pr);
-				ld8(rowj + 4, 0, grr);
+				rowj = &fz[lrl.y*FZW];
 				rr = *reinterpret_cast<const double2*>(rowj + 12);
 			}
-			const double rcl[2] = {ri.x, ri.y}, rcr[2] = {rr.x, rr.y};
 			double vf[4];
-			viscous_flux_core<true>(G, n, rcl, rcr, pl, pr, gl, grr, muRe, va, vf);
+			fz_viscous(G, rowi, rowj, gpr, ri, rr, n, muRe, va, vf);
 			#pragma unroll
 			for(int k = 0; k < 4; k++) f[k] += vf[k]*flen;
 		}
@@ -1385,7 +1445,7 @@ __device__ __forceinline__ void fz_body(const DevMesh& M, const DevPhys& P, cons
 #define FVHIP_FUSED_WAVES_LIM 4      // Barth-Jespersen / Venkatakrishnan: 124-126 VGPRs
 #endif
 #ifndef FVHIP_FUSED_WAVES_VISC
-#define FVHIP_FUSED_WAVES_VISC 3     // viscous: 144-156 VGPRs (at 4 waves 20-48 spilled)
+#define FVHIP_FUSED_WAVES_VISC 4     // viscous: 110-122 VGPRs (fz_viscous streams the LDS rows; 144-156 before)
 #endif
 
 template <int FLUX, int REC, bool DT, int VISC, int LIM>

@@ -42,8 +42,7 @@ FVHIP_HD double relaxation_factor(const gd::Gas& G, double minfactor, const doub
 	return omega;
 }
 
-/// dinv[c] = diag[c]^-1 (Gauss-Jordan with row pivoting), c < ncell
-/// lines of the line-implicit preconditioner (internal cell ids): cells cell[start[l]..start[l+1]) in
+/// Lines of the line-implicit preconditioner (internal cell ids): cells cell[start[l]..start[l+1]) in
 /// line order; face[k] (k > start[l]) = interior face between cells k-1 and k, fi<<1 | (cell k-1 is R)
 /// lines sorted by length, longest first; lines [0, nlong) have at least LINE_WAVE_MIN cells and take
 /// the wave-per-line kernels, the short rest (most of them single cells) the thread-per-line ones
@@ -61,6 +60,7 @@ void launch_line_solve(const LineSet& Ls, const double* dinvp, const double* low
                        double* z, hipStream_t s);
 /// z += e over n cells
 void launch_add_rows(int n, const double* e, double* z, hipStream_t s);
+/// dinv[c] = diag[c]^-1 (Gauss-Jordan with row pivoting), c < ncell
 void launch_bjac_invert(int ncell, const double* diag, double* dinv, hipStream_t s);
 /// y[c] = dinv[c] x[c]
 void launch_bjac_apply(int ncell, const double* dinv, const double* x, double* y, hipStream_t s);

@@ -187,6 +187,12 @@ int fvhip_compute_residual(fvhip_handle h, const double* u, double* r, int getti
  *  the sweep of the patches whose inputs are ready on a second stream (single domain, WLS +
  *  MUSCL/unlimited linear, viscous too); same results. Opt-in: slower than the serial path on C4 */
 #define FVHIP_RES_PIPELINED 4
+/** flags: FVHIP_RES_HALO_READY = partitioned handle (two-layer halo, fused single-exchange
+ *  configurations): the caller has already filled the ghost rows of d_u (both layers), as the
+ *  reference's drivers do with VecGhostUpdate before compute_residual (aodesolver.cpp:514/558); no
+ *  exchange runs, the layer-1 ghosts' gradients are computed and every patch is swept on the handle's
+ *  stream. For a rank's compute time alone (tools/scale_proxy.py) and callers that own the exchange. */
+#define FVHIP_RES_HALO_READY 8
 int fvhip_compute_residual_device(fvhip_handle h, const double* d_u, double* d_r, int gettimesteps,
                                   double* d_dtm, int flags);
 /** FlowFV_base::getGradients: conserved-variable gradients, GradBlock layout [nelem][4 vars][2 dims] */

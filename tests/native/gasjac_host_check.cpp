@@ -30,7 +30,7 @@ static bool same(const double* a, const double* b, int n) { return std::memcmp(a
 int main(int argc, char** argv) {
 	const int ncase = argc > 1 ? std::atoi(argv[1]) : 20000;
 	const double gas[5] = {1.4, 0.8, 288.15, 5000.0, 0.72};
-	const Gas G{gas[0], gas[1], gas[2], gas[3], gas[4], 110.5};
+	const Gas G = make_gas(gas[0], gas[1], gas[2], gas[3], gas[4]);
 	std::mt19937_64 rng(7);
 	std::uniform_real_distribution<double> U(-1.0, 1.0);
 	int bad = 0;

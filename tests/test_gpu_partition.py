@@ -102,6 +102,22 @@ def test_partitioned_c2_eight_ranks_venkatakrishnan(partitioner):
         assert s["interior_patches"] >= 0.7 * s["patches"], s
 
 
+@pytest.mark.parametrize("rec", ["VANALBADA", "VENKATAKRISHNAN"])
+def test_partitioned_c4_eight_ranks(rec):
+    """BASELINE config 4 at its full size on the partitioned path the driver's 8-GPU run takes: the
+    4,063,232-cell C4 mesh split 8 ways by the graph partitioner, all ranks in one process (device
+    copies for RCCL), overlapped schedule (interior patches, one exchange of the two-layer halo, border
+    patches on the comm stream) -- every owned row's residual and time step bitwise the single-GPU ones,
+    for the headline numerics and config 4's Venkatakrishnan"""
+    r, dt, r1, dt1, stats = run_partitioned("naca_c4", "naca", "ROE", "LEASTSQUARES", rec, True, 8, partitioner="graph")
+    np.testing.assert_array_equal(r, r1)
+    np.testing.assert_array_equal(dt, dt1)
+    for s in stats:
+        assert 0 < s["interior_patches"] < s["patches"]
+    print("per-rank cells", [s["cells"] for s in stats], "ghosts", [s["ghosts"] for s in stats],
+          "interior patch fraction", [round(s["interior_patches"] / s["patches"], 3) for s in stats])
+
+
 def test_partitioned_fast_math_within_tolerance():
     # fast kernels contract FMAs per inlining context (a neighbour converted from LDS or from
     # global memory), so partitioned and single-GPU fast results agree to the fast-mode tolerance
@@ -155,3 +171,37 @@ def test_overlapped_group_repeated_residuals(nparts):
     for r, dt, r1, dt1 in results:
         np.testing.assert_array_equal(r, r1)
         np.testing.assert_array_equal(dt, dt1)
+
+
+def test_halo_ready_residual_bitwise():
+    """FVHIP_RES_HALO_READY (the caller keeps the ghost rows current, as the reference's drivers do with
+    VecGhostUpdate): after one group residual has filled every rank's ghost rows, each rank's residual
+    with no exchange is bitwise the group's"""
+    import torch
+    m, _ = get_mesh("naca_c2")
+    p = cases.physics("naca")
+    n = cases.numerics("ROE", "LEASTSQUARES", "VENKATAKRISHNAN")
+    u = cases.state(m, p, seed=5)
+    part = fa.partition_graph(m, 4)
+    sps = [fa.FlowFV(m, p, n, partition=part, rank=k) for k in range(4)]
+    dus, drs, dts = [], [], []
+    for k, sp in enumerate(sps):
+        g = np.nonzero(part == k)[0][sp.permutation()]
+        x = torch.full((sp.nown + sp.nghost, 4), float("nan"), dtype=torch.float64, device="cuda")
+        x[:sp.nown] = torch.tensor(u[g], device="cuda")
+        dus.append(x)
+        drs.append(torch.zeros((sp.nown, 4), dtype=torch.float64, device="cuda"))
+        dts.append(torch.zeros(sp.nown, dtype=torch.float64, device="cuda"))
+    grp = fa.FlowFVGroup(sps)
+    grp.compute_residual_device([x.data_ptr() for x in dus], [x.data_ptr() for x in drs],
+                                [x.data_ptr() for x in dts], True, True)
+    torch.cuda.synchronize()
+    for k, sp in enumerate(sps):
+        r2 = torch.zeros_like(drs[k])
+        t2 = torch.zeros_like(dts[k])
+        sp.compute_residual_device(dus[k].data_ptr(), r2.data_ptr(), t2.data_ptr(), True, True, halo_ready=True)
+        sp.synchronize()
+        assert torch.equal(r2, drs[k]) and torch.equal(t2, dts[k]), k
+    grp.close()
+    for sp in sps:
+        sp.close()

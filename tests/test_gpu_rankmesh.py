@@ -117,6 +117,7 @@ def test_trace_exchange_known_answer(meshname, nranks):
     d = fa.UMesh.partition_trivial(gm.nelem, nranks)
     lms = [gm.restrict(d, r) for r in range(nranks)]
     p = cases.physics("cyl")
+    p.bcconf = [fa.FlowBCConfig("farfield", int(t)) for t in np.unique(gm.btags[:, 0])]   # the markers it has
     n = cases.numerics("HLLC", "LEASTSQUARES", "NONE")
     sps = [fa.FlowFV(lm, p, n) for lm in lms]
     for r, sp in enumerate(sps):

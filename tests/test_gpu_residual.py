@@ -29,6 +29,8 @@ def get_mesh(key):
         elif key == "naca_c2":
             m = fa.UMesh.naca_ogrid(512, 64, 192)          # C2 of SURVEY.md 8d: 229,376 cells
             om = orc.OracleMesh.from_raw(m.raw())
+        elif key == "naca_c4":                               # the bench's C4 mesh (no oracle mesh)
+            m, om = fa.UMesh.naca_ogrid(2048, 256, 864, 20.0, 1e-5, farmap=1), None
         elif key == "plate_small":
             m = fa.UMesh.flat_plate(48, 32)
             om = orc.OracleMesh.from_raw(m.raw())

@@ -18,7 +18,8 @@ the reference's viscous functional regression.
     0.7 % in CL (3.154e-5 .. 3.177e-5, near zero at zero incidence): the answer at the deck's 1e-6
     residual drop depends on the solver path at that level, so 1e-8 is not a property of the
     discretisation. Bars here: CDp and CDsf within 1e-6 relative of regr-LeastSquares_Roe.txt, CL
-    within 2 % of it (the reference's own files span 0.7 %). Preconditioner: line-implicit (block-
+    within 1e-3 of it (the reference's own files span 0.7 %; measured 2.3e-4 matrix-free, 3.2e-4
+    assembled). Preconditioner: line-implicit (block-
     tridiagonal along the wall-normal lines) with 3 sweeps, GMRES(60) rtol 1e-1. Measured on MI355X
     (tools/experiments/visc_probe.py): assembled, 93 steps to the deck's 1e-6 drop, CDp 6.5e-8 / CDsf 4.0e-8 /
     CL 3.2e-4 relative to the file; the matrix-free Newton path reaches 1e-6 in 30 steps but there
@@ -122,7 +123,7 @@ def test_visc_naca0012_functional_regression(matrix_free):
     CL, CDP, CDSF = REGR
     assert abs(cdp - CDP) / abs(CDP) <= 1e-6
     assert abs(cdsf - CDSF) / abs(CDSF) <= 1e-6
-    assert abs(cl - CL) / abs(CL) <= 2e-2
+    assert abs(cl - CL) / abs(CL) <= 1e-3
     start.close()
     main.close()
 
@@ -160,7 +161,11 @@ def test_flatplate_cdsf_convergence(tmp_path):
     robust_flow update, minimum factor 0.2; Jacobian 'consistent' = Roe). Bar (flow_clcd_conv.cpp:
     103-146): the skin-friction drag error against exact_clcd_flatplate.dat's CDsf = 1.423765e-3 falls
     with slope in [0.95, 1.5] between the two finest meshes, h = 1/sqrt(nelem) (casesolvers.cpp:96).
-    The reference preconditions with ILU(0) (flatplate.solverc); here line-implicit, GMRES(30), rtol 1e-1."""
+    The reference preconditions with ILU(0) (flatplate.solverc); here line-implicit, GMRES(30), rtol 1e-1.
+    The first-order starter ends after one step, as the reference's loop does (aodesolver.cpp:419-528):
+    the free stream's energy residual is exactly zero on these meshes (the adiabatic plate's fluxes
+    carry no energy at first order), so its ratio to the first residual is 0/0; the main solve starts
+    from that state. Measured on MI355X: CDsf 1.1664e-3 / 1.3195e-3 / 1.3779e-3, slopes 1.30 / 1.19."""
     import torch
     from flatplate_meshes import write_flatplate_msh
     exact = [float(x) for x in open(os.path.join(os.path.dirname(cases.MESHDIR), "exact_clcd_flatplate.dat"))
