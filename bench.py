@@ -409,12 +409,12 @@ def main():
         k = max(km, key=km.get)
         return k, km[k]
 
-    # the secondary paths run first: by the time the primary (library default) path is timed the
-    # GPU has been busy for seconds and its clocks have settled (kernel times fall ~15 % over the
-    # first ~100 ms of a cold run)
+    # every path is timed after the same wall-clock pre-heat (--preheat-ms, reported): kernel times
+    # fall ~12 % over the first few hundred ms of a cold GPU, and handle set-up between the paths
+    # leaves it idle for ~1 s; the primary (library default) path is timed last
     fast = None
     if not args.no_fast:
-        fms, fk, stats = measure(True)
+        fms, fk, stats = measure(True, preheat_ms=args.preheat_ms)
         cnt = (stats["cells"], stats["faces"], stats["bfaces"])
         fname, fsms = dominant(fk)
         fab = kernel_bytes(fname, *cnt, args.numerics) / (fsms * 1e-3) / 1e9
@@ -427,7 +427,7 @@ def main():
                              "(tests/test_gpu_residual.py::test_fast_math_within_tolerance)"}
     # the two-kernel path (WLS gradient kernel + face sweep), same results bit for bit: one after
     # the other, and pipelined (gradient chunks overlapped with the sweep groups on a second stream)
-    sms, sk, stats = measure(False, "staged")
+    sms, sk, stats = measure(False, "staged", preheat_ms=args.preheat_ms)
     # this rank's algorithmic bytes (its owned cells, its faces incl. both copies of cut faces)
     cnt = (stats["cells"], stats["faces"], stats["bfaces"])
     sname, ssweep = [(k, v) for k, v in sk.items() if k.startswith("k_sweep")][0]
@@ -437,7 +437,7 @@ def main():
               "sweep_algorithmic_bytes": sweep_algorithmic_bytes(*cnt)}
     pipelined = None
     if world == 1 and not args.no_pipelined:
-        pms, pk, _ = measure(False, "pipelined")
+        pms, pk, _ = measure(False, "pipelined", preheat_ms=args.preheat_ms)
         pipelined = {"ms_per_step": round(pms, 5), "value": round(F / (pms * 1e-3) / 1e6, 3),
                      "kernels_ms_summed_over_chunks": {k: round(v, 5) for k, v in pk.items()},
                      "hbm_GBs_both_kernels": round((sweep_algorithmic_bytes(*cnt) + prep_algorithmic_bytes(*cnt))
