@@ -150,7 +150,12 @@ def test_entropy_convergence_four_rank_meshes():
     must match the single-rank one to 1e-4 relative and the finest slope lies in [1.65, 2.1]."""
     import torch
     from test_gpu_convergence import CASES, solve_entropy
-    grad, flux, implicit, init, main, nmesh, drop, prec = CASES["ls_hllc_implicit"]
+    grad, flux, implicit, init, main, nmesh, drop, _ = CASES["ls_hllc_implicit"]
+    # point-block Jacobi on every rank: the single-rank case's multicolour Gauss-Seidel becomes
+    # block-Jacobi across the ranks (as PETSc's bjacobi does) and, on 2dcylinder0, that weaker
+    # preconditioner lets the CFL-5000 main solve diverge; with point-block Jacobi the 4-rank and the
+    # 1-rank solves run the same preconditioner and their histories agree to rounding
+    prec = dict(prec_sweeps=1, lin_rtol=1e-2)
     nranks = 4
     lh, le = [], []
     for i in range(nmesh):

@@ -15,10 +15,11 @@ step() {  # name timeout cmd...
 }
 for s in "$@"; do
   case $s in
-    smoke) step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
-    tests) step pytest_gpu 1200 python -m pytest tests -m gpu -q -rf ;;
-    jtests) step pytest_jac 900 python -m pytest tests/test_gpu_jacobian.py -m gpu -q -rf -x ;;
-    bench) step bench 600 python bench.py ;;
+    smoke) step smoke 300 python -u -c "import __graft_entry__ as g; g.smoke()" ;;
+    tests) step pytest_gpu 1100 python -u -m pytest tests -m gpu -q -rf --timeout 300 --timeout-method thread ;;
+    jtests) step pytest_jac 900 python -u -m pytest tests/test_gpu_jacobian.py -m gpu -q -rf -x ;;
+    bench) step bench 600 python -u bench.py ;;
+    benchd) step bench_driver 600 python -u bench.py --steps 20 --warmup 5 ;;
     benchq) step bench 600 python bench.py --steps 20 --warmup 3 ;;
     prof) step rocprof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python3 bench.py --steps 20 --warmup 3 --no-cpu-baseline ;;
   esac
