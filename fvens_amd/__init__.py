@@ -388,6 +388,23 @@ class FlowFV:
                                                    float(rtol), int(maxit), int(restart), int(sweeps), iptr(it), dptr(rn)))
         return int(it[0]), float(rn[0])
 
+    def line_precondition_device(self, d_diag, d_lower, d_upper, d_v, d_z, line_threshold=0.0):
+        """z = M^-1 v, M the block-tridiagonal line part of the block operator (prec_lines)"""
+        check(_ffi.lib().fvhip_line_precondition_device(self._h, *[ctypes.c_void_p(p) for p in (d_diag, d_lower, d_upper)],
+                                                        float(line_threshold), ctypes.c_void_p(d_v), ctypes.c_void_p(d_z)))
+
+    def lines(self, line_threshold=0.0):
+        """the preconditioner's lines: list of (cells, faces) in line order, internal cell ids; faces[k] =
+        interior face fi << 1 | (cells[k-1] is its R) linking cells[k-1] and cells[k] (-1 at k = 0)"""
+        nl = np.zeros(1, np.int32)
+        check(_ffi.lib().fvhip_lines(self._h, float(line_threshold), iptr(nl), None, None, None))
+        n = self.nown
+        st = np.zeros(int(nl[0]) + 1, np.int32)
+        cells = np.zeros(n, np.int32)
+        faces = np.zeros(n, np.int32)
+        check(_ffi.lib().fvhip_lines(self._h, float(line_threshold), iptr(nl), iptr(st), iptr(cells), iptr(faces)))
+        return [(cells[st[i]:st[i+1]], faces[st[i]:st[i+1]]) for i in range(int(nl[0]))]
+
     def matfree_set_state_device(self, d_u, d_r, d_mdt):
         check(_ffi.lib().fvhip_matfree_set_state_device(self._h, *[ctypes.c_void_p(p) for p in (d_u, d_r, d_mdt)]))
 

@@ -110,6 +110,9 @@ _SIGS = {
                                                                 ctypes.POINTER(FvSolveStats), c_dbl_p]),
     "fvhip_gmres_blocks_device": (ctypes.c_int, [ctypes.c_void_p] + [ctypes.c_void_p] * 5 +
                                   [ctypes.c_double, ctypes.c_int, ctypes.c_int, ctypes.c_int, c_int_p, c_dbl_p]),
+    "fvhip_line_precondition_device": (ctypes.c_int, [ctypes.c_void_p] + [ctypes.c_void_p] * 3 +
+                                       [ctypes.c_double, ctypes.c_void_p, ctypes.c_void_p]),
+    "fvhip_lines": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_double, c_int_p, c_int_p, c_int_p, c_int_p]),
     "fvhip_group_matfree_set_state_device": (ctypes.c_int, [ctypes.c_void_p, _vpp, _vpp, _vpp]),
     "fvhip_group_matfree_apply_device": (ctypes.c_int, [ctypes.c_void_p, _vpp, _vpp]),
     "fvhip_matfree_set_state": (ctypes.c_int, [ctypes.c_void_p, c_dbl_p, c_dbl_p, c_dbl_p]),

@@ -728,14 +728,16 @@ struct fvhip_ctx
 	/// so that a wave's threads walk lines of similar length.
 	LineSet lines{};
 	double lines_thr = -1.0;
-	std::vector<int> h_line_start;
+	std::vector<int> h_line_start, h_line_cells, h_line_faces;   ///< the lines in line order (fvhip_lines)
 	void ensureLines(double thr) {
 		if(!(thr >= 0.0) || !std::isfinite(thr)) throw std::invalid_argument("line_threshold must be finite and >= 0 (0: 4)");
 		if(thr == 0.0) thr = 4.0;
-		if(lines.start && lines_thr == thr) return;
+		if(lines.gstart && lines_thr == thr) return;
 		// a rebuild (another threshold) releases the previous line set's device arrays
-		for(const void* p : {static_cast<const void*>(lines.start), static_cast<const void*>(lines.cell),
-		                     static_cast<const void*>(lines.face)}) release(p);
+		for(const void* p : {static_cast<const void*>(lines.gstart), static_cast<const void*>(lines.cell),
+		                     static_cast<const void*>(lines.face), static_cast<const void*>(lines.D),
+		                     static_cast<const void*>(lines.Lb), static_cast<const void*>(lines.W),
+		                     static_cast<const void*>(lines.G)}) release(p);
 		lines = LineSet{};
 		const int N = L.ncell, nb = L.nbface;
 		struct Nb { int c, fi; double w; };
@@ -804,23 +806,42 @@ struct fvhip_ctx
 		}
 		std::stable_sort(all.begin(), all.end(), [](const std::vector<std::pair<int,int>>& a,
 		                                            const std::vector<std::pair<int,int>>& b) { return a.size() > b.size(); });
-		std::vector<int> st(1, 0), cells, faces;
-		for(const auto& ln : all) {
+		// groups of 64 lines (a wave's lanes), rows line-interleaved (krylov.hpp LineSet)
+		const int nl = static_cast<int>(all.size()), ng = (nl + 63)/64;
+		std::vector<int> gst(static_cast<size_t>(ng) + 1, 0);
+		for(int g = 0; g < ng; g++) gst[g+1] = gst[g] + static_cast<int>(all[64*static_cast<size_t>(g)].size());
+		const size_t nslot = 64*static_cast<size_t>(gst[ng]);
+		std::vector<int> cells(std::max<size_t>(nslot, 1), -1), faces(std::max<size_t>(nslot, 1), -1);
+		h_line_start.assign(1, 0);
+		h_line_cells.clear(); h_line_faces.clear();
+		for(int l = 0; l < nl; l++) {
+			const auto& ln = all[l];
+			const size_t g = static_cast<size_t>(l/64), lane = static_cast<size_t>(l%64);
 			for(size_t k = 0; k < ln.size(); k++) {
-				cells.push_back(ln[k].first);
-				if(k == 0) { faces.push_back(-1); continue; }
-				const int fi = ln[k].second, p = ln[k-1].first;
-				faces.push_back((fi << 1) | (L.if_L[fi] == p ? 0 : 1));
+				const size_t slot = (static_cast<size_t>(gst[g]) + k)*64 + lane;
+				cells[slot] = ln[k].first;
+				int code = -1;
+				if(k > 0) {
+					const int fi = ln[k].second, p = ln[k-1].first;
+					code = (fi << 1) | (L.if_L[fi] == p ? 0 : 1);
+				}
+				faces[slot] = code;
+				h_line_cells.push_back(ln[k].first);
+				h_line_faces.push_back(code);
 			}
-			st.push_back(static_cast<int>(cells.size()));
+			h_line_start.push_back(static_cast<int>(h_line_cells.size()));
 		}
-		lines.nlines = static_cast<int>(all.size());
-		lines.nlong = 0;
-		while(lines.nlong < lines.nlines && static_cast<int>(all[lines.nlong].size()) >= LINE_WAVE_MIN) lines.nlong++;
-		lines.start = upload(st, owned);
+		lines.nlines = nl;
+		lines.ngroups = ng;
+		lines.nrows = gst[ng];
+		lines.gstart = upload(gst, owned);
 		lines.cell = upload(cells, owned);
 		lines.face = upload(faces, owned);
-		h_line_start = st;
+		const size_t rows = std::max<size_t>(static_cast<size_t>(gst[ng]), 1);
+		lines.D = dalloc(1024*rows, owned);
+		lines.Lb = dalloc(1024*rows, owned);
+		lines.W = dalloc(1024*rows, owned);
+		lines.G = dalloc(256*rows, owned);
 		lines_thr = thr;
 	}
 

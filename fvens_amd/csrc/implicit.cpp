@@ -166,13 +166,13 @@ struct LinOp
 		const ArrayOf aux = [&](size_t i) { return S.hs[i]->iw.aux; };
 		const ArrayOf t = [&](size_t i) { return S.hs[i]->iw.t; };
 		S.each([&](size_t i, fvhip_ctx* h) {
-			h->timed("k_line_solve", [&]{ launch_line_solve(h->lines, h->iw.dinv, Lo[i], Up[i], v(i), z(i), h->stream); });
+			h->timed("k_line_solve", [&]{ launch_line_solve(h->lines, v(i), z(i), h->stream); });
 		});
 		for(int k = 1; k < sweeps; k++) {
 			blocks(z, t);
 			S.each([&](size_t i, fvhip_ctx* h) {
 				launch_axpby(4LL*h->L.ncell, 1.0, v(i), -1.0, t(i), h->stream);
-				h->timed("k_line_solve", [&]{ launch_line_solve(h->lines, h->iw.dinv, Lo[i], Up[i], t(i), aux(i), h->stream); });
+				h->timed("k_line_solve", [&]{ launch_line_solve(h->lines, t(i), aux(i), h->stream); });
 				launch_add_rows(h->L.ncell, aux(i), z(i), h->stream);
 			});
 		}
@@ -182,7 +182,7 @@ struct LinOp
 		S.each([&](size_t i, fvhip_ctx* h) {
 			if(lines) {
 				h->ensureLines(line_thr);
-				h->timed("k_line_factor", [&]{ launch_line_factor(h->lines, D[i], Lo[i], Up[i], h->iw.dinv, h->stream); });
+				h->timed("k_line_factor", [&]{ launch_line_factor(h->lines, D[i], Lo[i], Up[i], h->stream); });
 				return;
 			}
 			h->timed("k_bjac_invert", [&]{ launch_bjac_invert(h->L.ncell, D[i], h->iw.dinv, h->stream); });
@@ -501,6 +501,32 @@ int fvhip_gmres_blocks_device(fvhip_handle h, const double* d_diag, const double
 		S.sync();
 		if(iters) *iters = g.iters;
 		if(resnorm) *resnorm = g.rnorm;
+	});
+}
+
+int fvhip_line_precondition_device(fvhip_handle h, const double* d_diag, const double* d_lower, const double* d_upper,
+                                   double line_threshold, const double* d_v, double* d_z)
+{
+	return guard([&] {
+		if(!d_diag || !d_v || !d_z || (h->L.ninface > 0 && (!d_lower || !d_upper))) throw std::invalid_argument("null argument");
+		HC(hipSetDevice(h->device));
+		h->ensureLines(line_threshold);
+		launch_line_factor(h->lines, d_diag, d_lower, d_upper, h->stream);
+		launch_line_solve(h->lines, d_v, d_z, h->stream);
+		HC(hipGetLastError());
+		HC(hipStreamSynchronize(h->stream));
+	});
+}
+
+int fvhip_lines(fvhip_handle h, double line_threshold, int* nlines, int* start, int* cells, int* faces)
+{
+	return guard([&] {
+		HC(hipSetDevice(h->device));
+		h->ensureLines(line_threshold);
+		if(nlines) *nlines = h->lines.nlines;
+		if(start) std::copy(h->h_line_start.begin(), h->h_line_start.end(), start);
+		if(cells) std::copy(h->h_line_cells.begin(), h->h_line_cells.end(), cells);
+		if(faces) std::copy(h->h_line_faces.begin(), h->h_line_faces.end(), faces);
 	});
 }
 

@@ -264,211 +264,153 @@ __device__ __forceinline__ const double* blk_pc(int fc, const double* lower, con
 	return ((fc & 1) ? lower : upper) + 16*static_cast<size_t>(fc >> 1);
 }
 
-/// block-Thomas factorisation per line (one thread per line): dinvp_k = (D_k - A[k][k-1] dinvp_{k-1} A[k-1][k])^-1
-__global__ __launch_bounds__(64)
-void k_line_factor(int nlines, const int* __restrict__ lstart, const int* __restrict__ lcell, const int* __restrict__ lface,
-                   const double* __restrict__ diag, const double* __restrict__ lower, const double* __restrict__ upper,
-                   double* __restrict__ dinvp, int first)
+/// row r of a line-interleaved 4x4 block array: element e of lane j at X[(16 r + e)*64 + j]
+__device__ __forceinline__ void ldI16(const double* __restrict__ X, long long r, int j, double (&a)[4][4])
 {
-	const int l = first + static_cast<int>(blockIdx.x*blockDim.x + threadIdx.x);
-	if(l >= nlines) return;
-	const int k0 = lstart[l], k1 = lstart[l+1];
-	double prev[4][4];             // dinvp of the previous line cell
-	for(int k = k0; k < k1; k++) {
-		const int c = lcell[k];
-		double a[4][4], b[4][4];
-		ld16(diag + 16*static_cast<size_t>(c), a);
-		if(k > k0) {
-			const int fc = lface[k];
-			double L[4][4], U[4][4], t[4][4];
-			ld16(blk_cp(fc, lower, upper), L);
-			ld16(blk_pc(fc, lower, upper), U);
-			// t = prev * U ; a -= L * t
-			#pragma unroll
-			for(int i = 0; i < 4; i++)
-				#pragma unroll
-				for(int j = 0; j < 4; j++) t[i][j] = prev[i][0]*U[0][j] + prev[i][1]*U[1][j] + prev[i][2]*U[2][j] + prev[i][3]*U[3][j];
-			#pragma unroll
-			for(int i = 0; i < 4; i++)
-				#pragma unroll
-				for(int j = 0; j < 4; j++) a[i][j] -= L[i][0]*t[0][j] + L[i][1]*t[1][j] + L[i][2]*t[2][j] + L[i][3]*t[3][j];
+	const double* p = X + 1024*r + j;
+	#pragma unroll
+	for(int i = 0; i < 4; i++)
+		#pragma unroll
+		for(int q = 0; q < 4; q++) a[i][q] = p[64*(4*i+q)];
+}
+__device__ __forceinline__ void stI16(double* __restrict__ X, long long r, int j, const double (&a)[4][4])
+{
+	double* p = X + 1024*r + j;
+	#pragma unroll
+	for(int i = 0; i < 4; i++)
+		#pragma unroll
+		for(int q = 0; q < 4; q++) p[64*(4*i+q)] = a[i][q];
+}
+
+/// block-Thomas factorisation, lane j of workgroup g on line 64g + j (LineSet): per line cell k
+///   W_{k-1} = dinvp_{k-1} A[k-1][k],  dinvp_k = (D_k - A[k][k-1] W_{k-1})^-1
+/// and D, Lb, W stored line-interleaved for the solve. The next cell's blocks are requested before the
+/// current cell's arithmetic (their addresses do not depend on it) and the cell/face codes two cells
+/// ahead, so the recurrence does not wait a memory round trip per cell.
+__global__ __launch_bounds__(64)
+void k_line_factor(const int* __restrict__ gstart, const int* __restrict__ lcell, const int* __restrict__ lface,
+                   const double* __restrict__ diag, const double* __restrict__ lower, const double* __restrict__ upper,
+                   double* __restrict__ D, double* __restrict__ Lb, double* __restrict__ W)
+{
+	const int g = blockIdx.x, j = threadIdx.x;
+	const long long r0 = gstart[g];
+	const int len = gstart[g+1] - static_cast<int>(r0);
+	int c = lcell[64*r0 + j];
+	int c1 = len > 1 ? lcell[64*(r0+1) + j] : -1, f1 = len > 1 ? lface[64*(r0+1) + j] : -1;
+	double a[4][4], Lk[4][4], Uk[4][4], prev[4][4];
+	if(c < 0) return;
+	ld16(diag + 16*static_cast<size_t>(c), a);
+	for(int k = 0; k < len; k++) {
+		// requests for cell k+1 (blocks) and k+2 (codes)
+		const int cn = c1, fn = f1;
+		c1 = -1; f1 = -1;
+		if(cn >= 0 && k + 2 < len) { c1 = lcell[64*(r0+k+2) + j]; f1 = lface[64*(r0+k+2) + j]; }
+		double an[4][4], Ln[4][4], Un[4][4];
+		if(cn >= 0) {
+			ld16(diag + 16*static_cast<size_t>(cn), an);
+			ld16(blk_cp(fn, lower, upper), Ln);
+			ld16(blk_pc(fn, lower, upper), Un);
 		}
-		inv4(a, b);
-		st16(dinvp + 16*static_cast<size_t>(c), b);
+		if(k > 0) {
+			double t[4][4];
+			#pragma unroll
+			for(int r = 0; r < 4; r++)
+				#pragma unroll
+				for(int q = 0; q < 4; q++) t[r][q] = prev[r][0]*Uk[0][q] + prev[r][1]*Uk[1][q] + prev[r][2]*Uk[2][q] + prev[r][3]*Uk[3][q];
+			stI16(W, r0 + k - 1, j, t);
+			stI16(Lb, r0 + k, j, Lk);
+			#pragma unroll
+			for(int r = 0; r < 4; r++)
+				#pragma unroll
+				for(int q = 0; q < 4; q++) a[r][q] -= Lk[r][0]*t[0][q] + Lk[r][1]*t[1][q] + Lk[r][2]*t[2][q] + Lk[r][3]*t[3][q];
+		}
+		inv4(a, prev);
+		stI16(D, r0 + k, j, prev);
+		if(cn < 0) break;
+		#pragma unroll
+		for(int r = 0; r < 4; r++)
+			#pragma unroll
+			for(int q = 0; q < 4; q++) { a[r][q] = an[r][q]; Lk[r][q] = Ln[r][q]; Uk[r][q] = Un[r][q]; }
+	}
+}
+
+/// z = (block-tridiagonal line part)^-1 v, lanes as in k_line_factor: forward g_k = dinvp_k (v_k -
+/// A[k][k-1] g_{k-1}) into the interleaved scratch G, backward z_k = g_k - W_k z_{k+1}; the next
+/// cell's rows (and its v row) are requested before the current cell's arithmetic
+__global__ __launch_bounds__(64)
+void k_line_solve(const int* __restrict__ gstart, const int* __restrict__ lcell, const double* __restrict__ D,
+                  const double* __restrict__ Lb, const double* __restrict__ W, double* __restrict__ G,
+                  const double* __restrict__ v, double* __restrict__ z)
+{
+	const int g = blockIdx.x, j = threadIdx.x;
+	const long long r0 = gstart[g];
+	const int len = gstart[g+1] - static_cast<int>(r0);
+	int c = lcell[64*r0 + j];
+	if(c < 0) return;
+	double Dk[4][4], Lk[4][4];
+	double4 vk = reinterpret_cast<const double4*>(v)[c];
+	ldI16(D, r0, j, Dk);
+	double4 gp = make_double4(0, 0, 0, 0);
+	int kl = 0;
+	for(int k = 0; ; k++) {
+		const int cn = k + 1 < len ? lcell[64*(r0+k+1) + j] : -1;
+		double Dn[4][4], Ln[4][4];
+		double4 vn = make_double4(0, 0, 0, 0);
+		if(cn >= 0) {
+			vn = reinterpret_cast<const double4*>(v)[cn];
+			ldI16(D, r0 + k + 1, j, Dn);
+			ldI16(Lb, r0 + k + 1, j, Ln);
+		}
+		double r[4] = {vk.x, vk.y, vk.z, vk.w};
+		if(k > 0) {
+			#pragma unroll
+			for(int i = 0; i < 4; i++) r[i] -= Lk[i][0]*gp.x + Lk[i][1]*gp.y + Lk[i][2]*gp.z + Lk[i][3]*gp.w;
+		}
+		double y[4];
+		#pragma unroll
+		for(int i = 0; i < 4; i++) y[i] = Dk[i][0]*r[0] + Dk[i][1]*r[1] + Dk[i][2]*r[2] + Dk[i][3]*r[3];
+		gp = make_double4(y[0], y[1], y[2], y[3]);
+		if(cn < 0) { kl = k; break; }
+		double* gq = G + 256*(r0 + k) + j;
+		gq[0] = y[0]; gq[64] = y[1]; gq[128] = y[2]; gq[192] = y[3];
 		#pragma unroll
 		for(int i = 0; i < 4; i++)
 			#pragma unroll
-			for(int j = 0; j < 4; j++) prev[i][j] = b[i][j];
+			for(int q = 0; q < 4; q++) { Dk[i][q] = Dn[i][q]; Lk[i][q] = Ln[i][q]; }
+		vk = vn;
+		c = cn;
 	}
-}
-
-/// z = Lines^-1 v per line (one thread per line): forward g_k = dinvp_k (v_k - A[k][k-1] g_{k-1}) into z,
-/// then backward z_k = g_k - dinvp_k A[k][k+1] z_{k+1}
-__global__ __launch_bounds__(64)
-void k_line_solve(int nlines, const int* __restrict__ lstart, const int* __restrict__ lcell, const int* __restrict__ lface,
-                  const double* __restrict__ dinvp, const double* __restrict__ lower, const double* __restrict__ upper,
-                  const double* __restrict__ v, double* __restrict__ z, int first)
-{
-	const int l = first + static_cast<int>(blockIdx.x*blockDim.x + threadIdx.x);
-	if(l >= nlines) return;
-	const int k0 = lstart[l], k1 = lstart[l+1];
-	double4 g = make_double4(0, 0, 0, 0);
-	for(int k = k0; k < k1; k++) {
-		const int c = lcell[k];
-		double4 r = reinterpret_cast<const double4*>(v)[c];
-		if(k > k0) {
-			double t[4];
-			blk_mv(blk_cp(lface[k], lower, upper), g, t);
-			r.x -= t[0]; r.y -= t[1]; r.z -= t[2]; r.w -= t[3];
+	// backward from the line's last cell (kl): z_kl = g_kl
+	double4 x = gp;
+	reinterpret_cast<double4*>(z)[c] = x;
+	if(kl == 0) return;
+	int ck = lcell[64*(r0+kl-1) + j];
+	double Wk[4][4];
+	ldI16(W, r0 + kl - 1, j, Wk);
+	const double* gq = G + 256*(r0 + kl - 1) + j;
+	double4 gk = make_double4(gq[0], gq[64], gq[128], gq[192]);
+	for(int k = kl - 1; k >= 0; k--) {
+		int cp = -1;
+		double Wn[4][4];
+		double4 gn = make_double4(0, 0, 0, 0);
+		if(k > 0) {
+			cp = lcell[64*(r0+k-1) + j];
+			ldI16(W, r0 + k - 1, j, Wn);
+			const double* gm = G + 256*(r0 + k - 1) + j;
+			gn = make_double4(gm[0], gm[64], gm[128], gm[192]);
 		}
 		double y[4];
-		blk_mv(dinvp + 16*static_cast<size_t>(c), r, y);
-		g = make_double4(y[0], y[1], y[2], y[3]);
-		reinterpret_cast<double4*>(z)[c] = g;
-	}
-	double4 x = g;                 // z of the last cell
-	for(int k = k1 - 2; k >= k0; k--) {
-		const int c = lcell[k];
-		double t[4], y[4];
-		blk_mv(blk_pc(lface[k+1], lower, upper), x, t);
-		blk_mv(dinvp + 16*static_cast<size_t>(c), make_double4(t[0], t[1], t[2], t[3]), y);
-		const double4 gk = reinterpret_cast<const double4*>(z)[c];
+		#pragma unroll
+		for(int i = 0; i < 4; i++) y[i] = Wk[i][0]*x.x + Wk[i][1]*x.y + Wk[i][2]*x.z + Wk[i][3]*x.w;
 		x = make_double4(gk.x - y[0], gk.y - y[1], gk.z - y[2], gk.w - y[3]);
-		reinterpret_cast<double4*>(z)[c] = x;
-	}
-}
-
-/// Wave-per-line forms of the two kernels above (one 64-lane workgroup per line): the lanes stage 64
-/// cells' blocks of the line in LDS with independent loads, then one lane runs the recurrence over them
-/// from LDS and the lanes write the results back. The recurrence is the same arithmetic in the same
-/// order, so the results are bitwise those of the one-thread-per-line kernels; what goes is the global
-/// load latency inside the sequential chain (a line of a few hundred cells walked by one thread paid
-/// one memory round trip per cell).
-constexpr int LCH = 64;
-
-__global__ __launch_bounds__(64)
-void k_line_factor_w(int nlines, const int* __restrict__ lstart, const int* __restrict__ lcell, const int* __restrict__ lface,
-                     const double* __restrict__ diag, const double* __restrict__ lower, const double* __restrict__ upper,
-                     double* __restrict__ dinvp)
-{
-	__shared__ __attribute__((aligned(32))) double sD[LCH][16], sL[LCH][16], sU[LCH][16];
-	__shared__ int sc[LCH];
-	const int l = blockIdx.x, j = threadIdx.x;
-	if(l >= nlines) return;
-	const int k0 = lstart[l], k1 = lstart[l+1];
-	double prev[4][4];
-	for(int base = k0; base < k1; base += LCH) {
-		const int n = min(LCH, k1 - base);
-		__syncthreads();                         // the previous chunk is written back
-		if(j < n) {
-			const int k = base + j, c = lcell[k];
-			sc[j] = c;
-			for(int e = 0; e < 16; e++) sD[j][e] = diag[16*static_cast<size_t>(c) + e];
-			if(k > k0) {
-				const double* L = blk_cp(lface[k], lower, upper);
-				const double* U = blk_pc(lface[k], lower, upper);
-				for(int e = 0; e < 16; e++) { sL[j][e] = L[e]; sU[j][e] = U[e]; }
-			}
-		}
-		__syncthreads();
-		if(j == 0) {
-			for(int i = 0; i < n; i++) {
-				double a[4][4], b[4][4];
-				#pragma unroll
-				for(int r = 0; r < 4; r++)
-					#pragma unroll
-					for(int q = 0; q < 4; q++) a[r][q] = sD[i][4*r+q];
-				if(base + i > k0) {
-					double t[4][4];
-					#pragma unroll
-					for(int r = 0; r < 4; r++)
-						#pragma unroll
-						for(int q = 0; q < 4; q++)
-							t[r][q] = prev[r][0]*sU[i][q] + prev[r][1]*sU[i][4+q] + prev[r][2]*sU[i][8+q] + prev[r][3]*sU[i][12+q];
-					#pragma unroll
-					for(int r = 0; r < 4; r++)
-						#pragma unroll
-						for(int q = 0; q < 4; q++)
-							a[r][q] -= sL[i][4*r]*t[0][q] + sL[i][4*r+1]*t[1][q] + sL[i][4*r+2]*t[2][q] + sL[i][4*r+3]*t[3][q];
-				}
-				inv4(a, b);
-				#pragma unroll
-				for(int r = 0; r < 4; r++)
-					#pragma unroll
-					for(int q = 0; q < 4; q++) { sD[i][4*r+q] = b[r][q]; prev[r][q] = b[r][q]; }
-			}
-		}
-		__syncthreads();
-		if(j < n) for(int e = 0; e < 16; e++) dinvp[16*static_cast<size_t>(sc[j]) + e] = sD[j][e];
-	}
-}
-
-__global__ __launch_bounds__(64)
-void k_line_solve_w(int nlines, const int* __restrict__ lstart, const int* __restrict__ lcell, const int* __restrict__ lface,
-                    const double* __restrict__ dinvp, const double* __restrict__ lower, const double* __restrict__ upper,
-                    const double* __restrict__ v, double* __restrict__ z)
-{
-	__shared__ __attribute__((aligned(32))) double sD[LCH][16], sB[LCH][16], sv[LCH][4];
-	__shared__ int sc[LCH];
-	const int l = blockIdx.x, j = threadIdx.x;
-	if(l >= nlines) return;
-	const int k0 = lstart[l], k1 = lstart[l+1];
-	double4 g = make_double4(0, 0, 0, 0);
-	// forward: g_k = dinvp_k (v_k - A[k][k-1] g_{k-1})
-	for(int base = k0; base < k1; base += LCH) {
-		const int n = min(LCH, k1 - base);
-		__syncthreads();
-		if(j < n) {
-			const int k = base + j, c = lcell[k];
-			sc[j] = c;
-			for(int e = 0; e < 16; e++) sD[j][e] = dinvp[16*static_cast<size_t>(c) + e];
-			for(int e = 0; e < 4; e++) sv[j][e] = v[4*static_cast<size_t>(c) + e];
-			if(k > k0) { const double* L = blk_cp(lface[k], lower, upper); for(int e = 0; e < 16; e++) sB[j][e] = L[e]; }
-		}
-		__syncthreads();
-		if(j == 0) {
-			for(int i = 0; i < n; i++) {
-				double4 r = make_double4(sv[i][0], sv[i][1], sv[i][2], sv[i][3]);
-				if(base + i > k0) {
-					double t[4];
-					blk_mv(sB[i], g, t);
-					r.x -= t[0]; r.y -= t[1]; r.z -= t[2]; r.w -= t[3];
-				}
-				double y[4];
-				blk_mv(sD[i], r, y);
-				g = make_double4(y[0], y[1], y[2], y[3]);
-				sv[i][0] = y[0]; sv[i][1] = y[1]; sv[i][2] = y[2]; sv[i][3] = y[3];
-			}
-		}
-		__syncthreads();
-		if(j < n) for(int e = 0; e < 4; e++) z[4*static_cast<size_t>(sc[j]) + e] = sv[j][e];
-	}
-	// backward: z_k = g_k - dinvp_k A[k][k+1] z_{k+1}, chunks from the end (the last cell keeps g)
-	double4 x = g;
-	const int kl = k1 - 2;                      // last cell the backward pass updates
-	for(int top = kl; top >= k0; top -= LCH) {
-		const int n = min(LCH, top - k0 + 1);   // cells top, top-1, ..., top-n+1
-		__syncthreads();
-		if(j < n) {
-			const int k = top - j, c = lcell[k];
-			sc[j] = c;
-			for(int e = 0; e < 16; e++) sD[j][e] = dinvp[16*static_cast<size_t>(c) + e];
-			for(int e = 0; e < 4; e++) sv[j][e] = z[4*static_cast<size_t>(c) + e];
-			const double* U = blk_pc(lface[k+1], lower, upper);
-			for(int e = 0; e < 16; e++) sB[j][e] = U[e];
-		}
-		__syncthreads();
-		if(j == 0) {
-			for(int i = 0; i < n; i++) {
-				double t[4], y[4];
-				blk_mv(sB[i], x, t);
-				blk_mv(sD[i], make_double4(t[0], t[1], t[2], t[3]), y);
-				x = make_double4(sv[i][0] - y[0], sv[i][1] - y[1], sv[i][2] - y[2], sv[i][3] - y[3]);
-				sv[i][0] = x.x; sv[i][1] = x.y; sv[i][2] = x.z; sv[i][3] = x.w;
-			}
-		}
-		__syncthreads();
-		if(j < n) for(int e = 0; e < 4; e++) z[4*static_cast<size_t>(sc[j]) + e] = sv[j][e];
+		reinterpret_cast<double4*>(z)[ck] = x;
+		if(k == 0) break;
+		#pragma unroll
+		for(int i = 0; i < 4; i++)
+			#pragma unroll
+			for(int q = 0; q < 4; q++) Wk[i][q] = Wn[i][q];
+		gk = gn;
+		ck = cp;
 	}
 }
 
@@ -484,27 +426,18 @@ void k_add_rows(int n, const double* __restrict__ e, double* __restrict__ z)
 	reinterpret_cast<double4*>(z)[c] = b;
 }
 
-void launch_line_factor(const LineSet& Ls, const double* diag, const double* lower, const double* upper, double* dinvp,
-                        hipStream_t s)
+void launch_line_factor(const LineSet& Ls, const double* diag, const double* lower, const double* upper, hipStream_t s)
 {
-	// long lines: a workgroup each; the short rest (same arithmetic, bitwise the same): a thread each
-	if(Ls.nlong > 0)
-		hipLaunchKernelGGL(k_line_factor_w, dim3(Ls.nlong), dim3(64), 0, s, Ls.nlines, Ls.start, Ls.cell, Ls.face,
-		                   diag, lower, upper, dinvp);
-	if(Ls.nlines > Ls.nlong)
-		hipLaunchKernelGGL(k_line_factor, dim3(nblk(Ls.nlines - Ls.nlong, 64)), dim3(64), 0, s, Ls.nlines, Ls.start,
-		                   Ls.cell, Ls.face, diag, lower, upper, dinvp, Ls.nlong);
+	if(Ls.ngroups > 0)
+		hipLaunchKernelGGL(k_line_factor, dim3(Ls.ngroups), dim3(64), 0, s, Ls.gstart, Ls.cell, Ls.face, diag, lower,
+		                   upper, Ls.D, Ls.Lb, Ls.W);
 }
 
-void launch_line_solve(const LineSet& Ls, const double* dinvp, const double* lower, const double* upper, const double* v,
-                       double* z, hipStream_t s)
+void launch_line_solve(const LineSet& Ls, const double* v, double* z, hipStream_t s)
 {
-	if(Ls.nlong > 0)
-		hipLaunchKernelGGL(k_line_solve_w, dim3(Ls.nlong), dim3(64), 0, s, Ls.nlines, Ls.start, Ls.cell, Ls.face,
-		                   dinvp, lower, upper, v, z);
-	if(Ls.nlines > Ls.nlong)
-		hipLaunchKernelGGL(k_line_solve, dim3(nblk(Ls.nlines - Ls.nlong, 64)), dim3(64), 0, s, Ls.nlines, Ls.start,
-		                   Ls.cell, Ls.face, dinvp, lower, upper, v, z, Ls.nlong);
+	if(Ls.ngroups > 0)
+		hipLaunchKernelGGL(k_line_solve, dim3(Ls.ngroups), dim3(64), 0, s, Ls.gstart, Ls.cell, Ls.D, Ls.Lb, Ls.W, Ls.G,
+		                   v, z);
 }
 
 void launch_add_rows(int n, const double* e, double* z, hipStream_t s)

@@ -42,22 +42,30 @@ FVHIP_HD double relaxation_factor(const gd::Gas& G, double minfactor, const doub
 	return omega;
 }
 
-/// Lines of the line-implicit preconditioner (internal cell ids): cells cell[start[l]..start[l+1]) in
-/// line order; face[k] (k > start[l]) = interior face between cells k-1 and k, fi<<1 | (cell k-1 is R)
-/// lines sorted by length, longest first; lines [0, nlong) have at least LINE_WAVE_MIN cells and take
-/// the wave-per-line kernels, the short rest (most of them single cells) the thread-per-line ones
-struct LineSet { int nlines = 0; const int* start = nullptr; const int* cell = nullptr; const int* face = nullptr; int nlong = 0; };
-constexpr int LINE_WAVE_MIN = 8;
+/// Lines of the line-implicit preconditioner (internal cell ids), sorted by length (longest first) and
+/// dealt to groups of 64: lane j of group g walks line 64g + j, so one wave runs 64 recurrences side by
+/// side. Everything per line cell is stored line-interleaved: row r = gstart[g] + k holds step k of the
+/// group's 64 lines, slot r*64 + lane; a 4x4 block of row r is X[(16r + e)*64 + lane] (one coalesced
+/// load per element across the 64 lines). cell[slot] = the lane's k-th line cell or -1 once its line
+/// has ended; face[slot] (k > 0) = interior face between its cells k-1 and k, fi<<1 | (cell k-1 is R).
+/// Device arrays written by the factorisation and read by the solve: D = dinvp_k (the inverted pivot
+/// blocks), Lb = A[k][k-1], W = dinvp_k A[k][k+1]; G = forward-sweep scratch [rows][4][64].
+struct LineSet {
+	int nlines = 0, ngroups = 0;
+	long long nrows = 0;             ///< rows over all groups (slots = 64 nrows)
+	const int* gstart = nullptr;     ///< [ngroups+1]
+	const int* cell = nullptr;       ///< [64 nrows]
+	const int* face = nullptr;       ///< [64 nrows]
+	double *D = nullptr, *Lb = nullptr, *W = nullptr, *G = nullptr;
+};
 #ifndef FVHIP_LINE_MAX
 #define FVHIP_LINE_MAX 256
 #endif
 constexpr int LINE_MAX_CELLS = FVHIP_LINE_MAX;   ///< longest line piece (ctx.hpp ensureLines)
-/// block-Thomas factorisation of every line into dinvp [ncell][16]
-void launch_line_factor(const LineSet& Ls, const double* diag, const double* lower, const double* upper, double* dinvp,
-                        hipStream_t s);
+/// block-Thomas factorisation of every line (D, Lb, W of the line set) from the block operator
+void launch_line_factor(const LineSet& Ls, const double* diag, const double* lower, const double* upper, hipStream_t s);
 /// z = (block-tridiagonal line part of A)^-1 v
-void launch_line_solve(const LineSet& Ls, const double* dinvp, const double* lower, const double* upper, const double* v,
-                       double* z, hipStream_t s);
+void launch_line_solve(const LineSet& Ls, const double* v, double* z, hipStream_t s);
 /// z += e over n cells
 void launch_add_rows(int n, const double* e, double* z, hipStream_t s);
 /// dinv[c] = diag[c]^-1 (Gauss-Jordan with row pivoting), c < ncell

@@ -295,6 +295,17 @@ int fvhip_gmres_blocks_device(fvhip_handle h, const double* d_diag, const double
                               const double* d_b, double* d_x, double rtol, int maxit, int restart, int sweeps,
                               int* iters, double* resnorm);
 
+/** The line-implicit preconditioner alone (fvhip_implicit_config::prec_lines): block-Thomas factorisation
+ *  of M, the block-tridiagonal part of the block operator along the lines built with `line_threshold`
+ *  (0: 4), then z = M^-1 v (internal order, [ncell][4]). Blocks as in fvhip_gmres_blocks_device. */
+int fvhip_line_precondition_device(fvhip_handle h, const double* d_diag, const double* d_lower, const double* d_upper,
+                                   double line_threshold, const double* d_v, double* d_z);
+/** The lines of that preconditioner (pieces of at most 256 cells), longest first: *nlines; start
+ *  [nlines+1] into cells [ncell] (internal ids, line order) and faces [ncell] (link of a cell to the previous
+ *  one: interior face fi << 1 | (previous cell is the face's R), -1 for a line's first cell); NULL
+ *  arrays are skipped */
+int fvhip_lines(fvhip_handle h, double line_threshold, int* nlines, int* start, int* cells, int* faces);
+
 /** MatrixFreeSpatialJacobian: set_state(u, r = -r(u), mdt = area/(CFL*dt)) then y = J x */
 int fvhip_matfree_set_state(fvhip_handle h, const double* u, const double* r, const double* mdt);
 int fvhip_matfree_apply(fvhip_handle h, const double* x, double* y);

@@ -151,6 +151,46 @@ def test_line_preconditioner_cuts_iterations():
     assert np.all(d <= 1e-5 * np.abs(u0 - out[False][1]).max(axis=0))
 
 
+def test_line_solve_inverts_line_blocks():
+    """the line preconditioner alone: z = M^-1 v with M the block-tridiagonal part of the operator along
+    the lines it reports (fvhip_lines), checked as |M z - v| <= 1e-10 |v| with M assembled on the host
+    from the same blocks. The O-grid's wall-normal lines of 300 quad layers are cut at 256 cells, and the
+    rest of the cells are short lines or lines of one, so a wave's lanes walk lines that end at
+    different steps and waves of every length run (krylov.hip k_line_factor / k_line_solve)."""
+    torch = _torch()
+    m = fa.UMesh.naca_ogrid(64, 300, 8, 20.0, 1e-6)
+    p = cases.physics("naca")
+    n = cases.numerics("ROE", "LEASTSQUARES", "VANALBADA")
+    N, Fi = m.nelem, m.naface - m.nbface
+    rng = np.random.default_rng(3)
+    # block diagonally dominant (block Thomas without pivoting across blocks is stable for these)
+    D = rng.standard_normal((N, 4, 4)) + 16.0 * np.eye(4)[None]
+    lo, up = 0.5 * rng.standard_normal((Fi, 4, 4)), 0.5 * rng.standard_normal((Fi, 4, 4))
+    dev = fa.FlowFV(m, p, n)
+    perm = dev.permutation()
+    Dint = D[perm]                                   # internal order, as the device holds it
+    lines = dev.lines()
+    lens = np.array([len(c) for c, _ in lines])
+    assert lens.sum() == N and np.array_equal(np.sort(np.concatenate([c for c, _ in lines])), np.arange(N))
+    assert lens.max() == 256 and (lens == 1).sum() > 0 and len(lines) > 64, (lens.max(), len(lines))
+    assert np.all(np.diff(lens) <= 0)                # longest first
+    v = rng.standard_normal((N, 4))
+    dz = torch.zeros((N, 4), dtype=torch.float64, device="cuda")
+    held = [to_device(a) for a in (Dint.reshape(N, 16), lo.reshape(Fi, 16), up.reshape(Fi, 16), v)]
+    dev.line_precondition_device(*[t.data_ptr() for t in held], dz.data_ptr())
+    z = dz.cpu().numpy()
+    Mz = np.einsum("cij,cj->ci", Dint, z)
+    for cells, faces in lines:
+        for k in range(1, len(cells)):
+            c, pv, fi, side = cells[k], cells[k - 1], faces[k] >> 1, faces[k] & 1
+            a_cp, a_pc = (up[fi], lo[fi]) if side else (lo[fi], up[fi])
+            Mz[c] += a_cp @ z[pv]
+            Mz[pv] += a_pc @ z[c]
+    err = np.abs(Mz - v).max()
+    assert err <= 1e-10 * np.abs(v).max(), err
+    dev.close()
+
+
 def test_matfree_vs_matrix_same_steps():
     """tests/solvers/testmatrixfree.cpp:65 (matfree.ctrl: HLLC, first order, CFL 50-3000, tol 1e-8,
     100 steps, full update; matfree.solverc: GMRES rtol 1e-2, 30 iterations; step 1e-6)"""

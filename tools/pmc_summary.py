@@ -8,7 +8,8 @@ run_counter_collection.csv, and writes
                                        2 x FETCH_SIZE + WRITE_SIZE, KB -> bytes)
 The FETCH_SIZE x2 calibration (gfx950 reports half of 16-byte-per-lane reads) is checked on the
 streaming kernel k_prep_cells when present (it must read exactly 32 B per cell), and recorded.
-usage: python tools/pmc_summary.py gpurun_out/prof profiles/r01 "<workload text with cell count>" [cells]
+usage: python tools/pmc_summary.py gpurun_out/prof profiles/r01 "<workload text with cell count>" [cells] [name]
+(name: output basename instead of pmc_traffic)
 """
 import csv
 import json
@@ -42,11 +43,14 @@ def counters(path):
 
 def main():
     prof, out, workload = sys.argv[1], sys.argv[2], sys.argv[3]
-    cells = int(sys.argv[4]) if len(sys.argv) > 4 else None
+    cells = int(sys.argv[4]) if len(sys.argv) > 4 and sys.argv[4] else None
+    name = sys.argv[5] if len(sys.argv) > 5 else "pmc_traffic"
     os.makedirs(out, exist_ok=True)
-    shutil.copy(os.path.join(prof, "trace", "run_kernel_stats.csv"), os.path.join(out, "kernel_stats.csv"))
+    stats = os.path.join(prof, "trace", "run_kernel_stats.csv")
+    if os.path.exists(stats):
+        shutil.copy(stats, os.path.join(out, "kernel_stats.csv" if name == "pmc_traffic" else name + "_kernel_stats.csv"))
     merged = defaultdict(dict)
-    for sub in ("fetch", "write", "sq", "sq2", "sq3", "lds"):
+    for sub in sorted(os.listdir(prof)):          # every PMC pass (one subdirectory each)
         p = os.path.join(prof, sub, "run_counter_collection.csv")
         if not os.path.exists(p):
             continue
@@ -69,7 +73,7 @@ def main():
            "method": "rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE / --pmc SQ_* in separate passes over "
                      "bench.py; mean per dispatch",
            "calibration": cal, "kernels": kernels}
-    with open(os.path.join(out, "pmc_traffic.json"), "w") as f:
+    with open(os.path.join(out, name + ".json"), "w") as f:
         json.dump(doc, f, indent=1)
     print(json.dumps({k: round(v.get("hbm_bytes_corrected", 0) / 1e6, 1) for k, v in kernels.items()}))
 
