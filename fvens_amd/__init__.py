@@ -505,10 +505,23 @@ def comm_unique_id():
     return bytes(buf.raw)
 
 
-def partition_graph(mesh, nparts):
-    """Graph partition of the cell dual graph (stand-in for the reference's Scotch, absent here)"""
+def cell_face_counts(mesh):
+    """faces per cell (3 triangle, 4 quadrangle): the work weights of partition_graph(weights="faces")"""
+    return np.ascontiguousarray(mesh.raw()["nnode"], np.int32)
+
+
+def partition_graph(mesh, nparts, weights=None):
+    """Graph partition of the cell dual graph (stand-in for the reference's Scotch, absent here).
+    weights: None (every cell 1, as the reference's Scotch graph), "faces" (the cell's face count:
+    balances the fused residual's work on mixed triangle/quadrangle meshes) or an int array [nelem]"""
     part = np.zeros(mesh.nelem, np.int32)
-    check(_ffi.lib().fvhip_partition_graph(ctypes.byref(mesh.view), int(nparts), iptr(part)))
+    if weights is None:
+        check(_ffi.lib().fvhip_partition_graph(ctypes.byref(mesh.view), int(nparts), iptr(part)))
+        return part
+    w = cell_face_counts(mesh) if isinstance(weights, str) and weights == "faces" else np.ascontiguousarray(weights, np.int32)
+    if w.shape != (mesh.nelem,):
+        raise ValueError("partition_graph: weights must be 'faces' or one int per cell")
+    check(_ffi.lib().fvhip_partition_graph_weighted(ctypes.byref(mesh.view), int(nparts), iptr(w), iptr(part)))
     return part
 
 

@@ -61,6 +61,7 @@ _SIGS = {
     "fvhip_set_rank": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_int]),
     "fvhip_partition_rcb": (ctypes.c_int, [ctypes.POINTER(FvMeshView), ctypes.c_int, c_int_p]),
     "fvhip_partition_graph": (ctypes.c_int, [ctypes.POINTER(FvMeshView), ctypes.c_int, c_int_p]),
+    "fvhip_partition_graph_weighted": (ctypes.c_int, [ctypes.POINTER(FvMeshView), ctypes.c_int, c_int_p, c_int_p]),
     "fvhip_partition_edge_cut": (ctypes.c_longlong, [ctypes.POINTER(FvMeshView), c_int_p]),
     "fvhip_partition_info": (ctypes.c_int, [ctypes.POINTER(FvMeshView), c_int_p, ctypes.c_int, c_int_p, c_int_p,
                                             c_int_p, c_int_p, c_int_p, c_int_p]),

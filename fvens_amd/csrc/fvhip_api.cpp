@@ -221,6 +221,14 @@ int fvhip_partition_graph(const fvhip_mesh* mesh, int nparts, int* part)
 	});
 }
 
+int fvhip_partition_graph_weighted(const fvhip_mesh* mesh, int nparts, const int* weight, int* part)
+{
+	return guard([&] {
+		const std::vector<int> p = partitionGraph(*mesh, nparts, weight);
+		std::memcpy(part, p.data(), p.size()*sizeof(int));
+	});
+}
+
 long long fvhip_partition_edge_cut(const fvhip_mesh* mesh, const int* part)
 {
 	long long c = -1;

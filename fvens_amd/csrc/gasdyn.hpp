@@ -73,6 +73,18 @@ FVHIP_HD double twice_minus(double a, double b) {
 
 FVHIP_HD double dot2(const double* a, const double* b) { double d = mul0(a[0], b[0]); d += a[1]*b[1]; return d; }
 
+/// `c + s*p` for a power of two s (here +-0.5, +-0.25), which scales exactly: on the device one fma,
+/// bitwise c + RN(s*p) short of s*p leaving the normal range. The reference's `c - 0.5*a*b` and
+/// `c + x/4.0*y` forms are this with p = RN(a*b) resp. RN(x*y): (0.5*a)*b is exactly 0.5*RN(a*b) and
+/// (x/4)*y exactly RN(x*y)/4 -- one multiply less per term
+FVHIP_HD double add_pow2(double c, double p, double s) {
+#if defined(__HIP_DEVICE_COMPILE__)
+	return __builtin_fma(p, s, c);
+#else
+	return c + s*p;
+#endif
+}
+
 /// a/b and sqrt(x), correctly rounded, for the parity kernels. On the device these are the compiler's
 /// own f64 sequences -- division: v_rcp, two Newton steps, Markstein's correction; square root:
 /// v_rsq and Goldschmidt steps -- without their range scaling and special-value fix-ups
@@ -127,12 +139,12 @@ FVHIP_HD void flow_vars(const Gas& G, const double* uc, const double* n, double*
 	v[1] = div_rn(uc[2], uc[0]);
 	vn = dot2(v,n);
 	const double vm2 = dot2(v,v);
-	p = (G.g-1.0)*(uc[3] - 0.5*uc[0]*vm2);
+	p = (G.g-1.0)*add_pow2(uc[3], uc[0]*vm2, -0.5);           // uc[3] - 0.5*uc[0]*vm2
 	H = div_rn(uc[3]+p, uc[0]);
 }
 
 FVHIP_HD double pressure_cons(const Gas& G, const double* uc) {
-	return (G.g-1.0)*(uc[3] - div_rn(0.5*dot2(&uc[1],&uc[1]), uc[0]));
+	return (G.g-1.0)*add_pow2(uc[3], div_rn(dot2(&uc[1],&uc[1]), uc[0]), -0.5);   // uc[3] - (0.5*|m|^2)/uc[0]
 }
 FVHIP_HD double sound_speed(const Gas& G, double rho, double p) { return sqrt_rn(div_rn(G.g * p, rho)); }
 FVHIP_HD double sound_speed_cons(const Gas& G, const double* uc) { return sound_speed(G, uc[0], pressure_cons(G, uc)); }
@@ -149,7 +161,9 @@ FVHIP_HD double div_rcp(double a, double b, double r) {
 	return a/b;
 #endif
 }
-FVHIP_HD double energy_from_pressure(const Gas& G, double p, double d, double vm2) { return div_rcp(p, G.g-1.0, G.rgm1) + 0.5*d*vm2; }
+FVHIP_HD double energy_from_pressure(const Gas& G, double p, double d, double vm2) {
+	return add_pow2(div_rcp(p, G.g-1.0, G.rgm1), d*vm2, 0.5);          // p/(g-1) + 0.5*d*vm2
+}
 FVHIP_HD double energy_from_temperature(const Gas& G, double T, double d, double vm2) {
 	return d * (div_rn(T, G.g*(G.g-1.0)*G.Minf*G.Minf) + 0.5*vm2);
 }
@@ -205,7 +219,7 @@ FVHIP_HD RoeAvg roe_average(const Gas& G, const double* ul, const double* ur, co
 	a.H = div_rn(a.R*Hj + Hi, a.R + 1.0);
 	a.vm2 = dot2(a.v,a.v);
 	a.vn = dot2(a.v,n);
-	a.c = sqrt_rn( (G.g-1.0)*(a.H - a.vm2*0.5) );
+	a.c = sqrt_rn( (G.g-1.0)*add_pow2(a.H, a.vm2, -0.5) );       // (g-1)*(H - vm2*0.5)
 	return a;
 }
 
@@ -213,6 +227,8 @@ FVHIP_HD RoeAvg roe_average(const Gas& G, const double* ul, const double* ur, co
 // Numerical fluxes. Output: flux per unit length along unit normal n (L -> R).
 // ---------------------------------------------------------------------------------------------
 
+/// HALVE = false: f = (...) without the final 0.5*(...) (inviscid_flux_len folds it into the length)
+template <bool HALVE = true>
 FVHIP_HD void flux_llf(const Gas& G, const double* ul, const double* ur, const double* n, double* f) {
 	double vi[2], vj[2], vni, vnj, pi, pj, Hi, Hj;
 	flow_vars(G, ul, n, vi, vni, pi, Hi);
@@ -224,15 +240,18 @@ FVHIP_HD void flux_llf(const Gas& G, const double* ul, const double* ur, const d
 	double fl[4], fr[4];
 	{
 		const double vn = div_rn(dot2(&ul[1],n), ul[0]);
-		const double p = (G.g-1.0)*(ul[3] - div_rn(0.5*dot2(&ul[1],&ul[1]), ul[0]));
+		const double p = pressure_cons(G, ul);
 		directional_flux(G, ul, n, vn, p, fl);
 	}
 	{
 		const double vn = div_rn(dot2(&ur[1],n), ur[0]);
-		const double p = (G.g-1.0)*(ur[3] - div_rn(0.5*dot2(&ur[1],&ur[1]), ur[0]));
+		const double p = pressure_cons(G, ur);
 		directional_flux(G, ur, n, vn, p, fr);
 	}
-	for(int k = 0; k < 4; k++) f[k] = 0.5*( fl[k] + fr[k] - eig*(ur[k]-ul[k]) );
+	for(int k = 0; k < 4; k++) {
+		const double s = fl[k] + fr[k] - eig*(ur[k]-ul[k]);
+		f[k] = HALVE ? 0.5*s : s;
+	}
 }
 
 FVHIP_HD double sq(double x) { return x*x; }   // std::pow(x,2) folds to x*x
@@ -321,6 +340,7 @@ FVHIP_HD void flux_ausmplus(const Gas& G, const double* ul, const double* ur, co
 	f[3] = ch* (Mh/2.0*(ul[3]+pi+ur[3]+pj) -fabs(Mh)/2.0*((ur[3]+pj)-(ul[3]+pi)));
 }
 
+template <bool HALVE = true>
 FVHIP_HD void flux_roe(const Gas& G, const double* ul, const double* ur, const double* n, double* f) {
 	double vi[2], vj[2], vni, vnj, pi, pj, Hi, Hj;
 	flow_vars(G, ul, n, vi, vni, pi, Hi);
@@ -349,7 +369,7 @@ FVHIP_HD void flux_roe(const Gas& G, const double* ul, const double* ur, const d
 	d0 += a1;
 	d1 += a1*a.v[0] +      a2*(vj[0]-vi[0] - devn*n[0]);
 	d2 += a1*a.v[1] +      a2*(vj[1]-vi[1] - devn*n[1]);
-	d3 += a1*a.vm2/2.0 + a2 *(a.v[0]*(vj[0]-vi[0]) +a.v[1]*(vj[1]-vi[1]) -a.vn*devn);
+	d3 += add_pow2(a2 *(a.v[0]*(vj[0]-vi[0]) +a.v[1]*(vj[1]-vi[1]) -a.vn*devn), a1*a.vm2, 0.5);   // a1*vm2/2.0 + a2*(...)
 	d0 += a3;
 	d1 += a3*(a.v[0]+a.c*n[0]);
 	d2 += a3*(a.v[1]+a.c*n[1]);
@@ -357,10 +377,8 @@ FVHIP_HD void flux_roe(const Gas& G, const double* ul, const double* ur, const d
 	double fi[4], fj[4];
 	directional_flux(G, ul, n, vni, pi, fi);
 	directional_flux(G, ur, n, vnj, pj, fj);
-	f[0] = 0.5*(fi[0]+fj[0] - d0);
-	f[1] = 0.5*(fi[1]+fj[1] - d1);
-	f[2] = 0.5*(fi[2]+fj[2] - d2);
-	f[3] = 0.5*(fi[3]+fj[3] - d3);
+	const double s[4] = {fi[0]+fj[0] - d0, fi[1]+fj[1] - d1, fi[2]+fj[2] - d2, fi[3]+fj[3] - d3};
+	for(int k = 0; k < 4; k++) f[k] = HALVE ? 0.5*s[k] : s[k];
 }
 
 FVHIP_HD void einfeldt(double vni, double ci, double vnj, double cj, const RoeAvg& a, double& sl, double& sr) {
@@ -436,6 +454,24 @@ FVHIP_HD void inviscid_flux(const Gas& G, const double* ul, const double* ur, co
 		case 5: flux_hll(G, ul, ur, n, f); break;
 		default: flux_hllc(G, ul, ur, n, f); break;
 	}
+}
+
+/// the flux times the face length, f*len, as the sweeps form it. Roe and LLF end in 0.5*(...): on the
+/// device the halving moves into the length, RN(RN(0.5 s) len) = RN(s (0.5 len)) bitwise (both
+/// halvings exact), one multiply per face instead of four
+template <int FLUX>
+FVHIP_HD void inviscid_flux_len(const Gas& G, const double* ul, const double* ur, const double* n, double len, double* f) {
+#if defined(__HIP_DEVICE_COMPILE__)
+	if(FLUX == 0 || FLUX == 4) {
+		if(FLUX == 0) flux_llf<false>(G, ul, ur, n, f);
+		else flux_roe<false>(G, ul, ur, n, f);
+		const double hl = 0.5*len;
+		for(int k = 0; k < 4; k++) f[k] *= hl;
+		return;
+	}
+#endif
+	inviscid_flux<FLUX>(G, ul, ur, n, f);
+	for(int k = 0; k < 4; k++) f[k] *= len;
 }
 
 FVHIP_HD void inviscid_flux_rt(int type, const Gas& G, const double* ul, const double* ur, const double* n, double* f) {

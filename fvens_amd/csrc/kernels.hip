@@ -553,19 +553,22 @@ __global__ void __launch_bounds__(256) k_weno(DevMesh M, double lambda, const do
 // THE SWEEP
 // ------------------------------------------------------------------------------------------------
 
-/// MUSCL / Van Albada pieces (musclreconstruction.cpp:33-59)
+/// MUSCL / Van Albada pieces (musclreconstruction.cpp:33-59, 86-90, 112-120), bitwise in fewer
+/// instructions: the numerator 2.0*d*du + eps as fma(d*du, 2, eps) (2d is exact, so RN(2d*du) =
+/// 2 RN(d*du)); `phi < 0 -> 0` as one v_max (phi is never -0: the numerator RN(x + 1e-8) is +0 when
+/// x = -1e-8, and the denominator is positive); ui + phi/4.0*S as fma(phi*S, 1/4, ui) (add_pow2)
 __device__ __forceinline__ double muscl_phi(double d, double du) {
 	const double eps = 1e-8;
-	double ph = div_rn(2.0*d * du + eps, d*d + du*du + eps);
-	return ph < 0.0 ? 0.0 : ph;
+	const double ph = div_rn(__builtin_fma(d*du, 2.0, eps), d*d + du*du + eps);
+	return __builtin_fmax(ph, 0.0);
 }
 __device__ __forceinline__ double muscl_left(double ui, double uj, double dm, double ph) {
 	const double k = 1.0/3.0;
-	return ui + ph/4.0*( (1.0-k*ph)*dm + (1.0+k*ph)*(uj - ui) );
+	return add_pow2(ui, ph*( (1.0-k*ph)*dm + (1.0+k*ph)*(uj - ui) ), 0.25);
 }
 __device__ __forceinline__ double muscl_right(double ui, double uj, double dp, double ph) {
 	const double k = 1.0/3.0;
-	return uj - ph/4.0*( (1.0-k*ph)*dp + (1.0+k*ph)*(uj - ui) );
+	return add_pow2(uj, ph*( (1.0-k*ph)*dp + (1.0+k*ph)*(uj - ui) ), -0.25);
 }
 
 /// Per-cell words (doubles) staged in LDS for a sweep variant, one 16-byte-aligned row per cell:
@@ -735,9 +738,7 @@ __global__ void __launch_bounds__(SLOTS_MAX) k_sweep(const DevMesh M, const DevP
 			}
 		}
 
-		inviscid_flux<FLUX>(G, ul, ur, n, f);
-		#pragma unroll
-		for(int k = 0; k < 4; k++) f[k] *= len;
+		inviscid_flux_len<FLUX>(G, ul, ur, n, len, f);
 
 		if(VISC != SV_NONE) {
 			// order 2: primitive states (up / ghost ug); order 1: conserved states
@@ -1342,9 +1343,7 @@ __device__ __forceinline__ void fz_body(const DevMesh& M, const DevPhys& P, cons
 				ghost_c(P, M.bf_bc[bf], ul, n, ur);
 			}
 		}
-		inviscid_flux<FLUX>(G, ul, ur, n, f);
-		#pragma unroll
-		for(int k = 0; k < 4; k++) f[k] *= flen;
+		inviscid_flux_len<FLUX>(G, ul, ur, n, flen, f);
 		if(DT) {
 			const double ci = sound_speed_cons(G, ul), cj = sound_speed_cons(G, ur);
 			const double vni = div_rn(dot2(&ul[1],n), ul[0]);

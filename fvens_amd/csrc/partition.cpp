@@ -4,6 +4,7 @@
 #include "partition.hpp"
 #include <algorithm>
 #include <cmath>
+#include <cstdlib>
 #include <map>
 #include <numeric>
 #include <stdexcept>
@@ -73,10 +74,13 @@ namespace {
 /// one bisection of the cells `sub` (global ids) of the dual graph into `nl` and the rest: grown
 /// breadth-first from a pseudo-peripheral cell (farthest from the farthest of the first cell, every
 /// component in turn), then improved by passes of balanced boundary swaps (Kernighan-Lin gains)
-void graphBisect(const fvhip_mesh& m, const std::vector<int>& sub, int nl, std::vector<int>& side,
+void graphBisect(const fvhip_mesh& m, const std::vector<int>& sub, long long tw, const int* wt, std::vector<int>& side,
                  std::vector<int>& loc, std::vector<int>& dist)
 {
 	const int n = static_cast<int>(sub.size());
+	auto w = [&](int a) { return wt ? wt[sub[a]] : 1; };   // weight of local cell a
+	long long wmax = 1;
+	for(int a = 0; a < n; a++) wmax = std::max<long long>(wmax, w(a));
 	for(int i = 0; i < n; i++) loc[sub[i]] = i;
 	auto nbrs = [&](int c, int* out) {          // neighbours of global cell c inside `sub` (local ids)
 		int k = 0;
@@ -116,8 +120,14 @@ void graphBisect(const fvhip_mesh& m, const std::vector<int>& sub, int nl, std::
 		bfs(root);
 		for(const int a : queue) { done[a] = 1; order.push_back(a); dist[a] = -1; }
 	}
+	// side 0 = the BFS prefix whose weight comes closest to the target tw
 	for(int i = 0; i < n; i++) side[i] = 1;
-	for(int i = 0; i < nl; i++) side[order[i]] = 0;
+	long long w0 = 0;
+	for(int i = 0; i < n; i++) {
+		const int a = order[i];
+		if(w0 + w(a) > tw && (w0 + w(a) - tw) >= (tw - w0)) break;
+		side[a] = 0; w0 += w(a);
+	}
 	// refinement: swap the best-gain boundary cells of the two sides while the swap cuts edges
 	auto gain = [&](int a) {
 		int nb[4];
@@ -143,13 +153,17 @@ void graphBisect(const fvhip_mesh& m, const std::vector<int>& sub, int nl, std::
 			int nb[4], adj = 0;
 			const int k = nbrs(sub[a], nb);
 			for(int j = 0; j < k; j++) if(nb[j] == b) adj = 1;
-			if(ga + gb - 2*adj <= 0) {
+			// a swap of unequal weights may move the balance by at most the largest weight
+			const long long w0n = w0 - w(a) + w(b);
+			const bool balanced = w0n == w0 || std::llabs(w0n - tw) <= std::max(std::llabs(w0 - tw), wmax);
+			if(ga + gb - 2*adj <= 0 || !balanced) {
 				// the stale-sorted lists ran out of improving pairs
 				if(ga <= 0 && -cand[0][i0].first <= 0) break;
 				if(ga < gb) i0++; else i1++;
 				continue;
 			}
 			side[a] = 1; side[b] = 0;
+			w0 = w0n;
 			i0++; i1++; moved++;
 		}
 		if(!moved) break;
@@ -179,50 +193,58 @@ void graphBisect(const fvhip_mesh& m, const std::vector<int>& sub, int nl, std::
 		for(int a = 0; a < n; a++)
 			if(comp[a] != big[side[a]]) { side[a] = 1 - side[a]; flipped = true; }
 		if(!flipped) break;
-		int n0 = 0;
-		for(int a = 0; a < n; a++) n0 += side[a] == 0;
-		while(n0 != nl) {
-			const int from = n0 > nl ? 0 : 1;
+		// restore the balance: move the best-gain cell off the heavier side while that brings side 0's
+		// weight closer to the target
+		w0 = 0;
+		for(int a = 0; a < n; a++) if(side[a] == 0) w0 += w(a);
+		while(w0 != tw) {
+			const int from = w0 > tw ? 0 : 1;
 			int best = -1, bg = -1000;
 			for(int a = 0; a < n; a++) {
 				if(side[a] != from) continue;
+				const long long w0n = from == 0 ? w0 - w(a) : w0 + w(a);
+				if(std::llabs(w0n - tw) >= std::llabs(w0 - tw)) continue;
 				const int g = gain(a);
 				if(g > bg) { bg = g; best = a; }
 			}
 			if(best < 0) break;
 			side[best] = 1 - from;
-			n0 += from == 0 ? -1 : 1;
+			w0 += from == 0 ? -w(best) : w(best);
 		}
 	}
 	for(int i = 0; i < n; i++) loc[sub[i]] = -1;
 }
 
-void graphRecurse(const fvhip_mesh& m, std::vector<int>& sub, int p0, int np, int* part,
+void graphRecurse(const fvhip_mesh& m, std::vector<int>& sub, int p0, int np, const int* wt, int* part,
                   std::vector<int>& loc, std::vector<int>& dist)
 {
 	if(np == 1) { for(const int c : sub) part[c] = p0; return; }
 	const int npl = np/2;
 	const int n = static_cast<int>(sub.size());
-	const int nl = static_cast<int>((static_cast<long long>(n)*npl)/np);
+	long long W = 0;
+	for(const int c : sub) W += wt ? wt[c] : 1;
 	std::vector<int> side(n);
-	graphBisect(m, sub, nl, side, loc, dist);
+	graphBisect(m, sub, (W*npl)/np, wt, side, loc, dist);
 	std::vector<int> a, b;
 	for(int i = 0; i < n; i++) (side[i] == 0 ? a : b).push_back(sub[i]);
 	sub.clear(); sub.shrink_to_fit();
-	graphRecurse(m, a, p0, npl, part, loc, dist);
-	graphRecurse(m, b, p0 + npl, np - npl, part, loc, dist);
+	graphRecurse(m, a, p0, npl, wt, part, loc, dist);
+	graphRecurse(m, b, p0 + npl, np - npl, wt, part, loc, dist);
 }
 
 }
 
-std::vector<int> partitionGraph(const fvhip_mesh& m, int nparts)
+std::vector<int> partitionGraph(const fvhip_mesh& m, int nparts, const int* weight)
 {
 	if(nparts < 1) throw std::invalid_argument("partitionGraph: nparts < 1");
 	if(m.nconnface != 0) throw std::invalid_argument("partitionGraph: expects the single-domain mesh");
 	checkLinearCells(m, "partitionGraph");
+	if(weight)
+		for(int e = 0; e < m.nelem; e++)
+			if(weight[e] < 1 || weight[e] > 4096) throw std::invalid_argument("partitionGraph: cell weights must lie in 1..4096");
 	std::vector<int> part(m.nelem, 0), sub(m.nelem), loc(m.nelem, -1), dist(m.nelem, -1);
 	std::iota(sub.begin(), sub.end(), 0);
-	if(m.nelem > 0) graphRecurse(m, sub, 0, nparts, part.data(), loc, dist);
+	if(m.nelem > 0) graphRecurse(m, sub, 0, nparts, weight, part.data(), loc, dist);
 	return part;
 }
 

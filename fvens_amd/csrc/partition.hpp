@@ -89,8 +89,11 @@ std::vector<int> partitionRCB(const double* rc, int ncell, int nparts);
 /// Graph partition of the cell dual graph (the reference's Scotch SCOTCH_graphPart on the same graph,
 /// meshpartitioning.cpp:376-458; Scotch is absent from the image): recursive bisection, each grown
 /// breadth-first from a pseudo-peripheral cell and refined by balanced Kernighan-Lin boundary swaps.
-/// Part sizes as RCB's (exact split per level); deterministic.
-std::vector<int> partitionGraph(const fvhip_mesh& m, int nparts);
+/// Part sizes as RCB's (exact split per level); deterministic. weight (optional, [nelem], 1..4096):
+/// cell weights -- each bisection then splits the weight instead of the cell count, to within the
+/// largest weight (the hot path's cost per cell grows with its face count: weight = nfael balances the
+/// fused residual's time across ranks of a mixed triangle/quad mesh)
+std::vector<int> partitionGraph(const fvhip_mesh& m, int nparts, const int* weight = nullptr);
 
 /// interior faces whose two cells lie in different parts
 long long edgeCut(const fvhip_mesh& m, const int* part);

@@ -141,6 +141,11 @@ int fvhip_partition_rcb(const fvhip_mesh* mesh, int nparts, int* part);
  *  SCOTCH_graphPart, mesh/meshpartitioning.cpp:376-458): recursive bisection grown breadth-first from
  *  a pseudo-peripheral cell and refined by balanced Kernighan-Lin boundary swaps */
 int fvhip_partition_graph(const fvhip_mesh* mesh, int nparts, int* part);
+/** The same with cell weights weight[nelem] in 1..4096 (NULL: 1): every bisection splits the total
+ *  weight to within the largest weight. Not a reference option (its Scotch graph carries no vertex
+ *  weights, meshpartitioning.cpp:443-444): weight = the cell's face count balances the fused residual's
+ *  time per rank on a mixed triangle/quadrangle mesh (a quadrangle costs ~1.3 triangles) */
+int fvhip_partition_graph_weighted(const fvhip_mesh* mesh, int nparts, const int* weight, int* part);
 /** Number of interior faces cut by a partition */
 long long fvhip_partition_edge_cut(const fvhip_mesh* mesh, const int* part);
 /** Halo description of one rank (host only). counts[6] = {owned, ghosts, boundary faces, faces,

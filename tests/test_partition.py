@@ -211,3 +211,29 @@ def test_graph_partition(nparts):
     assert ncomp == nparts
     # edge cut matches a direct count
     assert cut == int((part[L] != part[R]).sum())
+
+
+@pytest.mark.parametrize("nparts", [2, 3, 8])
+def test_graph_partition_weighted(nparts):
+    """cell weights (fvhip_partition_graph_weighted; "faces" = the cell's face count): every part's
+    weight within the largest weight per bisection level of the ideal share, parts connected,
+    deterministic; unit weights give exactly the unweighted partition"""
+    m = fa.UMesh.naca_ogrid(128, 8, 24)           # quadrangle layers at the wall, triangles outside
+    w = fa.cell_face_counts(m)
+    assert set(np.unique(w)) == {3, 4}
+    part = fa.partition_graph(m, nparts, weights="faces")
+    np.testing.assert_array_equal(part, fa.partition_graph(m, nparts, weights=w))
+    ws = np.bincount(part, weights=w, minlength=nparts)
+    levels = int(np.ceil(np.log2(nparts)))
+    assert ws.max() - ws.min() <= 2 * 4 * levels + nparts
+    nb = m.nbface
+    L, R = m.intfac[nb:, 0], m.intfac[nb:, 1]
+    same = part[L] == part[R]
+    import scipy.sparse as sps
+    from scipy.sparse.csgraph import connected_components
+    g = sps.coo_matrix((np.ones(same.sum()), (L[same], R[same])), shape=(m.nelem, m.nelem))
+    assert connected_components(g, directed=False)[0] == nparts
+    np.testing.assert_array_equal(fa.partition_graph(m, nparts, weights=np.ones(m.nelem, np.int32)),
+                                  fa.partition_graph(m, nparts))
+    with pytest.raises(RuntimeError):
+        fa.partition_graph(m, nparts, weights=np.zeros(m.nelem, np.int32))

@@ -6,7 +6,7 @@ timed ALONE with its halo already current (FVHIP_RES_HALO_READY: layer-1 ghost g
 patch, no exchange). Reports per rank: owned / ghost cells, patches and interior-patch fraction, ms
 per residual and its kernels; per N: the edge cut, the slowest rank (the compute floor of an N-GPU
 step if the exchange is hidden) and the speed-up that floor implies over the 1-GPU residual.
-    python tools/scale_proxy.py [--parts 2 4 8] [--rec VANALBADA|VENKATAKRISHNAN] [--steps 200]
+    python tools/scale_proxy.py [--parts 2 4 8] [--rec VANALBADA|VENKATAKRISHNAN] [--steps 200] [--weights faces|none]
 """
 import argparse
 import json
@@ -49,6 +49,8 @@ def main():
     ap.add_argument("--steps", type=int, default=200)
     ap.add_argument("--preheat", type=float, default=0.3, help="seconds of untimed residuals before each timing")
     ap.add_argument("--scale", type=int, default=1)
+    ap.add_argument("--weights", choices=["faces", "none"], default="faces",
+                    help="graph partition weights: the cells' face counts (bench.py's default) or none (equal cells)")
     args = ap.parse_args()
     import torch
     torch.cuda.set_device(0)
@@ -70,7 +72,7 @@ def main():
           flush=True)
     for nparts in args.parts:
         tp = time.time()
-        part = fa.partition_graph(mesh, nparts)
+        part = fa.partition_graph(mesh, nparts, weights=None if args.weights == "none" else "faces")
         tp = time.time() - tp
         sps = [fa.FlowFV(mesh, p, n, partition=part, rank=k) for k in range(nparts)]
         dus, drs, dts = [], [], []
@@ -96,7 +98,7 @@ def main():
         for sp in sps:
             sp.close()
         worst = max(r["ms_per_residual"] for r in ranks)
-        print(json.dumps({"parts": nparts, "partitioner": "graph", "partition_s": round(tp, 2),
+        print(json.dumps({"parts": nparts, "partitioner": "graph", "weights": args.weights, "partition_s": round(tp, 2),
                           "edge_cut": fa.partition_edge_cut(mesh, part),
                           "edge_cut_rcb": fa.partition_edge_cut(mesh, fa.partition_rcb(mesh, nparts)),
                           "slowest_rank_ms": worst, "mean_rank_ms": round(float(np.mean([r["ms_per_residual"] for r in ranks])), 5),
