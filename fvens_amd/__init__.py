@@ -85,6 +85,7 @@ class ImplicitConfig:
     prec_gs: bool = False           # multicolour block Gauss-Seidel sweeps instead of block-Jacobi
     prec_lines: bool = False        # line-implicit (block-tridiagonal along strongly coupled lines)
     line_threshold: float = 0.0     # strongest/weakest coupling ratio for a cell to join a line (0: 4)
+    prec_ilu: bool = False          # block ILU(0) in multicolour order (-sub_pc_type ilu)
 
     def _struct(self):
         c = _ffi.FvImplicitConfig()
@@ -96,6 +97,7 @@ class ImplicitConfig:
         c.prec_gs = int(self.prec_gs)
         c.prec_lines = int(self.prec_lines)
         c.line_threshold = float(self.line_threshold)
+        c.prec_ilu = int(self.prec_ilu)
         return c
 
 
@@ -392,6 +394,19 @@ class FlowFV:
         """z = M^-1 v, M the block-tridiagonal line part of the block operator (prec_lines)"""
         check(_ffi.lib().fvhip_line_precondition_device(self._h, *[ctypes.c_void_p(p) for p in (d_diag, d_lower, d_upper)],
                                                         float(line_threshold), ctypes.c_void_p(d_v), ctypes.c_void_p(d_z)))
+
+    def ilu_precondition_device(self, d_diag, d_lower, d_upper, d_v, d_z):
+        """z = M^-1 v, M the block ILU(0) of the block operator in colour order (prec_ilu)"""
+        check(_ffi.lib().fvhip_ilu_precondition_device(self._h, *[ctypes.c_void_p(p) for p in
+                                                                  (d_diag, d_lower, d_upper, d_v, d_z)]))
+
+    def colouring(self):
+        """(colour per owned cell in internal order, number of pairwise-adjacent cell triples)"""
+        nc = np.zeros(1, np.int32)
+        tr = ctypes.c_longlong(0)
+        col = np.zeros(self.nown, np.int32)
+        check(_ffi.lib().fvhip_colouring(self._h, iptr(nc), iptr(col), ctypes.byref(tr)))
+        return col, int(tr.value)
 
     def lines(self, line_threshold=0.0):
         """the preconditioner's lines: list of (cells, faces) in line order, internal cell ids; faces[k] =

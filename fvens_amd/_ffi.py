@@ -40,7 +40,7 @@ class FvImplicitConfig(ctypes.Structure):
                 ("lin_rtol", ctypes.c_double), ("lin_maxit", ctypes.c_int), ("restart", ctypes.c_int),
                 ("prec_sweeps", ctypes.c_int), ("min_relax", ctypes.c_double),
                 ("prec_single", ctypes.c_int), ("prec_gs", ctypes.c_int), ("prec_lines", ctypes.c_int),
-                ("line_threshold", ctypes.c_double)]
+                ("line_threshold", ctypes.c_double), ("prec_ilu", ctypes.c_int)]
 
 
 class FvSolveStats(ctypes.Structure):
@@ -114,6 +114,8 @@ _SIGS = {
     "fvhip_line_precondition_device": (ctypes.c_int, [ctypes.c_void_p] + [ctypes.c_void_p] * 3 +
                                        [ctypes.c_double, ctypes.c_void_p, ctypes.c_void_p]),
     "fvhip_lines": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_double, c_int_p, c_int_p, c_int_p, c_int_p]),
+    "fvhip_ilu_precondition_device": (ctypes.c_int, [ctypes.c_void_p] * 6),
+    "fvhip_colouring": (ctypes.c_int, [ctypes.c_void_p, c_int_p, c_int_p, ctypes.POINTER(ctypes.c_longlong)]),
     "fvhip_group_matfree_set_state_device": (ctypes.c_int, [ctypes.c_void_p, _vpp, _vpp, _vpp]),
     "fvhip_group_matfree_apply_device": (ctypes.c_int, [ctypes.c_void_p, _vpp, _vpp]),
     "fvhip_matfree_set_state": (ctypes.c_int, [ctypes.c_void_p, c_dbl_p, c_dbl_p, c_dbl_p]),

@@ -690,10 +690,30 @@ struct fvhip_ctx
 	/// cells in internal (Hilbert) order over interior faces; ghost cells are not coloured (within a
 	/// sweep they hold the values of the last exchange)
 	std::vector<int> gs_colour_start;
+	std::vector<int> gs_colour;          ///< colour of every owned cell (also the ILU(0) order)
+	long long gs_triples = 0;            ///< owned cells sharing faces pairwise three at a time (ILU(0) fill off the diagonal)
 	int* d_gs_cells = nullptr;
+	int* d_gs_colour = nullptr;
 	void ensureColouring() {
 		if(d_gs_cells) return;
 		const int N = L.ncell;
+		auto nbr = [&](int c, int j) {        // owned neighbour across interior face j of c, else -1
+			const int code = L.cell_rfaces[4*static_cast<size_t>(c)+j];
+			if(code < 0 || (code >> 1) < L.nbface) return -1;
+			const int nb = L.cell_nbr_fo[4*static_cast<size_t>(c)+j];
+			return (nb >= 0 && nb < N) ? nb : -1;
+		};
+		gs_triples = 0;
+		for(int c = 0; c < N; c++)
+			for(int j = 0; j < 4; j++) {
+				const int a = nbr(c, j);
+				if(a <= c) continue;
+				for(int k = j + 1; k < 4; k++) {
+					const int b = nbr(c, k);
+					if(b <= c) continue;
+					for(int m = 0; m < 4; m++) if(nbr(a, m) == b) gs_triples++;
+				}
+			}
 		std::vector<int> col(static_cast<size_t>(N), -1);
 		int ncol = 0;
 		for(int c = 0; c < N; c++) {
@@ -716,6 +736,22 @@ struct fvhip_ctx
 		std::vector<int> pos(gs_colour_start.begin(), gs_colour_start.end() - 1);
 		for(int c = 0; c < N; c++) cells[pos[col[c]]++] = c;   // ascending within a colour
 		d_gs_cells = upload(cells, owned);
+		d_gs_colour = upload(col, owned);
+		gs_colour = std::move(col);
+	}
+	/// block ILU(0) factorisation in colour order (fvhip_implicit_config::prec_ilu): dinv = the inverted
+	/// pivot blocks Dt^-1, colour after colour (each colour reads the earlier colours' pivots)
+	void iluFactor(const double* diag, const double* lower, const double* upper, double* dinv, hipStream_t st = nullptr) {
+		if(!st) st = stream;
+		ensureColouring();
+		const int nc = static_cast<int>(gs_colour_start.size()) - 1;
+		timed_on(st, "k_ilu_factor", [&]{
+			for(int q = 0; q < nc; q++) {
+				const int b = gs_colour_start[q], n = gs_colour_start[q+1] - b;
+				launch_ilu_factor_colour(L.ncell, L.nbface, J.cell_rfaces, J.cell_nbr_fo, d_gs_colour, q, diag, lower, upper,
+				                         dinv, d_gs_cells + b, n, st);
+			}
+		});
 	}
 
 	/// lines of the line-implicit preconditioner (fvhip_implicit_config::prec_lines), built on first use

@@ -96,6 +96,7 @@ struct LinOp
 	bool single = false;                      ///< preconditioner blocks in fp32 (iw.sdinv/slo/sup)
 	bool gs = false;                          ///< multicolour block Gauss-Seidel instead of Jacobi
 	bool lines = false;                       ///< line-implicit (block-tridiagonal along lines)
+	bool ilu = false;                         ///< block ILU(0) in multicolour order
 	double line_thr = 0.0;
 	int sweeps = 1;
 	std::vector<const double*> D, Lo, Up;     ///< per handle: diagonal / lower / upper blocks
@@ -116,6 +117,7 @@ struct LinOp
 	void precondition(const ArrayOf& v, const ArrayOf& z) {
 		if(gs) { gaussSeidel(v, z); return; }
 		if(lines) { lineSweeps(v, z); return; }
+		if(ilu) { iluSweeps(v, z); return; }
 		const ArrayOf aux = [&](size_t i) { return S.hs[i]->iw.aux; };
 		auto buf = [&](int k) -> const ArrayOf& { return ((sweeps - 1 - k) % 2 == 0) ? z : aux; };
 		S.each([&](size_t i, fvhip_ctx* h) {
@@ -160,6 +162,36 @@ struct LinOp
 			});
 		}
 	}
+	/// z = M^-1 v for the block ILU(0) M = (Dt + L) Dt^-1 (Dt + U) in colour order: a forward pass over
+	/// the colours from z = 0 gives y = (Dt + L)^-1 v, the backward pass z_i = Dt_i^-1 (v_i - sum_{earlier}
+	/// A_ik y_k - sum_{later} A_ij z_j) = y_i - Dt_i^-1 sum_{later} A_ij z_j -- both are the Gauss-Seidel
+	/// colour kernel with the ILU pivots. Ghost rows stay zero (no exchange: block-Jacobi across ranks)
+	void iluApply(const ArrayOf& v, const ArrayOf& z) {
+		S.each([&](size_t i, fvhip_ctx* h) {
+			exact::launch_fill(z(i), 0.0, 4LL*(h->L.ncell + h->L.nghost), h->stream);
+			const int nc = static_cast<int>(h->gs_colour_start.size()) - 1;
+			h->timed("k_ilu_solve", [&]{
+				for(int q = 0; q < 2*nc; q++) {
+					const int col = q < nc ? q : 2*nc - 1 - q;
+					const int b = h->gs_colour_start[col], n = h->gs_colour_start[col+1] - b;
+					if(single) launch_bgs_colour(h->J, h->iw.sdinv, h->iw.slo, h->iw.sup, v(i), z(i), h->d_gs_cells + b, n, h->stream);
+					else launch_bgs_colour(h->J, h->iw.dinv, Lo[i], Up[i], v(i), z(i), h->d_gs_cells + b, n, h->stream);
+				}
+			});
+		});
+	}
+	/// ILU(0), then `sweeps` - 1 corrections z += M^-1 (v - A z) (A with the ghost coupling)
+	void iluSweeps(const ArrayOf& v, const ArrayOf& z) {
+		const ArrayOf aux = [&](size_t i) { return S.hs[i]->iw.aux; };
+		const ArrayOf t = [&](size_t i) { return S.hs[i]->iw.t; };
+		iluApply(v, z);
+		for(int k = 1; k < sweeps; k++) {
+			blocks(z, t);
+			S.each([&](size_t i, fvhip_ctx* h) { launch_axpby(4LL*h->L.ncell, 1.0, v(i), -1.0, t(i), h->stream); });
+			iluApply(t, aux);
+			S.each([&](size_t i, fvhip_ctx* h) { launch_add_rows(h->L.ncell, aux(i), z(i), h->stream); });
+		}
+	}
 	/// z = M^-1 v with M the block-tridiagonal line part of A (factorised in setup), then `sweeps` - 1
 	/// corrections z += M^-1 (v - A z) (A with the ghost coupling: block-Jacobi across ranks)
 	void lineSweeps(const ArrayOf& v, const ArrayOf& z) {
@@ -185,14 +217,15 @@ struct LinOp
 				h->timed("k_line_factor", [&]{ launch_line_factor(h->lines, D[i], Lo[i], Up[i], h->stream); });
 				return;
 			}
-			h->timed("k_bjac_invert", [&]{ launch_bjac_invert(h->L.ncell, D[i], h->iw.dinv, h->stream); });
+			if(ilu) h->iluFactor(D[i], Lo[i], Up[i], h->iw.dinv);
+			else h->timed("k_bjac_invert", [&]{ launch_bjac_invert(h->L.ncell, D[i], h->iw.dinv, h->stream); });
 			if(gs) h->ensureColouring();
 			if(single) {
 				h->ensureSinglePrecond();
 				const long long nf = 16LL*std::max(h->L.ninface, 0);
 				h->timed("k_to_single", [&]{
 					launch_to_single(16LL*h->L.ncell, h->iw.dinv, h->iw.sdinv, h->stream);
-					if(sweeps > 1 || gs) {
+					if(sweeps > 1 || gs || ilu) {
 						launch_to_single(nf, Lo[i], h->iw.slo, h->stream);
 						launch_to_single(nf, Up[i], h->iw.sup, h->stream);
 					}
@@ -345,7 +378,9 @@ static void backwardEuler(System& S, const std::vector<double*>& us, const fvhip
 	A.gs = c.prec_gs != 0;
 	A.lines = c.prec_lines != 0;
 	A.line_thr = c.line_threshold;
+	A.ilu = c.prec_ilu != 0;
 	if(A.lines && (A.gs || A.single)) throw std::invalid_argument("prec_lines does not combine with prec_gs / prec_single");
+	if(A.ilu && (A.gs || A.lines)) throw std::invalid_argument("prec_ilu does not combine with prec_gs / prec_lines");
 	for(fvhip_ctx* h : S.hs) { A.D.push_back(h->iw.jd); A.Lo.push_back(h->iw.jlo); A.Up.push_back(h->iw.jup); }
 	std::vector<const double*> cu(us.begin(), us.end());
 	std::vector<double*> rs, dts;
@@ -515,6 +550,33 @@ int fvhip_line_precondition_device(fvhip_handle h, const double* d_diag, const d
 		launch_line_solve(h->lines, d_v, d_z, h->stream);
 		HC(hipGetLastError());
 		HC(hipStreamSynchronize(h->stream));
+	});
+}
+
+int fvhip_ilu_precondition_device(fvhip_handle h, const double* d_diag, const double* d_lower, const double* d_upper,
+                                  const double* d_v, double* d_z)
+{
+	return guard([&] {
+		if(!d_diag || !d_v || !d_z || (h->L.ninface > 0 && (!d_lower || !d_upper))) throw std::invalid_argument("null argument");
+		System S = single(h);
+		h->ensureImplicit(1);
+		LinOp A{S};
+		A.ilu = true;
+		A.D = {d_diag}; A.Lo = {d_lower}; A.Up = {d_upper};
+		A.setup();
+		A.precondition([&](size_t) { return const_cast<double*>(d_v); }, [&](size_t) { return d_z; });
+		HC(hipGetLastError());
+		S.sync();
+	});
+}
+
+int fvhip_colouring(fvhip_handle h, int* ncolours, int* colour, long long* triples)
+{
+	return guard([&] {
+		h->ensureColouring();
+		if(ncolours) *ncolours = static_cast<int>(h->gs_colour_start.size()) - 1;
+		if(colour) std::copy(h->gs_colour.begin(), h->gs_colour.end(), colour);
+		if(triples) *triples = h->gs_triples;
 	});
 }
 

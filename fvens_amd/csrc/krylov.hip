@@ -108,6 +108,57 @@ void k_bjac_invert(int n, const double* __restrict__ diag, double* __restrict__ 
 	st16(dinv + 16*static_cast<size_t>(c), b);
 }
 
+/// c = a b for row-major 4x4 blocks
+__device__ __forceinline__ void mm4(const double (&a)[4][4], const double (&b)[4][4], double (&c)[4][4])
+{
+	#pragma unroll
+	for(int i = 0; i < 4; i++)
+		#pragma unroll
+		for(int j = 0; j < 4; j++) c[i][j] = a[i][0]*b[0][j] + a[i][1]*b[1][j] + a[i][2]*b[2][j] + a[i][3]*b[3][j];
+}
+
+/// Block ILU(0) of the operator in multicolour order (prec_ilu), the factorisation of colour q: for each
+/// listed cell i
+///     Dt_i = A_ii - sum_{k ~ i, colour(k) < q} A_ik Dt_k^-1 A_ki,     dinv_i = Dt_i^-1
+/// over the owned neighbours across interior faces (ghost couplings are dropped: block-Jacobi across
+/// ranks, as PETSc's bjacobi + ilu). The product of row i's lower factor with a neighbour's upper
+/// factor lands only on the diagonal unless three cells pairwise share faces, so this D-ILU form is
+/// ILU(0) itself on meshes without such triples (fvhip_colouring reports their count). Face blocks:
+/// lower[fi] = A[R][L], upper[fi] = A[L][R]; rfaces code = face << 1 | cell-is-R.
+__global__ __launch_bounds__(256)
+void k_ilu_factor_colour(int ncell, int nbface, const int4* __restrict__ rfaces, const int4* __restrict__ nbrs,
+                         const int* __restrict__ colour, int q, const double* __restrict__ diag,
+                         const double* __restrict__ lower, const double* __restrict__ upper, double* dinv,
+                         const int* __restrict__ cells, int n)
+{
+	const int t = blockIdx.x*blockDim.x + threadIdx.x;
+	if(t >= n) return;
+	const int c = cells[t];
+	double a[4][4];
+	ld16(diag + 16*static_cast<size_t>(c), a);
+	const int4 fc = rfaces[c], nb = nbrs[c];
+	const int codes[4] = {fc.x, fc.y, fc.z, fc.w};
+	const int ks[4] = {nb.x, nb.y, nb.z, nb.w};
+	for(int j = 0; j < 4; j++) {
+		const int code = codes[j], k = ks[j];
+		if(code < 0 || (code >> 1) < nbface || k < 0 || k >= ncell || colour[k] >= q) continue;
+		const size_t fi = static_cast<size_t>((code >> 1) - nbface);
+		double aik[4][4], aki[4][4], dk[4][4], tk[4][4], p[4][4];
+		ld16(((code & 1) ? lower : upper) + 16*fi, aik);
+		ld16(((code & 1) ? upper : lower) + 16*fi, aki);
+		ld16(dinv + 16*static_cast<size_t>(k), dk);
+		mm4(dk, aki, tk);
+		mm4(aik, tk, p);
+		#pragma unroll
+		for(int r = 0; r < 4; r++)
+			#pragma unroll
+			for(int s = 0; s < 4; s++) a[r][s] -= p[r][s];
+	}
+	double b[4][4];
+	inv4(a, b);
+	st16(dinv + 16*static_cast<size_t>(c), b);
+}
+
 /// y = B x for a row-major fp32 4x4 block, entries widened to fp64
 __device__ __forceinline__ void blk_mv(const float* __restrict__ B, const double4 x, double* y)
 {
@@ -447,6 +498,13 @@ void launch_add_rows(int n, const double* e, double* z, hipStream_t s)
 
 void launch_bjac_invert(int n, const double* diag, double* dinv, hipStream_t s)
 { if(n > 0) k_bjac_invert<<<nblk(n,256), 256, 0, s>>>(n, diag, dinv); }
+void launch_ilu_factor_colour(int ncell, int nbface, const int4* rfaces, const int4* nbrs, const int* colour, int q,
+                              const double* diag, const double* lower, const double* upper, double* dinv,
+                              const int* cells, int n, hipStream_t s)
+{
+	if(n > 0) k_ilu_factor_colour<<<nblk(n,256), 256, 0, s>>>(ncell, nbface, rfaces, nbrs, colour, q, diag, lower, upper,
+	                                                           dinv, cells, n);
+}
 void launch_bjac_apply(int n, const double* dinv, const double* x, double* y, hipStream_t s)
 { if(n > 0) k_bjac_apply<double><<<nblk(n,256), 256, 0, s>>>(n, dinv, x, y); }
 void launch_bjac_apply(int n, const float* dinv, const double* x, double* y, hipStream_t s)

@@ -68,6 +68,11 @@ void launch_line_factor(const LineSet& Ls, const double* diag, const double* low
 void launch_line_solve(const LineSet& Ls, const double* v, double* z, hipStream_t s);
 /// z += e over n cells
 void launch_add_rows(int n, const double* e, double* z, hipStream_t s);
+/// block ILU(0) in multicolour order, colour q's rows: dinv[c] = (A_cc - sum_{earlier-colour owned
+/// neighbours k} A_ck dinv[k] A_kc)^-1 for the n listed cells (k_ilu_factor_colour)
+void launch_ilu_factor_colour(int ncell, int nbface, const int4* rfaces, const int4* nbrs, const int* colour, int q,
+                              const double* diag, const double* lower, const double* upper, double* dinv,
+                              const int* cells, int n, hipStream_t s);
 /// dinv[c] = diag[c]^-1 (Gauss-Jordan with row pivoting), c < ncell
 void launch_bjac_invert(int ncell, const double* diag, double* dinv, hipStream_t s);
 /// y[c] = dinv[c] x[c]

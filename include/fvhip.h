@@ -277,6 +277,11 @@ typedef struct fvhip_implicit_config {
 	                             residual-correction sweeps. Not combined with prec_gs / prec_single. */
 	double line_threshold;    /* a cell joins a line if its strongest coupling (face length / centre distance)
 	                             is at least this many times its weakest (0: 4.0) */
+	int prec_ilu;             /* 1: block ILU(0) of the assembled operator in multicolour order (the reference's
+	                             -pc_type bjacobi -sub_pc_type ilu, opts.solverc / flatplate.solverc, with a colour
+	                             order instead of PETSc's row order): one forward and one backward colour pass per
+	                             application, block-Jacobi across ranks; prec_sweeps - 1 further residual-correction
+	                             sweeps. Not combined with prec_gs / prec_lines. */
 } fvhip_implicit_config;
 
 typedef struct fvhip_solve_stats {
@@ -305,6 +310,14 @@ int fvhip_gmres_blocks_device(fvhip_handle h, const double* d_diag, const double
  *  (0: 4), then z = M^-1 v (internal order, [ncell][4]). Blocks as in fvhip_gmres_blocks_device. */
 int fvhip_line_precondition_device(fvhip_handle h, const double* d_diag, const double* d_lower, const double* d_upper,
                                    double line_threshold, const double* d_v, double* d_z);
+/** The block ILU(0) preconditioner alone (fvhip_implicit_config::prec_ilu): factorisation of the block
+ *  operator in the colour order of fvhip_colouring, then z = M^-1 v (internal order, [ncell][4]) */
+int fvhip_ilu_precondition_device(fvhip_handle h, const double* d_diag, const double* d_lower, const double* d_upper,
+                                  const double* d_v, double* d_z);
+/** The colouring of the owned cells that prec_gs and prec_ilu use (greedy over interior faces in internal
+ *  order): *ncolours, colour [ncell] (internal order; may be NULL), and *triples = the number of owned
+ *  cells sharing faces pairwise three at a time (0: the colour-order D-ILU is exactly ILU(0)) */
+int fvhip_colouring(fvhip_handle h, int* ncolours, int* colour, long long* triples);
 /** The lines of that preconditioner (pieces of at most 256 cells), longest first: *nlines; start
  *  [nlines+1] into cells [ncell] (internal ids, line order) and faces [ncell] (link of a cell to the previous
  *  one: interior face fi << 1 | (previous cell is the face's R), -1 for a line's first cell); NULL

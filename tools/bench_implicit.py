@@ -45,6 +45,8 @@ def main():
     ap.add_argument("--prec-single", action="store_true", help="preconditioner blocks in fp32")
     ap.add_argument("--gs", action="store_true", help="multicolour block Gauss-Seidel sweeps")
     ap.add_argument("--lines", action="store_true", help="line-implicit preconditioner")
+    ap.add_argument("--ilu", action="store_true", help="block ILU(0) in multicolour order")
+    ap.add_argument("--operators", default="assembled,matrix-free")
     args = ap.parse_args()
 
     import torch
@@ -64,13 +66,14 @@ def main():
         mesh, dims = c4_mesh(fa, args.scale)
     for out in implicit_steps(mesh, args.case, steps=args.steps, warmup=args.warmup, init_steps=args.init_steps,
                               cfl=args.cfl, restart=args.restart, lin_maxit=args.lin_maxit, sweeps=args.sweeps,
-                              single=args.prec_single, gs=args.gs, lines=args.lines):
+                              single=args.prec_single, gs=args.gs, lines=args.lines, ilu=args.ilu,
+                              operators=tuple(o == "matrix-free" for o in args.operators.split(","))):
         out["dims"] = dims
         print(json.dumps(out), flush=True)
 
 
 def implicit_steps(mesh, case="naca", steps=5, warmup=2, init_steps=10, cfl=25.0, restart=30, lin_maxit=30,
-                   sweeps=4, single=False, gs=False, operators=(False, True), lines=False):
+                   sweeps=4, single=False, gs=False, operators=(False, True), lines=False, ilu=False):
     """time `steps` second-order backward-Euler steps per operator kind (False: assembled, True:
     matrix-free) after a first-order start; yields one dict per operator"""
     import torch
@@ -90,7 +93,7 @@ def implicit_steps(mesh, case="naca", steps=5, warmup=2, init_steps=10, cfl=25.0
     # second-order main solve. Its CFL ramps (25/50 -> 500) blow up on this O-grid's 1e-5 wall cells
     # during the start-up transient (measured), so the CFL is held fixed
     lin = dict(lin_rtol=1e-2, lin_maxit=lin_maxit, restart=restart, prec_sweeps=sweeps, prec_single=single,
-               prec_gs=gs, prec_lines=lines)
+               prec_gs=gs, prec_lines=lines, prec_ilu=ilu)
     dinit = torch.tensor(u0, dtype=torch.float64, device="cuda")
     st0, _ = sp1.steady_backward_euler_device(dinit.data_ptr(), fa.ImplicitConfig(
         cflinit=cfl, cflfin=cfl, tol=0.0, maxiter=init_steps, **lin))
@@ -113,7 +116,7 @@ def implicit_steps(mesh, case="naca", steps=5, warmup=2, init_steps=10, cfl=25.0
                "lin_iters_per_step": round(st["lin_iters"] / k, 2),
                "ms_per_lin_iter": round(dt * 1e3 / max(st["lin_iters"], 1), 4),
                "resratio": st["resratio"], "cells": mesh.nelem, "faces": mesh.naface,
-               "restart": restart, "prec_sweeps": sweeps, "prec_single": single, "prec_gs": gs, "prec_lines": lines, "cfl": cfl,
+               "restart": restart, "prec_sweeps": sweeps, "prec_single": single, "prec_gs": gs, "prec_lines": lines, "prec_ilu": ilu, "cfl": cfl,
                "init": {"steps": st0["steps"], "resratio": st0["resratio"]}}
     sp.close()
 
