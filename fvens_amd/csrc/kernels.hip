@@ -169,7 +169,13 @@ __global__ void __launch_bounds__(256) k_grad_wls(DevMesh M, const double* __res
 /// block are gathered from global memory.
 /// limiter values of one cell (k_limiter's arithmetic): uc its primitive state, g its gradient,
 /// un[j] / gp[j] the state across and the centre of its face j (any face order: dmin/dmax and the
-/// minimum over faces do not depend on it), nf faces
+/// minimum over faces do not depend on it), nf faces.
+/// Venkatakrishnan (limitedlinearreconstruction.cpp:219-246) in fewer instructions, bitwise: 2*dp*dm
+/// and 2*dm*dm scale exact products (2 RN(dp dm), 2 RN(dm dm)), so each sum that adds one is an fma with
+/// the factor 2, and dp*dm is formed once for numerator and denominator; the running max / min are
+/// v_max / v_min -- they differ from the reference's compare-and-assign only in the sign of a zero
+/// dmin/dmax (max(+0, -0)), and a signed zero dp gives the same phi (dp*dp = +0, +0 + (+-0) = +0); phi
+/// is never NaN or -0 (its denominator is >= eps2 > 0, its numerator RN(x + eps2) is +0 at x = -eps2)
 template <bool VENK>
 __device__ __forceinline__ void cell_limiter(const double* uc, const double* g, const double (*un)[4],
                                              const double2* gp, const bool* has, double2 r, double eps2,
@@ -182,8 +188,11 @@ __device__ __forceinline__ void cell_limiter(const double* uc, const double* g, 
 		for(int j = 0; j < 4; j++) {
 			if(!has[j]) continue;
 			const double d = un[j][iv]-uc[iv];
-			if(d > dmax) dmax = d;
-			if(d < dmin) dmin = d;
+			if(VENK) { dmax = __builtin_fmax(dmax, d); dmin = __builtin_fmin(dmin, d); }
+			else {
+				if(d > dmax) dmax = d;
+				if(d < dmin) dmin = d;
+			}
 		}
 		double lim = 1.0;
 		#pragma unroll
@@ -196,7 +205,11 @@ __device__ __forceinline__ void cell_limiter(const double* uc, const double* g, 
 			if(VENK) {
 				const double dm = uf - uc[iv];
 				const double dp = dm < 0 ? dmin : dmax;
-				ph = div_rn(dp*dp + 2*dp*dm + eps2, dp*dp + dp*dm + 2*dm*dm + eps2);
+				const double pp = dp*dp, pm = dp*dm;
+				// (dp*dp + 2*dp*dm + eps2)/(dp*dp + dp*dm + 2*dm*dm + eps2)
+				ph = div_rn(__builtin_fma(pm, 2.0, pp) + eps2, __builtin_fma(dm*dm, 2.0, pp + pm) + eps2);
+				lim = __builtin_fmin(lim, ph);
+				continue;
 			} else {
 				const double diff = uf - uc[iv];
 				if(diff > 0) ph = 1 < dmax/diff ? 1 : dmax/diff;
