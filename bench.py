@@ -277,10 +277,11 @@ def main():
     ap.add_argument("--cpu-sweeps", type=int, default=20, help="timed CPU-baseline sweeps (median)")
     ap.add_argument("--no-fast", action="store_true", help="skip the fast-math mode measurement")
     ap.add_argument("--scaling", choices=["weak", "strong"], default="strong")
-    ap.add_argument("--partitioner", choices=["graph", "graph-cells", "rcb"], default="graph",
-                    help="graph: graph bisection balancing the cells' face counts (the fused residual's work: a "
-                         "quadrangle costs ~1.3 triangles); graph-cells: balancing cell counts (the reference's "
-                         "unweighted Scotch graph); rcb: coordinate bisection")
+    ap.add_argument("--partitioner", choices=["graph", "graph-faces", "graph-cells", "rcb"], default="graph",
+                    help="graph: graph bisection balancing the fused residual's measured cost per cell (a quadrangle "
+                         "costs ~1.44 triangles, fvens_amd.RESIDUAL_COST_WEIGHTS); graph-faces: balancing face counts; "
+                         "graph-cells: balancing cell counts (the reference's unweighted Scotch graph); rcb: "
+                         "coordinate bisection")
     ap.add_argument("--no-pipelined", action="store_true", help="skip the pipelined staged path")
     ap.add_argument("--no-implicit", action="store_true", help="skip the implicit-step figure (1 GPU only)")
     ap.add_argument("--preheat-ms", type=float, default=400.0,
@@ -321,10 +322,13 @@ def main():
         if args.partitioner == "rcb":
             part = fa.partition_rcb(mesh, world)
         else:
-            part = fa.partition_graph(mesh, world, weights="faces" if args.partitioner == "graph" else None)
+            part = fa.partition_graph(mesh, world, weights={"graph": "cost", "graph-faces": "faces",
+                                                            "graph-cells": None}[args.partitioner])
         tp = time.time() - tp
         partinfo = {"partitioner": args.partitioner + {
-                        "graph": " (recursive graph bisection, Scotch stand-in, cells weighted by face count)",
+                        "graph": " (recursive graph bisection, Scotch stand-in, cells weighted by their measured residual "
+                                 "cost, triangle : quadrangle = 7 : 10)",
+                        "graph-faces": " (recursive graph bisection, Scotch stand-in, cells weighted by face count)",
                         "graph-cells": " (recursive graph bisection, Scotch stand-in, equal cell counts)",
                         "rcb": " (coordinate bisection)"}[args.partitioner],
                     "edge_cut": fa.partition_edge_cut(mesh, part),

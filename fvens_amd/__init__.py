@@ -525,14 +525,22 @@ def cell_face_counts(mesh):
     return np.ascontiguousarray(mesh.raw()["nnode"], np.int32)
 
 
+# fused-residual cost of a triangle : quadrangle, measured per rank on C4 split 8 ways
+# (profiles/r03/scale_proxy_faces2.jsonl: a quadrangle ~1.44 triangles)
+RESIDUAL_COST_WEIGHTS = (7, 10)
+
+
 def partition_graph(mesh, nparts, weights=None):
     """Graph partition of the cell dual graph (stand-in for the reference's Scotch, absent here).
-    weights: None (every cell 1, as the reference's Scotch graph), "faces" (the cell's face count:
-    balances the fused residual's work on mixed triangle/quadrangle meshes) or an int array [nelem]"""
+    weights: None (every cell 1, as the reference's Scotch graph), "faces" (the cell's face count),
+    "cost" (RESIDUAL_COST_WEIGHTS: the fused residual's measured cost of a triangle / quadrangle) or an
+    int array [nelem]"""
     part = np.zeros(mesh.nelem, np.int32)
     if weights is None:
         check(_ffi.lib().fvhip_partition_graph(ctypes.byref(mesh.view), int(nparts), iptr(part)))
         return part
+    if isinstance(weights, str) and weights == "cost":
+        weights = np.where(cell_face_counts(mesh) == 4, RESIDUAL_COST_WEIGHTS[1], RESIDUAL_COST_WEIGHTS[0])
     w = cell_face_counts(mesh) if isinstance(weights, str) and weights == "faces" else np.ascontiguousarray(weights, np.int32)
     if w.shape != (mesh.nelem,):
         raise ValueError("partition_graph: weights must be 'faces' or one int per cell")

@@ -396,10 +396,21 @@ __global__ void __launch_bounds__(256) k_grad_ghost(DevMesh M, DevPhys P, const 
 	const Gas& G = P.gas;
 	const int4 nb4 = M.gg_nbr[i];
 	const int nb[4] = {nb4.x, nb4.y, nb4.z, nb4.w};
+	// every row this ghost reads is requested at once (a second dependent round trip after the cell
+	// and neighbour ids), not one neighbour after another: the kernel is latency-bound (a few
+	// thousand ghosts per rank) and sits on the halo's critical path
 	double ucons[4], uc[4];
 	ld4(u, c, ucons);
-	cons2prim(G, ucons, uc);
 	const double2 rcc = M.rc[c];
+	double t4[4][4];
+	double2 rn4[4];
+	#pragma unroll
+	for(int k = 0; k < 4; k++) {
+		const int j = nb[k] >= 0 ? nb[k] : c;
+		ld4(u, j, t4[k]);
+		rn4[k] = M.rc[j];
+	}
+	cons2prim(G, ucons, uc);
 	double f[8] = {0,0,0,0,0,0,0,0};
 	double un[4][4];
 	#pragma unroll
@@ -415,10 +426,8 @@ __global__ void __launch_bounds__(256) k_grad_ghost(DevMesh M, DevPhys P, const 
 			cons2prim(G, gs, un[k]);
 			rn = M.xb_rcbp[x];
 		} else {
-			double t4[4];
-			ld4(u, nb[k], t4);
-			cons2prim(G, t4, un[k]);
-			rn = M.rc[nb[k]];
+			cons2prim(G, t4[k], un[k]);
+			rn = rn4[k];
 		}
 		double w2 = 0;
 		w2 += (rcc.x-rn.x)*(rcc.x-rn.x);
@@ -1155,11 +1164,10 @@ __device__ __forceinline__ void fz_viscous(const Gas& G, const double* rowi, con
 	double ldiv = 0;
 	ldiv += grad[0][1]; ldiv += grad[1][2];
 	ldiv *= 2.0/3.0*muRe;
+	// s[i][i] = muRe*(g + g) - ldiv: muRe*(2g) = 2 RN(muRe g) exactly, so one fma with the factor 2
 	double s[2][2];
-	s[0][0] = muRe*(grad[0][1] + grad[0][1]); s[0][1] = muRe*(grad[0][2] + grad[1][1]);
-	s[0][0] -= ldiv;
-	s[1][0] = muRe*(grad[1][1] + grad[0][2]); s[1][1] = muRe*(grad[1][2] + grad[1][2]);
-	s[1][1] -= ldiv;
+	s[0][0] = __builtin_fma(muRe*grad[0][1], 2.0, -ldiv); s[0][1] = muRe*(grad[0][2] + grad[1][1]);
+	s[1][0] = muRe*(grad[1][1] + grad[0][2]); s[1][1] = __builtin_fma(muRe*grad[1][2], 2.0, -ldiv);
 	vf[0] = 0;
 	for(int i = 0; i < 2; i++) { double t = 0; t -= s[i][0]*n[0]; t -= s[i][1]*n[1]; vf[i+1] = t; }
 	double e = 0;

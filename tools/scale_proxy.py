@@ -49,8 +49,8 @@ def main():
     ap.add_argument("--steps", type=int, default=200)
     ap.add_argument("--preheat", type=float, default=0.3, help="seconds of untimed residuals before each timing")
     ap.add_argument("--scale", type=int, default=1)
-    ap.add_argument("--weights", choices=["faces", "none"], default="faces",
-                    help="graph partition weights: the cells' face counts (bench.py's default) or none (equal cells)")
+    ap.add_argument("--weights", choices=["cost", "faces", "none"], default="cost",
+                    help="graph partition weights: measured cost (bench.py's default), face counts or none (equal cells)")
     args = ap.parse_args()
     import torch
     torch.cuda.set_device(0)
@@ -72,7 +72,7 @@ def main():
           flush=True)
     for nparts in args.parts:
         tp = time.time()
-        part = fa.partition_graph(mesh, nparts, weights=None if args.weights == "none" else "faces")
+        part = fa.partition_graph(mesh, nparts, weights=None if args.weights == "none" else args.weights)
         tp = time.time() - tp
         sps = [fa.FlowFV(mesh, p, n, partition=part, rank=k) for k in range(nparts)]
         dus, drs, dts = [], [], []
