@@ -610,11 +610,13 @@ struct fvhip_ctx
 		jac_ready = true;
 	}
 
-	/// Spatial::assemble_jacobian into (diag internal order, lower/upper reference face order)
-	void assemble(const double* u, double* diag, double* lower, double* upper) {
+	/// Spatial::assemble_jacobian into (diag internal order, lower/upper reference face order); with
+	/// cfl > 0 also the pseudo-time term (SteadyBackwardEulerSolver, aodesolver.cpp:300-329, 467) in the
+	/// diagonal pass: dtm <- area/(cfl dtm), diag += dtm I
+	void assemble(const double* u, double* diag, double* lower, double* upper, double cfl = 0.0, double* dtm = nullptr) {
 		ensureJacobian();
 		timed("k_jac_faces", [&]{ launch_jac_faces(J, P, cfg.conv_numflux_jac, viscKind(), u, d_jb, lower, upper, stream); });
-		timed("k_jac_diag", [&]{ launch_jac_diag(J, d_jb, lower, upper, diag, stream); });
+		timed("k_jac_diag", [&]{ launch_jac_diag(J, d_jb, lower, upper, diag, stream, cfl > 0 ? M.area : nullptr, cfl, dtm); });
 		HC(hipGetLastError());
 	}
 
@@ -773,6 +775,7 @@ struct fvhip_ctx
 		for(const void* p : {static_cast<const void*>(lines.gstart), static_cast<const void*>(lines.cell),
 		                     static_cast<const void*>(lines.face), static_cast<const void*>(lines.D),
 		                     static_cast<const void*>(lines.Lb), static_cast<const void*>(lines.W),
+		                     static_cast<const void*>(lines.len),
 		                     static_cast<const void*>(lines.G)}) release(p);
 		lines = LineSet{};
 		const int N = L.ncell, nb = L.nbface;
@@ -848,11 +851,13 @@ struct fvhip_ctx
 		for(int g = 0; g < ng; g++) gst[g+1] = gst[g] + static_cast<int>(all[64*static_cast<size_t>(g)].size());
 		const size_t nslot = 64*static_cast<size_t>(gst[ng]);
 		std::vector<int> cells(std::max<size_t>(nslot, 1), -1), faces(std::max<size_t>(nslot, 1), -1);
+		std::vector<int> lens(std::max<size_t>(64*static_cast<size_t>(ng), 1), 0);
 		h_line_start.assign(1, 0);
 		h_line_cells.clear(); h_line_faces.clear();
 		for(int l = 0; l < nl; l++) {
 			const auto& ln = all[l];
 			const size_t g = static_cast<size_t>(l/64), lane = static_cast<size_t>(l%64);
+			lens[64*g + lane] = static_cast<int>(ln.size());
 			for(size_t k = 0; k < ln.size(); k++) {
 				const size_t slot = (static_cast<size_t>(gst[g]) + k)*64 + lane;
 				cells[slot] = ln[k].first;
@@ -873,6 +878,7 @@ struct fvhip_ctx
 		lines.gstart = upload(gst, owned);
 		lines.cell = upload(cells, owned);
 		lines.face = upload(faces, owned);
+		lines.len = upload(lens, owned);
 		const size_t rows = std::max<size_t>(static_cast<size_t>(gst[ng]), 1);
 		lines.D = dalloc(1024*rows, owned);
 		lines.Lb = dalloc(1024*rows, owned);

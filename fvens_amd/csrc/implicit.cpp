@@ -393,11 +393,9 @@ static void backwardEuler(System& S, const std::vector<double*>& us, const fvhip
 	while(resi/initres > c.tol && step < c.maxiter) {
 		// r = 0 + (-r(u)) with local time steps (:421-452); fills the ghost rows of u
 		fvhip_ctx::residual_seq(S.hs, cu, rs, true, dts, true, S.exg);
-		S.each([&](size_t i, fvhip_ctx* h) { h->assemble(us[i], h->iw.jd, h->iw.jlo, h->iw.jup); });   // :456-457
 		curCFL = expResidualRamp(c.cflinit, c.cflfin, curCFL, resiold/resi, 0.25, 0.3);           // :462
-		S.each([&](size_t, fvhip_ctx* h) {                                                          // :467
-			h->timed("k_pseudo_time", [&]{ launch_pseudo_time(h->L.ncell, h->M.area, curCFL, h->d_dtm, h->iw.jd, h->stream); });
-		});
+		// Jacobian (:456-457) with the pseudo-time term (:467) added in its diagonal pass
+		S.each([&](size_t i, fvhip_ctx* h) { h->assemble(us[i], h->iw.jd, h->iw.jlo, h->iw.jup, curCFL, h->d_dtm); });
 		A.setup();
 		if(A.matfree)                                                                               // :386-394
 			S.each([&](size_t i, fvhip_ctx* h) { h->mf_u = us[i]; h->mf_r = h->d_r; h->mf_mdt = h->d_dtm; });

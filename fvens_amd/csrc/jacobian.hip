@@ -113,7 +113,8 @@ void k_jac_boundary(JacMesh J, DevPhys P, const double* __restrict__ u, double* 
 // -------------------------------------------------------------------------------------------------
 __global__ __launch_bounds__(256)
 void k_jac_diag(JacMesh J, const double* __restrict__ bblk, const double* __restrict__ lower,
-                const double* __restrict__ upper, double* __restrict__ diag)
+                const double* __restrict__ upper, double* __restrict__ diag, const double* __restrict__ area,
+                double cfl, double* __restrict__ dtm)
 {
 	const int c = blockIdx.x*blockDim.x + threadIdx.x;
 	if(c >= J.ncell) return;
@@ -136,6 +137,15 @@ void k_jac_diag(JacMesh J, const double* __restrict__ bblk, const double* __rest
 			const double4 v = b4[q];
 			d[4*q+0] += -1.0*v.x; d[4*q+1] += -1.0*v.y; d[4*q+2] += -1.0*v.z; d[4*q+3] += -1.0*v.w;
 		}
+	}
+	if(area) {
+		// the pseudo-time term of k_pseudo_time, same operations, while the block is in registers
+		const double m = area[c] / (cfl*dtm[c]);
+		dtm[c] = m;
+#pragma unroll
+		for(int i = 0; i < 4; i++)
+#pragma unroll
+			for(int k = 0; k < 4; k++) d[i*4+k] += m*(i == k ? 1.0 : 0.0);
 	}
 	double4* o = reinterpret_cast<double4*>(diag + 16*static_cast<size_t>(c));
 #pragma unroll
@@ -403,9 +413,9 @@ void launch_jac_faces(const JacMesh& J, const DevPhys& P, int jflux, int visc, c
 }
 
 void launch_jac_diag(const JacMesh& J, const double* bblk, const double* lower, const double* upper,
-                     double* diag, hipStream_t s)
+                     double* diag, hipStream_t s, const double* area, double cfl, double* dtm)
 {
-	hipLaunchKernelGGL(k_jac_diag, dim3(nblk(J.ncell,256)), dim3(256), 0, s, J, bblk, lower, upper, diag);
+	hipLaunchKernelGGL(k_jac_diag, dim3(nblk(J.ncell,256)), dim3(256), 0, s, J, bblk, lower, upper, diag, area, cfl, dtm);
 }
 
 void launch_pseudo_time(int ncell, const double* area, double cfl, double* dtm, double* diag, hipStream_t s)

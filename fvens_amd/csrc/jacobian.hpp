@@ -29,8 +29,10 @@ struct JacMesh
 /// flux (LLF, AUSM, Roe, HLL, HLLC), visc 0 none / 1 Sutherland / 2 constant
 void launch_jac_faces(const JacMesh& J, const DevPhys& P, int jflux, int visc, const double* u, double* bblk,
                       double* lower, double* upper, hipStream_t s);
+/// diag[c] = -(sum of the cell's face blocks); with area != nullptr also the pseudo-time term of
+/// launch_pseudo_time (dtm[c] <- area/(cfl dtm[c]), diag[c] += dtm[c] I), fused while the block is in registers
 void launch_jac_diag(const JacMesh& J, const double* bblk, const double* lower, const double* upper,
-                     double* diag, hipStream_t s);
+                     double* diag, hipStream_t s, const double* area = nullptr, double cfl = 0.0, double* dtm = nullptr);
 void launch_pseudo_time(int ncell, const double* area, double cfl, double* dtm, double* diag, hipStream_t s);
 void launch_block_apply(const JacMesh& J, const double* diag, const double* lower, const double* upper,
                         const double* x, double* y, hipStream_t s);

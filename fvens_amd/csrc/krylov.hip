@@ -315,27 +315,26 @@ __device__ __forceinline__ const double* blk_pc(int fc, const double* lower, con
 	return ((fc & 1) ? lower : upper) + 16*static_cast<size_t>(fc >> 1);
 }
 
-/// row r of a line-interleaved 4x4 block array: element e of lane j at X[(16 r + e)*64 + j]
-__device__ __forceinline__ void ldI16(const double* __restrict__ X, long long r, int j, double (&a)[4][4])
+/// Row r of a pair-interleaved 4x4 block array (LineSet): elements 2q, 2q+1 of lane j's block at
+/// double2 index 512 r + 64 q + j -- one 16-byte load per lane per element pair, 1 KB contiguous per
+/// wave instruction, 8 instructions per block instead of 16 8-byte loads (C4 line-implicit step
+/// 9.41 -> 9.12 ms, same-box A/B, profiles/r03/ab/abl_*)
+__device__ __forceinline__ void ldP16(const double* __restrict__ X, long long r, int j, double (&a)[4][4])
 {
-	const double* p = X + 1024*r + j;
+	const double2* p = reinterpret_cast<const double2*>(X) + 512*r + j;
 	#pragma unroll
-	for(int i = 0; i < 4; i++)
-		#pragma unroll
-		for(int q = 0; q < 4; q++) a[i][q] = p[64*(4*i+q)];
+	for(int q = 0; q < 8; q++) { const double2 t = p[64*q]; a[q >> 1][(q & 1)*2] = t.x; a[q >> 1][(q & 1)*2 + 1] = t.y; }
 }
-__device__ __forceinline__ void stI16(double* __restrict__ X, long long r, int j, const double (&a)[4][4])
+__device__ __forceinline__ void stP16(double* __restrict__ X, long long r, int j, const double (&a)[4][4])
 {
-	double* p = X + 1024*r + j;
+	double2* p = reinterpret_cast<double2*>(X) + 512*r + j;
 	#pragma unroll
-	for(int i = 0; i < 4; i++)
-		#pragma unroll
-		for(int q = 0; q < 4; q++) p[64*(4*i+q)] = a[i][q];
+	for(int q = 0; q < 8; q++) p[64*q] = make_double2(a[q >> 1][(q & 1)*2], a[q >> 1][(q & 1)*2 + 1]);
 }
 
 /// block-Thomas factorisation, lane j of workgroup g on line 64g + j (LineSet): per line cell k
 ///   W_{k-1} = dinvp_{k-1} A[k-1][k],  dinvp_k = (D_k - A[k][k-1] W_{k-1})^-1
-/// and D, Lb, W stored line-interleaved for the solve. The next cell's blocks are requested before the
+/// and D, Lb, W stored pair-interleaved for the solve. The next cell's blocks are requested before the
 /// current cell's arithmetic (their addresses do not depend on it) and the cell/face codes two cells
 /// ahead, so the recurrence does not wait a memory round trip per cell.
 __global__ __launch_bounds__(64)
@@ -368,15 +367,15 @@ void k_line_factor(const int* __restrict__ gstart, const int* __restrict__ lcell
 			for(int r = 0; r < 4; r++)
 				#pragma unroll
 				for(int q = 0; q < 4; q++) t[r][q] = prev[r][0]*Uk[0][q] + prev[r][1]*Uk[1][q] + prev[r][2]*Uk[2][q] + prev[r][3]*Uk[3][q];
-			stI16(W, r0 + k - 1, j, t);
-			stI16(Lb, r0 + k, j, Lk);
+			stP16(W, r0 + k - 1, j, t);
+			stP16(Lb, r0 + k, j, Lk);
 			#pragma unroll
 			for(int r = 0; r < 4; r++)
 				#pragma unroll
 				for(int q = 0; q < 4; q++) a[r][q] -= Lk[r][0]*t[0][q] + Lk[r][1]*t[1][q] + Lk[r][2]*t[2][q] + Lk[r][3]*t[3][q];
 		}
 		inv4(a, prev);
-		stI16(D, r0 + k, j, prev);
+		stP16(D, r0 + k, j, prev);
 		if(cn < 0) break;
 		#pragma unroll
 		for(int r = 0; r < 4; r++)
@@ -385,32 +384,36 @@ void k_line_factor(const int* __restrict__ gstart, const int* __restrict__ lcell
 	}
 }
 
-/// z = (block-tridiagonal line part)^-1 v, lanes as in k_line_factor: forward g_k = dinvp_k (v_k -
-/// A[k][k-1] g_{k-1}) into the interleaved scratch G, backward z_k = g_k - W_k z_{k+1}; the next
-/// cell's rows (and its v row) are requested before the current cell's arithmetic
+/// z = (block-tridiagonal line part)^-1 v, lanes as in k_line_factor, lane j's line llen[64g + j] cells
+/// long: forward g_k = dinvp_k (v_k - A[k][k-1] g_{k-1}) into the pair-interleaved scratch G, backward
+/// z_k = g_k - W_k z_{k+1}; the next cell's rows (and its v row) are requested before the current
+/// cell's arithmetic. (A deeper register ring of rows in flight -- 3 or 4 cells ahead -- exceeds the 256
+/// architected VGPRs and turns into accumulator-register copies that wait on the loads: measured
+/// slower, profiles/r03/ab/abl_*.)
 __global__ __launch_bounds__(64)
-void k_line_solve(const int* __restrict__ gstart, const int* __restrict__ lcell, const double* __restrict__ D,
-                  const double* __restrict__ Lb, const double* __restrict__ W, double* __restrict__ G,
-                  const double* __restrict__ v, double* __restrict__ z)
+void k_line_solve(const int* __restrict__ gstart, const int* __restrict__ lcell, const int* __restrict__ llen,
+                  const double* __restrict__ D, const double* __restrict__ Lb, const double* __restrict__ W,
+                  double* __restrict__ G, const double* __restrict__ v, double* __restrict__ z)
 {
 	const int g = blockIdx.x, j = threadIdx.x;
 	const long long r0 = gstart[g];
-	const int len = gstart[g+1] - static_cast<int>(r0);
-	int c = lcell[64*r0 + j];
-	if(c < 0) return;
+	const int n = llen[64*g + j];
+	if(n == 0) return;
+	const int* cl = lcell + 64*r0 + j;
+	const double4* v4 = reinterpret_cast<const double4*>(v);
+	double4* z4 = reinterpret_cast<double4*>(z);
+	double2* G2 = reinterpret_cast<double2*>(G) + 128*r0 + j;     // row k: G2[128k], G2[128k + 64]
 	double Dk[4][4], Lk[4][4];
-	double4 vk = reinterpret_cast<const double4*>(v)[c];
-	ldI16(D, r0, j, Dk);
+	double4 vk = v4[cl[0]];
+	ldP16(D, r0, j, Dk);
 	double4 gp = make_double4(0, 0, 0, 0);
-	int kl = 0;
-	for(int k = 0; ; k++) {
-		const int cn = k + 1 < len ? lcell[64*(r0+k+1) + j] : -1;
+	for(int k = 0; k < n; k++) {
 		double Dn[4][4], Ln[4][4];
 		double4 vn = make_double4(0, 0, 0, 0);
-		if(cn >= 0) {
-			vn = reinterpret_cast<const double4*>(v)[cn];
-			ldI16(D, r0 + k + 1, j, Dn);
-			ldI16(Lb, r0 + k + 1, j, Ln);
+		if(k + 1 < n) {
+			vn = v4[cl[64*(k+1)]];
+			ldP16(D, r0 + k + 1, j, Dn);
+			ldP16(Lb, r0 + k + 1, j, Ln);
 		}
 		double r[4] = {vk.x, vk.y, vk.z, vk.w};
 		if(k > 0) {
@@ -421,47 +424,42 @@ void k_line_solve(const int* __restrict__ gstart, const int* __restrict__ lcell,
 		#pragma unroll
 		for(int i = 0; i < 4; i++) y[i] = Dk[i][0]*r[0] + Dk[i][1]*r[1] + Dk[i][2]*r[2] + Dk[i][3]*r[3];
 		gp = make_double4(y[0], y[1], y[2], y[3]);
-		if(cn < 0) { kl = k; break; }
-		double* gq = G + 256*(r0 + k) + j;
-		gq[0] = y[0]; gq[64] = y[1]; gq[128] = y[2]; gq[192] = y[3];
+		if(k + 1 == n) break;
+		G2[128*k] = make_double2(y[0], y[1]); G2[128*k + 64] = make_double2(y[2], y[3]);
 		#pragma unroll
 		for(int i = 0; i < 4; i++)
 			#pragma unroll
 			for(int q = 0; q < 4; q++) { Dk[i][q] = Dn[i][q]; Lk[i][q] = Ln[i][q]; }
 		vk = vn;
-		c = cn;
 	}
-	// backward from the line's last cell (kl): z_kl = g_kl
+	// backward from the line's last cell: z_{n-1} = g_{n-1}
 	double4 x = gp;
-	reinterpret_cast<double4*>(z)[c] = x;
-	if(kl == 0) return;
-	int ck = lcell[64*(r0+kl-1) + j];
+	z4[cl[64*(n-1)]] = x;
+	if(n == 1) return;
 	double Wk[4][4];
-	ldI16(W, r0 + kl - 1, j, Wk);
-	const double* gq = G + 256*(r0 + kl - 1) + j;
-	double4 gk = make_double4(gq[0], gq[64], gq[128], gq[192]);
-	for(int k = kl - 1; k >= 0; k--) {
-		int cp = -1;
+	ldP16(W, r0 + n - 2, j, Wk);
+	double2 ga = G2[128*(n-2)], gb = G2[128*(n-2) + 64];
+	int ck = cl[64*(n-2)];
+	for(int k = n - 2; k >= 0; k--) {
 		double Wn[4][4];
-		double4 gn = make_double4(0, 0, 0, 0);
+		double2 na = make_double2(0, 0), nb = make_double2(0, 0);
+		int cp = -1;
 		if(k > 0) {
-			cp = lcell[64*(r0+k-1) + j];
-			ldI16(W, r0 + k - 1, j, Wn);
-			const double* gm = G + 256*(r0 + k - 1) + j;
-			gn = make_double4(gm[0], gm[64], gm[128], gm[192]);
+			ldP16(W, r0 + k - 1, j, Wn);
+			na = G2[128*(k-1)]; nb = G2[128*(k-1) + 64];
+			cp = cl[64*(k-1)];
 		}
 		double y[4];
 		#pragma unroll
 		for(int i = 0; i < 4; i++) y[i] = Wk[i][0]*x.x + Wk[i][1]*x.y + Wk[i][2]*x.z + Wk[i][3]*x.w;
-		x = make_double4(gk.x - y[0], gk.y - y[1], gk.z - y[2], gk.w - y[3]);
-		reinterpret_cast<double4*>(z)[ck] = x;
+		x = make_double4(ga.x - y[0], ga.y - y[1], gb.x - y[2], gb.y - y[3]);
+		z4[ck] = x;
 		if(k == 0) break;
 		#pragma unroll
 		for(int i = 0; i < 4; i++)
 			#pragma unroll
 			for(int q = 0; q < 4; q++) Wk[i][q] = Wn[i][q];
-		gk = gn;
-		ck = cp;
+		ga = na; gb = nb; ck = cp;
 	}
 }
 
@@ -487,8 +485,8 @@ void launch_line_factor(const LineSet& Ls, const double* diag, const double* low
 void launch_line_solve(const LineSet& Ls, const double* v, double* z, hipStream_t s)
 {
 	if(Ls.ngroups > 0)
-		hipLaunchKernelGGL(k_line_solve, dim3(Ls.ngroups), dim3(64), 0, s, Ls.gstart, Ls.cell, Ls.D, Ls.Lb, Ls.W, Ls.G,
-		                   v, z);
+		hipLaunchKernelGGL(k_line_solve, dim3(Ls.ngroups), dim3(64), 0, s, Ls.gstart, Ls.cell, Ls.len, Ls.D, Ls.Lb, Ls.W,
+		                   Ls.G, v, z);
 }
 
 void launch_add_rows(int n, const double* e, double* z, hipStream_t s)

@@ -45,9 +45,11 @@ FVHIP_HD double relaxation_factor(const gd::Gas& G, double minfactor, const doub
 /// Lines of the line-implicit preconditioner (internal cell ids), sorted by length (longest first) and
 /// dealt to groups of 64: lane j of group g walks line 64g + j, so one wave runs 64 recurrences side by
 /// side. Everything per line cell is stored line-interleaved: row r = gstart[g] + k holds step k of the
-/// group's 64 lines, slot r*64 + lane; a 4x4 block of row r is X[(16r + e)*64 + lane] (one coalesced
-/// load per element across the 64 lines). cell[slot] = the lane's k-th line cell or -1 once its line
-/// has ended; face[slot] (k > 0) = interior face between its cells k-1 and k, fi<<1 | (cell k-1 is R).
+/// group's 64 lines, slot r*64 + lane; a 4x4 block of row r is pair-interleaved, elements 2q, 2q+1 at
+/// double2 index 512 r + 64 q + lane (one coalesced 16-byte load per element pair across the 64
+/// lines). cell[slot] = the lane's k-th line cell or -1 once its line has ended; face[slot] (k > 0) =
+/// interior face between its cells k-1 and k, fi<<1 | (cell k-1 is R); len[64 g + lane] = the lane's
+/// line length (0: no line).
 /// Device arrays written by the factorisation and read by the solve: D = dinvp_k (the inverted pivot
 /// blocks), Lb = A[k][k-1], W = dinvp_k A[k][k+1]; G = forward-sweep scratch [rows][4][64].
 struct LineSet {
@@ -56,6 +58,7 @@ struct LineSet {
 	const int* gstart = nullptr;     ///< [ngroups+1]
 	const int* cell = nullptr;       ///< [64 nrows]
 	const int* face = nullptr;       ///< [64 nrows]
+	const int* len = nullptr;        ///< [64 ngroups]
 	double *D = nullptr, *Lb = nullptr, *W = nullptr, *G = nullptr;
 };
 #ifndef FVHIP_LINE_MAX
