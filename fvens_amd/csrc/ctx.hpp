@@ -845,33 +845,67 @@ struct fvhip_ctx
 		}
 		std::stable_sort(all.begin(), all.end(), [](const std::vector<std::pair<int,int>>& a,
 		                                            const std::vector<std::pair<int,int>>& b) { return a.size() > b.size(); });
-		// groups of 64 lines (a wave's lanes), rows line-interleaved (krylov.hpp LineSet)
-		const int nl = static_cast<int>(all.size()), ng = (nl + 63)/64;
+		// lanes: a line of at least LINE_TWIST_MIN cells is solved from both ends (twisted factorisation):
+		// its top half t = (n-1)/2 cells in order, then the twist cell t, on lane j of a twisted group; its
+		// bottom half n-1 .. t+1 in reverse order, then t, on lane j+32. Every other line is one lane of a
+		// group of 64. Entries (cell, interior face to the previous entry); rows line-interleaved
+		// (krylov.hpp LineSet)
+		const int nl = static_cast<int>(all.size());
+		int ntw = 0;
+		while(ntw < nl && static_cast<int>(all[static_cast<size_t>(ntw)].size()) >= LINE_TWIST_MIN) ntw++;
+		typedef std::vector<std::pair<int,int>> Lane;
+		std::vector<std::array<Lane,64>> grp;
+		for(int l0 = 0; l0 < ntw; l0 += 32) {
+			grp.emplace_back();
+			for(int q = 0; q < 32 && l0 + q < ntw; q++) {
+				const auto& ln = all[static_cast<size_t>(l0 + q)];
+				const int n = static_cast<int>(ln.size()), tc = (n - 1)/2;
+				Lane top(ln.begin(), ln.begin() + tc + 1), bot;
+				for(int k = n - 1; k >= tc; k--)
+					bot.push_back({ln[static_cast<size_t>(k)].first, k == n - 1 ? -1 : ln[static_cast<size_t>(k) + 1].second});
+				grp.back()[static_cast<size_t>(q)] = std::move(top);
+				grp.back()[static_cast<size_t>(q) + 32] = std::move(bot);
+			}
+		}
+		const int ntg = static_cast<int>(grp.size());
+		for(int l0 = ntw; l0 < nl; l0 += 64) {
+			grp.emplace_back();
+			for(int q = 0; q < 64 && l0 + q < nl; q++) grp.back()[static_cast<size_t>(q)] = all[static_cast<size_t>(l0 + q)];
+		}
+		const int ng = static_cast<int>(grp.size());
 		std::vector<int> gst(static_cast<size_t>(ng) + 1, 0);
-		for(int g = 0; g < ng; g++) gst[g+1] = gst[g] + static_cast<int>(all[64*static_cast<size_t>(g)].size());
+		for(int g = 0; g < ng; g++) {
+			size_t mx = 0;
+			for(const Lane& ln : grp[static_cast<size_t>(g)]) mx = std::max(mx, ln.size());
+			gst[g+1] = gst[g] + static_cast<int>(mx);
+		}
 		const size_t nslot = 64*static_cast<size_t>(gst[ng]);
 		std::vector<int> cells(std::max<size_t>(nslot, 1), -1), faces(std::max<size_t>(nslot, 1), -1);
 		std::vector<int> lens(std::max<size_t>(64*static_cast<size_t>(ng), 1), 0);
+		for(int g = 0; g < ng; g++)
+			for(size_t lane = 0; lane < 64; lane++) {
+				const Lane& ln = grp[static_cast<size_t>(g)][lane];
+				lens[64*static_cast<size_t>(g) + lane] = static_cast<int>(ln.size());
+				for(size_t k = 0; k < ln.size(); k++) {
+					const size_t slot = (static_cast<size_t>(gst[g]) + k)*64 + lane;
+					cells[slot] = ln[k].first;
+					if(k > 0) {
+						const int fi = ln[k].second, p = ln[k-1].first;
+						faces[slot] = (fi << 1) | (L.if_L[fi] == p ? 0 : 1);
+					}
+				}
+			}
+		// the lines as built (fvhip_lines), longest first
 		h_line_start.assign(1, 0);
 		h_line_cells.clear(); h_line_faces.clear();
-		for(int l = 0; l < nl; l++) {
-			const auto& ln = all[l];
-			const size_t g = static_cast<size_t>(l/64), lane = static_cast<size_t>(l%64);
-			lens[64*g + lane] = static_cast<int>(ln.size());
+		for(const auto& ln : all) {
 			for(size_t k = 0; k < ln.size(); k++) {
-				const size_t slot = (static_cast<size_t>(gst[g]) + k)*64 + lane;
-				cells[slot] = ln[k].first;
-				int code = -1;
-				if(k > 0) {
-					const int fi = ln[k].second, p = ln[k-1].first;
-					code = (fi << 1) | (L.if_L[fi] == p ? 0 : 1);
-				}
-				faces[slot] = code;
 				h_line_cells.push_back(ln[k].first);
-				h_line_faces.push_back(code);
+				h_line_faces.push_back(k > 0 ? (ln[k].second << 1) | (L.if_L[ln[k].second] == ln[k-1].first ? 0 : 1) : -1);
 			}
 			h_line_start.push_back(static_cast<int>(h_line_cells.size()));
 		}
+		lines.twisted_groups = ntg;
 		lines.nlines = nl;
 		lines.ngroups = ng;
 		lines.nrows = gst[ng];

@@ -337,18 +337,25 @@ __device__ __forceinline__ void stP16(double* __restrict__ X, long long r, int j
 /// and D, Lb, W stored pair-interleaved for the solve. The next cell's blocks are requested before the
 /// current cell's arithmetic (their addresses do not depend on it) and the cell/face codes two cells
 /// ahead, so the recurrence does not wait a memory round trip per cell.
+/// Twisted groups (g < twisted_groups; ctx.hpp ensureLines): lane j walks the top half of line j and
+/// lane j+32 the bottom half backwards, each list ending in the twist cell t. A half stops at t with the
+/// Schur term S = A[t][last] W_last of its side instead of a pivot; the two lanes swap S and lane j
+/// stores the twist pivot (A_tt - S_top - S_bottom)^-1 in its row of t. That is the same block
+/// elimination of the same block-tridiagonal matrix, ordered from both ends: the chain per lane halves.
 __global__ __launch_bounds__(64)
 void k_line_factor(const int* __restrict__ gstart, const int* __restrict__ lcell, const int* __restrict__ lface,
+                   const int* __restrict__ llen, int twisted_groups,
                    const double* __restrict__ diag, const double* __restrict__ lower, const double* __restrict__ upper,
                    double* __restrict__ D, double* __restrict__ Lb, double* __restrict__ W)
 {
 	const int g = blockIdx.x, j = threadIdx.x;
 	const long long r0 = gstart[g];
-	const int len = gstart[g+1] - static_cast<int>(r0);
+	const int len = llen[64*g + j];
+	const bool tw = g < twisted_groups;
+	double a[4][4], Lk[4][4], Uk[4][4], prev[4][4], S[4][4];
+	if(len > 0) {
 	int c = lcell[64*r0 + j];
 	int c1 = len > 1 ? lcell[64*(r0+1) + j] : -1, f1 = len > 1 ? lface[64*(r0+1) + j] : -1;
-	double a[4][4], Lk[4][4], Uk[4][4], prev[4][4];
-	if(c < 0) return;
 	ld16(diag + 16*static_cast<size_t>(c), a);
 	for(int k = 0; k < len; k++) {
 		// requests for cell k+1 (blocks) and k+2 (codes)
@@ -369,6 +376,13 @@ void k_line_factor(const int* __restrict__ gstart, const int* __restrict__ lcell
 				for(int q = 0; q < 4; q++) t[r][q] = prev[r][0]*Uk[0][q] + prev[r][1]*Uk[1][q] + prev[r][2]*Uk[2][q] + prev[r][3]*Uk[3][q];
 			stP16(W, r0 + k - 1, j, t);
 			stP16(Lb, r0 + k, j, Lk);
+			if(tw && k == len - 1) {                   // the twist: this side's Schur term, no pivot
+				#pragma unroll
+				for(int r = 0; r < 4; r++)
+					#pragma unroll
+					for(int q = 0; q < 4; q++) S[r][q] = Lk[r][0]*t[0][q] + Lk[r][1]*t[1][q] + Lk[r][2]*t[2][q] + Lk[r][3]*t[3][q];
+				break;
+			}
 			#pragma unroll
 			for(int r = 0; r < 4; r++)
 				#pragma unroll
@@ -382,6 +396,22 @@ void k_line_factor(const int* __restrict__ gstart, const int* __restrict__ lcell
 			#pragma unroll
 			for(int q = 0; q < 4; q++) { a[r][q] = an[r][q]; Lk[r][q] = Ln[r][q]; Uk[r][q] = Un[r][q]; }
 	}
+	}
+	if(!tw) return;
+	// twist pivot: lane j (top half) combines both sides' Schur terms, a = A_tt on both lanes
+	double So[4][4];
+	#pragma unroll
+	for(int r = 0; r < 4; r++)
+		#pragma unroll
+		for(int q = 0; q < 4; q++) So[r][q] = __shfl_xor(S[r][q], 32);
+	if(j < 32 && len > 0) {
+		#pragma unroll
+		for(int r = 0; r < 4; r++)
+			#pragma unroll
+			for(int q = 0; q < 4; q++) a[r][q] = (a[r][q] - S[r][q]) - So[r][q];
+		inv4(a, prev);
+		stP16(D, r0 + len - 1, j, prev);
+	}
 }
 
 /// z = (block-tridiagonal line part)^-1 v, lanes as in k_line_factor, lane j's line llen[64g + j] cells
@@ -390,23 +420,26 @@ void k_line_factor(const int* __restrict__ gstart, const int* __restrict__ lcell
 /// cell's arithmetic. (A deeper register ring of rows in flight -- 3 or 4 cells ahead -- exceeds the 256
 /// architected VGPRs and turns into accumulator-register copies that wait on the loads: measured
 /// slower, profiles/r03/ab/abl_*.)
+/// Twisted groups: each half's forward sweep ends at the twist cell t with s = A[t][last] g_last; the
+/// lanes swap s, lane j forms z_t = pivot_t (v_t - s_top - s_bottom) and hands it to lane j+32, and both
+/// sweep back from z_t.
 __global__ __launch_bounds__(64)
 void k_line_solve(const int* __restrict__ gstart, const int* __restrict__ lcell, const int* __restrict__ llen,
-                  const double* __restrict__ D, const double* __restrict__ Lb, const double* __restrict__ W,
-                  double* __restrict__ G, const double* __restrict__ v, double* __restrict__ z)
+                  int twisted_groups, const double* __restrict__ D, const double* __restrict__ Lb,
+                  const double* __restrict__ W, double* __restrict__ G, const double* __restrict__ v, double* __restrict__ z)
 {
 	const int g = blockIdx.x, j = threadIdx.x;
 	const long long r0 = gstart[g];
 	const int n = llen[64*g + j];
-	if(n == 0) return;
+	const bool tw = g < twisted_groups;
+	if(n == 0 && !tw) return;
 	const int* cl = lcell + 64*r0 + j;
 	const double4* v4 = reinterpret_cast<const double4*>(v);
 	double4* z4 = reinterpret_cast<double4*>(z);
 	double2* G2 = reinterpret_cast<double2*>(G) + 128*r0 + j;     // row k: G2[128k], G2[128k + 64]
 	double Dk[4][4], Lk[4][4];
-	double4 vk = v4[cl[0]];
-	ldP16(D, r0, j, Dk);
-	double4 gp = make_double4(0, 0, 0, 0);
+	double4 gp = make_double4(0, 0, 0, 0), vk = make_double4(0, 0, 0, 0), s = make_double4(0, 0, 0, 0);
+	if(n > 0) { vk = v4[cl[0]]; ldP16(D, r0, j, Dk); }
 	for(int k = 0; k < n; k++) {
 		double Dn[4][4], Ln[4][4];
 		double4 vn = make_double4(0, 0, 0, 0);
@@ -414,6 +447,13 @@ void k_line_solve(const int* __restrict__ gstart, const int* __restrict__ lcell,
 			vn = v4[cl[64*(k+1)]];
 			ldP16(D, r0 + k + 1, j, Dn);
 			ldP16(Lb, r0 + k + 1, j, Ln);
+		}
+		if(tw && k == n - 1) {                         // the twist: this side's term A[t][last] g_last
+			s = make_double4(Lk[0][0]*gp.x + Lk[0][1]*gp.y + Lk[0][2]*gp.z + Lk[0][3]*gp.w,
+			                 Lk[1][0]*gp.x + Lk[1][1]*gp.y + Lk[1][2]*gp.z + Lk[1][3]*gp.w,
+			                 Lk[2][0]*gp.x + Lk[2][1]*gp.y + Lk[2][2]*gp.z + Lk[2][3]*gp.w,
+			                 Lk[3][0]*gp.x + Lk[3][1]*gp.y + Lk[3][2]*gp.z + Lk[3][3]*gp.w);
+			break;
 		}
 		double r[4] = {vk.x, vk.y, vk.z, vk.w};
 		if(k > 0) {
@@ -432,9 +472,25 @@ void k_line_solve(const int* __restrict__ gstart, const int* __restrict__ lcell,
 			for(int q = 0; q < 4; q++) { Dk[i][q] = Dn[i][q]; Lk[i][q] = Ln[i][q]; }
 		vk = vn;
 	}
-	// backward from the line's last cell: z_{n-1} = g_{n-1}
+	// backward from the line's last cell: z_{n-1} = g_{n-1}; twisted: from the twist cell's z_t
 	double4 x = gp;
-	z4[cl[64*(n-1)]] = x;
+	if(tw) {
+		const double4 so = make_double4(__shfl_xor(s.x, 32), __shfl_xor(s.y, 32), __shfl_xor(s.z, 32), __shfl_xor(s.w, 32));
+		if(j < 32 && n > 0) {
+			double Dt[4][4];
+			ldP16(D, r0 + n - 1, j, Dt);                 // lane j's row of t holds the twist pivot
+			const double r[4] = {(vk.x - s.x) - so.x, (vk.y - s.y) - so.y, (vk.z - s.z) - so.z, (vk.w - s.w) - so.w};
+			double y[4];
+			#pragma unroll
+			for(int i = 0; i < 4; i++) y[i] = Dt[i][0]*r[0] + Dt[i][1]*r[1] + Dt[i][2]*r[2] + Dt[i][3]*r[3];
+			x = make_double4(y[0], y[1], y[2], y[3]);
+			z4[cl[64*(n-1)]] = x;
+		}
+		const double4 xo = make_double4(__shfl_xor(x.x, 32), __shfl_xor(x.y, 32), __shfl_xor(x.z, 32), __shfl_xor(x.w, 32));
+		if(j >= 32) x = xo;                            // z_t from lane j
+		if(n == 0) return;
+	}
+	else z4[cl[64*(n-1)]] = x;
 	if(n == 1) return;
 	double Wk[4][4];
 	ldP16(W, r0 + n - 2, j, Wk);
@@ -478,15 +534,15 @@ void k_add_rows(int n, const double* __restrict__ e, double* __restrict__ z)
 void launch_line_factor(const LineSet& Ls, const double* diag, const double* lower, const double* upper, hipStream_t s)
 {
 	if(Ls.ngroups > 0)
-		hipLaunchKernelGGL(k_line_factor, dim3(Ls.ngroups), dim3(64), 0, s, Ls.gstart, Ls.cell, Ls.face, diag, lower,
-		                   upper, Ls.D, Ls.Lb, Ls.W);
+		hipLaunchKernelGGL(k_line_factor, dim3(Ls.ngroups), dim3(64), 0, s, Ls.gstart, Ls.cell, Ls.face, Ls.len,
+		                   Ls.twisted_groups, diag, lower, upper, Ls.D, Ls.Lb, Ls.W);
 }
 
 void launch_line_solve(const LineSet& Ls, const double* v, double* z, hipStream_t s)
 {
 	if(Ls.ngroups > 0)
-		hipLaunchKernelGGL(k_line_solve, dim3(Ls.ngroups), dim3(64), 0, s, Ls.gstart, Ls.cell, Ls.len, Ls.D, Ls.Lb, Ls.W,
-		                   Ls.G, v, z);
+		hipLaunchKernelGGL(k_line_solve, dim3(Ls.ngroups), dim3(64), 0, s, Ls.gstart, Ls.cell, Ls.len, Ls.twisted_groups,
+		                   Ls.D, Ls.Lb, Ls.W, Ls.G, v, z);
 }
 
 void launch_add_rows(int n, const double* e, double* z, hipStream_t s)

@@ -59,12 +59,17 @@ struct LineSet {
 	const int* cell = nullptr;       ///< [64 nrows]
 	const int* face = nullptr;       ///< [64 nrows]
 	const int* len = nullptr;        ///< [64 ngroups]
+	int twisted_groups = 0;          ///< leading groups of 32 lines solved from both ends (lanes j, j+32)
 	double *D = nullptr, *Lb = nullptr, *W = nullptr, *G = nullptr;
 };
 #ifndef FVHIP_LINE_MAX
 #define FVHIP_LINE_MAX 256
 #endif
 constexpr int LINE_MAX_CELLS = FVHIP_LINE_MAX;   ///< longest line piece (ctx.hpp ensureLines)
+#ifndef FVHIP_LINE_TWIST_MIN
+#define FVHIP_LINE_TWIST_MIN 16
+#endif
+constexpr int LINE_TWIST_MIN = FVHIP_LINE_TWIST_MIN;   ///< shortest line solved from both ends
 /// block-Thomas factorisation of every line (D, Lb, W of the line set) from the block operator
 void launch_line_factor(const LineSet& Ls, const double* diag, const double* lower, const double* upper, hipStream_t s);
 /// z = (block-tridiagonal line part of A)^-1 v
