@@ -8,7 +8,8 @@
 
 namespace fvhip {
 
-constexpr int KRY_BLOCKS = 512;   ///< partial sums per dot product (= ode.hip's ODE_RED_BLOCKS)
+constexpr int KRY_BLOCKS = 512;   ///< partial sums of the energy norm (= ode.hip's ODE_RED_BLOCKS)
+constexpr int KRY_DOT_BLOCKS = 2048;   ///< partial sums per GMRES dot product (8 blocks per CU: enough loads in flight)
 constexpr int KRY_GROUP = 4;      ///< dot products per block row of the multi-dot
 
 static inline int nblk(long long n, int b) { return static_cast<int>((n + b - 1)/b); }
@@ -221,12 +222,20 @@ void k_mdot_partial(long long n, int k, int kt, const double* __restrict__ V, lo
 	double acc[KRY_GROUP];
 	#pragma unroll
 	for(int q = 0; q < KRY_GROUP; q++) acc[q] = 0.0;
-	for(long long i = blockIdx.x*256LL + threadIdx.x; i < n; i += 256LL*gridDim.x) {
-		const double wi = w[i];
+	// 16-byte loads (n is a multiple of 4: four unknowns per cell); the same fixed order every call
+	const long long n2 = n >> 1;
+	const double2* w2 = reinterpret_cast<const double2*>(w);
+	for(long long i = blockIdx.x*256LL + threadIdx.x; i < n2; i += 256LL*gridDim.x) {
+		const double2 wi = w2[i];
 		#pragma unroll
-		for(int q = 0; q < KRY_GROUP; q++) if(j0 + q < kt) acc[q] += vp[q][i]*wi;
+		for(int q = 0; q < KRY_GROUP; q++)
+			if(j0 + q < kt) {
+				const double2 vi = reinterpret_cast<const double2*>(vp[q])[i];
+				acc[q] += vi.x*wi.x;
+				acc[q] += vi.y*wi.y;
+			}
 	}
-	block_sum<KRY_GROUP>(acc, part + static_cast<size_t>(j0)*KRY_BLOCKS + blockIdx.x, KRY_BLOCKS);
+	block_sum<KRY_GROUP>(acc, part + static_cast<size_t>(j0)*KRY_DOT_BLOCKS + blockIdx.x, KRY_DOT_BLOCKS);
 }
 
 /// out[b] = sum of the np partials of product b (one block per product)
@@ -570,7 +579,7 @@ void launch_bjac_correct(int n, const double* dinv, const double* b, const doubl
 
 size_t kry_scratch(int k)
 {
-	return static_cast<size_t>(KRY_BLOCKS)*static_cast<size_t>((k + KRY_GROUP)/KRY_GROUP*KRY_GROUP);
+	return static_cast<size_t>(KRY_DOT_BLOCKS)*static_cast<size_t>((k + KRY_GROUP)/KRY_GROUP*KRY_GROUP);
 }
 
 void launch_mdot(long long n, int k, const double* V, long long ld, const double* w, bool self,
@@ -578,8 +587,8 @@ void launch_mdot(long long n, int k, const double* V, long long ld, const double
 {
 	const int kt = k + (self ? 1 : 0);
 	if(kt <= 0) return;
-	k_mdot_partial<<<dim3(KRY_BLOCKS, (kt + KRY_GROUP - 1)/KRY_GROUP), 256, 0, s>>>(n, k, kt, V, ld, w, part);
-	k_sum_partials<<<kt, 256, 0, s>>>(KRY_BLOCKS, part, out);
+	k_mdot_partial<<<dim3(KRY_DOT_BLOCKS, (kt + KRY_GROUP - 1)/KRY_GROUP), 256, 0, s>>>(n, k, kt, V, ld, w, part);
+	k_sum_partials<<<kt, 256, 0, s>>>(KRY_DOT_BLOCKS, part, out);
 }
 
 void launch_maxpy(long long n, int k, const double* V, long long ld, const double* h, double* w, hipStream_t s)
