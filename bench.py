@@ -95,11 +95,13 @@ def kernel_bytes(label, N, F, Fb, numerics="headline"):
 
 
 def kernel_symbol(label, numerics="headline"):
-    """profiling label -> rocprofv3 kernel symbol suffix of the Roe/MUSCL/dt (headline) or
-    Roe/linear/Venkatakrishnan/dt (config4) instantiation"""
+    """profiling label -> rocprofv3 kernel symbol suffix of the Roe/MUSCL/dt (headline), Roe/linear/
+    Venkatakrishnan/dt (config4) or Roe/MUSCL/Sutherland/dt (config5) instantiation"""
     if label.startswith("k_residual_wls"):
-        return "k_residual_wls<4, 1, true, 0, 0>" if numerics == "headline" else "k_residual_wls<4, 2, true, 0, 2>"
-    return "k_sweep<4, 1, 0, true, false>" if numerics == "headline" else "k_sweep<4, 2, 0, true, true>"
+        return {"headline": "k_residual_wls<4, 1, true, 0, 0>", "config4": "k_residual_wls<4, 2, true, 0, 2>",
+                "config5": "k_residual_wls<4, 1, true, 1, 0>"}[numerics]
+    return {"headline": "k_sweep<4, 1, 0, true, false>", "config4": "k_sweep<4, 2, 0, true, true>",
+            "config5": "k_sweep<4, 1, 1, true, false>"}[numerics]
 
 
 def pmc_traffic(kernel_symbol, workload_cells):
@@ -180,7 +182,7 @@ def host_cpu_info():
             "affinity_cpus": aff, "cgroup_cpu_quota": quota, "physical_cores_used": cores}
 
 
-def cpu_baseline(mesh, u, nrep, rec="VANALBADA"):
+def cpu_baseline(mesh, u, nrep, rec="VANALBADA", kind="naca"):
     """BASELINE.md's CPU baseline: the oracle's OpenMP restatement (the reference's omp parallel for /
     omp atomic structure) on this host's physical cores, in a child process so that OMP_PROC_BIND /
     OMP_PLACES take effect (torch has already loaded the OpenMP runtime here); median of `nrep` sweeps
@@ -198,7 +200,7 @@ def cpu_baseline(mesh, u, nrep, rec="VANALBADA"):
         for threads, reps in ((nt, nrep), (1, max(3, nrep // 4))):
             env = dict(os.environ, OMP_NUM_THREADS=str(threads), OMP_PROC_BIND="close", OMP_PLACES="cores")
             out = subprocess.run([sys.executable, os.path.abspath(__file__), "--cpu-child", path, str(threads),
-                                  str(reps), rec], env=env, capture_output=True, text=True, timeout=900)
+                                  str(reps), rec, kind], env=env, capture_output=True, text=True, timeout=900)
             if out.returncode != 0:
                 raise RuntimeError("cpu baseline child failed: " + out.stderr[-2000:])
             res[threads] = json.loads(out.stdout.strip().splitlines()[-1])
@@ -215,14 +217,14 @@ def cpu_baseline(mesh, u, nrep, rec="VANALBADA"):
                       f"{med_1:.3f} s"}
 
 
-def cpu_child(path, threads, nrep, rec="VANALBADA"):
+def cpu_child(path, threads, nrep, rec="VANALBADA", kind="naca"):
     """child of cpu_baseline: builds the oracle from the saved mesh and times it (prints one JSON line)"""
     import _oracle as orc
     import cases
     d = np.load(path)
     raw = {k: (int(d[k]) if d[k].ndim == 0 else d[k]) for k in d.files if k != "u"}
     om = orc.OracleMesh.from_raw(raw)
-    ref = orc.OracleSpatial(om, cases.physics("naca"), cases.numerics("ROE", "LEASTSQUARES", rec))
+    ref = orc.OracleSpatial(om, cases.physics(kind), cases.numerics("ROE", "LEASTSQUARES", rec))
     med, times = ref.time_residual(np.ascontiguousarray(d["u"]), nrep, True, threads=threads, nwarm=3)
     print(json.dumps({"median_s": med, "nrep": nrep, "threads": threads, "min_s": float(times.min()),
                       "max_s": float(times.max())}))
@@ -287,9 +289,11 @@ def main():
     ap.add_argument("--preheat-ms", type=float, default=400.0,
                     help="untimed steps for this long (wall clock) after the warm-up steps of the primary path, "
                          "so the timed steps run at the clock the GPU holds under this load (reported)")
-    ap.add_argument("--numerics", choices=["headline", "config4"], default="headline",
+    ap.add_argument("--numerics", choices=["headline", "config4", "config5"], default="headline",
                     help="headline: Roe + WLS + MUSCL/Van Albada (north_star's sweep); config4: BASELINE config 4's "
-                         "Roe + WLS + Venkatakrishnan (K = 20)")
+                         "Roe + WLS + Venkatakrishnan (K = 20); config5: BASELINE config 5, the laminar NACA0012 "
+                         "(M 0.5, Re 5000) on the 8.1M-cell C5 O-grid (C4 with 4096 cells around), Roe + WLS + "
+                         "MUSCL/Van Albada + Sutherland viscous flux")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -309,9 +313,12 @@ def main():
 
     t0 = time.time()
     mult = world if (world > 1 and args.scaling == "weak") else 1
+    if args.numerics == "config5":
+        mult *= 2
     mesh, dims = c4_mesh(fa, args.scale, mult)
-    p = cases.physics("naca")
-    rec = "VANALBADA" if args.numerics == "headline" else "VENKATAKRISHNAN"
+    kind = "visc" if args.numerics == "config5" else "naca"
+    p = cases.physics(kind)
+    rec = "VENKATAKRISHNAN" if args.numerics == "config4" else "VANALBADA"
     n = cases.numerics("ROE", "LEASTSQUARES", rec)
     u = cases.state(mesh, p, seed=42)
     N, F, Fb = mesh.nelem, mesh.naface, mesh.nbface
@@ -489,13 +496,13 @@ def main():
     if world == 1 and not args.no_implicit:
         sys.path.insert(0, os.path.join(ROOT, "tools"))
         from bench_implicit import implicit_steps
-        implicit = next(implicit_steps(mesh, "naca", steps=3, warmup=1, init_steps=5, sweeps=1, lines=True,
-                                       operators=(False,)))
+        implicit = next(implicit_steps(mesh, "visc-c5" if args.numerics == "config5" else "naca", steps=3, warmup=1,
+                                       init_steps=5, sweeps=1, lines=True, operators=(False,)))
         implicit.pop("faces", None)
     # recorded (NOT measured by this run): the committed full-size convergence runs of the same
     # device solver (~10 min each), kept apart from the measured figures
     recorded = None
-    if world == 1 and not args.no_implicit:
+    if world == 1 and not args.no_implicit and args.numerics != "config5":
         recorded = {"note": "read from committed profiles, not re-run here"}
         runs = (("c4_first_order_converged_bench_mesh.txt",
                  "first-order LLF, line-implicit preconditioner, GMRES(40), expResidualRamp CFL 5 -> 1000"),
@@ -514,15 +521,17 @@ def main():
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        cpu = cpu_baseline(mesh, u, args.cpu_sweeps, rec)
+        cpu = cpu_baseline(mesh, u, args.cpu_sweeps, rec, kind)
 
     if rank == 0:
         # template of the timed sweep: k_residual_wls<FLUX=ROE(4), REC=MUSCL(1), DT, VISC=none(0), LIM=0>
         # (config4: REC=linear(2), LIM=Venkatakrishnan(2))
         tr = pmc_traffic("exact::" + kernel_symbol(sweep_name[0], args.numerics), N) if world == 1 else None
         cb = counter_bound(tr[3] if tr else None, sweep_ms)
-        wl = ("Roe + WLS gradients + MUSCL/Van Albada" if args.numerics == "headline" else
-              "Roe + WLS gradients + Venkatakrishnan (K = 20), BASELINE config 4's numerics")
+        wl = {"headline": "C4 mesh, Roe + WLS gradients + MUSCL/Van Albada",
+              "config4": "C4 mesh, Roe + WLS gradients + Venkatakrishnan (K = 20), BASELINE config 4's numerics",
+              "config5": "C5 mesh (8.1M cells), laminar M 0.5 Re 5000, Roe + WLS gradients + MUSCL/Van Albada + "
+                         "Sutherland viscous flux, BASELINE config 5's numerics"}[args.numerics]
         out = {
             "metric": "Mfaces/s (flux+residual sweep) + achieved HBM GB/s, 1/2/4/8 MI355X",
             "value": round(value, 3),
@@ -537,7 +546,7 @@ def main():
             "vs_baseline": None,
             "dtype": "f64",
             "data": "synthetic (generated C4 NACA0012 hybrid O-grid; seeded perturbed free stream)",
-            "config": {"workload": f"C4 mesh, {wl}, 2nd-order residual sweep with local time steps "
+            "config": {"workload": f"{wl}, 2nd-order residual sweep with local time steps "
                                    "(explicit pseudo-time step)",
                        "cells": N, "faces": F, "boundary_faces": Fb, **dims,
                        "parallelism": (f"dp{world}: {args.partitioner} {world}-way partition, two-layer halo, one RCCL "
@@ -556,8 +565,8 @@ def main():
                          "traffic_source": tr[1] if tr else None,
                          "kernel": sweep_name[0] if sweep_name else None,
                          "kernel_ms": round(sweep_ms, 5), "algorithmic_bytes": ab,
-                         "bytes_basis": ("SURVEY.md 8(d) 32F + 144N + 48Fb (124.0 B/face on C4) + 8N time step"
-                                         if args.numerics == "headline" else
+                         "bytes_basis": ("SURVEY.md 8(d) 32F + 144N + 48Fb (124.0 B/face) + 8N time step"
+                                         if args.numerics != "config4" else
                                          "SURVEY.md 8(d) Roe + linear/Venkatakrishnan: 48F + 144N + 48Fb + 8N time step"),
                          "frac_area_dt_basis": round(sweep_bytes_area_dt(*cnt) / (sweep_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
                          "area_dt_basis": "same + 8N (time step as area read 8 + dtm write 8 = 16 B/cell)",
@@ -581,7 +590,7 @@ def main():
 
 
 if __name__ == "__main__":
-    if len(sys.argv) == 6 and sys.argv[1] == "--cpu-child":
-        cpu_child(sys.argv[2], int(sys.argv[3]), int(sys.argv[4]), sys.argv[5])
+    if len(sys.argv) == 7 and sys.argv[1] == "--cpu-child":
+        cpu_child(sys.argv[2], int(sys.argv[3]), int(sys.argv[4]), sys.argv[5], sys.argv[6])
     else:
         main()

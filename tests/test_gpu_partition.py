@@ -19,6 +19,8 @@ CONFIGS = [("naca_small", "naca", "ROE", "LEASTSQUARES", "VANALBADA", True),
            ("naca_small", "naca", "AUSM", "GREENGAUSS", "WENO", True),
            ("naca_small", "viscconst", "ROE", "LEASTSQUARES", "VANALBADA", True),
            ("plate_small", "plate", "HLLC", "LEASTSQUARES", "NONE", True),
+           # BASELINE config 5's numerics: Roe + WLS + Van Albada + Sutherland (fused viscous, two-layer halo)
+           ("naca_small", "visc", "ROE", "LEASTSQUARES", "VANALBADA", True),
            ("naca_c2", "naca", "ROE", "LEASTSQUARES", "VANALBADA", True),
            # BASELINE config 4's numerics: Roe + WLS + Venkatakrishnan (K = 20)
            ("naca_c2", "naca", "ROE", "LEASTSQUARES", "VENKATAKRISHNAN", True)]
@@ -37,7 +39,8 @@ def run_partitioned(meshkey, kind, flux, grad, rec, order2, nparts, fast=False, 
     dt1 = np.zeros(m.nelem)
     one.compute_residual(u, r1, True, dt1)
     one.close()
-    part = fa.partition_rcb(m, nparts) if partitioner == "rcb" else fa.partition_graph(m, nparts)
+    part = (fa.partition_rcb(m, nparts) if partitioner == "rcb" else
+            fa.partition_graph(m, nparts, weights="cost" if partitioner == "graph-cost" else None))
     sps = [fa.FlowFV(m, p, n, partition=part, rank=k) for k in range(nparts)]
     glob = []
     dus, drs, dts = [], [], []
@@ -67,7 +70,7 @@ def run_partitioned(meshkey, kind, flux, grad, rec, order2, nparts, fast=False, 
 
 
 @pytest.mark.parametrize("nparts", [2, 3, 8])
-@pytest.mark.parametrize("cfg", CONFIGS[:8], ids=lambda c: f"{c[0]}-{c[2]}-{c[3]}-{c[4]}")
+@pytest.mark.parametrize("cfg", CONFIGS[:9], ids=lambda c: f"{c[0]}-{c[1]}-{c[2]}-{c[3]}-{c[4]}")
 def test_partitioned_residual_bitwise(cfg, nparts):
     r, dt, r1, dt1, stats = run_partitioned(*cfg, nparts)
     assert sum(s["ghosts"] for s in stats) > 0
@@ -79,7 +82,7 @@ def test_partitioned_residual_bitwise(cfg, nparts):
 
 
 def test_partitioned_c2_eight_ranks():
-    r, dt, r1, dt1, stats = run_partitioned(*CONFIGS[8], 8)
+    r, dt, r1, dt1, stats = run_partitioned(*CONFIGS[9], 8)
     np.testing.assert_array_equal(r, r1)
     np.testing.assert_array_equal(dt, dt1)
     # the fused residual runs most patches before the halo arrives (overlapped with the exchange)
@@ -88,12 +91,12 @@ def test_partitioned_c2_eight_ranks():
         assert s["interior_patches"] >= 0.7 * s["patches"], s
 
 
-@pytest.mark.parametrize("partitioner", ["rcb", "graph"])
+@pytest.mark.parametrize("partitioner", ["rcb", "graph", "graph-cost"])
 def test_partitioned_c2_eight_ranks_venkatakrishnan(partitioner):
     """config 4's numerics on the partitioned path: ONE exchange of the two-layer halo, the layer-1
     ghosts' gradients AND Venkatakrishnan limiter values computed locally, the fused kernel with
     interior patches ahead of the halo -- every owned row bitwise the single-GPU residual"""
-    r, dt, r1, dt1, stats = run_partitioned(*CONFIGS[9], 8, partitioner=partitioner)
+    r, dt, r1, dt1, stats = run_partitioned(*CONFIGS[10], 8, partitioner=partitioner)
     np.testing.assert_array_equal(r, r1)
     np.testing.assert_array_equal(dt, dt1)
     for s in stats:
@@ -105,11 +108,13 @@ def test_partitioned_c2_eight_ranks_venkatakrishnan(partitioner):
 @pytest.mark.parametrize("rec", ["VANALBADA", "VENKATAKRISHNAN"])
 def test_partitioned_c4_eight_ranks(rec):
     """BASELINE config 4 at its full size on the partitioned path the driver's 8-GPU run takes: the
-    4,063,232-cell C4 mesh split 8 ways by the graph partitioner, all ranks in one process (device
+    4,063,232-cell C4 mesh split 8 ways by the cost-weighted graph partitioner (bench.py's default), all
+    ranks in one process (device
     copies for RCCL), overlapped schedule (interior patches, one exchange of the two-layer halo, border
     patches on the comm stream) -- every owned row's residual and time step bitwise the single-GPU ones,
     for the headline numerics and config 4's Venkatakrishnan"""
-    r, dt, r1, dt1, stats = run_partitioned("naca_c4", "naca", "ROE", "LEASTSQUARES", rec, True, 8, partitioner="graph")
+    r, dt, r1, dt1, stats = run_partitioned("naca_c4", "naca", "ROE", "LEASTSQUARES", rec, True, 8,
+                                            partitioner="graph-cost")
     np.testing.assert_array_equal(r, r1)
     np.testing.assert_array_equal(dt, dt1)
     for s in stats:

@@ -46,6 +46,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--parts", type=int, nargs="+", default=[2, 4, 8])
     ap.add_argument("--rec", default="VANALBADA")
+    ap.add_argument("--config5", action="store_true", help="BASELINE config 5: C5 mesh (4096 around), laminar viscous")
     ap.add_argument("--steps", type=int, default=200)
     ap.add_argument("--preheat", type=float, default=0.3, help="seconds of untimed residuals before each timing")
     ap.add_argument("--scale", type=int, default=1)
@@ -57,8 +58,8 @@ def main():
     import fvens_amd as fa
     import cases
     from bench import c4_mesh
-    mesh, dims = c4_mesh(fa, args.scale)
-    p = cases.physics("naca")
+    mesh, dims = c4_mesh(fa, args.scale, 2 if args.config5 else 1)
+    p = cases.physics("visc" if args.config5 else "naca")
     n = cases.numerics("ROE", "LEASTSQUARES", args.rec)
     u = cases.state(mesh, p, seed=42)
     N = mesh.nelem
