@@ -371,6 +371,14 @@ class FlowFV:
                                                            int(maxiter), iptr(steps), dptr(ratio), dptr(hist)))
         return int(steps[0]), float(ratio[0]), hist[:int(steps[0])]
 
+    def tvdrk_device(self, d_u, order, cfl, finaltime, maxsteps):
+        """TVDRKSolver::solve on the device (aodesolver.cpp:669-758); returns (steps, physical time)"""
+        steps = np.zeros(1, np.int32)
+        t = np.zeros(1)
+        check(_ffi.lib().fvhip_tvdrk_device(self._h, ctypes.c_void_p(d_u), int(order), float(cfl), float(finaltime),
+                                            int(maxsteps), iptr(steps), dptr(t)))
+        return int(steps[0]), float(t[0])
+
     def steady_backward_euler_device(self, d_u, cfg: ImplicitConfig):
         """SteadyBackwardEulerSolver::solve on the device (aodesolver.cpp:363-638), linear systems by
         device GMRES; returns (stats dict, residual-norm history)"""
@@ -629,6 +637,13 @@ class FlowFVGroup:
         check(_ffi.lib().fvhip_group_steady_forward_euler_device(self._g, self._ptrs(d_us), float(cfl), float(tol),
                                                                  int(maxiter), iptr(steps), dptr(ratio), dptr(hist)))
         return int(steps[0]), float(ratio[0]), hist[:int(steps[0])]
+
+    def tvdrk_device(self, d_us, order, cfl, finaltime, maxsteps):
+        steps = np.zeros(1, np.int32)
+        t = np.zeros(1)
+        check(_ffi.lib().fvhip_group_tvdrk_device(self._g, self._ptrs(d_us), int(order), float(cfl), float(finaltime),
+                                                  int(maxsteps), iptr(steps), dptr(t)))
+        return int(steps[0]), float(t[0])
 
     def steady_backward_euler_device(self, d_us, cfg: ImplicitConfig):
         st = _ffi.FvSolveStats()

@@ -103,6 +103,10 @@ _SIGS = {
     "fvhip_group_steady_forward_euler_device": (ctypes.c_int, [ctypes.c_void_p, _vpp, ctypes.c_double,
                                                                ctypes.c_double, ctypes.c_int, c_int_p, c_dbl_p,
                                                                c_dbl_p]),
+    "fvhip_tvdrk_device": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_double,
+                                          ctypes.c_double, ctypes.c_int, c_int_p, c_dbl_p]),
+    "fvhip_group_tvdrk_device": (ctypes.c_int, [ctypes.c_void_p, _vpp, ctypes.c_int, ctypes.c_double,
+                                                ctypes.c_double, ctypes.c_int, c_int_p, c_dbl_p]),
     "fvhip_steady_backward_euler_device": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p,
                                                           ctypes.POINTER(FvImplicitConfig),
                                                           ctypes.POINTER(FvSolveStats), c_dbl_p]),

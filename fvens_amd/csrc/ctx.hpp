@@ -109,6 +109,7 @@ struct fvhip_ctx
 	const double *mf_u = nullptr, *mf_r = nullptr, *mf_mdt = nullptr;   // device state of the operator
 	double *d_part = nullptr, *d_pm = nullptr;
 	double *d_rn_part = nullptr, *d_rn = nullptr;   // residual-norm reduction of the explicit driver
+	double* d_ustage = nullptr;                      // TVD Runge-Kutta stage state (owned rows)
 	double* d_ent = nullptr;                        // entropy-error partial sums (fvhip_entropy_error_device)
 	/// work space of the implicit solver (implicit.cpp), allocated on first use
 	struct ImplicitWork {

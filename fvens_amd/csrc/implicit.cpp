@@ -451,6 +451,64 @@ static void forwardEuler(System& S, const std::vector<double*>& us, double cfl, 
 	if(resratio) *resratio = resi/initres;
 }
 
+/// TVDRKSolver::solve (aodesolver.cpp:669-758) on the device, restated as written: ustage = u once
+/// before the time loop (:701-704); per step, every stage's residual is computed at u -- the step's
+/// start state, since the reference passes uvec, not the stage state, to compute_residual (:719) --
+/// dtmin = min over cells of the first stage's local time steps (:722-728; across ranks the global
+/// minimum, so a partitioned run takes the 1-GPU steps, where the reference's ranks would each take
+/// their own), ustage = c0 u + c1 ustage - c2 dtmin cfl / area r (:735-744), then u = ustage and
+/// time += dtmin cfl (:747-757), while time <= finaltime - 1e-12 (A_SMALL_NUMBER). The stages' residuals
+/// are the same bits (same input, deterministic kernels), so one residual per step is computed and
+/// reused. maxsteps caps the loop (the reference has no cap).
+static void tvdrk(System& S, const std::vector<double*>& us, int order, double cfl, double finaltime, int maxsteps,
+                  int* steps, double* time_out)
+{
+	static const double coef[3][3][3] = {                                       // initialize_TVDRK_Coeffs :45-67
+		{{1.0, 0.0, 1.0}, {0, 0, 0}, {0, 0, 0}},
+		{{1.0, 0.0, 1.0}, {0.5, 0.5, 0.5}, {0, 0, 0}},
+		{{1.0, 0.0, 1.0}, {0.75, 0.25, 0.25}, {0.3333333333333333, 0.6666666666666667, 0.6666666666666667}}};
+	if(order < 1 || order > 3) throw std::invalid_argument("TVD RK: temporal order must be 1, 2 or 3");
+	if(maxsteps < 1) throw std::invalid_argument("TVD RK: maxsteps must be >= 1");
+	const double (*tc)[3] = coef[order-1];
+	S.each([&](size_t i, fvhip_ctx* h) {
+		h->ensureReductions();
+		if(!h->d_ustage) h->d_ustage = dalloc(4*static_cast<size_t>(std::max(h->L.ncell, 1)), h->owned);
+		HC(hipMemcpyAsync(h->d_ustage, us[i], sizeof(double)*4*static_cast<size_t>(h->L.ncell), hipMemcpyDeviceToDevice,
+		                  h->stream));
+	});
+	std::vector<const double*> cu(us.begin(), us.end());
+	std::vector<double*> rs, dts;
+	for(fvhip_ctx* h : S.hs) { rs.push_back(h->d_r); dts.push_back(h->d_dtm); }
+	int step = 0;
+	double time = 0;
+	while(time <= finaltime - 1e-12 && step < maxsteps) {
+		fvhip_ctx::residual_seq(S.hs, cu, rs, true, dts, true, S.exg);              // :712-719 (zeroed, -r(u))
+		S.each([&](size_t, fvhip_ctx* h) {
+			launch_min(h->L.ncell, h->d_dtm, h->iw.part, h->iw.red, h->stream);
+			if(h->comm) NC(ncclAllReduce(h->iw.red, h->iw.red, 1, ncclDouble, ncclMin, h->comm, h->stream));
+			HC(hipMemcpyAsync(h->iw.h_red, h->iw.red, sizeof(double), hipMemcpyDeviceToHost, h->stream));
+		});
+		double dtmin = INFINITY;
+		S.each([&](size_t, fvhip_ctx* h) { HC(hipStreamSynchronize(h->stream)); dtmin = std::min(dtmin, h->iw.h_red[0]); });
+		if(!std::isfinite(dtmin)) throw std::runtime_error("TVDRK solver diverged - dtmin is Nan or inf!");   // :730-731
+		for(int s = 0; s < order; s++) {
+			const double sc = tc[s][2]*dtmin*cfl;
+			S.each([&](size_t i, fvhip_ctx* h) {
+				launch_tvdrk_stage(h->L.ncell, tc[s][0], tc[s][1], sc, h->M.area, h->d_r, us[i], h->d_ustage, h->stream);
+			});
+		}
+		S.each([&](size_t i, fvhip_ctx* h) {
+			HC(hipMemcpyAsync(us[i], h->d_ustage, sizeof(double)*4*static_cast<size_t>(h->L.ncell), hipMemcpyDeviceToDevice,
+			                  h->stream));
+			HC(hipGetLastError());
+		});
+		step++;
+		time += dtmin*cfl;
+	}
+	if(steps) *steps = step;
+	if(time_out) *time_out = time;
+}
+
 static System single(fvhip_ctx* h)
 {
 	if(h->in_group) throw std::runtime_error("handle belongs to a group: use the fvhip_group_* entry point");
@@ -512,6 +570,26 @@ int fvhip_group_steady_forward_euler_device(fvhip_group g, double* const* d_u, d
 	return guard([&] {
 		System S = ofGroup(g);
 		forwardEuler(S, std::vector<double*>(d_u, d_u + S.size()), cfl, tol, maxiter, steps, resratio, reshistory);
+		S.sync();
+	});
+}
+
+int fvhip_tvdrk_device(fvhip_handle h, double* d_u, int order, double cfl, double finaltime, int maxsteps,
+                       int* steps, double* time)
+{
+	return guard([&] {
+		System S = single(h);
+		tvdrk(S, {d_u}, order, cfl, finaltime, maxsteps, steps, time);
+		S.sync();
+	});
+}
+
+int fvhip_group_tvdrk_device(fvhip_group g, double* const* d_u, int order, double cfl, double finaltime, int maxsteps,
+                             int* steps, double* time)
+{
+	return guard([&] {
+		System S = ofGroup(g);
+		tvdrk(S, std::vector<double*>(d_u, d_u + S.size()), order, cfl, finaltime, maxsteps, steps, time);
 		S.sync();
 	});
 }

@@ -242,6 +242,26 @@ private:
 	fvhip_implicit_config conf;
 };
 
+/// TVDRKSolver (aodesolver.hpp: UnsteadySolver / TVDRKSolver; aodesolver.cpp:646-758) on the device:
+/// constructed with the reference's (temporal order, physical CFL), solve(finaltime) advances d_u
+class TVDRKSolver_HIP
+{
+public:
+	TVDRKSolver_HIP(const FlowFV_HIP* s, int temporal_order, double cfl_num, int max_steps = 1 << 30)
+		: spatial(s), order(temporal_order), cfl(cfl_num), maxsteps(max_steps) { }
+	StatusCode solve(double* d_u, double finaltime) {
+		check(fvhip_tvdrk_device(spatial->handle(), d_u, order, cfl, finaltime, maxsteps, &steps, &time));
+		return 0;
+	}
+	int steps = 0;
+	double time = 0;              ///< physical time reached
+private:
+	const FlowFV_HIP* spatial;
+	int order;
+	double cfl;
+	int maxsteps;
+};
+
 /// Batched InviscidFlux::get_flux / get_jacobian on the device (anumericalflux.hpp:32-45)
 class InviscidFlux_HIP
 {

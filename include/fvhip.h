@@ -248,6 +248,15 @@ int fvhip_steady_forward_euler_device(fvhip_handle h, double* d_u, double cfl, d
                                       int* steps, double* resratio, double* reshistory);
 int fvhip_group_steady_forward_euler_device(fvhip_group g, double* const* d_u, double cfl, double tol, int maxiter,
                                             int* steps, double* resratio, double* reshistory);
+/** TVDRKSolver::solve (aodesolver.cpp:669-758), the unsteady explicit driver, restated as written:
+ *  temporal order 1-3 (initialize_TVDRK_Coeffs :45-67), dtmin = min over cells of the local time steps
+ *  (over all ranks), every stage's residual at the step's start state (the reference passes uvec to
+ *  compute_residual, :719), until time > finaltime - 1e-12 or maxsteps steps; returns the steps taken
+ *  and the physical time reached */
+int fvhip_tvdrk_device(fvhip_handle h, double* d_u, int order, double cfl, double finaltime, int maxsteps,
+                       int* steps, double* time);
+int fvhip_group_tvdrk_device(fvhip_group g, double* const* d_u, int order, double cfl, double finaltime, int maxsteps,
+                             int* steps, double* time);
 
 /** SteadySolverConfig of the main (or starter) solve (aodesolver.hpp, controlparser.cpp:150-206) and
  *  the linear-solver options of the reference's .solverc files */
