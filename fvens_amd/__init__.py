@@ -212,9 +212,18 @@ class UMesh:
             pass
 
 
+def _named(table, name, what):
+    """the factories' string -> scheme lookup (afactory.cpp:38-81, 178-211; abc.cpp:460-500): an unknown
+    name is refused here (the reference prints a warning and returns nullptr, dereferenced later)"""
+    try:
+        return table[name]
+    except KeyError:
+        raise ValueError(f"{what} {name!r} not available (one of {', '.join(table)})") from None
+
+
 def _config_struct(pconf: FlowPhysicsConfig, nconf: FlowNumericsConfig):
     n = len(pconf.bcconf)
-    types = np.array([BCTYPES[b.bc_type.lower()] for b in pconf.bcconf], np.int32)
+    types = np.array([_named(BCTYPES, b.bc_type.lower(), "boundary condition") for b in pconf.bcconf], np.int32)
     tags = np.array([b.bc_tag for b in pconf.bcconf], np.int32)
     vals = np.zeros(2 * max(n, 1))
     for i, b in enumerate(pconf.bcconf):
@@ -224,12 +233,12 @@ def _config_struct(pconf: FlowPhysicsConfig, nconf: FlowNumericsConfig):
     c.gamma, c.Minf, c.Tinf, c.Reinf, c.Pr, c.aoa = (pconf.gamma, pconf.Minf, pconf.Tinf, pconf.Reinf,
                                                      pconf.Pr, pconf.aoa)
     c.viscous_sim, c.const_visc = int(pconf.viscous_sim), int(pconf.const_visc)
-    c.conv_numflux = FLUXES[nconf.conv_numflux.upper()]
+    c.conv_numflux = _named(FLUXES, nconf.conv_numflux.upper(), "inviscid flux")
     c.fast_math = int(getattr(nconf, "fast_math", False))
-    c.conv_numflux_jac = FLUXES[nconf.conv_numflux_jac.upper()]
+    c.conv_numflux_jac = _named(FLUXES, nconf.conv_numflux_jac.upper(), "inviscid flux (Jacobian)")
     grad = nconf.gradientscheme.upper()
     c.gradientscheme = GRADIENTS.get(grad, 0)
-    c.reconstruction = RECONSTRUCTIONS[nconf.reconstruction.upper()]
+    c.reconstruction = _named(RECONSTRUCTIONS, nconf.reconstruction.upper(), "reconstruction")
     c.limiter_param = nconf.limiter_param
     c.order2 = int(nconf.order2 and grad != "NONE")       # controlparser.cpp:180-181
     c.nbc = n
@@ -502,7 +511,7 @@ def local_flux(flux, gas, ul, ur, n):
     n = np.ascontiguousarray(n, np.float64)
     out = np.zeros_like(ul)
     g = np.array(gas, np.float64)
-    check(_ffi.lib().fvhip_local_flux(FLUXES[flux.upper()] if isinstance(flux, str) else flux, dptr(g),
+    check(_ffi.lib().fvhip_local_flux(_named(FLUXES, flux.upper(), "inviscid flux") if isinstance(flux, str) else flux, dptr(g),
                                       ul.shape[0], dptr(ul), dptr(ur), dptr(n), dptr(out)))
     return out
 
@@ -516,7 +525,7 @@ def local_flux_jacobian(flux, gas, ul, ur, n):
     dl = np.zeros((nf, 4, 4))
     dr = np.zeros((nf, 4, 4))
     g = np.array(gas, np.float64)
-    check(_ffi.lib().fvhip_local_flux_jacobian(FLUXES[flux.upper()] if isinstance(flux, str) else flux, dptr(g),
+    check(_ffi.lib().fvhip_local_flux_jacobian(_named(FLUXES, flux.upper(), "inviscid flux") if isinstance(flux, str) else flux, dptr(g),
                                                nf, dptr(ul), dptr(ur), dptr(n), dptr(dl), dptr(dr)))
     return dl, dr
 

@@ -52,10 +52,24 @@ int fvhip_device_count(void) {
 	return n;
 }
 
+/// what FlowFV_base's constructor builds from the config (flow_spatial.cpp:45-50, 320): the factories
+/// return nullptr for an unknown flux or reconstruction name (afactory.cpp:79-81, 208-211) and the
+/// first residual then dereferences it; here the handle is refused instead. An unknown gradient
+/// scheme is the reference's ZeroGradients (afactory.cpp:123-127) and stays allowed.
 static void checkConfig(const fvhip_flow_config* cfg)
 {
-	if(cfg->nbc > MAXBC) throw std::invalid_argument("too many boundary conditions");
+	if(cfg->nbc < 0 || cfg->nbc > MAXBC) throw std::invalid_argument("too many boundary conditions");
+	if(cfg->nbc > 0 && (!cfg->bc_type || !cfg->bc_tag || !cfg->bc_vals)) throw std::invalid_argument("null argument");
 	if(cfg->conv_numflux < 0 || cfg->conv_numflux > 6) throw std::invalid_argument("unknown flux"); // afactory.cpp:78-80
+	if(cfg->conv_numflux_jac < 0 || cfg->conv_numflux_jac > 6) throw std::invalid_argument("unknown Jacobian flux");
+	if(cfg->reconstruction < 0 || cfg->reconstruction > 4)
+		throw std::invalid_argument("Invalid reconstruction");                              // afactory.cpp:208-211
+	// Venkatakrishnan's eps^2 = (K clength)^3 (limitedlinearreconstruction.cpp:222): K = 0 makes phi 0/0
+	// wherever a cell's neighbours all equal it; the reference never parses K (controlparser.cpp:227-232)
+	if(cfg->reconstruction == FVHIP_REC_VENKATAKRISHNAN && !(cfg->limiter_param > 0 && std::isfinite(cfg->limiter_param)))
+		throw std::invalid_argument("Venkatakrishnan limiter: limiter_param (K) must be finite and > 0");
+	if(cfg->reconstruction == FVHIP_REC_WENO && !(cfg->limiter_param >= 0 && std::isfinite(cfg->limiter_param)))
+		throw std::invalid_argument("WENO: limiter_param (lambda) must be finite and >= 0");
 	for(int i = 0; i < cfg->nbc; i++) {
 		const int t = cfg->bc_type[i];
 		if(t == FVHIP_BC_PERIODIC || t < 0 || t > 7) throw std::invalid_argument("BC type not implemented yet!"); // abc.cpp:493-494
