@@ -58,6 +58,19 @@ inline int guard(F&& f) {
 	catch(...) { g_err = "unknown error"; return 1; }
 }
 
+/// entry-point argument check: a null handle or a null array the call reads or writes is refused
+/// with "null <what>" before any host or device access (a null device pointer would fault the GPU)
+inline void need(const void* p, const char* what) {
+	if(!p) throw std::invalid_argument(std::string("null ") + what);
+}
+
+/// the same for a group call's per-rank arrays: the array of pointers and each rank's entry
+template <typename T>
+inline void needEach(T* const* p, size_t n, const char* what) {
+	need(p, what);
+	for(size_t i = 0; i < n; i++) need(p[i], what);
+}
+
 template <typename T>
 inline T* upload(const std::vector<T>& v, std::vector<void*>& owned) {
 	if(v.empty()) return nullptr;

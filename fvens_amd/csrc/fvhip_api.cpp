@@ -196,6 +196,7 @@ int fvhip_create(const fvhip_mesh* mesh, const fvhip_flow_config* cfg, int devic
 int fvhip_set_rank(fvhip_handle h, int rank, int nranks)
 {
 	return guard([&] {
+		need(h, "handle");
 		if(!h->rankmesh) throw std::invalid_argument("fvhip_set_rank: not a per-rank mesh handle");
 		if(rank < 0 || rank >= nranks) throw std::invalid_argument("rank out of range");
 		for(int q : h->L.nbr_rank)
@@ -290,6 +291,7 @@ int fvhip_comm_unique_id(void* id128)
 int fvhip_comm_init(fvhip_handle h, int nranks, int rank, const void* id128)
 {
 	return guard([&] {
+		need(h, "handle");
 		if(h->rankmesh && h->rank < 0 && fvhip_set_rank(h, rank, nranks)) throw std::runtime_error(g_err);
 		if(nranks != h->nparts || rank != h->rank)
 			throw std::invalid_argument("communicator does not match the handle's partition");
@@ -303,6 +305,8 @@ int fvhip_comm_init(fvhip_handle h, int nranks, int rank, const void* id128)
 int fvhip_group_create(fvhip_handle* hs, int n, fvhip_group* out)
 {
 	return guard([&] {
+		need(hs, "handles"); need(out, "group");
+		if(n < 1) throw std::invalid_argument("a group needs one handle per rank of one partition");
 		std::unique_ptr<fvhip_group_s> g(new fvhip_group_s());
 		std::vector<int> seen(n, 0);
 		for(int i = 0; i < n; i++) {
@@ -315,12 +319,14 @@ int fvhip_group_create(fvhip_handle* hs, int n, fvhip_group* out)
 	});
 }
 
-int fvhip_group_destroy(fvhip_group g) { return guard([&] { for(fvhip_ctx* h : g->hs) h->in_group = false; delete g; }); }
+int fvhip_group_destroy(fvhip_group g) { return guard([&] { if(!g) return; for(fvhip_ctx* h : g->hs) h->in_group = false; delete g; }); }
 
 int fvhip_group_compute_residual_device(fvhip_group g, const double* const* d_u, double* const* d_r,
                                         int gettimesteps, double* const* d_dtm, int flags)
 {
 	return guard([&] {
+		need(g, "group");
+		needEach(d_u, g->hs.size(), "u"); needEach(d_r, g->hs.size(), "residual"); if(gettimesteps) needEach(d_dtm, g->hs.size(), "dtm");
 		const size_t n = g->hs.size();
 		std::vector<const double*> us(d_u, d_u + n);
 		std::vector<double*> rs(d_r, d_r + n), dts(n, nullptr);
@@ -334,6 +340,8 @@ int fvhip_group_compute_residual_device(fvhip_group g, const double* const* d_u,
 int fvhip_trace_exchange_device(fvhip_handle h, const double* d_left, double* d_right, int width)
 {
 	return guard([&] {
+		need(h, "handle");
+		need(d_left, "left trace"); need(d_right, "right trace");
 		HC(hipSetDevice(h->device));
 		h->trace_exchange_rccl(d_left, d_right, width);
 		HC(hipStreamSynchronize(h->stream));
@@ -343,6 +351,8 @@ int fvhip_trace_exchange_device(fvhip_handle h, const double* d_left, double* d_
 int fvhip_group_trace_exchange_device(fvhip_group g, const double* const* d_left, double* const* d_right, int width)
 {
 	return guard([&] {
+		need(g, "group");
+		needEach(d_left, g->hs.size(), "left trace"); needEach(d_right, g->hs.size(), "right trace");
 		const std::vector<fvhip_ctx*>& hs = g->hs;
 		const size_t n = hs.size();
 		std::vector<fvhip_ctx*> byrank(n);
@@ -378,6 +388,8 @@ int fvhip_compute_residual_device(fvhip_handle h, const double* d_u, double* d_r
                                   double* d_dtm, int flags)
 {
 	return guard([&] {
+		need(h, "handle");
+		need(d_u, "u"); need(d_r, "residual"); if(gettimesteps) need(d_dtm, "dtm");
 		HC(hipSetDevice(h->device));
 		h->use_staged = (flags & FVHIP_RES_STAGED) != 0;
 		h->use_pipe = (flags & FVHIP_RES_PIPELINED) != 0;
@@ -401,6 +413,8 @@ static void fromInternal(fvhip_ctx* h, const double* src, double* dst, int width
 int fvhip_compute_residual(fvhip_handle h, const double* u, double* r, int gettimesteps, double* dtm)
 {
 	return guard([&] {
+		need(h, "handle");
+		need(u, "u"); need(r, "residual"); if(gettimesteps) need(dtm, "dtm");
 		HC(hipSetDevice(h->device));
 		const size_t N = static_cast<size_t>(h->L.ncell);
 		std::vector<double>& st = h->h_stage;
@@ -424,6 +438,8 @@ int fvhip_compute_residual(fvhip_handle h, const double* u, double* r, int getti
 int fvhip_get_gradients(fvhip_handle h, const double* u, double* grads)
 {
 	return guard([&] {
+		need(h, "handle");
+		need(u, "u"); need(grads, "grads");
 		HC(hipSetDevice(h->device));
 		const size_t N = static_cast<size_t>(h->L.ncell);
 		std::vector<double>& st = h->h_stage;
@@ -448,6 +464,8 @@ int fvhip_surface_data_device(fvhip_handle h, const double* d_u, int marker, dou
                               int* nfaces)
 {
 	return guard([&] {
+		need(h, "handle");
+		need(d_u, "u"); need(funcs, "funcs");
 		if(!funcs) throw std::invalid_argument("funcs must not be NULL");
 		HC(hipSetDevice(h->device));
 		fvhip_ctx::SurfCache& c = h->surfaceFaces(marker);
@@ -492,6 +510,8 @@ static double* entropySum(fvhip_ctx* h, const double* d_u)
 int fvhip_entropy_error_device(fvhip_handle h, const double* d_u, double* err)
 {
 	return guard([&] {
+		need(h, "handle");
+		need(d_u, "u");
 		if(!err) throw std::invalid_argument("err must not be NULL");
 		HC(hipSetDevice(h->device));
 		double* out = entropySum(h, d_u);
@@ -507,6 +527,8 @@ int fvhip_entropy_error_device(fvhip_handle h, const double* d_u, double* err)
 int fvhip_group_entropy_error_device(fvhip_group g, const double* const* d_u, double* err)
 {
 	return guard([&] {
+		need(g, "group");
+		needEach(d_u, g->hs.size(), "u");
 		double tot = 0;
 		for(size_t i = 0; i < g->hs.size(); i++) {          // rank order
 			fvhip_ctx* h = g->hs[i];
@@ -524,6 +546,8 @@ int fvhip_group_entropy_error_device(fvhip_group g, const double* const* d_u, do
 int fvhip_assemble_jacobian(fvhip_handle h, const double* u, double* diag, double* lower, double* upper)
 {
 	return guard([&] {
+		need(h, "handle");
+		need(u, "u"); need(diag, "diag"); need(lower, "lower"); need(upper, "upper");
 		HC(hipSetDevice(h->device));
 		const size_t N = static_cast<size_t>(h->L.ncell), Fi = static_cast<size_t>(h->L.ninface);
 		std::vector<double>& st = h->h_stage;
@@ -554,6 +578,8 @@ int fvhip_assemble_jacobian(fvhip_handle h, const double* u, double* diag, doubl
 int fvhip_assemble_jacobian_device(fvhip_handle h, const double* d_u, double* d_diag, double* d_lower, double* d_upper)
 {
 	return guard([&] {
+		need(h, "handle");
+		need(d_u, "u"); need(d_diag, "diag"); need(d_lower, "lower"); need(d_upper, "upper");
 		HC(hipSetDevice(h->device));
 		h->assemble(d_u, d_diag, d_lower, d_upper);
 	});
@@ -562,6 +588,8 @@ int fvhip_assemble_jacobian_device(fvhip_handle h, const double* d_u, double* d_
 int fvhip_add_pseudo_time_term_device(fvhip_handle h, double cfl, double* d_dtm, double* d_diag)
 {
 	return guard([&] {
+		need(h, "handle");
+		need(d_dtm, "dtm"); need(d_diag, "diag");
 		HC(hipSetDevice(h->device));
 		h->ensureJacobian();
 		h->timed("k_pseudo_time", [&]{ launch_pseudo_time(h->L.ncell, h->M.area, cfl, d_dtm, d_diag, h->stream); });
@@ -573,6 +601,8 @@ int fvhip_block_apply_device(fvhip_handle h, const double* d_diag, const double*
                              const double* d_x, double* d_y)
 {
 	return guard([&] {
+		need(h, "handle");
+		need(d_diag, "diag"); need(d_lower, "lower"); need(d_upper, "upper"); need(d_x, "x"); need(d_y, "y");
 		HC(hipSetDevice(h->device));
 		h->ensureJacobian();
 		h->timed("k_block_apply", [&]{ launch_block_apply(h->J, d_diag, d_lower, d_upper, d_x, d_y, h->stream); });
@@ -583,6 +613,8 @@ int fvhip_block_apply_device(fvhip_handle h, const double* d_diag, const double*
 int fvhip_jacobian_pattern(fvhip_handle h, int* rowptr, int* colind)
 {
 	return guard([&] {
+		need(h, "handle");
+		need(rowptr, "rowptr"); need(colind, "colind");
 		const int N = h->L.ncell, nb = h->L.nbface, Fi = h->L.ninface;
 		// reference cell numbering: diagonal plus one block per interior face on each side
 		std::vector<int> cnt(N, 1);
@@ -603,6 +635,8 @@ int fvhip_jacobian_pattern(fvhip_handle h, int* rowptr, int* colind)
 int fvhip_assemble_jacobian_bsr(fvhip_handle h, const double* u, const int* rowptr, const int* colind, double* vals)
 {
 	return guard([&] {
+		need(h, "handle");
+		need(u, "u"); need(rowptr, "rowptr"); need(colind, "colind"); need(vals, "vals");
 		const int N = h->L.ncell, Fi = h->L.ninface;
 		std::vector<double> diag(16*static_cast<size_t>(N)), lo(16*static_cast<size_t>(std::max(Fi,1))),
 			up(16*static_cast<size_t>(std::max(Fi,1)));
@@ -626,6 +660,7 @@ int fvhip_assemble_jacobian_bsr(fvhip_handle h, const double* u, const int* rowp
 int fvhip_matfree_set_state(fvhip_handle h, const double* u, const double* r, const double* mdt)
 {
 	return guard([&] {
+		need(h, "handle");
 		HC(hipSetDevice(h->device));
 		const size_t N = static_cast<size_t>(h->L.ncell);
 		if(!h->d_mf_u) { h->d_mf_u = dalloc(4*N, h->owned); h->d_mf_r = dalloc(4*N, h->owned); h->d_mf_mdt = dalloc(N, h->owned); }
@@ -643,6 +678,8 @@ int fvhip_matfree_set_state(fvhip_handle h, const double* u, const double* r, co
 int fvhip_matfree_apply(fvhip_handle h, const double* x, double* y)
 {
 	return guard([&] {
+		need(h, "handle");
+		need(x, "x"); need(y, "y");
 		HC(hipSetDevice(h->device));
 		const size_t N = static_cast<size_t>(h->L.ncell);
 		if(!h->d_mf_u) throw std::runtime_error("matrix-free operator: state not set");
@@ -664,12 +701,14 @@ int fvhip_matfree_apply(fvhip_handle h, const double* x, double* y)
 
 int fvhip_matfree_set_state_device(fvhip_handle h, const double* d_u, const double* d_r, const double* d_mdt)
 {
-	return guard([&] { h->mf_u = d_u; h->mf_r = d_r; h->mf_mdt = d_mdt; });
+	return guard([&] { need(h, "handle"); h->mf_u = d_u; h->mf_r = d_r; h->mf_mdt = d_mdt; });
 }
 
 int fvhip_matfree_apply_device(fvhip_handle h, const double* d_x, double* d_y)
 {
 	return guard([&] {
+		need(h, "handle");
+		need(d_x, "x"); need(d_y, "y");
 		HC(hipSetDevice(h->device));
 		if(!h->halo()) { h->matfree(d_x, d_y); return; }
 		if(!h->comm) throw std::runtime_error("partitioned handle: call fvhip_comm_init (or use a group) first");
@@ -681,6 +720,7 @@ int fvhip_group_matfree_set_state_device(fvhip_group g, const double* const* d_u
                                          const double* const* d_mdt)
 {
 	return guard([&] {
+		need(g, "group");
 		for(size_t i = 0; i < g->hs.size(); i++) { g->hs[i]->mf_u = d_u[i]; g->hs[i]->mf_r = d_r[i]; g->hs[i]->mf_mdt = d_mdt[i]; }
 	});
 }
@@ -688,16 +728,20 @@ int fvhip_group_matfree_set_state_device(fvhip_group g, const double* const* d_u
 int fvhip_group_matfree_apply_device(fvhip_group g, const double* const* d_x, double* const* d_y)
 {
 	return guard([&] {
+		need(g, "group");
+		needEach(d_x, g->hs.size(), "x"); needEach(d_y, g->hs.size(), "y");
 		const size_t n = g->hs.size();
 		sysMatfree(g->hs, groupExchange(g), std::vector<const double*>(d_x, d_x + n), std::vector<double*>(d_y, d_y + n));
 	});
 }
 
-int fvhip_matfree_set_eps(fvhip_handle h, double eps) { return guard([&] { h->mf_eps = eps; }); }
+int fvhip_matfree_set_eps(fvhip_handle h, double eps) { return guard([&] { need(h, "handle"); h->mf_eps = eps; }); }
 
 int fvhip_to_internal(fvhip_handle h, const double* host_ref, double* d_internal, int width)
 {
 	return guard([&] {
+		need(h, "handle");
+		need(host_ref, "host array"); need(d_internal, "device array");
 		HC(hipSetDevice(h->device));
 		std::vector<double> st(static_cast<size_t>(h->L.ncell)*width);
 		toInternal(h, host_ref, st.data(), width);
@@ -707,6 +751,8 @@ int fvhip_to_internal(fvhip_handle h, const double* host_ref, double* d_internal
 int fvhip_from_internal(fvhip_handle h, const double* d_internal, double* host_ref, int width)
 {
 	return guard([&] {
+		need(h, "handle");
+		need(d_internal, "device array"); need(host_ref, "host array");
 		HC(hipSetDevice(h->device));
 		HC(hipStreamSynchronize(h->stream));
 		std::vector<double> st(static_cast<size_t>(h->L.ncell)*width);
@@ -716,25 +762,26 @@ int fvhip_from_internal(fvhip_handle h, const double* d_internal, double* host_r
 }
 int fvhip_get_permutation(fvhip_handle h, int* perm)
 {
-	return guard([&] { std::memcpy(perm, h->L.perm.data(), h->L.perm.size()*sizeof(int)); });
+	return guard([&] { need(h, "handle"); need(perm, "perm"); std::memcpy(perm, h->L.perm.data(), h->L.perm.size()*sizeof(int)); });
 }
 int fvhip_device_alloc(fvhip_handle h, unsigned long long bytes, void** ptr)
 {
-	return guard([&] { HC(hipSetDevice(h->device)); HC(hipMalloc(ptr, bytes)); });
+	return guard([&] { need(h, "handle"); need(ptr, "ptr"); HC(hipSetDevice(h->device)); HC(hipMalloc(ptr, bytes)); });
 }
 int fvhip_device_free(fvhip_handle h, void* ptr)
 {
-	return guard([&] { HC(hipSetDevice(h->device)); HC(hipFree(ptr)); });
+	return guard([&] { need(h, "handle"); HC(hipSetDevice(h->device)); HC(hipFree(ptr)); });
 }
 int fvhip_synchronize(fvhip_handle h)
 {
-	return guard([&] { HC(hipSetDevice(h->device)); HC(hipStreamSynchronize(h->stream)); });
+	return guard([&] { need(h, "handle"); HC(hipSetDevice(h->device)); HC(hipStreamSynchronize(h->stream)); });
 }
 void* fvhip_stream(fvhip_handle h) { return h ? static_cast<void*>(h->stream) : nullptr; }
 
 int fvhip_profile(fvhip_handle h, int enable)
 {
 	return guard([&] {
+		need(h, "handle");
 		if(!enable && h->prof) h->collect();
 		h->prof = enable != 0;
 		if(enable) { h->collect(); h->acc.clear(); }
@@ -745,6 +792,8 @@ int fvhip_kernel_times(fvhip_handle h, int maxk, char* names, int namelen, doubl
 {
 	int n = 0;
 	const int rc = guard([&] {
+		need(h, "handle");
+		if(maxk > 0) { need(names, "names"); need(ms, "ms"); need(counts, "counts"); }
 		h->collect();
 		for(auto& kv : h->acc) {
 			if(n >= maxk) break;
@@ -782,7 +831,7 @@ static void layoutStats(const Layout& L, long long* s, int n)
 
 int fvhip_layout_stats(fvhip_handle h, long long* s)
 {
-	return guard([&] { layoutStats(h->L, s, 12); });
+	return guard([&] { need(h, "handle"); need(s, "stats"); layoutStats(h->L, s, 12); });
 }
 
 int fvhip_layout_probe(const fvhip_mesh* mesh, const fvhip_flow_config* cfg, long long* s)

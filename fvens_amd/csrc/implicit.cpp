@@ -536,6 +536,8 @@ int fvhip_steady_backward_euler_device(fvhip_handle h, double* d_u, const fvhip_
                                        fvhip_solve_stats* stats, double* reshistory)
 {
 	return guard([&] {
+		need(h, "handle");
+		need(d_u, "u");
 		if(!cfg || !stats) throw std::invalid_argument("null argument");
 		System S = single(h);
 		backwardEuler(S, {d_u}, *cfg, stats, reshistory);
@@ -547,6 +549,8 @@ int fvhip_group_steady_backward_euler_device(fvhip_group g, double* const* d_u, 
                                              fvhip_solve_stats* stats, double* reshistory)
 {
 	return guard([&] {
+		need(g, "group");
+		needEach(d_u, g->hs.size(), "u");
 		if(!cfg || !stats) throw std::invalid_argument("null argument");
 		System S = ofGroup(g);
 		backwardEuler(S, std::vector<double*>(d_u, d_u + S.size()), *cfg, stats, reshistory);
@@ -558,6 +562,8 @@ int fvhip_steady_forward_euler_device(fvhip_handle h, double* d_u, double cfl, d
                                       int* steps, double* resratio, double* reshistory)
 {
 	return guard([&] {
+		need(h, "handle");
+		need(d_u, "u");
 		System S = single(h);
 		forwardEuler(S, {d_u}, cfl, tol, maxiter, steps, resratio, reshistory);
 		S.sync();
@@ -568,6 +574,8 @@ int fvhip_group_steady_forward_euler_device(fvhip_group g, double* const* d_u, d
                                             int* steps, double* resratio, double* reshistory)
 {
 	return guard([&] {
+		need(g, "group");
+		needEach(d_u, g->hs.size(), "u");
 		System S = ofGroup(g);
 		forwardEuler(S, std::vector<double*>(d_u, d_u + S.size()), cfl, tol, maxiter, steps, resratio, reshistory);
 		S.sync();
@@ -578,6 +586,8 @@ int fvhip_tvdrk_device(fvhip_handle h, double* d_u, int order, double cfl, doubl
                        int* steps, double* time)
 {
 	return guard([&] {
+		need(h, "handle");
+		need(d_u, "u");
 		System S = single(h);
 		tvdrk(S, {d_u}, order, cfl, finaltime, maxsteps, steps, time);
 		S.sync();
@@ -588,6 +598,8 @@ int fvhip_group_tvdrk_device(fvhip_group g, double* const* d_u, int order, doubl
                              int* steps, double* time)
 {
 	return guard([&] {
+		need(g, "group");
+		needEach(d_u, g->hs.size(), "u");
 		System S = ofGroup(g);
 		tvdrk(S, std::vector<double*>(d_u, d_u + S.size()), order, cfl, finaltime, maxsteps, steps, time);
 		S.sync();
@@ -599,6 +611,8 @@ int fvhip_gmres_blocks_device(fvhip_handle h, const double* d_diag, const double
                               int* iters, double* resnorm)
 {
 	return guard([&] {
+		need(h, "handle");
+		need(d_diag, "diag"); need(d_lower, "lower"); need(d_upper, "upper"); need(d_b, "b"); need(d_x, "x");
 		if(restart < 1 || restart > KRY_MAXK) throw std::invalid_argument("restart must be in [1, 128]");
 		if(sweeps < 1) throw std::invalid_argument("sweeps must be >= 1");
 		System S = single(h);
@@ -619,6 +633,8 @@ int fvhip_line_precondition_device(fvhip_handle h, const double* d_diag, const d
                                    double line_threshold, const double* d_v, double* d_z)
 {
 	return guard([&] {
+		need(h, "handle");
+		need(d_diag, "diag"); need(d_lower, "lower"); need(d_upper, "upper"); need(d_v, "v"); need(d_z, "z");
 		if(!d_diag || !d_v || !d_z || (h->L.ninface > 0 && (!d_lower || !d_upper))) throw std::invalid_argument("null argument");
 		HC(hipSetDevice(h->device));
 		h->ensureLines(line_threshold);
@@ -633,6 +649,8 @@ int fvhip_ilu_precondition_device(fvhip_handle h, const double* d_diag, const do
                                   const double* d_v, double* d_z)
 {
 	return guard([&] {
+		need(h, "handle");
+		need(d_diag, "diag"); need(d_lower, "lower"); need(d_upper, "upper"); need(d_v, "v"); need(d_z, "z");
 		if(!d_diag || !d_v || !d_z || (h->L.ninface > 0 && (!d_lower || !d_upper))) throw std::invalid_argument("null argument");
 		System S = single(h);
 		h->ensureImplicit(1);
@@ -649,6 +667,7 @@ int fvhip_ilu_precondition_device(fvhip_handle h, const double* d_diag, const do
 int fvhip_colouring(fvhip_handle h, int* ncolours, int* colour, long long* triples)
 {
 	return guard([&] {
+		need(h, "handle");
 		h->ensureColouring();
 		if(ncolours) *ncolours = static_cast<int>(h->gs_colour_start.size()) - 1;
 		if(colour) std::copy(h->gs_colour.begin(), h->gs_colour.end(), colour);
@@ -659,6 +678,7 @@ int fvhip_colouring(fvhip_handle h, int* ncolours, int* colour, long long* tripl
 int fvhip_lines(fvhip_handle h, double line_threshold, int* nlines, int* start, int* cells, int* faces)
 {
 	return guard([&] {
+		need(h, "handle");
 		HC(hipSetDevice(h->device));
 		h->ensureLines(line_threshold);
 		if(nlines) *nlines = h->lines.nlines;

@@ -24,7 +24,11 @@
  *  - compute_residual ADDS -r(u) into r; dtm[i] = area_i / sum_faces(spectral radius * length).
  *  - Jacobian blocks are row-major 4x4 and are ADDED (ADD_VALUES) into the caller's arrays.
  *  - Every function returns 0 on success, nonzero on failure; fvhip_last_error() describes it.
- *    No C++ exception crosses this boundary. Calls on one handle are not thread-safe
+ *    No C++ exception crosses this boundary. A null handle, or a null array the call reads or
+ *    writes, is refused ("null <what>") before any host or device access; fvhip_create refuses a
+ *    configuration the reference's factories cannot build (unknown flux, Jacobian flux or
+ *    reconstruction, periodic or unknown BC type, Venkatakrishnan K <= 0). fvhip_destroy(NULL) and
+ *    fvhip_group_destroy(NULL) do nothing. Calls on one handle are not thread-safe
  *    (like the reference, flow_spatial.hpp:196-197); each handle owns one HIP stream.
  *  - *_device variants take device pointers in the library's internal cell order (see
  *    fvhip_to_internal / fvhip_from_internal) and are asynchronous on the handle's stream.

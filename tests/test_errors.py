@@ -116,3 +116,19 @@ def test_unknown_gradient_scheme_is_zero_gradients():
     """afactory.cpp:123-127: any other gradient name is ZeroGradients, not an error"""
     cfg, keep = fa._config_struct(cases.physics("naca"), cases.numerics("ROE", "SOMETHING", "NONE"))
     assert cfg.gradientscheme == fa.GRADIENTS["ZERO"]
+
+
+def test_null_handle_is_refused_before_any_access():
+    lib = ffi.lib()
+    null = ctypes.c_void_p()
+    assert lib.fvhip_destroy(null) == 0 and lib.fvhip_group_destroy(null) == 0
+    r = np.zeros((4, 4))
+    calls = [lambda: lib.fvhip_compute_residual(null, fa.dptr(r), fa.dptr(r), 0, None),
+             lambda: lib.fvhip_compute_residual_device(null, None, None, 0, None, 0),
+             lambda: lib.fvhip_synchronize(null),
+             lambda: lib.fvhip_matfree_set_eps(null, 1e-7),
+             lambda: lib.fvhip_tvdrk_device(null, None, 3, 0.5, 1.0, 10, None, None),
+             lambda: lib.fvhip_group_compute_residual_device(null, None, None, 0, None, 0)]
+    for call in calls:
+        assert call() != 0
+        assert lib.fvhip_last_error().decode() in ("null handle", "null group")

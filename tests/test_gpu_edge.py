@@ -109,3 +109,34 @@ def test_div_sqrt_rn_domain():
     e = _divsqrt(a_e, b_e)
     print("edge operands: div_rn", e[:, 0], "IEEE", e[:, 1])
     assert np.isnan(e[2, 0]) and np.isinf(e[2, 1])               # overflow: NaN instead of inf
+
+
+def test_null_device_pointers_refused_handle_survives():
+    """a null device array is refused by name before any launch (it would fault the GPU), and the
+    handle still computes the oracle's residual afterwards"""
+    import torch
+    m = fa.UMesh.flat_plate(8, 4)
+    p = cases.physics("plate_inviscid")
+    n = cases.numerics("ROE", "LEASTSQUARES", "VANALBADA")
+    dev = fa.FlowFV(m, p, n)
+    u = cases.state(m, p, 3)
+    du = torch.tensor(u[dev.permutation()], device="cuda")
+    dr = torch.zeros((m.nelem, 4), dtype=torch.float64, device="cuda")
+    dt = torch.zeros(m.nelem, dtype=torch.float64, device="cuda")
+    for args, what in [((0, dr.data_ptr(), dt.data_ptr(), True), "null u"),
+                       ((du.data_ptr(), 0, dt.data_ptr(), True), "null residual"),
+                       ((du.data_ptr(), dr.data_ptr(), 0, True), "null dtm")]:
+        with pytest.raises(RuntimeError, match=what):
+            dev.compute_residual_device(*args)
+    with pytest.raises(RuntimeError, match="null u"):
+        fa.FlowFVGroup([dev]).compute_residual_device([0], [dr.data_ptr()])
+    dev.compute_residual_device(du.data_ptr(), dr.data_ptr(), dt.data_ptr(), True)
+    dev.synchronize()
+    inv = np.empty_like(dev.permutation())
+    inv[dev.permutation()] = np.arange(m.nelem)
+    r = dr.cpu().numpy()[inv]
+    dev.close()
+    ref = orc.OracleSpatial(orc.OracleMesh.from_raw(m.raw()), p, n)
+    r0 = np.zeros((m.nelem, 4))
+    ref.compute_residual(u, r0, True, np.zeros(m.nelem))
+    np.testing.assert_array_equal(r, r0)
