@@ -24,8 +24,16 @@ using namespace gd;
 // -------------------------------------------------------------------------------------------------
 // interior faces
 // -------------------------------------------------------------------------------------------------
+// waves per SIMD the face-Jacobian kernels are compiled for: 2 (256 registers) where that costs at most a
+// 12-byte spill; Roe with the viscous terms and constant-viscosity HLLC would spill 92-380 bytes per
+// lane, so they keep the allocator's choice (up to 256 VGPRs + AGPRs, one wave)
+#ifndef FVHIP_JAC_WAVES
+#define FVHIP_JAC_WAVES 2
+#endif
 template <int FLUX, int VISC>
-__global__ __launch_bounds__(256)
+constexpr int jacWaves() { return (FLUX == 4 /* Roe */ && VISC) || (FLUX == 6 /* HLLC */ && VISC == 1) ? 1 : FVHIP_JAC_WAVES; }
+template <int FLUX, int VISC>
+__global__ __launch_bounds__(256, (jacWaves<FLUX, VISC>()))
 void k_jac_interior(JacMesh J, gd::Gas G, const double* __restrict__ u,
                     double* __restrict__ lower, double* __restrict__ upper)
 {
