@@ -106,13 +106,14 @@ def kernel_symbol(label, numerics="headline"):
 
 def pmc_traffic(kernel_symbol, workload_cells):
     """HBM bytes per launch of `kernel_symbol` from the newest committed rocprofv3 PMC summary
-    (profiles/r*/pmc_traffic.json, or pmc_schemes.json for the limited and viscous instantiations:
-    FETCH_SIZE x2 + WRITE_SIZE, calibrated as MI355X_MICROARCH.md prescribes), if it was measured on
-    the same workload; else None."""
+    (profiles/r*/pmc_traffic.json; pmc_schemes.json / pmc_config5.json for the limited and viscous
+    instantiations: FETCH_SIZE x2 + WRITE_SIZE, calibrated as MI355X_MICROARCH.md prescribes), if it was
+    measured on the same workload; else None."""
     import glob
     best = None
     files = [f for r in sorted(glob.glob(os.path.join(ROOT, "profiles", "r*")))
-             for f in (os.path.join(r, "pmc_schemes.json"), os.path.join(r, "pmc_traffic.json")) if os.path.exists(f)]
+             for f in (os.path.join(r, n) for n in ("pmc_schemes.json", "pmc_config5.json", "pmc_traffic.json"))
+             if os.path.exists(f)]
     for f in files:
         try:
             d = json.load(open(f))
