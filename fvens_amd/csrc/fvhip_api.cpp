@@ -547,7 +547,7 @@ int fvhip_assemble_jacobian(fvhip_handle h, const double* u, double* diag, doubl
 {
 	return guard([&] {
 		need(h, "handle");
-		need(u, "u"); need(diag, "diag"); need(lower, "lower"); need(upper, "upper");
+		need(u, "u"); need(diag, "diag"); if(h->L.ninface > 0) { need(lower, "lower"); need(upper, "upper"); }
 		HC(hipSetDevice(h->device));
 		const size_t N = static_cast<size_t>(h->L.ncell), Fi = static_cast<size_t>(h->L.ninface);
 		std::vector<double>& st = h->h_stage;
@@ -579,7 +579,7 @@ int fvhip_assemble_jacobian_device(fvhip_handle h, const double* d_u, double* d_
 {
 	return guard([&] {
 		need(h, "handle");
-		need(d_u, "u"); need(d_diag, "diag"); need(d_lower, "lower"); need(d_upper, "upper");
+		need(d_u, "u"); need(d_diag, "diag"); if(h->L.ninface > 0) { need(d_lower, "lower"); need(d_upper, "upper"); }
 		HC(hipSetDevice(h->device));
 		h->assemble(d_u, d_diag, d_lower, d_upper);
 	});
@@ -602,7 +602,7 @@ int fvhip_block_apply_device(fvhip_handle h, const double* d_diag, const double*
 {
 	return guard([&] {
 		need(h, "handle");
-		need(d_diag, "diag"); need(d_lower, "lower"); need(d_upper, "upper"); need(d_x, "x"); need(d_y, "y");
+		need(d_diag, "diag"); if(h->L.ninface > 0) { need(d_lower, "lower"); need(d_upper, "upper"); } need(d_x, "x"); need(d_y, "y");
 		HC(hipSetDevice(h->device));
 		h->ensureJacobian();
 		h->timed("k_block_apply", [&]{ launch_block_apply(h->J, d_diag, d_lower, d_upper, d_x, d_y, h->stream); });

@@ -612,7 +612,7 @@ int fvhip_gmres_blocks_device(fvhip_handle h, const double* d_diag, const double
 {
 	return guard([&] {
 		need(h, "handle");
-		need(d_diag, "diag"); need(d_lower, "lower"); need(d_upper, "upper"); need(d_b, "b"); need(d_x, "x");
+		need(d_diag, "diag"); if(h->L.ninface > 0) { need(d_lower, "lower"); need(d_upper, "upper"); } need(d_b, "b"); need(d_x, "x");
 		if(restart < 1 || restart > KRY_MAXK) throw std::invalid_argument("restart must be in [1, 128]");
 		if(sweeps < 1) throw std::invalid_argument("sweeps must be >= 1");
 		System S = single(h);
@@ -634,7 +634,7 @@ int fvhip_line_precondition_device(fvhip_handle h, const double* d_diag, const d
 {
 	return guard([&] {
 		need(h, "handle");
-		need(d_diag, "diag"); need(d_lower, "lower"); need(d_upper, "upper"); need(d_v, "v"); need(d_z, "z");
+		need(d_diag, "diag"); if(h->L.ninface > 0) { need(d_lower, "lower"); need(d_upper, "upper"); } need(d_v, "v"); need(d_z, "z");
 		if(!d_diag || !d_v || !d_z || (h->L.ninface > 0 && (!d_lower || !d_upper))) throw std::invalid_argument("null argument");
 		HC(hipSetDevice(h->device));
 		h->ensureLines(line_threshold);
@@ -650,7 +650,7 @@ int fvhip_ilu_precondition_device(fvhip_handle h, const double* d_diag, const do
 {
 	return guard([&] {
 		need(h, "handle");
-		need(d_diag, "diag"); need(d_lower, "lower"); need(d_upper, "upper"); need(d_v, "v"); need(d_z, "z");
+		need(d_diag, "diag"); if(h->L.ninface > 0) { need(d_lower, "lower"); need(d_upper, "upper"); } need(d_v, "v"); need(d_z, "z");
 		if(!d_diag || !d_v || !d_z || (h->L.ninface > 0 && (!d_lower || !d_upper))) throw std::invalid_argument("null argument");
 		System S = single(h);
 		h->ensureImplicit(1);
