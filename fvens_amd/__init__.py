@@ -81,7 +81,7 @@ class ImplicitConfig:
     restart: int = 30               # -ksp_gmres_restart
     prec_sweeps: int = 1            # block-Jacobi sweeps per preconditioner application
     min_relax: float = 1.0          # nonlinear_update_scheme: >= 1 "full", else "robust_flow" factor
-    prec_single: bool = False       # preconditioner blocks stored in fp32 (operator stays fp64)
+    prec_single: bool = False       # preconditioner blocks / line factors stored in fp32 (operator stays fp64)
     prec_gs: bool = False           # multicolour block Gauss-Seidel sweeps instead of block-Jacobi
     prec_lines: bool = False        # line-implicit (block-tridiagonal along strongly coupled lines)
     line_threshold: float = 0.0     # strongest/weakest coupling ratio for a cell to join a line (0: 4)
@@ -407,10 +407,12 @@ class FlowFV:
                                                    float(rtol), int(maxit), int(restart), int(sweeps), iptr(it), dptr(rn)))
         return int(it[0]), float(rn[0])
 
-    def line_precondition_device(self, d_diag, d_lower, d_upper, d_v, d_z, line_threshold=0.0):
-        """z = M^-1 v, M the block-tridiagonal line part of the block operator (prec_lines)"""
+    def line_precondition_device(self, d_diag, d_lower, d_upper, d_v, d_z, line_threshold=0.0, single=False):
+        """z = M^-1 v, M the block-tridiagonal line part of the block operator (prec_lines; single: the
+        factors in fp32, as prec_single)"""
         check(_ffi.lib().fvhip_line_precondition_device(self._h, *[ctypes.c_void_p(p) for p in (d_diag, d_lower, d_upper)],
-                                                        float(line_threshold), ctypes.c_void_p(d_v), ctypes.c_void_p(d_z)))
+                                                        float(line_threshold), int(single), ctypes.c_void_p(d_v),
+                                                        ctypes.c_void_p(d_z)))
 
     def ilu_precondition_device(self, d_diag, d_lower, d_upper, d_v, d_z):
         """z = M^-1 v, M the block ILU(0) of the block operator in colour order (prec_ilu)"""

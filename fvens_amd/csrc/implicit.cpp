@@ -93,7 +93,7 @@ struct LinOp
 {
 	System& S;
 	bool matfree = false;
-	bool single = false;                      ///< preconditioner blocks in fp32 (iw.sdinv/slo/sup)
+	bool single = false;                      ///< preconditioner blocks in fp32 (iw.sdinv/slo/sup; line factors: LineSet::single)
 	bool gs = false;                          ///< multicolour block Gauss-Seidel instead of Jacobi
 	bool lines = false;                       ///< line-implicit (block-tridiagonal along lines)
 	bool ilu = false;                         ///< block ILU(0) in multicolour order
@@ -214,6 +214,7 @@ struct LinOp
 		S.each([&](size_t i, fvhip_ctx* h) {
 			if(lines) {
 				h->ensureLines(line_thr);
+				h->lines.single = single;
 				h->timed("k_line_factor", [&]{ launch_line_factor(h->lines, D[i], Lo[i], Up[i], h->stream); });
 				return;
 			}
@@ -379,7 +380,7 @@ static void backwardEuler(System& S, const std::vector<double*>& us, const fvhip
 	A.lines = c.prec_lines != 0;
 	A.line_thr = c.line_threshold;
 	A.ilu = c.prec_ilu != 0;
-	if(A.lines && (A.gs || A.single)) throw std::invalid_argument("prec_lines does not combine with prec_gs / prec_single");
+	if(A.lines && A.gs) throw std::invalid_argument("prec_lines does not combine with prec_gs");
 	if(A.ilu && (A.gs || A.lines)) throw std::invalid_argument("prec_ilu does not combine with prec_gs / prec_lines");
 	for(fvhip_ctx* h : S.hs) { A.D.push_back(h->iw.jd); A.Lo.push_back(h->iw.jlo); A.Up.push_back(h->iw.jup); }
 	std::vector<const double*> cu(us.begin(), us.end());
@@ -630,7 +631,7 @@ int fvhip_gmres_blocks_device(fvhip_handle h, const double* d_diag, const double
 }
 
 int fvhip_line_precondition_device(fvhip_handle h, const double* d_diag, const double* d_lower, const double* d_upper,
-                                   double line_threshold, const double* d_v, double* d_z)
+                                   double line_threshold, int single, const double* d_v, double* d_z)
 {
 	return guard([&] {
 		need(h, "handle");
@@ -638,6 +639,7 @@ int fvhip_line_precondition_device(fvhip_handle h, const double* d_diag, const d
 		if(!d_diag || !d_v || !d_z || (h->L.ninface > 0 && (!d_lower || !d_upper))) throw std::invalid_argument("null argument");
 		HC(hipSetDevice(h->device));
 		h->ensureLines(line_threshold);
+		h->lines.single = single != 0;
 		launch_line_factor(h->lines, d_diag, d_lower, d_upper, h->stream);
 		launch_line_solve(h->lines, d_v, d_z, h->stream);
 		HC(hipGetLastError());

@@ -340,6 +340,22 @@ __device__ __forceinline__ void stP16(double* __restrict__ X, long long r, int j
 	#pragma unroll
 	for(int q = 0; q < 8; q++) p[64*q] = make_double2(a[q >> 1][(q & 1)*2], a[q >> 1][(q & 1)*2 + 1]);
 }
+/// fp32 storage of the same rows (prec_single): row q of lane j's block as one float4 at index
+/// 256 r + 64 q + j -- 4 KB per row, 4 coalesced 16-byte loads per block; the recurrence itself runs in fp64
+__device__ __forceinline__ void ldP16(const float* __restrict__ X, long long r, int j, double (&a)[4][4])
+{
+	const float4* p = reinterpret_cast<const float4*>(X) + 256*r + j;
+	#pragma unroll
+	for(int q = 0; q < 4; q++) { const float4 t = p[64*q]; a[q][0] = t.x; a[q][1] = t.y; a[q][2] = t.z; a[q][3] = t.w; }
+}
+__device__ __forceinline__ void stP16(float* __restrict__ X, long long r, int j, const double (&a)[4][4])
+{
+	float4* p = reinterpret_cast<float4*>(X) + 256*r + j;
+	#pragma unroll
+	for(int q = 0; q < 4; q++)
+		p[64*q] = make_float4(static_cast<float>(a[q][0]), static_cast<float>(a[q][1]), static_cast<float>(a[q][2]),
+		                      static_cast<float>(a[q][3]));
+}
 
 /// block-Thomas factorisation, lane j of workgroup g on line 64g + j (LineSet): per line cell k
 ///   W_{k-1} = dinvp_{k-1} A[k-1][k],  dinvp_k = (D_k - A[k][k-1] W_{k-1})^-1
@@ -351,11 +367,12 @@ __device__ __forceinline__ void stP16(double* __restrict__ X, long long r, int j
 /// Schur term S = A[t][last] W_last of its side instead of a pivot; the two lanes swap S and lane j
 /// stores the twist pivot (A_tt - S_top - S_bottom)^-1 in its row of t. That is the same block
 /// elimination of the same block-tridiagonal matrix, ordered from both ends: the chain per lane halves.
+template <typename T>
 __global__ __launch_bounds__(64)
 void k_line_factor(const int* __restrict__ gstart, const int* __restrict__ lcell, const int* __restrict__ lface,
                    const int* __restrict__ llen, int twisted_groups,
                    const double* __restrict__ diag, const double* __restrict__ lower, const double* __restrict__ upper,
-                   double* __restrict__ D, double* __restrict__ Lb, double* __restrict__ W)
+                   T* __restrict__ D, T* __restrict__ Lb, T* __restrict__ W)
 {
 	const int g = blockIdx.x, j = threadIdx.x;
 	const long long r0 = gstart[g];
@@ -432,10 +449,11 @@ void k_line_factor(const int* __restrict__ gstart, const int* __restrict__ lcell
 /// Twisted groups: each half's forward sweep ends at the twist cell t with s = A[t][last] g_last; the
 /// lanes swap s, lane j forms z_t = pivot_t (v_t - s_top - s_bottom) and hands it to lane j+32, and both
 /// sweep back from z_t.
+template <typename T>
 __global__ __launch_bounds__(64)
 void k_line_solve(const int* __restrict__ gstart, const int* __restrict__ lcell, const int* __restrict__ llen,
-                  int twisted_groups, const double* __restrict__ D, const double* __restrict__ Lb,
-                  const double* __restrict__ W, double* __restrict__ G, const double* __restrict__ v, double* __restrict__ z)
+                  int twisted_groups, const T* __restrict__ D, const T* __restrict__ Lb,
+                  const T* __restrict__ W, double* __restrict__ G, const double* __restrict__ v, double* __restrict__ z)
 {
 	const int g = blockIdx.x, j = threadIdx.x;
 	const long long r0 = gstart[g];
@@ -542,16 +560,26 @@ void k_add_rows(int n, const double* __restrict__ e, double* __restrict__ z)
 
 void launch_line_factor(const LineSet& Ls, const double* diag, const double* lower, const double* upper, hipStream_t s)
 {
-	if(Ls.ngroups > 0)
-		hipLaunchKernelGGL(k_line_factor, dim3(Ls.ngroups), dim3(64), 0, s, Ls.gstart, Ls.cell, Ls.face, Ls.len,
+	if(Ls.ngroups <= 0) return;
+	if(Ls.single)
+		hipLaunchKernelGGL(k_line_factor<float>, dim3(Ls.ngroups), dim3(64), 0, s, Ls.gstart, Ls.cell, Ls.face, Ls.len,
+		                   Ls.twisted_groups, diag, lower, upper, reinterpret_cast<float*>(Ls.D),
+		                   reinterpret_cast<float*>(Ls.Lb), reinterpret_cast<float*>(Ls.W));
+	else
+		hipLaunchKernelGGL(k_line_factor<double>, dim3(Ls.ngroups), dim3(64), 0, s, Ls.gstart, Ls.cell, Ls.face, Ls.len,
 		                   Ls.twisted_groups, diag, lower, upper, Ls.D, Ls.Lb, Ls.W);
 }
 
 void launch_line_solve(const LineSet& Ls, const double* v, double* z, hipStream_t s)
 {
-	if(Ls.ngroups > 0)
-		hipLaunchKernelGGL(k_line_solve, dim3(Ls.ngroups), dim3(64), 0, s, Ls.gstart, Ls.cell, Ls.len, Ls.twisted_groups,
-		                   Ls.D, Ls.Lb, Ls.W, Ls.G, v, z);
+	if(Ls.ngroups <= 0) return;
+	if(Ls.single)
+		hipLaunchKernelGGL(k_line_solve<float>, dim3(Ls.ngroups), dim3(64), 0, s, Ls.gstart, Ls.cell, Ls.len,
+		                   Ls.twisted_groups, reinterpret_cast<const float*>(Ls.D), reinterpret_cast<const float*>(Ls.Lb),
+		                   reinterpret_cast<const float*>(Ls.W), Ls.G, v, z);
+	else
+		hipLaunchKernelGGL(k_line_solve<double>, dim3(Ls.ngroups), dim3(64), 0, s, Ls.gstart, Ls.cell, Ls.len,
+		                   Ls.twisted_groups, Ls.D, Ls.Lb, Ls.W, Ls.G, v, z);
 }
 
 void launch_add_rows(int n, const double* e, double* z, hipStream_t s)

@@ -61,6 +61,7 @@ struct LineSet {
 	const int* len = nullptr;        ///< [64 ngroups]
 	int twisted_groups = 0;          ///< leading groups of 32 lines solved from both ends (lanes j, j+32)
 	double *D = nullptr, *Lb = nullptr, *W = nullptr, *G = nullptr;
+	bool single = false;             ///< D, Lb, W held in fp32 (prec_single; float4 rows in the same buffers)
 };
 #ifndef FVHIP_LINE_MAX
 #define FVHIP_LINE_MAX 256

@@ -277,9 +277,10 @@ typedef struct fvhip_implicit_config {
 	int prec_sweeps;          /* block-Jacobi sweeps per preconditioner application (1: point-block Jacobi) */
 	double min_relax;         /* nonlinear_update_scheme: >= 1 "full"; else "robust_flow" with
 	                             min_nonlinear_relaxation_factor = min_relax (nonlinearrelaxation.cpp) */
-	int prec_single;          /* 1: the preconditioner's blocks (inverted diagonal, lower, upper) are kept in
-	                             fp32 (sweeps read half the bytes; vectors and arithmetic stay fp64). The
-	                             operator itself is unchanged, so the solution tolerance is too. */
+	int prec_single;          /* 1: the preconditioner's blocks (inverted diagonal, lower, upper; with
+	                             prec_lines the line factors) are kept in fp32 (sweeps read half the bytes;
+	                             vectors and arithmetic stay fp64). The operator itself is unchanged, so the
+	                             solution tolerance is too. */
 	int prec_gs;              /* 1: multicolour block Gauss-Seidel sweeps (forward/backward colour order on
 	                             alternate sweeps; block-Jacobi across ranks, i.e. PETSc's bjacobi + sor)
 	                             instead of block-Jacobi sweeps */
@@ -287,7 +288,7 @@ typedef struct fvhip_implicit_config {
 	                             strongly coupled cells (wall-normal in boundary layers; the coupling the
 	                             reference's line ordering, mesh/ameshutils.cpp hybridLineReorder, exploits),
 	                             block-Jacobi between lines and across ranks; prec_sweeps - 1 further
-	                             residual-correction sweeps. Not combined with prec_gs / prec_single. */
+	                             residual-correction sweeps. Not combined with prec_gs. */
 	double line_threshold;    /* a cell joins a line if its strongest coupling (face length / centre distance)
 	                             is at least this many times its weakest (0: 4.0) */
 	int prec_ilu;             /* 1: block ILU(0) of the assembled operator in multicolour order (the reference's
@@ -320,9 +321,10 @@ int fvhip_gmres_blocks_device(fvhip_handle h, const double* d_diag, const double
 
 /** The line-implicit preconditioner alone (fvhip_implicit_config::prec_lines): block-Thomas factorisation
  *  of M, the block-tridiagonal part of the block operator along the lines built with `line_threshold`
- *  (0: 4), then z = M^-1 v (internal order, [ncell][4]). Blocks as in fvhip_gmres_blocks_device. */
+ *  (0: 4), then z = M^-1 v (internal order, [ncell][4]). Blocks as in fvhip_gmres_blocks_device.
+ *  single: the factors are stored in fp32 (prec_single), the recurrence runs in fp64. */
 int fvhip_line_precondition_device(fvhip_handle h, const double* d_diag, const double* d_lower, const double* d_upper,
-                                   double line_threshold, const double* d_v, double* d_z);
+                                   double line_threshold, int single, const double* d_v, double* d_z);
 /** The block ILU(0) preconditioner alone (fvhip_implicit_config::prec_ilu): factorisation of the block
  *  operator in the colour order of fvhip_colouring, then z = M^-1 v (internal order, [ncell][4]) */
 int fvhip_ilu_precondition_device(fvhip_handle h, const double* d_diag, const double* d_lower, const double* d_upper,
