@@ -567,6 +567,18 @@ def partition_graph(mesh, nparts, weights=None):
     return part
 
 
+def find_lines(mesh, threshold):
+    """the reference's line finder (mesh/meshordering.cpp:143-264, findLines): list of int arrays of
+    reference cell numbers, in discovery order"""
+    nl, nc = np.zeros(1, np.int32), np.zeros(1, np.int32)
+    check(_ffi.lib().fvhip_find_lines(ctypes.byref(mesh.view), float(threshold), iptr(nl), iptr(nc), None, None))
+    st = np.zeros(int(nl[0]) + 1, np.int32)
+    cells = np.zeros(max(int(nc[0]), 1), np.int32)
+    check(_ffi.lib().fvhip_find_lines(ctypes.byref(mesh.view), float(threshold), iptr(nl), iptr(nc), iptr(st),
+                                      iptr(cells)))
+    return [cells[st[i]:st[i + 1]].copy() for i in range(int(nl[0]))]
+
+
 def partition_edge_cut(mesh, part):
     """interior faces whose cells lie in different parts"""
     p = np.ascontiguousarray(part, np.int32)

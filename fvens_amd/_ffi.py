@@ -118,6 +118,7 @@ _SIGS = {
     "fvhip_line_precondition_device": (ctypes.c_int, [ctypes.c_void_p] + [ctypes.c_void_p] * 3 +
                                        [ctypes.c_double, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p]),
     "fvhip_lines": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_double, c_int_p, c_int_p, c_int_p, c_int_p]),
+    "fvhip_find_lines": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_double, c_int_p, c_int_p, c_int_p, c_int_p]),
     "fvhip_ilu_precondition_device": (ctypes.c_int, [ctypes.c_void_p] * 6),
     "fvhip_colouring": (ctypes.c_int, [ctypes.c_void_p, c_int_p, c_int_p, ctypes.POINTER(ctypes.c_longlong)]),
     "fvhip_group_matfree_set_state_device": (ctypes.c_int, [ctypes.c_void_p, _vpp, _vpp, _vpp]),

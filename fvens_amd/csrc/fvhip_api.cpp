@@ -220,6 +220,23 @@ int fvhip_create_partitioned(const fvhip_mesh* mesh, const fvhip_flow_config* cf
 	});
 }
 
+int fvhip_find_lines(const fvhip_mesh* mesh, double threshold, int* nlines, int* ncells, int* start, int* cells)
+{
+	return guard([&] {
+		need(mesh, "mesh");
+		const std::vector<std::vector<int>> lines = findLinesReference(*mesh, threshold);
+		int n = 0;
+		if(start) start[0] = 0;
+		for(size_t i = 0; i < lines.size(); i++) {
+			if(cells) std::copy(lines[i].begin(), lines[i].end(), cells + n);
+			n += static_cast<int>(lines[i].size());
+			if(start) start[i+1] = n;
+		}
+		if(nlines) *nlines = static_cast<int>(lines.size());
+		if(ncells) *ncells = n;
+	});
+}
+
 int fvhip_partition_rcb(const fvhip_mesh* mesh, int nparts, int* part)
 {
 	return guard([&] {

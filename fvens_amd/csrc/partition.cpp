@@ -60,6 +60,71 @@ void rcbRecurse(const double* rc, int* idx, int n, int p0, int np, int* part)
 
 }
 
+std::vector<std::vector<int>> findLinesReference(const fvhip_mesh& m, double threshold)
+{
+	checkLinearCells(m, "findLines");
+	const int N = m.nelem;
+	// computeWeights (meshordering.cpp:143-205): per cell, 1/|c_i - c_j| to every neighbour that is a
+	// cell (vertex-average centres, ameshutils.hpp:48-60), divided by the smallest, in decreasing order
+	// (ties keep face order: libstdc++ sorts these <= 4 entries by insertion, which is stable)
+	std::vector<double> cc(2*static_cast<size_t>(N));
+	for(int e = 0; e < N; e++) {
+		double c[2] = {0, 0};
+		for(int j = 0; j < m.nnode[e]; j++)
+			for(int k = 0; k < 2; k++) c[k] += m.coords[2*static_cast<size_t>(m.inpoel[static_cast<size_t>(e)*m.maxnnode+j])+k];
+		for(int k = 0; k < 2; k++) cc[2*static_cast<size_t>(e)+k] = c[k] / m.nnode[e];
+	}
+	std::vector<double> aniso(4*static_cast<size_t>(N), 0.0);
+	std::vector<int> fidx(4*static_cast<size_t>(N), -1), nreal(N, 0);
+	for(int e = 0; e < N; e++) {
+		std::vector<std::pair<double,int>> w;
+		double minw = 1e20;
+		for(int j = 0; j < m.nnode[e]; j++) {
+			const int je = m.esuel[static_cast<size_t>(e)*m.maxnfael+j];
+			if(je < 0 || je >= N) continue;                  // ghost across a boundary or connectivity face
+			double dist = 0;
+			for(int k = 0; k < 2; k++) dist += std::pow(cc[2*static_cast<size_t>(e)+k] - cc[2*static_cast<size_t>(je)+k], 2);
+			const double wt = 1.0/std::sqrt(dist);
+			if(wt < minw) minw = wt;
+			w.push_back({wt, j});
+		}
+		for(auto& x : w) x.first /= minw;
+		std::stable_sort(w.begin(), w.end(), [](const std::pair<double,int>& a, const std::pair<double,int>& b) {
+			return a.first > b.first; });
+		nreal[e] = static_cast<int>(w.size());
+		for(size_t j = 0; j < w.size(); j++) { aniso[4*static_cast<size_t>(e)+j] = w[j].first; fidx[4*static_cast<size_t>(e)+j] = w[j].second; }
+	}
+	// findLines (meshordering.cpp:207-264): from the cell of every physical boundary face in face order,
+	// walk while the cell's largest anisotropy exceeds the threshold, always to the first (strongest)
+	// neighbour not yet in a line whose anisotropy exceeds it; a one-cell walk is no line. A cell without
+	// cell neighbours has no weights (the reference reads an unset entry there): it starts no line.
+	std::vector<int> celline(N, -1);
+	std::vector<std::vector<int>> lines;
+	for(int f = 0; f < m.nbface; f++) {
+		const int belem = m.intfac[4*static_cast<size_t>(f)];
+		if(belem < 0 || belem >= N || celline[belem] >= 0) continue;
+		std::vector<int> le;
+		int cur = belem;
+		for(;;) {
+			if(nreal[cur] > 0 && aniso[4*static_cast<size_t>(cur)] > threshold) {
+				le.push_back(cur);
+				celline[cur] = static_cast<int>(lines.size());
+			}
+			else break;
+			int next = -1;
+			for(int j = 0; j < nreal[cur]; j++) {
+				const int nb = m.esuel[static_cast<size_t>(cur)*m.maxnfael+fidx[4*static_cast<size_t>(cur)+j]];
+				if(celline[nb] == -1 && aniso[4*static_cast<size_t>(cur)+j] > threshold) { next = nb; break; }
+			}
+			if(next < 0) break;
+			cur = next;
+		}
+		if(le.size() > 1) lines.push_back(le);
+		else if(le.size() == 1) celline[le[0]] = -1;
+	}
+	return lines;
+}
+
 std::vector<int> partitionRCB(const double* rc, int ncell, int nparts)
 {
 	if(nparts < 1) throw std::invalid_argument("partitionRCB: nparts < 1");

@@ -85,6 +85,9 @@ MeshTopo extractPartition(const fvhip_mesh& m, const int* part, int rank, int la
 /// Recursive coordinate bisection of cell centres into nparts parts with sizes differing by at
 /// most one cell per bisection level; deterministic (ties broken by cell index)
 std::vector<int> partitionRCB(const double* rc, int ncell, int nparts);
+/// the reference's line finder for its line orderings (mesh/meshordering.cpp:143-264, computeWeights +
+/// findLines): lines of cells (reference numbering) in discovery order, each of at least two cells
+std::vector<std::vector<int>> findLinesReference(const fvhip_mesh& m, double threshold);
 
 /// Graph partition of the cell dual graph (the reference's Scotch SCOTCH_graphPart on the same graph,
 /// meshpartitioning.cpp:376-458; Scotch is absent from the image): recursive bisection, each grown

@@ -152,6 +152,12 @@ int fvhip_partition_graph(const fvhip_mesh* mesh, int nparts, int* part);
 int fvhip_partition_graph_weighted(const fvhip_mesh* mesh, int nparts, const int* weight, int* part);
 /** Number of interior faces cut by a partition */
 long long fvhip_partition_edge_cut(const fvhip_mesh* mesh, const int* part);
+/** The reference's line finder for its line orderings (host only): findLines + computeWeights,
+ *  mesh/meshordering.cpp:143-264 -- from each physical boundary face's cell, walk to the neighbour of
+ *  largest inverse centre distance (relative to the cell's smallest) while that ratio exceeds
+ *  `threshold`. *nlines, *ncells (cells on lines); start [nlines+1] into cells [ncells] (reference cell
+ *  numbers, discovery order); NULL arrays are skipped (call once for the sizes) */
+int fvhip_find_lines(const fvhip_mesh* mesh, double threshold, int* nlines, int* ncells, int* start, int* cells);
 /** Halo description of one rank (host only). counts[6] = {owned, ghosts, boundary faces, faces,
  *  neighbour ranks, send rows}; arrays may be NULL: cell_global [owned+ghosts] (owned ascending,
  *  then ghosts by owner rank), nbr_rank [nnbr], ghost_start/send_start [nnbr+1], send_global [nsend] */
