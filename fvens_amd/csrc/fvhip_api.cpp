@@ -299,6 +299,7 @@ int fvhip_partition_halo_layers(const fvhip_mesh* mesh, const int* part, int ran
 int fvhip_comm_unique_id(void* id128)
 {
 	return guard([&] {
+		need(id128, "unique id");
 		ncclUniqueId id;
 		NC(ncclGetUniqueId(&id));
 		std::memcpy(id128, &id, sizeof(id));
@@ -308,7 +309,7 @@ int fvhip_comm_unique_id(void* id128)
 int fvhip_comm_init(fvhip_handle h, int nranks, int rank, const void* id128)
 {
 	return guard([&] {
-		need(h, "handle");
+		need(h, "handle"); need(id128, "unique id");
 		if(h->rankmesh && h->rank < 0 && fvhip_set_rank(h, rank, nranks)) throw std::runtime_error(g_err);
 		if(nranks != h->nparts || rank != h->rank)
 			throw std::invalid_argument("communicator does not match the handle's partition");
