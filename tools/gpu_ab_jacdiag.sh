@@ -8,7 +8,7 @@ for v in jd0 jd1; do
   python3 -c "
 import csv
 for r in csv.DictReader(open('gpurun_out/p_${v}_$rep/run_kernel_stats.csv')):
-    if 'jac_diag' in r['Name']: print('$v', r['Calls'], r['AverageNs'])
+    if 'jac_diag' in r['Name'] or 'block_apply' in r['Name']: print('$v', r['Name'][:22], r['Calls'], r['AverageNs'])
 "
 done
 done
