@@ -1,0 +1,24 @@
+#!/bin/bash
+# round-4 probe call: implicit schedules (item 6), steady-state headline trace (item 3), Jacobian
+# assembly trace + PMC passes (item 5). Each step under its own limit; stop at the first failure.
+set -u
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+export TMPDIR=/tmp
+OUT=gpurun_out/r04a
+mkdir -p $OUT
+run() {  # name timeout cmd...
+  local name=$1 to=$2; shift 2
+  echo "== $name"; date
+  timeout -k 10 "$to" "$@" > "$OUT/$name.log" 2>&1
+  local rc=$?
+  echo "rc=$rc"; tail -c 600 "$OUT/$name.log"; echo
+  [ $rc -eq 0 ] || { echo "stopping after $name"; exit $rc; }
+}
+run jac 200 python3 -u tools/jac_probe.py --reps 100
+run jac_trace 200 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/jtrace -o run -- python3 tools/jac_probe.py --reps 100
+run jac_fetch 120 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $OUT/jfetch -o run -- python3 tools/jac_probe.py --reps 20
+run jac_write 120 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $OUT/jwrite -o run -- python3 tools/jac_probe.py --reps 20
+run jac_sq 120 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_ANY SQ_INSTS_VMEM_RD GRBM_GUI_ACTIVE --output-format csv -d $OUT/jsq -o run -- python3 tools/jac_probe.py --reps 20
+run steady_trace 400 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/trace -o run -- python3 bench.py --steps 2000 --warmup 20 --no-cpu-baseline --no-pipelined --no-implicit
+run implicit_probe 500 python3 -u tools/implicit_probe.py
+echo done
