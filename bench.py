@@ -15,6 +15,10 @@ gradients itself, overlapped with the patches that need no halo data.
 --scaling strong (default): the C4 mesh itself is split N ways (BASELINE.json config 4); afterwards every
 rank's owned residual is compared bit for bit with a 1-GPU residual of the whole mesh (halo_parity);
 --scaling weak: the O-grid has N x 2048 cells around, so every GPU owns a C4-size part.
+Launch: under torchrun (WORLD_SIZE set, it must equal --gpus), or `python bench.py --gpus N` alone, which
+starts the N ranks itself (one child process per GPU, env:// rendezvous on 127.0.0.1, a wall-clock
+watchdog, exit status of the first failing rank) before anything touches a GPU; --launch-dry-run prints
+the plan.
 """
 import argparse
 import json
@@ -273,9 +277,84 @@ def halo_parity(fa, torch, dist, mesh, p, n, u, part, rank, world, new_uid):
     return bool(bad.item() == 0)
 
 
+def free_port():
+    """a TCP port on 127.0.0.1 that nothing listens on now (the children's rendezvous)"""
+    import socket
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def rank_launch_plan(n, argv, port=None):
+    """the N child processes of `bench.py --gpus N` started without a torchrun environment: one rank per
+    GPU, this script with the same arguments, the torch.distributed env:// variables set (rendezvous on
+    127.0.0.1). Returns a list of (command, env additions)."""
+    port = int(os.environ.get("MASTER_PORT") or 0) or port or free_port()
+    cmd = [sys.executable, "-u", os.path.abspath(__file__)] + list(argv)
+    return [(cmd, {"RANK": str(r), "LOCAL_RANK": str(r), "WORLD_SIZE": str(n), "LOCAL_WORLD_SIZE": str(n),
+                   "GROUP_RANK": "0", "MASTER_ADDR": "127.0.0.1", "MASTER_PORT": str(port)})
+            for r in range(n)]
+
+
+def run_ranks(plan, timeout_s, poll_s=0.2):
+    """start every child of `plan` in its own process group (this process touches no GPU), wait for all
+    of them, and return the exit status: 0 if every child succeeded, else the first failing child's
+    status (the others are killed); 124 when the wall-clock watchdog `timeout_s` expires (all killed).
+    The children inherit stdout/stderr: rank 0 prints the JSON line."""
+    import signal
+    import subprocess
+    procs = [subprocess.Popen(cmd, env=dict(os.environ, **env), start_new_session=True) for cmd, env in plan]
+
+    def kill_all():
+        for p in procs:
+            if p.poll() is None:
+                try:
+                    os.killpg(p.pid, signal.SIGTERM)
+                except ProcessLookupError:
+                    pass
+        t_end = time.time() + 10
+        for p in procs:
+            try:
+                p.wait(timeout=max(t_end - time.time(), 0.1))
+            except subprocess.TimeoutExpired:
+                try:
+                    os.killpg(p.pid, signal.SIGKILL)
+                except ProcessLookupError:
+                    pass
+                p.wait()
+
+    def on_signal(signum, frame):
+        kill_all()
+        sys.exit(128 + signum)
+    old = {s: signal.signal(s, on_signal) for s in (signal.SIGTERM, signal.SIGINT)}
+    try:
+        t0 = time.time()
+        while True:
+            codes = [p.poll() for p in procs]
+            bad = [c for c in codes if c not in (None, 0)]
+            if bad:
+                sys.stderr.write("bench.py launcher: a rank exited with status %d; stopping the others\n" % bad[0])
+                kill_all()
+                return bad[0] if bad[0] > 0 else 128 - bad[0]
+            if all(c == 0 for c in codes):
+                return 0
+            if time.time() - t0 > timeout_s:
+                sys.stderr.write("bench.py launcher: ranks still running after %.0f s; killed\n" % timeout_s)
+                kill_all()
+                return 124
+            time.sleep(poll_s)
+    finally:
+        for s, h in old.items():
+            signal.signal(s, h)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--launch-timeout", type=float, default=1500.0,
+                    help="--gpus N without torchrun: wall-clock limit for the N ranks this script starts")
+    ap.add_argument("--launch-dry-run", action="store_true",
+                    help="print the rank processes --gpus N would start (commands, environment) and exit")
     ap.add_argument("--steps", type=int, default=200)
     ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--scale", type=int, default=1, help="divide the C4 mesh dimensions (debug)")
@@ -299,6 +378,26 @@ def main():
                          "(M 0.5, Re 5000) on the 8.1M-cell C5 O-grid (C4 with 4096 cells around), Roe + WLS + "
                          "MUSCL/Van Albada + Sutherland viscous flux")
     args = ap.parse_args()
+
+    # one process per GPU: under torchrun WORLD_SIZE must agree with --gpus; without it, --gpus N > 1
+    # starts the N ranks here, before anything touches a GPU, and this process only waits for them
+    env_world = os.environ.get("WORLD_SIZE")
+    if args.gpus < 1:
+        sys.exit("bench.py: --gpus must be >= 1")
+    if env_world is not None and int(env_world) != args.gpus:
+        sys.exit("bench.py: WORLD_SIZE=%s from the launcher differs from --gpus %d; refusing to run"
+                 % (env_world, args.gpus))
+    if env_world is None and (args.gpus > 1 or args.launch_dry_run):
+        argv = [a for a in sys.argv[1:] if a != "--launch-dry-run"]
+        plan = rank_launch_plan(args.gpus, argv) if args.gpus > 1 else []
+        if args.launch_dry_run:
+            print(json.dumps({"ranks": [{"cmd": c, "env": e} for c, e in plan],
+                              "in_process": args.gpus == 1, "watchdog_s": args.launch_timeout}))
+            return
+        sys.exit(run_ranks(plan, args.launch_timeout))
+    if args.launch_dry_run:
+        print(json.dumps({"ranks": [], "in_process": True, "under_launcher": True, "world_size": int(env_world)}))
+        return
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
