@@ -929,6 +929,10 @@ struct fvhip_ctx
 		lines.len = upload(lens, owned);
 		const size_t rows = std::max<size_t>(static_cast<size_t>(gst[ng]), 1);
 		lines.D = dalloc(1024*rows, owned);
+		// zeroed once: in a twisted group the factorisation writes the twist row of D for lane j only
+		// (the pivot); k_line_solve's forward prefetch also requests that row for lane j+32 and discards
+		// it, so it must hold defined values, never garbage a later change could start using
+		HC(hipMemsetAsync(lines.D, 0, sizeof(double)*1024*rows, stream));
 		lines.Lb = dalloc(1024*rows, owned);
 		lines.W = dalloc(1024*rows, owned);
 		lines.G = dalloc(256*rows, owned);

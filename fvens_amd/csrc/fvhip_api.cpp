@@ -240,6 +240,7 @@ int fvhip_find_lines(const fvhip_mesh* mesh, double threshold, int* nlines, int*
 int fvhip_partition_rcb(const fvhip_mesh* mesh, int nparts, int* part)
 {
 	return guard([&] {
+		need(mesh, "mesh"); need(part, "part");
 		const std::vector<int> p = partitionRCB(mesh->rc, mesh->nelem, nparts);
 		std::memcpy(part, p.data(), p.size()*sizeof(int));
 	});
@@ -248,6 +249,7 @@ int fvhip_partition_rcb(const fvhip_mesh* mesh, int nparts, int* part)
 int fvhip_partition_graph(const fvhip_mesh* mesh, int nparts, int* part)
 {
 	return guard([&] {
+		need(mesh, "mesh"); need(part, "part");
 		const std::vector<int> p = partitionGraph(*mesh, nparts);
 		std::memcpy(part, p.data(), p.size()*sizeof(int));
 	});
@@ -256,6 +258,7 @@ int fvhip_partition_graph(const fvhip_mesh* mesh, int nparts, int* part)
 int fvhip_partition_graph_weighted(const fvhip_mesh* mesh, int nparts, const int* weight, int* part)
 {
 	return guard([&] {
+		need(mesh, "mesh"); need(part, "part");
 		const std::vector<int> p = partitionGraph(*mesh, nparts, weight);
 		std::memcpy(part, p.data(), p.size()*sizeof(int));
 	});
@@ -264,7 +267,7 @@ int fvhip_partition_graph_weighted(const fvhip_mesh* mesh, int nparts, const int
 long long fvhip_partition_edge_cut(const fvhip_mesh* mesh, const int* part)
 {
 	long long c = -1;
-	if(guard([&] { c = edgeCut(*mesh, part); })) return -1;
+	if(guard([&] { need(mesh, "mesh"); need(part, "part"); c = edgeCut(*mesh, part); })) return -1;
 	return c;
 }
 
@@ -272,6 +275,7 @@ int fvhip_partition_info(const fvhip_mesh* mesh, const int* part, int rank, int*
                          int* nbr_rank, int* ghost_start, int* send_start, int* send_global)
 {
 	return guard([&] {
+		need(mesh, "mesh"); need(part, "part"); need(counts, "counts");
 		const MeshTopo T = extractPartition(*mesh, part, rank);
 		const int nnbr = static_cast<int>(T.nbr_rank.size());
 		counts[0] = T.nown; counts[1] = T.nghost; counts[2] = T.nbface; counts[3] = T.naface;
@@ -739,6 +743,7 @@ int fvhip_group_matfree_set_state_device(fvhip_group g, const double* const* d_u
 {
 	return guard([&] {
 		need(g, "group");
+		needEach(d_u, g->hs.size(), "u"); needEach(d_r, g->hs.size(), "residual"); needEach(d_mdt, g->hs.size(), "dtm");
 		for(size_t i = 0; i < g->hs.size(); i++) { g->hs[i]->mf_u = d_u[i]; g->hs[i]->mf_r = d_r[i]; g->hs[i]->mf_mdt = d_mdt[i]; }
 	});
 }

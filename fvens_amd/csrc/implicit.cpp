@@ -171,8 +171,10 @@ struct LinOp
 			exact::launch_fill(z(i), 0.0, 4LL*(h->L.ncell + h->L.nghost), h->stream);
 			const int nc = static_cast<int>(h->gs_colour_start.size()) - 1;
 			h->timed("k_ilu_solve", [&]{
-				for(int q = 0; q < 2*nc; q++) {
-					const int col = q < nc ? q : 2*nc - 1 - q;
+				// forward over colours 0..nc-1, backward over nc-2..0: the last colour's backward value
+				// would be its forward one again (all its neighbours are of earlier colours)
+				for(int q = 0; q < 2*nc - 1; q++) {
+					const int col = q < nc ? q : 2*nc - 2 - q;
 					const int b = h->gs_colour_start[col], n = h->gs_colour_start[col+1] - b;
 					if(single) launch_bgs_colour(h->J, h->iw.sdinv, h->iw.slo, h->iw.sup, v(i), z(i), h->d_gs_cells + b, n, h->stream);
 					else launch_bgs_colour(h->J, h->iw.dinv, Lo[i], Up[i], v(i), z(i), h->d_gs_cells + b, n, h->stream);

@@ -69,16 +69,20 @@ __global__ void __launch_bounds__(256) k_tvdrk_stage(int n, double c0, double c1
 	reinterpret_cast<double4*>(us)[e] = ss;
 }
 
-/// minimum over cells (order-free), two stages
+/// minimum that propagates NaN (fmin skips it): one NaN time step makes the minimum NaN
+__device__ __forceinline__ double nan_min(double a, double b) { return a != a ? a : (b != b ? b : fmin(a, b)); }
+
+/// minimum over cells (order-free), two stages; a NaN anywhere gives -inf (finite values and +inf
+/// otherwise as fmin), so the divergence check fires for it and ncclMin across ranks carries it
 __global__ void __launch_bounds__(256) k_min_partial(int n, const double* __restrict__ x, double* __restrict__ part)
 {
 	__shared__ double s[256];
 	double m = INFINITY;
-	for(int e = blockIdx.x*256 + threadIdx.x; e < n; e += 256*gridDim.x) m = fmin(m, x[e]);
+	for(int e = blockIdx.x*256 + threadIdx.x; e < n; e += 256*gridDim.x) m = nan_min(m, x[e]);
 	s[threadIdx.x] = m;
 	__syncthreads();
 	for(int w = 128; w > 0; w >>= 1) {
-		if(threadIdx.x < w) s[threadIdx.x] = fmin(s[threadIdx.x], s[threadIdx.x + w]);
+		if(threadIdx.x < w) s[threadIdx.x] = nan_min(s[threadIdx.x], s[threadIdx.x + w]);
 		__syncthreads();
 	}
 	if(threadIdx.x == 0) part[blockIdx.x] = s[0];
@@ -87,14 +91,14 @@ __global__ void __launch_bounds__(256) k_min_final(int np, const double* __restr
 {
 	__shared__ double s[256];
 	double m = INFINITY;
-	for(int i = threadIdx.x; i < np; i += 256) m = fmin(m, part[i]);
+	for(int i = threadIdx.x; i < np; i += 256) m = nan_min(m, part[i]);
 	s[threadIdx.x] = m;
 	__syncthreads();
 	for(int w = 128; w > 0; w >>= 1) {
-		if(threadIdx.x < w) s[threadIdx.x] = fmin(s[threadIdx.x], s[threadIdx.x + w]);
+		if(threadIdx.x < w) s[threadIdx.x] = nan_min(s[threadIdx.x], s[threadIdx.x + w]);
 		__syncthreads();
 	}
-	if(threadIdx.x == 0) out[0] = s[0];
+	if(threadIdx.x == 0) out[0] = s[0] != s[0] ? -INFINITY : s[0];
 }
 
 void launch_tvdrk_stage(int n, double c0, double c1, double sc, const double* area, const double* r, const double* u,

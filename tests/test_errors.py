@@ -132,3 +132,31 @@ def test_null_handle_is_refused_before_any_access():
     for call in calls:
         assert call() != 0
         assert lib.fvhip_last_error().decode() in ("null handle", "null group")
+
+
+def test_partition_entries_refuse_null_arrays(mesh):
+    """the host partition entry points check their mesh and output arrays before touching them"""
+    lib = ffi.lib()
+    part = np.zeros(mesh.nelem, np.int32)
+    w = np.ones(mesh.nelem, np.int32)
+    counts = np.zeros(6, np.int32)
+    mv = ctypes.byref(mesh.view)
+    calls = [(lambda: lib.fvhip_partition_rcb(None, 2, fa.iptr(part)), "null mesh"),
+             (lambda: lib.fvhip_partition_rcb(mv, 2, None), "null part"),
+             (lambda: lib.fvhip_partition_graph(None, 2, fa.iptr(part)), "null mesh"),
+             (lambda: lib.fvhip_partition_graph(mv, 2, None), "null part"),
+             (lambda: lib.fvhip_partition_graph_weighted(None, 2, fa.iptr(w), fa.iptr(part)), "null mesh"),
+             (lambda: lib.fvhip_partition_graph_weighted(mv, 2, fa.iptr(w), None), "null part"),
+             (lambda: lib.fvhip_partition_info(mv, None, 0, fa.iptr(counts), None, None, None, None, None), "null part"),
+             (lambda: lib.fvhip_partition_info(None, fa.iptr(part), 0, fa.iptr(counts), None, None, None, None, None),
+              "null mesh"),
+             (lambda: lib.fvhip_partition_info(mv, fa.iptr(part), 0, None, None, None, None, None, None), "null counts")]
+    for call, msg in calls:
+        assert call() != 0
+        assert lib.fvhip_last_error().decode() == msg
+    assert lib.fvhip_partition_edge_cut(mv, None) == -1
+    assert lib.fvhip_last_error().decode() == "null part"
+    # and the weighted partition still works with and without weights
+    assert lib.fvhip_partition_graph_weighted(mv, 2, fa.iptr(w), fa.iptr(part)) == 0
+    assert set(np.unique(part)) == {0, 1}
+    assert lib.fvhip_partition_graph_weighted(mv, 2, None, fa.iptr(part)) == 0

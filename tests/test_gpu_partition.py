@@ -123,6 +123,22 @@ def test_partitioned_c4_eight_ranks(rec):
           "interior patch fraction", [round(s["interior_patches"] / s["patches"], 3) for s in stats])
 
 
+def test_partitioned_c5_eight_ranks():
+    """BASELINE config 5 at its full size on the partitioned path: the 8,126,464-cell C5 O-grid (4096
+    cells around, 1e-5 wall spacing), laminar Roe + WLS + Van Albada + Sutherland (the fused viscous
+    kernel on the two-layer halo), split 8 ways by the cost-weighted graph partitioner, all ranks in one
+    process with the overlapped schedule -- every owned row's residual and time step bitwise the
+    single-GPU ones (the same device code evaluates Sutherland's law on both sides)"""
+    r, dt, r1, dt1, stats = run_partitioned("naca_c5", "visc", "ROE", "LEASTSQUARES", "VANALBADA", True, 8,
+                                            partitioner="graph-cost")
+    assert r.shape[0] == 8126464
+    np.testing.assert_array_equal(r, r1)
+    np.testing.assert_array_equal(dt, dt1)
+    for s in stats:
+        assert s["patches"] > 0 and 0 < s["interior_patches"] < s["patches"]
+    print("per-rank cells", [s["cells"] for s in stats], "ghosts", [s["ghosts"] for s in stats])
+
+
 def test_partitioned_fast_math_within_tolerance():
     # fast kernels contract FMAs per inlining context (a neighbour converted from LDS or from
     # global memory), so partitioned and single-GPU fast results agree to the fast-mode tolerance

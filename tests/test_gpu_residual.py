@@ -31,6 +31,8 @@ def get_mesh(key):
             om = orc.OracleMesh.from_raw(m.raw())
         elif key == "naca_c4":                               # the bench's C4 mesh (no oracle mesh)
             m, om = fa.UMesh.naca_ogrid(2048, 256, 864, 20.0, 1e-5, farmap=1), None
+        elif key == "naca_c5":                               # BASELINE config 5's 8,126,464-cell O-grid
+            m, om = fa.UMesh.naca_ogrid(4096, 256, 864, 20.0, 1e-5, farmap=1), None
         elif key == "plate_small":
             m = fa.UMesh.flat_plate(48, 32)
             om = orc.OracleMesh.from_raw(m.raw())

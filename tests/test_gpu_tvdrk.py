@@ -123,3 +123,44 @@ def test_tvdrk_partitioned_bitwise():
         sp.close()
     assert s == s1 == 4 and t == t1
     np.testing.assert_array_equal(u, u1)
+
+
+def test_tvdrk_nan_in_some_cells_diverges():
+    """a NaN state in a few cells makes their time steps NaN: the reduction carries it (fmin would skip
+    it and keep stepping), so the reference's 'dtmin is Nan or inf' error fires (aodesolver.cpp:730-731);
+    on a 3-rank partition too, with the NaN on one rank only"""
+    import torch
+    m, _ = get_mesh("naca_small")
+    p = cases.physics("naca")
+    n = cases.numerics("ROE", "LEASTSQUARES", "VANALBADA")
+    u0 = cases.state(m, p, 8)
+    bad = [m.nelem // 3]
+    u0[bad, 0] = np.nan
+    one = fa.FlowFV(m, p, n)
+    du = _dev(u0, one.permutation())
+    with pytest.raises(RuntimeError, match="dtmin is Nan or inf"):
+        one.tvdrk_device(du.data_ptr(), 3, 0.4, 1e9, 4)
+    one.close()
+    part = fa.partition_graph(m, 3, weights="cost")
+    sps = [fa.FlowFV(m, p, n, partition=part, rank=k) for k in range(3)]
+    dus = []
+    for k, sp in enumerate(sps):
+        g = np.nonzero(part == k)[0][sp.permutation()]
+        d = torch.zeros((sp.nown + sp.nghost, 4), dtype=torch.float64, device="cuda")
+        d[:sp.nown] = torch.tensor(u0[g], device="cuda")
+        dus.append(d)
+    grp = fa.FlowFVGroup(sps)
+    with pytest.raises(RuntimeError, match="dtmin is Nan or inf"):
+        grp.tvdrk_device([d.data_ptr() for d in dus], 3, 0.4, 1e9, 4)
+    # the group entry points check their per-rank arrays before indexing them
+    import ctypes
+    import fvens_amd._ffi as ffi
+    arr = (ctypes.c_void_p * 3)(*[d.data_ptr() for d in dus])
+    nul = (ctypes.c_void_p * 3)(dus[0].data_ptr(), None, dus[2].data_ptr())
+    assert ffi.lib().fvhip_group_matfree_set_state_device(grp._g, arr, nul, arr) != 0
+    assert ffi.lib().fvhip_last_error().decode() == "null residual"
+    assert ffi.lib().fvhip_group_matfree_set_state_device(grp._g, None, arr, arr) != 0
+    assert ffi.lib().fvhip_last_error().decode() == "null u"
+    grp.close()
+    for sp in sps:
+        sp.close()

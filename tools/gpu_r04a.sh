@@ -14,6 +14,7 @@ run() {  # name timeout cmd...
   echo "rc=$rc"; tail -c 600 "$OUT/$name.log"; echo
   [ $rc -eq 0 ] || { echo "stopping after $name"; exit $rc; }
 }
+run newtests 900 python3 -u -m pytest -x -v --timeout 600 --timeout-method thread tests/test_gpu_tvdrk.py tests/test_gpu_implicit.py::test_partitioned_line_implicit_same_solution tests/test_gpu_implicit.py::test_partitioned_ilu_same_solution tests/test_gpu_implicit.py::test_one_backward_euler_step_matches_host tests/test_gpu_partition.py::test_partitioned_c5_eight_ranks -s
 run jac 200 python3 -u tools/jac_probe.py --reps 100
 run jac_trace 200 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/jtrace -o run -- python3 tools/jac_probe.py --reps 100
 run jac_fetch 120 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $OUT/jfetch -o run -- python3 tools/jac_probe.py --reps 20
@@ -21,4 +22,5 @@ run jac_write 120 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $OUT/jwrite 
 run jac_sq 120 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_ANY SQ_INSTS_VMEM_RD GRBM_GUI_ACTIVE --output-format csv -d $OUT/jsq -o run -- python3 tools/jac_probe.py --reps 20
 run steady_trace 400 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/trace -o run -- python3 bench.py --steps 2000 --warmup 20 --no-cpu-baseline --no-pipelined --no-implicit
 run implicit_probe 500 python3 -u tools/implicit_probe.py
+run plines 600 python3 -u tools/partitioned_lines_probe.py
 echo done
