@@ -23,4 +23,5 @@ run jac_sq 120 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_WAV
 run steady_trace 400 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/trace -o run -- python3 bench.py --steps 2000 --warmup 20 --no-cpu-baseline --no-pipelined --no-implicit
 run implicit_probe 500 python3 -u tools/implicit_probe.py
 run plines 600 python3 -u tools/partitioned_lines_probe.py
+run enqueue 400 python3 -u tools/enqueue_probe.py
 echo done
