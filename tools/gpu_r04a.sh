@@ -24,4 +24,5 @@ run steady_trace 400 rocprofv3 --kernel-trace --stats --output-format csv -d $OU
 run implicit_probe 500 python3 -u tools/implicit_probe.py
 run plines 600 python3 -u tools/partitioned_lines_probe.py
 run enqueue 400 python3 -u tools/enqueue_probe.py
+run weno 400 python3 -u tools/weno_regression_probe.py --lambdas 20,0,1e-3,1
 echo done
