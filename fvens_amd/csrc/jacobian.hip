@@ -32,13 +32,26 @@ using namespace gd;
 #endif
 template <int FLUX, int VISC>
 constexpr int jacWaves() { return (FLUX == 4 /* Roe */ && VISC) || (FLUX == 6 /* HLLC */ && VISC == 1) ? 1 : FVHIP_JAC_WAVES; }
+// FVHIP_JAC_LDS_STORE = 1: where the face-Jacobian kernel runs at <= 2 waves per SIMD anyway (Roe, HLLC
+// and the viscous instantiations: 190-256 VGPRs), the face blocks go through LDS and leave as coalesced
+// 16-byte rows (a block's 256 faces own one contiguous 64 KB range of lower and of upper), instead of 32
+// scattered 8-byte stores per thread (one cache line per lane per store). The light ones (LLF, HLL,
+// AUSM without viscous terms: 3-5 waves) keep the direct stores: 64 KB of LDS per block would cap them
+// at 2 waves.
+#ifndef FVHIP_JAC_LDS_STORE
+#define FVHIP_JAC_LDS_STORE 1
+#endif
 template <int FLUX, int VISC>
-__global__ __launch_bounds__(256, (jacWaves<FLUX, VISC>()))
-void k_jac_interior(JacMesh J, gd::Gas G, const double* __restrict__ u,
-                    double* __restrict__ lower, double* __restrict__ upper)
+constexpr bool jacLds() {
+	return FVHIP_JAC_LDS_STORE && !((FLUX == 0 && VISC != 1) || (FLUX == 2 && VISC == 0) || (FLUX == 5 && VISC == 0));
+}
+constexpr int JAC_LDS_STRIDE = 257;   // entry-major rows of 256 faces, padded: 257 = 1 mod 32 double banks
+
+/// face fi's two blocks, column by column: out(i, k, lower entry, upper entry)
+template <int FLUX, int VISC, typename Out>
+__device__ __forceinline__ void jac_face(const JacMesh& J, const gd::Gas& G, const double* __restrict__ u, int fi,
+                                         Out&& out)
 {
-	const int fi = blockIdx.x*blockDim.x + threadIdx.x;
-	if(fi >= J.ninface) return;
 	const int2 lr = J.if_LR[fi];
 	const double2 nn = J.if_n[fi];
 	const double n[2] = {nn.x, nn.y};
@@ -58,17 +71,46 @@ void k_jac_interior(JacMesh J, gd::Gas G, const double* __restrict__ u,
 		const double cl[2] = {a.x, a.y}, cr[2] = {b.x, b.y};
 		visc_jac_prepare(G, VISC == 2, ul, ur, cl, cr, V);
 	}
-	double* Lo = lower + 16*static_cast<size_t>(fi);
-	double* Up = upper + 16*static_cast<size_t>(fi);
 #pragma unroll
 	for(int k = 0; k < 4; k++) {
 		double dl[4], dr[4];
 		jac_col<FLUX>(G, F, n, k, dl, dr);
 		if(VISC) visc_jac_col(G, V, ul, ur, n, k, dl, dr);
-		for(int i = 0; i < 4; i++) {
-			Lo[i*4+k] = dl[i]*len;
-			Up[i*4+k] = dr[i]*len;
+		for(int i = 0; i < 4; i++) out(i, k, dl[i]*len, dr[i]*len);
+	}
+}
+
+template <int FLUX, int VISC>
+__global__ __launch_bounds__(256, (jacWaves<FLUX, VISC>()))
+void k_jac_interior(JacMesh J, gd::Gas G, const double* __restrict__ u,
+                    double* __restrict__ lower, double* __restrict__ upper)
+{
+	const int t = static_cast<int>(threadIdx.x);
+	const int f0 = blockIdx.x*256;
+	const int fi = f0 + t;
+	if constexpr(jacLds<FLUX, VISC>()) {
+		// sb[side*16 + entry][face in block]: the columns land entry-major (consecutive threads,
+		// consecutive words: no bank conflicts); then each thread writes double2s of the block's range
+		__shared__ double sb[32*JAC_LDS_STRIDE];
+		if(fi < J.ninface)
+			jac_face<FLUX, VISC>(J, G, u, fi, [&](int i, int k, double lo, double up) {
+				sb[(i*4+k)*JAC_LDS_STRIDE + t] = lo;
+				sb[(16+i*4+k)*JAC_LDS_STRIDE + t] = up;
+			});
+		__syncthreads();
+		const int nf = min(256, J.ninface - f0);
+		double2* Lo2 = reinterpret_cast<double2*>(lower + 16*static_cast<size_t>(f0));
+		double2* Up2 = reinterpret_cast<double2*>(upper + 16*static_cast<size_t>(f0));
+		for(int j = t; j < 8*nf; j += 256) {
+			const int f = j >> 3, e = (j & 7)*2;
+			Lo2[j] = make_double2(sb[e*JAC_LDS_STRIDE + f], sb[(e+1)*JAC_LDS_STRIDE + f]);
+			Up2[j] = make_double2(sb[(16+e)*JAC_LDS_STRIDE + f], sb[(17+e)*JAC_LDS_STRIDE + f]);
 		}
+	} else {
+		if(fi >= J.ninface) return;
+		double* Lo = lower + 16*static_cast<size_t>(fi);
+		double* Up = upper + 16*static_cast<size_t>(fi);
+		jac_face<FLUX, VISC>(J, G, u, fi, [&](int i, int k, double lo, double up) { Lo[i*4+k] = lo; Up[i*4+k] = up; });
 	}
 }
 

@@ -16,6 +16,10 @@ run() {  # name timeout cmd...
 }
 run newtests 900 python3 -u -m pytest -x -v --timeout 600 --timeout-method thread tests/test_gpu_tvdrk.py tests/test_gpu_implicit.py::test_partitioned_line_implicit_same_solution tests/test_gpu_implicit.py::test_partitioned_ilu_same_solution tests/test_gpu_implicit.py::test_one_backward_euler_step_matches_host tests/test_gpu_partition.py::test_partitioned_c5_eight_ranks -s
 run jac 200 python3 -u tools/jac_probe.py --reps 100
+for rep in 1 2; do
+  FVHIP_LIB=$(realpath fvens_amd/build_ab/jl0.so) run jac_ab_jl0_$rep 200 python3 -u tools/jac_probe.py --reps 100
+  run jac_ab_jl1_$rep 200 python3 -u tools/jac_probe.py --reps 100
+done
 run jac_trace 200 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/jtrace -o run -- python3 tools/jac_probe.py --reps 100
 run jac_fetch 120 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $OUT/jfetch -o run -- python3 tools/jac_probe.py --reps 20
 run jac_write 120 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $OUT/jwrite -o run -- python3 tools/jac_probe.py --reps 20
