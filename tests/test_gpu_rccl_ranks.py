@@ -1,0 +1,64 @@
+"""The library's multi-rank RCCL legs on ONE GPU (tests/rccl_rank_worker.py): N processes, one rank
+each, every rank with its own NCCL_HOSTID so RCCL accepts them on the same device and routes them over
+its socket transport on the loopback interface. What runs is the real partitioned path of the driver's
+multi-GPU bench -- the two-layer halo exchanged by ncclSend/ncclRecv pairs inside ncclGroupStart/End on
+the comm stream, overlapped with the interior patches; ncclAllReduce of the GMRES dot products and the
+residual norms; ncclMin of the TVD-RK time step -- checked against one GPU:
+  * five back-to-back residuals on changing states: every owned row and time step bitwise;
+  * three implicit steps (point-block Jacobi, and the line-implicit preconditioner whose lines are cut
+    at rank boundaries): the same linear iterations, residual history and states as the in-process group
+    of the same partition (rounding of the dot-product sums aside: 1e-9);
+  * TVD-RK order 3: bitwise the one-GPU steps and time.
+"""
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+
+
+def _free_port():
+    import socket
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+@pytest.mark.parametrize("world,meshkey,partitioner", [(2, "naca_small", "graph"), (4, "naca_small", "rcb")])
+def test_rccl_ranks_on_one_gpu(tmp_path, world, meshkey, partitioner):
+    port = _free_port()
+    procs = []
+    for r in range(world):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK="0", WORLD_SIZE=str(world), MASTER_ADDR="127.0.0.1",
+                   MASTER_PORT=str(port), NCCL_HOSTID="fvhip-rank-%d" % r, NCCL_SOCKET_IFNAME="lo",
+                   NCCL_IB_DISABLE="1")
+        procs.append(subprocess.Popen([sys.executable, "-u", os.path.join(HERE, "rccl_rank_worker.py"),
+                                       str(tmp_path / ("r%d.json" % r)), meshkey, partitioner], env=env,
+                                      stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True))
+    logs = []
+    try:
+        for p in procs:
+            out, _ = p.communicate(timeout=240)
+            logs.append(out)
+    finally:
+        for p in procs:
+            if p.poll() is None:
+                p.kill()
+                p.wait()
+    for r, p in enumerate(procs):
+        assert p.returncode == 0, "rank %d failed:\n%s" % (r, logs[r][-3000:])
+    reps = [json.load(open(tmp_path / ("r%d.json" % r))) for r in range(world)]
+    print(json.dumps(reps))
+    for rep in reps:
+        assert rep["layout"]["neighbours"] > 0 and rep["layout"]["ghosts"] > 0
+        assert rep["residual_mismatched_rows"] == 0, rep
+        for key in ("implicit_pbj", "implicit_lines"):
+            im = rep[key]
+            assert im["steps"] == 3 and im["lin_iters"] == im["group_lin_iters"], (key, im)
+            assert im["hist_rel"] <= 1e-9 and im["u_rel"] <= 1e-9, (key, im)
+        assert rep["tvdrk"]["steps"] == 3 and rep["tvdrk"]["time_equal"] and rep["tvdrk"]["mismatched_rows"] == 0
