@@ -12,7 +12,7 @@ run() {  # name timeout cmd...
   timeout -k 10 "$to" "$@" > "$OUT/$name.log" 2>&1
   local rc=$?
   echo "rc=$rc"; tail -c 600 "$OUT/$name.log"; echo
-  [ $rc -eq 0 ] || { echo "stopping after $name"; exit $rc; }
+  if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then echo "stopping after $name"; exit $rc; fi
 }
 run rccl_ranks 600 python3 -u -m pytest -v --timeout 500 --timeout-method thread tests/test_gpu_rccl_ranks.py -s
 run newtests 900 python3 -u -m pytest -x -v --timeout 600 --timeout-method thread tests/test_gpu_tvdrk.py tests/test_gpu_implicit.py::test_partitioned_line_implicit_same_solution tests/test_gpu_implicit.py::test_partitioned_ilu_same_solution tests/test_gpu_implicit.py::test_one_backward_euler_step_matches_host tests/test_gpu_partition.py::test_partitioned_c5_eight_ranks -s
