@@ -73,9 +73,14 @@ def main():
 
 
 def implicit_steps(mesh, case="naca", steps=5, warmup=2, init_steps=10, cfl=25.0, restart=30, lin_maxit=30,
-                   sweeps=4, single=False, gs=False, operators=(False, True), lines=False, ilu=False):
+                   sweeps=4, single=False, gs=False, operators=(False, True), lines=False, ilu=False,
+                   init_cfl=None, part=None, rank=0, world=1, new_uid=None, allmax=None):
     """time `steps` second-order backward-Euler steps per operator kind (False: assembled, True:
-    matrix-free) after a first-order start; yields one dict per operator"""
+    matrix-free) after a first-order start; yields one dict per operator.
+    init_cfl: (cfl_min, cfl_max) of the first-order start's expResidualRamp (aodesolver.cpp:110-120,
+    462; default: `cfl` held fixed). part/rank/world/new_uid: this rank's piece of a partition, its
+    handles on the library's RCCL communicator (new_uid() -> a fresh unique id, the same on every rank);
+    allmax(x): the maximum of x over ranks (the slowest rank's time)"""
     import torch
     import fvens_amd as fa
     import cases
@@ -84,19 +89,30 @@ def implicit_steps(mesh, case="naca", steps=5, warmup=2, init_steps=10, cfl=25.0
     n = cases.numerics(flux, grad, rec)
     n1 = cases.numerics(flux, grad, rec, order2=False)
     dev = torch.cuda.current_device()
-    sp1 = fa.FlowFV(mesh, p, n1, device=dev)
-    sp = fa.FlowFV(mesh, p, n, device=dev)
+    kw = {} if part is None else dict(partition=part, rank=rank)
+
+    def handle(nn):
+        h = fa.FlowFV(mesh, p, nn, device=dev, **kw)
+        if part is not None:
+            h.comm_init(world, rank, new_uid())
+        return h
+    sp1 = handle(n1)
+    sp = handle(n)
     perm = sp.permutation()
     assert np.array_equal(perm, sp1.permutation())
-    u0 = np.tile(cases.freestream(p), (mesh.nelem, 1))[perm]
+    nown = sp.nown if part is not None else mesh.nelem
+    nrows = nown + (sp.nghost if part is not None else 0)
+    u0 = np.zeros((nrows, 4))
+    u0[:nown] = cases.freestream(p)
     # the reference's start-up (transonic-implicit.ctrl): a first-order initialisation solve, then the
     # second-order main solve. Its CFL ramps (25/50 -> 500) blow up on this O-grid's 1e-5 wall cells
-    # during the start-up transient (measured), so the CFL is held fixed
+    # during the start-up transient (measured), so the main solve's CFL is held fixed
     lin = dict(lin_rtol=1e-2, lin_maxit=lin_maxit, restart=restart, prec_sweeps=sweeps, prec_single=single,
                prec_gs=gs, prec_lines=lines, prec_ilu=ilu)
+    c0, c1 = init_cfl if init_cfl else (cfl, cfl)
     dinit = torch.tensor(u0, dtype=torch.float64, device="cuda")
     st0, _ = sp1.steady_backward_euler_device(dinit.data_ptr(), fa.ImplicitConfig(
-        cflinit=cfl, cflfin=cfl, tol=0.0, maxiter=init_steps, **lin))
+        cflinit=c0, cflfin=c1, tol=0.0, maxiter=init_steps, **lin))
     torch.cuda.synchronize()
     sp1.close()
     for mf in operators:
@@ -106,18 +122,25 @@ def implicit_steps(mesh, case="naca", steps=5, warmup=2, init_steps=10, cfl=25.0
         du = dinit.clone()
         cfg.maxiter = steps
         torch.cuda.synchronize()
+        if allmax:
+            allmax(0.0)                                          # a barrier before the timed steps
         t0 = time.perf_counter()
         st, hist = sp.steady_backward_euler_device(du.data_ptr(), cfg)
         torch.cuda.synchronize()
         dt = time.perf_counter() - t0
+        if allmax:
+            dt = allmax(dt)
         k = max(st["steps"], 1)
         yield {"metric": "implicit_step_time", "case": case, "operator": "matrix-free" if mf else "assembled",
                "ms_per_step": round(dt / k * 1e3, 3), "steps": st["steps"],
                "lin_iters_per_step": round(st["lin_iters"] / k, 2),
                "ms_per_lin_iter": round(dt * 1e3 / max(st["lin_iters"], 1), 4),
-               "resratio": st["resratio"], "cells": mesh.nelem, "faces": mesh.naface,
-               "restart": restart, "prec_sweeps": sweeps, "prec_single": single, "prec_gs": gs, "prec_lines": lines, "prec_ilu": ilu, "cfl": cfl,
-               "init": {"steps": st0["steps"], "resratio": st0["resratio"]}}
+               "resratio": st["resratio"], "res_history": [float(x) for x in hist],
+               "cells": mesh.nelem, "faces": mesh.naface, "ranks": world,
+               "restart": restart, "prec_sweeps": sweeps, "prec_single": single, "prec_gs": gs, "prec_lines": lines,
+               "prec_ilu": ilu, "cfl": cfl,
+               "init": {"steps": st0["steps"], "resratio": st0["resratio"], "cfl_ramp": [c0, c1],
+                        "final_cfl": st0["cfl"]}}
     sp.close()
 
 
