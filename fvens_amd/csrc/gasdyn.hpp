@@ -36,6 +36,7 @@ struct Gas {
 	double kden;     ///< Minf*Minf*(g-1.0)*Pr (getThermalConductivityFromViscosity, :449)
 	double rkden;    ///< 1/kden
 	double rPr;      ///< 1/Pr
+	double g43;      ///< 1 when g > 4/3 with a margin far above rounding (visc_coef), else 0
 };
 /// Gas with its derived constants (host IEEE arithmetic in the reference's association order)
 inline Gas make_gas(double g, double Minf, double Tinf, double Reinf, double Pr) {
@@ -46,6 +47,7 @@ inline Gas make_gas(double g, double Minf, double Tinf, double Reinf, double Pr)
 	G.kden = G.Minf*G.Minf*(G.g-1.0)*G.Pr;
 	G.rkden = 1.0/G.kden;
 	G.rPr = 1.0/G.Pr;
+	G.g43 = G.g > 4.0/3.0*(1.0 + 1e-9) ? 1.0 : 0.0;
 	return G;
 }
 
@@ -201,6 +203,16 @@ FVHIP_HD double pow15(double T) {
 #else
 	return pow(T, 1.5);
 #endif
+}
+/// std::max(4.0/(3*rho), g/rho) of the viscous spectral radius (flow_spatial.cpp:612-613). For g > 4/3
+/// and rho > 0 the second is always the larger -- the exact quotients differ by the factor 3g/4 (1.05
+/// for air), the roundings (RN(3 rho), then RN(4/.)) by at most 2^-52 relative, and RN is monotone -- so
+/// the max is g/rho bitwise and the first division is skipped; otherwise both are formed as written
+FVHIP_HD double visc_coef(const Gas& G, double rho) {
+	const double b = div_rn(G.g, rho);
+	if(G.g43 != 0.0 && rho > 0) return b;
+	const double a = div_rn(4.0, 3*rho);
+	return (a < b) ? b : a;
 }
 FVHIP_HD double sutherland(const Gas& G, const double* uc) {
 	const double T = temperature(G, uc[0], pressure_cons(G, uc));

@@ -799,10 +799,7 @@ __global__ void __launch_bounds__(SLOTS_MAX) k_sweep(const DevMesh M, const DevP
 			if(VISC != SV_NONE) {
 				const double mui = VISC == SV_CONST ? G.rReinf : sutherland(G, ul);
 				const double muj = VISC == SV_CONST ? G.rReinf : sutherland(G, ur);
-				const double ai = div_rn(4.0, 3*ul[0]), bi = div_rn(G.g, ul[0]);
-				const double aj = div_rn(4.0, 3*ur[0]), bj = div_rn(G.g, ur[0]);
-				const double coi = (ai < bi) ? bi : ai;          // std::max
-				const double coj = (aj < bj) ? bj : aj;
+				const double coi = visc_coef(G, ul[0]), coj = visc_coef(G, ur[0]);   // std::max(4/(3 rho), g/rho)
 				// a ghost cell's spectral radius is never summed (and its area is not stored)
 				if(lr.x < M.nown) sri += div_rn(div_rcp(coi*mui, G.Pr, G.rPr) * len*len, M.area[lr.x]);
 				if(!bnd && lr.y < M.nown) srj += div_rn(div_rcp(coj*muj, G.Pr, G.rPr) * len*len, M.area[lr.y]);
@@ -1120,15 +1117,12 @@ __device__ __forceinline__ void fused_limit_row(const DevMesh& M, const DevPhys&
 /// face gradient (unused by the flux) is not formed. Boundary face: rowj = nullptr, the right state is
 /// the ghost primitive state gpr and the right gradient the cell's own.
 __device__ __forceinline__ void fz_viscous(const Gas& G, const double* rowi, const double* rowj, const double* gpr,
-                                           double2 ri, double2 rr, const double* n, double muRe, const double* va,
-                                           double* vf)
+                                           double4 vg, const double* n, double muRe, const double* va, double* vf)
 {
 	const double* gsrc = rowj ? rowj : rowi;          // right gradient: the boundary cell's own
-	double dr[2], dist = 0;
-	dr[0] = rr.x-ri.x; dist += dr[0]*dr[0];
-	dr[1] = rr.y-ri.y; dist += dr[1]*dr[1];
-	dist = sqrt_rn(dist);
-	dr[0] = div_rn(dr[0], dist); dr[1] = div_rn(dr[1], dist);
+	// the face's unit vector between the centres and their distance (Layout::slot_vg: 0 + dx^2 + dy^2,
+	// correctly rounded root and quotients -- what this function formed per call until round 4)
+	const double dr[2] = {vg.x, vg.y}, dist = vg.z;
 	double grad[2][4];
 	{   // temperature: T = temperature(rho, p), dT from the density and pressure gradients
 		__asm__ volatile("" ::: "memory");
@@ -1287,6 +1281,9 @@ __device__ __forceinline__ void fz_body(const DevMesh& M, const DevPhys& P, cons
 #else
 	if(s < q.s1) {
 #endif
+		// viscous: the slot's centre-to-centre geometry, requested before the reconstruction and the
+		// inviscid flux, used by the viscous term after them
+		const double4 vg = VISC != SV_NONE ? M.slot_vg[s] : make_double4(0, 0, 0, 0);
 		const int2 lrl = a.lrl;
 		const double2 nn = a.nn;
 		const double flen = a.len;
@@ -1374,10 +1371,7 @@ __device__ __forceinline__ void fz_body(const DevMesh& M, const DevPhys& P, cons
 			if(VISC != SV_NONE) {
 				const double mui = VISC == SV_CONST ? G.rReinf : sutherland(G, ul);
 				const double muj = VISC == SV_CONST ? G.rReinf : sutherland(G, ur);
-				const double ai = div_rn(4.0, 3*ul[0]), bi = div_rn(G.g, ul[0]);
-				const double aj = div_rn(4.0, 3*ur[0]), bj = div_rn(G.g, ur[0]);
-				const double coi = (ai < bi) ? bi : ai;          // std::max
-				const double coj = (aj < bj) ? bj : aj;
+				const double coi = visc_coef(G, ul[0]), coj = visc_coef(G, ur[0]);   // std::max(4/(3 rho), g/rho)
 				// a ghost cell's spectral radius is never summed (and its area is not stored)
 				const int2 g = M.slot_LR[s];
 				if(g.x < M.nown) sri += div_rn(div_rcp(coi*mui, G.Pr, G.rPr) * flen*flen, M.area[g.x]);
@@ -1395,17 +1389,14 @@ __device__ __forceinline__ void fz_body(const DevMesh& M, const DevPhys& P, cons
 			viscous_face_terms<VISC == SV_CONST>(G, ul, ur, muRe, va);
 			double gpr[4] = {0, 0, 0, 0};
 			const double* rowj = nullptr;
-			double2 rr;
 			if(bnd) {
 				const double4 g4 = ghost_prim_of_cell(M, P, B.u, bcell, bf);
 				gpr[0] = g4.x; gpr[1] = g4.y; gpr[2] = g4.z; gpr[3] = g4.w;
-				rr = M.bf_rcbp[bf];
 			} else {
 				rowj = &fz[lrl.y*FZW];
-				rr = *reinterpret_cast<const double2*>(rowj + 12);
 			}
 			double vf[4];
-			fz_viscous(G, rowi, rowj, gpr, ri, rr, n, muRe, va, vf);
+			fz_viscous(G, rowi, rowj, gpr, vg, n, muRe, va, vf);
 			#pragma unroll
 			for(int k = 0; k < 4; k++) f[k] += vf[k]*flen;
 		}

@@ -27,6 +27,7 @@ struct DevMesh
 	const double2* slot_n;     // [S]
 	const double* slot_len;    // [S]
 	const double2* slot_gr;    // [S]
+	const double4* slot_vg;    // [S] viscous: unit vector L->R centre, distance (Layout::slot_vg); else null
 	const int4* cell_slots;    // [N] (slot<<1 | isRight), -1 padded, ascending reference face
 	const int4* cell_nbr;      // [N] esuel order neighbours (internal / ncell+bf)
 	const int4* cell_face;     // [N] esuel order slots

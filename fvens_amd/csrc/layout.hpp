@@ -44,6 +44,8 @@ struct Layout
 	std::vector<double> slot_n;            ///< [S][2]
 	std::vector<double> slot_len;          ///< [S]
 	std::vector<double> slot_gr;           ///< [S][2]
+	std::vector<double> slot_vg;           ///< [S][4] viscous configurations: (rR - rL)/d (2), d = |rR - rL|, 0
+	                                       ///<  (fz_viscous' face geometry, same IEEE operations: bitwise)
 	// cells (internal order)
 	std::vector<int> cell_slots;           ///< [ncell][4]: (slot << 1 | cell-is-right) of the cell's
 	                                       ///<  faces in ascending reference face index, -1 padded;

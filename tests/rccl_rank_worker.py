@@ -61,6 +61,7 @@ def main():
         dr1 = torch.zeros_like(du1)
         dt1 = torch.zeros(m.nelem, dtype=torch.float64, device="cuda")
         one.compute_residual_device(du1.data_ptr(), dr1.data_ptr(), dt1.data_ptr(), True, True)
+        one.synchronize()                 # the library's stream, not torch's
         r1 = np.empty((m.nelem, 4))
         t1 = np.empty(m.nelem)
         r1[p1] = dr1.cpu().numpy()
@@ -84,6 +85,7 @@ def main():
         du = torch.full((sp.nown + sp.nghost, 4), float("nan"), dtype=torch.float64, device="cuda")
         du[:sp.nown] = torch.tensor(u0[g], device="cuda")
         st, hist = sp.steady_backward_euler_device(du.data_ptr(), cfg)
+        sp.synchronize()
         ur = du[:sp.nown].cpu().numpy()
         # the in-process group of the same partition (device copies, host sums), on rank 0's view
         sps = [fa.FlowFV(m, p, n, partition=part, rank=k) for k in range(world)]
@@ -95,6 +97,8 @@ def main():
             dus.append(d)
         grp = fa.FlowFVGroup(sps)
         stg, histg = grp.steady_backward_euler_device([d.data_ptr() for d in dus], cfg)
+        for s_ in sps:
+            s_.synchronize()
         ug = dus[rank][:sps[rank].nown].cpu().numpy()
         grp.close()
         for s_ in sps:
@@ -109,11 +113,13 @@ def main():
     u0 = cases.state(m, p, seed=9)
     du1 = torch.tensor(u0[p1], device="cuda")
     s1, t1 = one.tvdrk_device(du1.data_ptr(), 3, 0.4, 1e9, 3)
+    one.synchronize()
     uo = np.empty_like(u0)
     uo[p1] = du1.cpu().numpy()
     du = torch.full((sp.nown + sp.nghost, 4), float("nan"), dtype=torch.float64, device="cuda")
     du[:sp.nown] = torch.tensor(u0[g], device="cuda")
     s, t = sp.tvdrk_device(du.data_ptr(), 3, 0.4, 1e9, 3)
+    sp.synchronize()
     rep["tvdrk"] = {"steps": s, "time_equal": t == t1,
                     "mismatched_rows": int((du[:sp.nown].cpu().numpy() != uo[g]).any(axis=1).sum())}
     sp.close()
