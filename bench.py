@@ -461,7 +461,7 @@ def main():
         torch.cuda.synchronize()
         sp.synchronize()
 
-    def measure(fast, path="default", preheat_ms=0.0):
+    def measure(fast, path="default", preheat_ms=0.0, graph=False):
         """ms per step (timed region bracketed by barrier + sync, max over ranks) and per-kernel ms;
         preheat_ms: after the warm-up steps, further untimed steps for that long (all ranks run the
         same count), outside the timed region"""
@@ -469,6 +469,8 @@ def main():
         if world > 1:
             sp = fa.FlowFV(mesh, p, n, device=torch.cuda.current_device(), partition=part, rank=rank)
             sp.comm_init(world, rank, new_uid())
+            if graph:
+                sp.set_residual_graph(True)
             owned = np.nonzero(part == rank)[0]
         else:
             sp = fa.FlowFV(mesh, p, n, device=torch.cuda.current_device())
@@ -568,6 +570,16 @@ def main():
                      "kernels_ms_summed_over_chunks": {k: round(v, 5) for k, v in pk.items()},
                      "hbm_GBs_both_kernels": round((sweep_algorithmic_bytes(*cnt) + prep_algorithmic_bytes(*cnt))
                                                    / (pms * 1e-3) / 1e9, 1)}
+    # N GPUs: the same step captured in a hipGraph (fvhip_set_residual_graph: pack, RCCL group, ghost
+    # gradients and both fused launches replayed by one hipGraphLaunch)
+    graph_path = None
+    if world > 1:
+        try:
+            gms, gk, _ = measure(False, preheat_ms=args.preheat_ms, graph=True)
+            graph_path = {"ms_per_step": round(gms, 5), "value": round(F / (gms * 1e-3) / 1e6, 3),
+                          "kernels_ms": {k: round(v, 5) for k, v in gk.items()}}
+        except Exception as e:          # report, do not lose the measurement
+            graph_path = {"error": str(e)}
     # the primary measurement: the library's default path for this configuration, after a wall-clock
     # pre-heat (untimed, reported): layout set-up between the secondary measurements leaves the GPU
     # idle for ~1 s, and a 20-step timed region (~6 ms) would otherwise run while the clocks ramp
@@ -701,6 +713,7 @@ def main():
             "fast_math": fast,
             "staged_path": staged,
             "pipelined_path": pipelined,
+            "graph_path": graph_path,
             "implicit_step": implicit,
             "recorded": recorded,
             "build": fa._ffi.build_info(),

@@ -272,6 +272,14 @@ class FlowFV:
             st = self.layout_stats()
             self.nown, self.nghost = st["cells"], st["ghosts"]
 
+    def set_residual_graph(self, enable=True):
+        """RCCL rank: capture the overlapped residual step in a hipGraph and replay it (fvhip_set_residual_graph);
+        enable None only queries. Returns (graphs captured, graph launches) so far"""
+        c, r = ctypes.c_int(0), ctypes.c_int(0)
+        check(_ffi.lib().fvhip_set_residual_graph(self._h, -1 if enable is None else int(bool(enable)),
+                                                  ctypes.byref(c), ctypes.byref(r)))
+        return c.value, r.value
+
     def set_rank(self, rank, nranks):
         """rank of a per-rank-mesh handle (before group use; comm_init implies it)"""
         check(_ffi.lib().fvhip_set_rank(self._h, int(rank), int(nranks)))

@@ -59,6 +59,8 @@ _SIGS = {
                                     ctypes.POINTER(ctypes.c_void_p)]),
     "fvhip_destroy": (ctypes.c_int, [ctypes.c_void_p]),
     "fvhip_set_rank": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_int]),
+    "fvhip_set_residual_graph": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.POINTER(ctypes.c_int),
+                                                ctypes.POINTER(ctypes.c_int)]),
     "fvhip_partition_rcb": (ctypes.c_int, [ctypes.POINTER(FvMeshView), ctypes.c_int, c_int_p]),
     "fvhip_partition_graph": (ctypes.c_int, [ctypes.POINTER(FvMeshView), ctypes.c_int, c_int_p]),
     "fvhip_partition_graph_weighted": (ctypes.c_int, [ctypes.POINTER(FvMeshView), ctypes.c_int, c_int_p, c_int_p]),

@@ -126,6 +126,14 @@ int fvhip_create(const fvhip_mesh* mesh, const fvhip_flow_config* cfg, int devic
 /** Rank of a per-rank-mesh handle within nranks (PETSC_COMM_WORLD's rank in the reference); needed
  *  before fvhip_group_create, implied by fvhip_comm_init */
 int fvhip_set_rank(fvhip_handle h, int rank, int nranks);
+/** Partitioned handle on an RCCL communicator: enable = 1 captures its overlapped residual step (the
+ *  halo exchange's pack and ncclSend/ncclRecv group, the ghost gradients, the interior and border fused
+ *  launches with their stream/event joins) in a hipGraph the first time it runs with a given (u, r, dtm,
+ *  time-step, overwrite) and replays it with one hipGraphLaunch while those repeat (every residual of
+ *  the drivers and of a caller's loop on fixed buffers); 0 turns it off (default), -1 only queries.
+ *  *captures / *replays (may be NULL): graphs built and launched so far. Not a reference option: the
+ *  reference's MPI step has no counterpart (host enqueue of the step: tools/enqueue_probe.py). */
+int fvhip_set_residual_graph(fvhip_handle h, int enable, int* captures, int* replays);
 int fvhip_destroy(fvhip_handle h);
 
 /* ---------------------------------------------------------------------------------------------

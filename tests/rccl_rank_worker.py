@@ -76,6 +76,33 @@ def main():
     rep["residual_mismatched_rows"] = bad
     rep["layout"] = sp.layout_stats()
 
+    # 1b. the same step captured in a hipGraph (fvhip_set_residual_graph): fixed buffers, five states
+    #     copied in -> one capture, five replays, every owned row bitwise the single-GPU residual
+    sp.set_residual_graph(True)
+    du = torch.full((sp.nown + sp.nghost, 4), float("nan"), dtype=torch.float64, device="cuda")
+    dr = torch.zeros((sp.nown, 4), dtype=torch.float64, device="cuda")
+    dt = torch.zeros(sp.nown, dtype=torch.float64, device="cuda")
+    bad = 0
+    for k in range(5):
+        u = cases.state(m, p, seed=30 + k)
+        du1 = torch.tensor(u[p1], device="cuda")
+        dr1 = torch.zeros_like(du1)
+        dt1 = torch.zeros(m.nelem, dtype=torch.float64, device="cuda")
+        one.compute_residual_device(du1.data_ptr(), dr1.data_ptr(), dt1.data_ptr(), True, True)
+        one.synchronize()
+        r1 = np.empty((m.nelem, 4))
+        t1 = np.empty(m.nelem)
+        r1[p1] = dr1.cpu().numpy()
+        t1[p1] = dt1.cpu().numpy()
+        du[:sp.nown] = torch.tensor(u[g], device="cuda")
+        du[sp.nown:] = float("nan")
+        torch.cuda.synchronize()
+        sp.compute_residual_device(du.data_ptr(), dr.data_ptr(), dt.data_ptr(), True, True)
+        sp.synchronize()
+        bad += int((dr.cpu().numpy() != r1[g]).any(axis=1).sum() + (dt.cpu().numpy() != t1[g]).sum())
+    caps, reps_ = sp.set_residual_graph(False)
+    rep["graph"] = {"mismatched_rows": bad, "captures": caps, "replays": reps_}
+
     # 2. implicit steps (GMRES dot products and norms through ncclAllReduce; block-Jacobi across ranks
     #    for the line preconditioner): the same steps as a one-process group of the same partition
     u0 = cases.state(m, p, seed=8)
@@ -108,6 +135,17 @@ def main():
         rep[key] = {"steps": st["steps"], "lin_iters": st["lin_iters"], "group_lin_iters": stg["lin_iters"],
                     "hist_rel": float(np.max(np.abs(np.asarray(hist) - np.asarray(histg)) / np.abs(histg))),
                     "u_rel": float(np.abs(ur - ug).max() / scale)}
+        # the same solve with the residual step graphed: the same operations, so the same bits
+        c0, r0 = sp.set_residual_graph(True)
+        du[:sp.nown] = torch.tensor(u0[g], device="cuda")
+        du[sp.nown:] = float("nan")
+        torch.cuda.synchronize()
+        stG, histG = sp.steady_backward_euler_device(du.data_ptr(), cfg)
+        sp.synchronize()
+        caps, reps_ = sp.set_residual_graph(False)
+        rep[key]["graph"] = {"lin_iters": stG["lin_iters"], "hist_equal": bool(np.array_equal(hist, histG)),
+                             "u_equal": bool(np.array_equal(du[:sp.nown].cpu().numpy(), ur)),
+                             "captures": caps - c0, "replays": reps_ - r0}
 
     # 3. TVD-RK: the global dtmin through ncclMin, bitwise the one-GPU steps
     u0 = cases.state(m, p, seed=9)

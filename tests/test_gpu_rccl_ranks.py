@@ -8,7 +8,9 @@ residual norms; ncclMin of the TVD-RK time step -- checked against one GPU:
   * three implicit steps (point-block Jacobi, and the line-implicit preconditioner whose lines are cut
     at rank boundaries): the same linear iterations, residual history and states as the in-process group
     of the same partition (rounding of the dot-product sums aside: 1e-9);
-  * TVD-RK order 3: bitwise the one-GPU steps and time.
+  * TVD-RK order 3: bitwise the one-GPU steps and time;
+  * the step captured in a hipGraph (fvhip_set_residual_graph): one capture and five replays on fixed
+    buffers, bitwise; the implicit solve with it graphed: the same bits as without.
 """
 import json
 import os
@@ -57,8 +59,13 @@ def test_rccl_ranks_on_one_gpu(tmp_path, world, meshkey, partitioner):
     for rep in reps:
         assert rep["layout"]["neighbours"] > 0 and rep["layout"]["ghosts"] > 0
         assert rep["residual_mismatched_rows"] == 0, rep
+        gr = rep["graph"]
+        assert gr["mismatched_rows"] == 0 and gr["captures"] == 1 and gr["replays"] == 5, gr
         for key in ("implicit_pbj", "implicit_lines"):
             im = rep[key]
             assert im["steps"] == 3 and im["lin_iters"] == im["group_lin_iters"], (key, im)
             assert im["hist_rel"] <= 1e-9 and im["u_rel"] <= 1e-9, (key, im)
+            ig = im["graph"]
+            assert ig["lin_iters"] == im["lin_iters"] and ig["hist_equal"] and ig["u_equal"], (key, ig)
+            assert ig["captures"] == 1 and ig["replays"] == 3, (key, ig)
         assert rep["tvdrk"]["steps"] == 3 and rep["tvdrk"]["time_equal"] and rep["tvdrk"]["mismatched_rows"] == 0
