@@ -854,9 +854,12 @@ __global__ void __launch_bounds__(SLOTS_MAX) k_sweep(const DevMesh M, const DevP
 // from global memory), then sweeps its faces and sums them per cell. Same operations, same order as
 // k_prep_grad_wls + k_sweep: the result is bitwise the staged path's. Ring-1 gradients are computed
 // by every patch that needs them (35 % more gradients on C4) instead of a round trip through HBM.
-// LDS row per staged cell (14 doubles): [up 4][gradient 8][rc 2]
+// LDS row per staged cell (14 doubles): [up 4][gradient 8][rc 2]; viscous instantiations 18:
+// [up 4][gradient 8][rc 2][T, dT/dx, dT/dy, pad] (the temperature terms of fz_viscous, per gradient row)
 // ------------------------------------------------------------------------------------------------
 constexpr int FZW = 14;
+constexpr int FZW_VISC = 18;
+template <int VISC> constexpr int fz_w() { return VISC != SV_NONE ? FZW_VISC : FZW; }
 
 /// primitive ghost state of a cell's value across boundary face bf (k_prep_bfaces arithmetic)
 /// the fused residual's ghost states: the common BC types' ghost_state (gasdyn.hpp ghost_state_common)
@@ -931,15 +934,30 @@ __device__ __forceinline__ void fz_face_centres(const DevMesh& M, int c, double2
 	#pragma unroll
 	for(int k = 0; k < 4; k++) gp[k] = sl[k] >= 0 ? M.slot_gr[sl[k] >> 1] : make_double2(0, 0);
 }
-template <int LIM>
+template <int LIM, int W = FZW>
 __device__ __forceinline__ void fused_limit_row(const DevMesh& M, const DevPhys& P, const SweepBuffers& B,
                                                 const double* fz, const double* row, int c, int4 nb4,
                                                 const double2* gp, double eps2, double* g);
-template <int LIM>
+/// viscous rows (W = FZW_VISC): the temperature and its gradient of the row's cell, the arithmetic
+/// fz_viscous applied per face side until round 4 (temperature(rho, p), grad_temperature per direction
+/// from the density and pressure gradients), formed once per gradient row instead
+template <int W>
+__device__ __forceinline__ void fz_row_temperature(const Gas& G, double* row, const double* g)
+{
+	if constexpr(W == FZW_VISC) {
+		const double rho = row[0], p = row[3];
+		const double tx = grad_temperature(G, rho, g[0*2+0], p, g[3*2+0]);
+		const double ty = grad_temperature(G, rho, g[0*2+1], p, g[3*2+1]);
+		*reinterpret_cast<double2*>(row + 14) = make_double2(temperature(G, rho, p), tx);
+		row[16] = ty;
+	}
+}
+template <int LIM, int W = FZW>
 __device__ __forceinline__ void fused_wls_row(const DevMesh& M, const DevPhys& P, const SweepBuffers& B,
                                               const double* fz, double* row, int c, int4 nb4, double4 V,
                                               const double2* gp = nullptr, double eps2 = 0.0)
 {
+	static_assert(!(LIM && W == FZW_VISC), "limited reconstructions are not fused with the viscous flux");
 	if(c >= M.nown) {
 		double g[8];
 		ld8(B.grad, c, g);
@@ -952,6 +970,7 @@ __device__ __forceinline__ void fused_wls_row(const DevMesh& M, const DevPhys& P
 			for(int iv = 0; iv < 4; iv++) { g[iv*2+0] = lim[iv]*g[iv*2+0]; g[iv*2+1] = lim[iv]*g[iv*2+1]; }
 		}
 		st8(row + 4, 0, g);
+		fz_row_temperature<W>(P.gas, row, g);
 		return;
 	}
 	double uc[4];
@@ -968,7 +987,7 @@ __device__ __forceinline__ void fused_wls_row(const DevMesh& M, const DevPhys& P
 		double w[3], d0[3], d1[3], un[3][4];
 		#pragma unroll
 		for(int k = 0; k < 3; k++) {
-			const double* nrow = &fz[nb[k]*FZW];
+			const double* nrow = &fz[nb[k]*W];
 			const double2 rn = *reinterpret_cast<const double2*>(nrow + 12);
 			ld4(nrow, 0, un[k]);
 			double w2 = mul0(rcc.x-rn.x, rcc.x-rn.x);
@@ -995,7 +1014,7 @@ __device__ __forceinline__ void fused_wls_row(const DevMesh& M, const DevPhys& P
 			wls_normal_add(vm, w[k], d0[k], d1[k]);
 		}
 		if(nb4.w >= 0) {
-			const double* nrow = &fz[nb4.w*FZW];
+			const double* nrow = &fz[nb4.w*W];
 			const double2 rn = *reinterpret_cast<const double2*>(nrow + 12);
 			double u3[4];
 			ld4(nrow, 0, u3);
@@ -1021,7 +1040,7 @@ __device__ __forceinline__ void fused_wls_row(const DevMesh& M, const DevPhys& P
 		// into one generic (flat) load of a selected pointer, which waits on every outstanding
 		// global load of the wave
 		double un[4];
-		const double* nrow = &fz[(nbk >= 0 ? nbk : 0)*FZW];
+		const double* nrow = &fz[(nbk >= 0 ? nbk : 0)*W];
 		ld4(nrow, 0, un);
 		double2 rn = *reinterpret_cast<const double2*>(nrow + 12);
 		pin_regs(un[0]); pin_regs(un[1]); pin_regs(un[2]); pin_regs(un[3]); pin_regs(rn.x); pin_regs(rn.y);
@@ -1053,15 +1072,16 @@ __device__ __forceinline__ void fused_wls_row(const DevMesh& M, const DevPhys& P
 		g[iv*2+0] = V.x*f[iv*2+0] + V.y*f[iv*2+1];
 		g[iv*2+1] = V.z*f[iv*2+0] + V.w*f[iv*2+1];
 	}
-	if(LIM) fused_limit_row<LIM>(M, P, B, fz, row, c, nb4, gp, eps2, g);
+	if(LIM) fused_limit_row<LIM, W>(M, P, B, fz, row, c, nb4, gp, eps2, g);
 	st8(row + 4, 0, g);
+	fz_row_temperature<W>(P.gas, row, g);
 }
 
 /// limited reconstructions in the fused residual: the row's Barth-Jespersen / Venkatakrishnan limiter
 /// values from the staged neighbour states (boundary: the ghost primitive state, as the staged path)
 /// and its face centres, k_prep_grad_wls<LIM>'s arithmetic; the staged row then holds lim*g, which is
 /// the product linearExtrapolate forms first ((lim*grad)*(gp - rc), reconstruction_utils.hpp:28-30)
-template <int LIM>
+template <int LIM, int W>
 __device__ __forceinline__ void fused_limit_row(const DevMesh& M, const DevPhys& P, const SweepBuffers& B,
                                                 const double* fz, const double* row, int c, int4 nb4,
                                                 const double2* gpre, double eps2, double* g)
@@ -1080,7 +1100,7 @@ __device__ __forceinline__ void fused_limit_row(const DevMesh& M, const DevPhys&
 		has[k] = nb[k] != -1;
 		un[k][0] = un[k][1] = un[k][2] = un[k][3] = 0.0;
 		if(!has[k]) continue;
-		if(nb[k] >= 0) ld4(&fz[nb[k]*FZW], 0, un[k]);
+		if(nb[k] >= 0) ld4(&fz[nb[k]*W], 0, un[k]);
 		else {
 			const double4 q = ghost_prim_of_cell(M, P, B.u, c, -2 - nb[k]);
 			un[k][0] = q.x; un[k][1] = q.y; un[k][2] = q.z; un[k][3] = q.w;
@@ -1116,24 +1136,37 @@ __device__ __forceinline__ void fused_limit_row(const DevMesh& M, const DevPhys&
 /// live at a time instead of both cells' full rows (24 doubles) -- register pressure. The density
 /// face gradient (unused by the flux) is not formed. Boundary face: rowj = nullptr, the right state is
 /// the ghost primitive state gpr and the right gradient the cell's own.
-__device__ __forceinline__ void fz_viscous(const Gas& G, const double* rowi, const double* rowj, const double* gpr,
+__device__ __forceinline__ void fz_viscous(const Gas& G, const double* rowi, const double* rowj, const double4 gpr,
                                            double4 vg, const double* n, double muRe, const double* va, double* vf)
 {
 	const double* gsrc = rowj ? rowj : rowi;          // right gradient: the boundary cell's own
-	// the face's unit vector between the centres and their distance (Layout::slot_vg: 0 + dx^2 + dy^2,
-	// correctly rounded root and quotients -- what this function formed per call until round 4)
+	// the face's unit vector between the centres and their distance: formed here, or (FVHIP_FZ_VGEO)
+	// read from Layout::slot_vg, the same operations on the host (0 + dx^2 + dy^2, correctly rounded
+	// root and quotients)
+#if FVHIP_FZ_VGEO
 	const double dr[2] = {vg.x, vg.y}, dist = vg.z;
+#else
+	double dr[2], dist = 0;
+	dr[0] = vg.z - vg.x; dist += dr[0]*dr[0];
+	dr[1] = vg.w - vg.y; dist += dr[1]*dr[1];
+	dist = sqrt_rn(dist);
+	dr[0] = div_rn(dr[0], dist); dr[1] = div_rn(dr[1], dist);
+#endif
 	double grad[2][4];
-	{   // temperature: T = temperature(rho, p), dT from the density and pressure gradients
+	{   // temperature: T and dT of each side, formed per staged row in phase 1 (fz_row_temperature); a
+		// boundary face's right side is the ghost state with the cell's own gradients, formed here
 		__asm__ volatile("" ::: "memory");
-		const double rl = rowi[0], pl = rowi[3];
-		const double rrr = rowj ? rowj[0] : gpr[0], prr = rowj ? rowj[3] : gpr[3];
-		double gL[2], gR[2];
-		for(int j = 0; j < 2; j++) {
-			gL[j] = grad_temperature(G, rl, rowi[4 + 0*2 + j], pl, rowi[4 + 3*2 + j]);
-			gR[j] = grad_temperature(G, rrr, gsrc[4 + 0*2 + j], prr, gsrc[4 + 3*2 + j]);
+		const double2 tgl = *reinterpret_cast<const double2*>(rowi + 14);
+		const double gL[2] = {tgl.y, rowi[16]}, tl = tgl.x;
+		double gR[2], tr;
+		if(rowj) {
+			const double2 tgr = *reinterpret_cast<const double2*>(rowj + 14);
+			gR[0] = tgr.y; gR[1] = rowj[16]; tr = tgr.x;
+		} else {
+			const double rrr = gpr.x, prr = gpr.w;
+			for(int j = 0; j < 2; j++) gR[j] = grad_temperature(G, rrr, gsrc[4 + 0*2 + j], prr, gsrc[4 + 3*2 + j]);
+			tr = temperature(G, rrr, prr);
 		}
-		const double tl = temperature(G, rl, pl), tr = temperature(G, rrr, prr);
 		double davg[2];
 		davg[0] = 0.5*(gL[0] + gR[0]);
 		davg[1] = 0.5*(gL[1] + gR[1]);
@@ -1145,7 +1178,7 @@ __device__ __forceinline__ void fz_viscous(const Gas& G, const double* rowi, con
 	#pragma unroll
 	for(int i = 1; i < 3; i++) {   // velocity components
 		__asm__ volatile("" ::: "memory");
-		const double tl = rowi[i], tr = rowj ? rowj[i] : gpr[i];
+		const double tl = rowi[i], tr = rowj ? rowj[i] : (i == 1 ? gpr.y : gpr.z);
 		double davg[2];
 		davg[0] = 0.5*(rowi[4 + i*2 + 0] + gsrc[4 + i*2 + 0]);
 		davg[1] = 0.5*(rowi[4 + i*2 + 1] + gsrc[4 + i*2 + 1]);
@@ -1247,14 +1280,15 @@ __device__ __forceinline__ void fz_body(const DevMesh& M, const DevPhys& P, cons
 	const Gas& G = P.gas;
 	const int t = static_cast<int>(threadIdx.x);
 	const int s = q.s0 + t;
+	constexpr int W = fz_w<VISC>();
 
 	// phase 0: primitive states and centres of the staged cells
-	if(t < q.nl) stage_row(G, &fz[t*FZW], a.ua, a.rca);
+	if(t < q.nl) stage_row(G, &fz[t*W], a.ua, a.rca);
 	for(int i = t + SLOTS_MAX; i < q.nl; i += SLOTS_MAX) {
 		const int c = fz_cell(M, q, i);
 		double b[4];
 		ld4(B.u, c, b);
-		stage_row(G, &fz[i*FZW], b, M.rc[c]);
+		stage_row(G, &fz[i*W], b, M.rc[c]);
 	}
 	__syncthreads();
 	FZ_STAMP(B, 1);
@@ -1263,10 +1297,10 @@ __device__ __forceinline__ void fz_body(const DevMesh& M, const DevPhys& P, cons
 	// (k_prep_grad_wls arithmetic, neighbours in the same ascending reference face order)
 	hookA();
 #ifndef FVHIP_PROBE_NOGRAD
-	if(t < q.ng) fused_wls_row<LIM>(M, P, B, fz, &fz[t*FZW], a.cf, a.nb4a, a.Va, LIM && FVHIP_FZ_LIM_PREFETCH ? a.gpa : nullptr, a.eps2a);
+	if(t < q.ng) fused_wls_row<LIM, W>(M, P, B, fz, &fz[t*W], a.cf, a.nb4a, a.Va, LIM && FVHIP_FZ_LIM_PREFETCH ? a.gpa : nullptr, a.eps2a);
 	for(int i = t + SLOTS_MAX; i < q.ng; i += SLOTS_MAX) {
 		const int c = fz_cell(M, q, i);
-		fused_wls_row<LIM>(M, P, B, fz, &fz[i*FZW], c, c < M.nown ? fz_nbrs(q, i) : make_int4(-1, -1, -1, -1),
+		fused_wls_row<LIM, W>(M, P, B, fz, &fz[i*W], c, c < M.nown ? fz_nbrs(q, i) : make_int4(-1, -1, -1, -1),
 		              c < M.nown && !FVHIP_FZ_WLSV ? M.wls_V[c] : make_double4(0, 0, 0, 0));
 	}
 #endif
@@ -1283,7 +1317,9 @@ __device__ __forceinline__ void fz_body(const DevMesh& M, const DevPhys& P, cons
 #endif
 		// viscous: the slot's centre-to-centre geometry, requested before the reconstruction and the
 		// inviscid flux, used by the viscous term after them
+#if FVHIP_FZ_VGEO
 		const double4 vg = VISC != SV_NONE ? M.slot_vg[s] : make_double4(0, 0, 0, 0);
+#endif
 		const int2 lrl = a.lrl;
 		const double2 nn = a.nn;
 		const double flen = a.len;
@@ -1292,14 +1328,14 @@ __device__ __forceinline__ void fz_body(const DevMesh& M, const DevPhys& P, cons
 		int bf = 0, bcell = 0;          // boundary face: its index and cell from the global slot
 		if(bnd) { const int2 g = M.slot_LR[s]; bf = g.y - M.ncell; bcell = g.x; }
 		double ul[4], ur[4];
-		const double* rowi = &fz[lrl.x*FZW];
+		const double* rowi = &fz[lrl.x*W];
 		const double2 ri = *reinterpret_cast<const double2*>(rowi + 12);
 		double ui[4], gi[8];
 		ld4(rowi, 0, ui);
 		ld8(rowi + 4, 0, gi);
 		if(REC == SR_MUSCL) {
 			if(!bnd) {
-				const double* rowj = &fz[lrl.y*FZW];
+				const double* rowj = &fz[lrl.y*W];
 				const double2 rj = *reinterpret_cast<const double2*>(rowj + 12);
 				double uj[4], gj[8];
 				ld4(rowj, 0, uj);
@@ -1344,7 +1380,7 @@ __device__ __forceinline__ void fz_body(const DevMesh& M, const DevPhys& P, cons
 			}
 			prim2cons(G, ul, ul);
 			if(!bnd) {
-				const double* rowj = &fz[lrl.y*FZW];
+				const double* rowj = &fz[lrl.y*W];
 				const double2 rj = *reinterpret_cast<const double2*>(rowj + 12);
 				double uj[4], gj[8];
 				ld4(rowj, 0, uj);
@@ -1387,14 +1423,14 @@ __device__ __forceinline__ void fz_body(const DevMesh& M, const DevPhys& P, cons
 			// the reconstruction's copies kept live through the inviscid flux -- 4 waves per SIMD
 			double muRe, va[2];
 			viscous_face_terms<VISC == SV_CONST>(G, ul, ur, muRe, va);
-			double gpr[4] = {0, 0, 0, 0};
+			double4 gpr = make_double4(0, 0, 0, 0);
 			const double* rowj = nullptr;
-			if(bnd) {
-				const double4 g4 = ghost_prim_of_cell(M, P, B.u, bcell, bf);
-				gpr[0] = g4.x; gpr[1] = g4.y; gpr[2] = g4.z; gpr[3] = g4.w;
-			} else {
-				rowj = &fz[lrl.y*FZW];
-			}
+			double2 rr;
+			if(bnd) { gpr = ghost_prim_of_cell(M, P, B.u, bcell, bf); rr = M.bf_rcbp[bf]; }
+			else { rowj = &fz[lrl.y*W]; rr = *reinterpret_cast<const double2*>(rowj + 12); }
+#if !FVHIP_FZ_VGEO
+			const double4 vg = make_double4(ri.x, ri.y, rr.x, rr.y);    // the two centres
+#endif
 			double vf[4];
 			fz_viscous(G, rowi, rowj, gpr, vg, n, muRe, va, vf);
 			#pragma unroll
@@ -1692,7 +1728,8 @@ const char* launch_residual_wls(const DevMesh& M, const DevPhys& P, const SweepB
 		default: fn = pickFused<6>(rec, visc, lim, dt); break;
 	}
 #endif
-	const size_t lds = std::max(static_cast<size_t>(M.fz_max_cells)*FZW, static_cast<size_t>(6*SLOTS_MAX))*sizeof(double);
+	const size_t W = visc != SV_NONE ? FZW_VISC : FZW;
+	const size_t lds = std::max(static_cast<size_t>(M.fz_max_cells)*W, static_cast<size_t>(6*SLOTS_MAX))*sizeof(double);
 	// raise the dynamic-LDS limit once per instantiation and device to the largest patch the layout
 	// allows (hipFuncSetAttribute is a host-side runtime call: not on every launch)
 	{
@@ -1702,7 +1739,7 @@ const char* launch_residual_wls(const DevMesh& M, const DevPhys& P, const SweepB
 		if(hipGetDevice(&dev) != hipSuccess) throw std::runtime_error("k_residual_wls: hipGetDevice failed");
 		std::lock_guard<std::mutex> lock(mu);
 		if(configured.insert({reinterpret_cast<const void*>(fn), dev}).second) {
-			const size_t maxlds = std::max(static_cast<size_t>(FUSED_LDS_CELLS)*FZW, static_cast<size_t>(6*SLOTS_MAX))*sizeof(double);
+			const size_t maxlds = std::max(static_cast<size_t>(FUSED_LDS_CELLS)*W, static_cast<size_t>(6*SLOTS_MAX))*sizeof(double);
 			const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(fn),
 			                                         hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(maxlds));
 			if(e != hipSuccess) {

@@ -435,7 +435,7 @@ Layout buildLayout(const MeshTopo& T, const fvhip_flow_config& cfg, bool renumbe
 	// --- viscous face geometry per slot: the modified-average viscous flux's unit vector between the
 	//     two cell centres (ghost centre for a boundary face) and their distance, in fz_viscous' operation
 	//     order (0 + dx*dx + dy*dy, correctly rounded sqrt and divisions: the device's bits) ---
-	if(cfg.viscous_sim) {
+	if(FVHIP_FZ_VGEO && cfg.viscous_sim) {
 		const size_t S = Lo.slot_L.size();
 		Lo.slot_vg.assign(4*S, 0.0);
 		for(size_t s = 0; s < S; s++) {
@@ -508,8 +508,10 @@ bool fusedEligible(const fvhip_flow_config& cfg)
 
 int fusedRowCap(const fvhip_flow_config& cfg)
 {
+	// inviscid unlimited: 14-double rows, five blocks per CU; viscous: 18-double rows (the temperature
+	// terms), four blocks per CU -- 284 rows either way (31.8 / 40.9 KB); limited: 14-double rows, four
 	const bool limited = cfg.reconstruction == FVHIP_REC_BARTHJESPERSEN || cfg.reconstruction == FVHIP_REC_VENKATAKRISHNAN;
-	return (!cfg.viscous_sim && !limited) ? FUSED_LDS_CELLS_5W : FUSED_LDS_CELLS;
+	return !limited ? FUSED_LDS_CELLS_5W : FUSED_LDS_CELLS;
 }
 
 void buildFused(Layout& Lo)

@@ -10,7 +10,7 @@ those of the one-GPU-per-rank run. torch.distributed (gloo) only rendezvouses th
 RCCL unique id and the results; the single-GPU reference results are computed by every rank itself.
 
 usage (set by the test): RANK, WORLD_SIZE, MASTER_ADDR, MASTER_PORT, NCCL_HOSTID in the environment;
-argv: <out.json> <mesh key> <partitioner>
+argv: <out.json> <mesh key> <partitioner> [graph]  (graph: the hipGraph sections only)
 """
 import json
 import os
@@ -25,6 +25,10 @@ sys.path.insert(0, HERE)
 
 def main():
     out_path, meshkey, partitioner = sys.argv[1], sys.argv[2], sys.argv[3]
+    graph = len(sys.argv) > 4 and sys.argv[4] == "graph"
+
+    def mark(msg):
+        print("[rank %s] %s" % (os.environ["RANK"], msg), flush=True)
     rank, world = int(os.environ["RANK"]), int(os.environ["WORLD_SIZE"])
     import torch
     import torch.distributed as dist
@@ -46,6 +50,7 @@ def main():
 
     rep = {"rank": rank, "world": world}
     owned = np.nonzero(part == rank)[0]
+    mark("mesh and partition ready")
 
     # 1. residuals: five back-to-back partitioned residuals on changing states, each owned row bitwise
     #    the single-GPU residual (ghost rows start as NaN: a missed exchange cannot pass)
@@ -55,7 +60,7 @@ def main():
     g = owned[sp.permutation()]
     p1 = one.permutation()
     bad = 0
-    for k in range(5):
+    for k in range(0 if graph else 5):
         u = cases.state(m, p, seed=20 + k)
         du1 = torch.tensor(u[p1], device="cuda")
         dr1 = torch.zeros_like(du1)
@@ -75,15 +80,18 @@ def main():
         bad += int((dr.cpu().numpy() != r1[g]).any(axis=1).sum() + (dt.cpu().numpy() != t1[g]).sum())
     rep["residual_mismatched_rows"] = bad
     rep["layout"] = sp.layout_stats()
+    mark("residuals done")
 
     # 1b. the same step captured in a hipGraph (fvhip_set_residual_graph): fixed buffers, five states
     #     copied in -> one capture, five replays, every owned row bitwise the single-GPU residual
-    sp.set_residual_graph(True)
+    if graph:
+        sp.set_residual_graph(True)
+        mark("graph on")
     du = torch.full((sp.nown + sp.nghost, 4), float("nan"), dtype=torch.float64, device="cuda")
     dr = torch.zeros((sp.nown, 4), dtype=torch.float64, device="cuda")
     dt = torch.zeros(sp.nown, dtype=torch.float64, device="cuda")
     bad = 0
-    for k in range(5):
+    for k in range(5 if graph else 0):
         u = cases.state(m, p, seed=30 + k)
         du1 = torch.tensor(u[p1], device="cuda")
         dr1 = torch.zeros_like(du1)
@@ -97,6 +105,7 @@ def main():
         du[:sp.nown] = torch.tensor(u[g], device="cuda")
         du[sp.nown:] = float("nan")
         torch.cuda.synchronize()
+        mark("graph residual %d" % k)
         sp.compute_residual_device(du.data_ptr(), dr.data_ptr(), dt.data_ptr(), True, True)
         sp.synchronize()
         bad += int((dr.cpu().numpy() != r1[g]).any(axis=1).sum() + (dt.cpu().numpy() != t1[g]).sum())
@@ -135,6 +144,9 @@ def main():
         rep[key] = {"steps": st["steps"], "lin_iters": st["lin_iters"], "group_lin_iters": stg["lin_iters"],
                     "hist_rel": float(np.max(np.abs(np.asarray(hist) - np.asarray(histg)) / np.abs(histg))),
                     "u_rel": float(np.abs(ur - ug).max() / scale)}
+        mark("implicit %s done" % key)
+        if not graph:
+            continue
         # the same solve with the residual step graphed: the same operations, so the same bits
         c0, r0 = sp.set_residual_graph(True)
         du[:sp.nown] = torch.tensor(u0[g], device="cuda")
@@ -148,6 +160,7 @@ def main():
                              "captures": caps - c0, "replays": reps_ - r0}
 
     # 3. TVD-RK: the global dtmin through ncclMin, bitwise the one-GPU steps
+    mark("tvdrk")
     u0 = cases.state(m, p, seed=9)
     du1 = torch.tensor(u0[p1], device="cuda")
     s1, t1 = one.tvdrk_device(du1.data_ptr(), 3, 0.4, 1e9, 3)

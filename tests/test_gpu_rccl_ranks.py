@@ -31,8 +31,7 @@ def _free_port():
         return s.getsockname()[1]
 
 
-@pytest.mark.parametrize("world,meshkey,partitioner", [(2, "naca_small", "graph"), (4, "naca_small", "rcb")])
-def test_rccl_ranks_on_one_gpu(tmp_path, world, meshkey, partitioner):
+def _run_ranks(tmp_path, world, meshkey, partitioner, mode=""):
     port = _free_port()
     procs = []
     for r in range(world):
@@ -40,8 +39,8 @@ def test_rccl_ranks_on_one_gpu(tmp_path, world, meshkey, partitioner):
                    MASTER_PORT=str(port), NCCL_HOSTID="fvhip-rank-%d" % r, NCCL_SOCKET_IFNAME="lo",
                    NCCL_IB_DISABLE="1")
         procs.append(subprocess.Popen([sys.executable, "-u", os.path.join(HERE, "rccl_rank_worker.py"),
-                                       str(tmp_path / ("r%d.json" % r)), meshkey, partitioner], env=env,
-                                      stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True))
+                                       str(tmp_path / ("r%d.json" % r)), meshkey, partitioner] + ([mode] if mode else []),
+                                      env=env, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True))
     logs = []
     try:
         for p in procs:
@@ -53,19 +52,29 @@ def test_rccl_ranks_on_one_gpu(tmp_path, world, meshkey, partitioner):
                 p.kill()
                 p.wait()
     for r, p in enumerate(procs):
-        assert p.returncode == 0, "rank %d failed:\n%s" % (r, logs[r][-3000:])
+        assert p.returncode == 0, "rank %d failed (%d):\n%s" % (r, p.returncode, logs[r][-3000:])
     reps = [json.load(open(tmp_path / ("r%d.json" % r))) for r in range(world)]
     print(json.dumps(reps))
-    for rep in reps:
+    return reps
+
+
+@pytest.mark.parametrize("world,meshkey,partitioner", [(2, "naca_small", "graph"), (4, "naca_small", "rcb")])
+def test_rccl_ranks_on_one_gpu(tmp_path, world, meshkey, partitioner):
+    for rep in _run_ranks(tmp_path, world, meshkey, partitioner):
         assert rep["layout"]["neighbours"] > 0 and rep["layout"]["ghosts"] > 0
         assert rep["residual_mismatched_rows"] == 0, rep
-        gr = rep["graph"]
-        assert gr["mismatched_rows"] == 0 and gr["captures"] == 1 and gr["replays"] == 5, gr
         for key in ("implicit_pbj", "implicit_lines"):
             im = rep[key]
             assert im["steps"] == 3 and im["lin_iters"] == im["group_lin_iters"], (key, im)
             assert im["hist_rel"] <= 1e-9 and im["u_rel"] <= 1e-9, (key, im)
-            ig = im["graph"]
-            assert ig["lin_iters"] == im["lin_iters"] and ig["hist_equal"] and ig["u_equal"], (key, ig)
-            assert ig["captures"] == 1 and ig["replays"] == 3, (key, ig)
         assert rep["tvdrk"]["steps"] == 3 and rep["tvdrk"]["time_equal"] and rep["tvdrk"]["mismatched_rows"] == 0
+
+
+def test_rccl_ranks_graph_on_one_gpu(tmp_path):
+    for rep in _run_ranks(tmp_path, 2, "naca_small", "graph", "graph"):
+        gr = rep["graph"]
+        assert gr["mismatched_rows"] == 0 and gr["captures"] == 1 and gr["replays"] == 5, gr
+        for key in ("implicit_pbj", "implicit_lines"):
+            ig = rep[key]["graph"]
+            assert ig["lin_iters"] == rep[key]["lin_iters"] and ig["hist_equal"] and ig["u_equal"], (key, ig)
+            assert ig["captures"] == 1 and ig["replays"] == 3, (key, ig)
