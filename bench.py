@@ -255,6 +255,7 @@ def halo_parity(fa, torch, dist, mesh, p, n, u, part, rank, world, new_uid):
         du = torch.tensor(u[perm], device="cuda")
         dr = torch.zeros((N, 4), dtype=torch.float64, device="cuda")
         dt = torch.zeros(N, dtype=torch.float64, device="cuda")
+        torch.cuda.synchronize()  # torch's stream vs the library's (non-blocking) streams
         one.compute_residual_device(du.data_ptr(), dr.data_ptr(), dt.data_ptr(), True, True)
         one.synchronize()
         idx = torch.tensor(perm, dtype=torch.int64, device="cuda")
@@ -271,6 +272,7 @@ def halo_parity(fa, torch, dist, mesh, p, n, u, part, rank, world, new_uid):
     du[:sp.nown] = torch.tensor(u[gint], device="cuda")
     dr = torch.zeros((sp.nown, 4), dtype=torch.float64, device="cuda")
     dt = torch.zeros(sp.nown, dtype=torch.float64, device="cuda")
+    torch.cuda.synchronize()  # torch's stream vs the library's (non-blocking) streams
     sp.compute_residual_device(du.data_ptr(), dr.data_ptr(), dt.data_ptr(), True, True)
     sp.synchronize()
     ref = full[torch.tensor(gint, dtype=torch.int64, device="cuda")]

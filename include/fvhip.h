@@ -31,8 +31,10 @@
  *    fvhip_group_destroy(NULL) do nothing. Calls on one handle are not thread-safe
  *    (like the reference, flow_spatial.hpp:196-197); each handle owns one HIP stream.
  *  - *_device variants take device pointers in the library's internal cell order (see
- *    fvhip_to_internal / fvhip_from_internal) and are asynchronous on the handle's stream.
- */
+ *    fvhip_to_internal / fvhip_from_internal) and are asynchronous on the handle's stream, a
+ *    non-blocking stream: input arrays a caller writes on another stream (e.g. PyTorch's) must be
+ *    complete before the call (synchronize that stream), and outputs are complete after
+ *    fvhip_synchronize (or any later call that returns host results). */
 #ifndef FVHIP_H
 #define FVHIP_H
 

@@ -65,6 +65,7 @@ def main():
         du1 = torch.tensor(u[p1], device="cuda")
         dr1 = torch.zeros_like(du1)
         dt1 = torch.zeros(m.nelem, dtype=torch.float64, device="cuda")
+        torch.cuda.synchronize()  # torch's stream vs the library's (non-blocking) streams
         one.compute_residual_device(du1.data_ptr(), dr1.data_ptr(), dt1.data_ptr(), True, True)
         one.synchronize()                 # the library's stream, not torch's
         r1 = np.empty((m.nelem, 4))
@@ -75,6 +76,7 @@ def main():
         du[:sp.nown] = torch.tensor(u[g], device="cuda")
         dr = torch.zeros((sp.nown, 4), dtype=torch.float64, device="cuda")
         dt = torch.zeros(sp.nown, dtype=torch.float64, device="cuda")
+        torch.cuda.synchronize()
         sp.compute_residual_device(du.data_ptr(), dr.data_ptr(), dt.data_ptr(), True, True)
         sp.synchronize()
         bad += int((dr.cpu().numpy() != r1[g]).any(axis=1).sum() + (dt.cpu().numpy() != t1[g]).sum())
@@ -96,6 +98,7 @@ def main():
         du1 = torch.tensor(u[p1], device="cuda")
         dr1 = torch.zeros_like(du1)
         dt1 = torch.zeros(m.nelem, dtype=torch.float64, device="cuda")
+        torch.cuda.synchronize()  # torch's stream vs the library's (non-blocking) streams
         one.compute_residual_device(du1.data_ptr(), dr1.data_ptr(), dt1.data_ptr(), True, True)
         one.synchronize()
         r1 = np.empty((m.nelem, 4))
@@ -120,6 +123,7 @@ def main():
                                 restart=20, prec_sweeps=2 if not lines else 1, min_relax=0.2, prec_lines=lines)
         du = torch.full((sp.nown + sp.nghost, 4), float("nan"), dtype=torch.float64, device="cuda")
         du[:sp.nown] = torch.tensor(u0[g], device="cuda")
+        torch.cuda.synchronize()
         st, hist = sp.steady_backward_euler_device(du.data_ptr(), cfg)
         sp.synchronize()
         ur = du[:sp.nown].cpu().numpy()
@@ -131,6 +135,7 @@ def main():
             d = torch.full((s_.nown + s_.nghost, 4), float("nan"), dtype=torch.float64, device="cuda")
             d[:s_.nown] = torch.tensor(u0[gk], device="cuda")
             dus.append(d)
+        torch.cuda.synchronize()
         grp = fa.FlowFVGroup(sps)
         stg, histg = grp.steady_backward_euler_device([d.data_ptr() for d in dus], cfg)
         for s_ in sps:
@@ -163,12 +168,14 @@ def main():
     mark("tvdrk")
     u0 = cases.state(m, p, seed=9)
     du1 = torch.tensor(u0[p1], device="cuda")
+    torch.cuda.synchronize()
     s1, t1 = one.tvdrk_device(du1.data_ptr(), 3, 0.4, 1e9, 3)
     one.synchronize()
     uo = np.empty_like(u0)
     uo[p1] = du1.cpu().numpy()
     du = torch.full((sp.nown + sp.nghost, 4), float("nan"), dtype=torch.float64, device="cuda")
     du[:sp.nown] = torch.tensor(u0[g], device="cuda")
+    torch.cuda.synchronize()
     s, t = sp.tvdrk_device(du.data_ptr(), 3, 0.4, 1e9, 3)
     sp.synchronize()
     rep["tvdrk"] = {"steps": s, "time_equal": t == t1,

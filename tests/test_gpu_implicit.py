@@ -321,6 +321,7 @@ def _partitioned(m, p, n, u0, nparts):
         d = torch.full((spk.nown + spk.nghost, 4), float("nan"), dtype=torch.float64, device="cuda")
         d[:spk.nown] = torch.tensor(u0[g], device="cuda")
         dus.append(d)
+    torch.cuda.synchronize()  # torch's stream vs the library's (non-blocking) streams
     return sps, dus, glob
 
 
@@ -478,6 +479,7 @@ def test_partitioned_line_implicit_same_solution(nparts):
                     d = torch.full((spk.nown + spk.nghost, 4), float("nan"), dtype=torch.float64, device="cuda")
                     d[:spk.nown] = torch.tensor(u0[g], device="cuda")
                     dus.append(d)
+                torch.cuda.synchronize()  # torch's stream vs the library's (non-blocking) streams
                 grp = fa.FlowFVGroup(sps)
                 st, _ = grp.steady_backward_euler_device([d.data_ptr() for d in dus], cfg)
                 u = _gather(u0, sps, dus, glob)

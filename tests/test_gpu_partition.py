@@ -53,6 +53,7 @@ def run_partitioned(meshkey, kind, flux, grad, rec, order2, nparts, fast=False, 
         dus.append(du)
         drs.append(torch.full((sp.nown, 4), float("nan"), dtype=torch.float64, device="cuda"))
         dts.append(torch.full((sp.nown,), float("nan"), dtype=torch.float64, device="cuda"))
+    torch.cuda.synchronize()  # torch's stream vs the library's (non-blocking) streams
     grp = fa.FlowFVGroup(sps)
     grp.compute_residual_device([d.data_ptr() for d in dus], [d.data_ptr() for d in drs],
                                 [d.data_ptr() for d in dts], True, True)
@@ -213,6 +214,7 @@ def test_halo_ready_residual_bitwise():
         dus.append(x)
         drs.append(torch.zeros((sp.nown, 4), dtype=torch.float64, device="cuda"))
         dts.append(torch.zeros(sp.nown, dtype=torch.float64, device="cuda"))
+    torch.cuda.synchronize()  # torch's stream vs the library's (non-blocking) streams
     grp = fa.FlowFVGroup(sps)
     grp.compute_residual_device([x.data_ptr() for x in dus], [x.data_ptr() for x in drs],
                                 [x.data_ptr() for x in dts], True, True)
@@ -220,6 +222,7 @@ def test_halo_ready_residual_bitwise():
     for k, sp in enumerate(sps):
         r2 = torch.zeros_like(drs[k])
         t2 = torch.zeros_like(dts[k])
+        torch.cuda.synchronize()
         sp.compute_residual_device(dus[k].data_ptr(), r2.data_ptr(), t2.data_ptr(), True, True, halo_ready=True)
         sp.synchronize()
         assert torch.equal(r2, drs[k]) and torch.equal(t2, dts[k]), k

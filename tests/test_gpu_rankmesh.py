@@ -60,6 +60,7 @@ def run_ranks(kind, flux, grad, rec, order2, nranks, part=None):
         dus.append(du)
         drs.append(torch.full((lm.nelem, 4), float("nan"), dtype=torch.float64, device="cuda"))
         dts.append(torch.full((lm.nelem,), float("nan"), dtype=torch.float64, device="cuda"))
+    torch.cuda.synchronize()  # torch's stream vs the library's (non-blocking) streams
     grp = fa.FlowFVGroup(sps)
     grp.compute_residual_device([x.data_ptr() for x in dus], [x.data_ptr() for x in drs],
                                 [x.data_ptr() for x in dts], True, True)

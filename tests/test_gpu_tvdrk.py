@@ -113,6 +113,7 @@ def test_tvdrk_partitioned_bitwise():
         d = torch.full((sp.nown + sp.nghost, 4), float("nan"), dtype=torch.float64, device="cuda")
         d[:sp.nown] = torch.tensor(u0[g], device="cuda")
         dus.append(d)
+    torch.cuda.synchronize()  # torch's stream vs the library's (non-blocking) streams
     grp = fa.FlowFVGroup(sps)
     s, t = grp.tvdrk_device([d.data_ptr() for d in dus], 3, 0.4, 1e9, 4)
     u = np.full_like(u0, np.nan)
@@ -149,6 +150,7 @@ def test_tvdrk_nan_in_some_cells_diverges():
         d = torch.zeros((sp.nown + sp.nghost, 4), dtype=torch.float64, device="cuda")
         d[:sp.nown] = torch.tensor(u0[g], device="cuda")
         dus.append(d)
+    torch.cuda.synchronize()  # torch's stream vs the library's (non-blocking) streams
     grp = fa.FlowFVGroup(sps)
     with pytest.raises(RuntimeError, match="dtmin is Nan or inf"):
         grp.tvdrk_device([d.data_ptr() for d in dus], 3, 0.4, 1e9, 4)

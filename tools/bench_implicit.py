@@ -114,6 +114,7 @@ def implicit_steps(mesh, case="naca", steps=5, warmup=2, init_steps=10, cfl=25.0
     # -> 3.8e-7 in 5 steps at CFL 25), where the second-order steps that follow are still in the start-up
     # transient (the residual rises for hundreds of steps while the shock forms, profiles/r04/)
     dw = torch.tensor(u0, dtype=torch.float64, device="cuda")
+    torch.cuda.synchronize()
     sp1.steady_backward_euler_device(dw.data_ptr(), fa.ImplicitConfig(cflinit=c0, cflfin=c1, tol=0.0, maxiter=1, **lin))
     del dw                                                       # warm-up: allocations, clocks
     dinit = torch.tensor(u0, dtype=torch.float64, device="cuda")
@@ -136,6 +137,7 @@ def implicit_steps(mesh, case="naca", steps=5, warmup=2, init_steps=10, cfl=25.0
     sp1.close()
     for mf in operators:
         du = dinit.clone()
+        torch.cuda.synchronize()  # torch's stream vs the library's (non-blocking) streams
         cfg = fa.ImplicitConfig(cflinit=cfl, cflfin=cfl, tol=0.0, maxiter=warmup, matrix_free=mf, **lin)
         sp.steady_backward_euler_device(du.data_ptr(), cfg)      # warm-up: allocations, clocks
         du = dinit.clone()

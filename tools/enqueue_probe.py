@@ -69,6 +69,7 @@ def main():
         sb = torch.zeros((max(tot, 1), 4), dtype=torch.float64, device="cuda")
         rb = torch.zeros((max(tot, 1), 4), dtype=torch.float64, device="cuda")
         out = np.zeros(6)
+        torch.cuda.synchronize()  # torch's stream vs the library's (non-blocking) streams
         rc = lib.enq_probe(sp._h, ctypes.c_void_p(du.data_ptr()), ctypes.c_void_p(dr.data_ptr()),
                            ctypes.c_void_p(dt.data_ptr()), int(len(counts)),
                            counts.ctypes.data_as(ctypes.POINTER(ctypes.c_int)), ctypes.c_void_p(sb.data_ptr()),

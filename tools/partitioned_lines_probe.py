@@ -74,6 +74,7 @@ def main():
                 d = torch.zeros((s_.nown + s_.nghost, 4), dtype=torch.float64, device="cuda")
                 d[:s_.nown] = torch.tensor(u0[g], device="cuda")
                 dus.append(d)
+            torch.cuda.synchronize()  # torch's stream vs the library's (non-blocking) streams
             grp = fa.FlowFVGroup(sps)
             t0 = time.perf_counter()
             st, hist = grp.steady_backward_euler_device([d.data_ptr() for d in dus], cfg)

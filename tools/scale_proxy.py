@@ -84,6 +84,7 @@ def main():
             dus.append(x)
             drs.append(torch.empty((sp.nown, 4), dtype=torch.float64, device="cuda"))
             dts.append(torch.empty(sp.nown, dtype=torch.float64, device="cuda"))
+        torch.cuda.synchronize()  # torch's stream vs the library's (non-blocking) streams
         grp = fa.FlowFVGroup(sps)
         grp.compute_residual_device([x.data_ptr() for x in dus], [x.data_ptr() for x in drs],
                                     [x.data_ptr() for x in dts], True, True)     # fills the ghost rows
