@@ -171,7 +171,11 @@ struct fvhip_ctx
 	// time it runs with given arguments, replayed afterwards as one hipGraphLaunch
 	bool graph_res = false;
 	hipGraphExec_t rg_exec = nullptr;
-	struct RgKey { const double* u; double* r; double* dtm; bool dt, overwrite; } rg_key{};
+	struct RgKey {
+		const double* u; double* r; double* dtm; bool dt, overwrite;
+		bool operator==(const RgKey& o) const { return u == o.u && r == o.r && dtm == o.dtm && dt == o.dt && overwrite == o.overwrite; }
+	} rg_key{}, rg_seen{};
+	bool rg_seen_valid = false;
 	int rg_captures = 0, rg_replays = 0;
 	// profiling
 	bool prof = false;
@@ -513,9 +517,18 @@ struct fvhip_ctx
 		// ghost gradients and both fused launches are enqueued once (~26 us of host work per C4/8 rank
 		// step, tools/enqueue_probe.py) and replayed by one hipGraphLaunch while the arguments repeat
 		const RgKey key{u, r, dtm, dt, overwrite};
-		if(!rg_exec || key.u != rg_key.u || key.r != rg_key.r || key.dtm != rg_key.dtm || key.dt != rg_key.dt ||
-		   key.overwrite != rg_key.overwrite) {
+		if(!rg_exec || !(key == rg_key)) {
+			// a step with new arguments runs uncaptured once first: RCCL connects to its peers on the
+			// first send/receive (host-side set-up that must not happen inside a capture) and the
+			// launchers configure their kernels; the next call with the same arguments is captured
+			if(!(rg_seen_valid && key == rg_seen)) {
+				rg_seen = key;
+				rg_seen_valid = true;
+				residual_fused_overlapped_enqueue(u, r, dt, dtm, overwrite);
+				return;
+			}
 			if(rg_exec) { HC(hipGraphExecDestroy(rg_exec)); rg_exec = nullptr; }
+			HC(hipStreamSynchronize(stream));      // nothing of the uncaptured steps left in flight
 			ensureOverlap();
 			hipGraph_t g = nullptr;
 			HC(hipStreamBeginCapture(stream, hipStreamCaptureModeRelaxed));

@@ -201,6 +201,7 @@ int fvhip_set_residual_graph(fvhip_handle h, int enable, int* captures, int* rep
 		if(enable >= 0) {
 			h->graph_res = enable != 0;
 			if(!h->graph_res && h->rg_exec) { HC(hipSetDevice(h->device)); HC(hipGraphExecDestroy(h->rg_exec)); h->rg_exec = nullptr; }
+			if(!h->graph_res) h->rg_seen_valid = false;
 		}
 		if(captures) *captures = h->rg_captures;
 		if(replays) *replays = h->rg_replays;

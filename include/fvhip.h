@@ -130,8 +130,9 @@ int fvhip_create(const fvhip_mesh* mesh, const fvhip_flow_config* cfg, int devic
 int fvhip_set_rank(fvhip_handle h, int rank, int nranks);
 /** Partitioned handle on an RCCL communicator: enable = 1 captures its overlapped residual step (the
  *  halo exchange's pack and ncclSend/ncclRecv group, the ghost gradients, the interior and border fused
- *  launches with their stream/event joins) in a hipGraph the first time it runs with a given (u, r, dtm,
- *  time-step, overwrite) and replays it with one hipGraphLaunch while those repeat (every residual of
+ *  launches with their stream/event joins) in a hipGraph the second time it runs with a given (u, r, dtm,
+ *  time-step, overwrite) -- the first runs uncaptured (RCCL's peer connections, kernel set-up) -- and
+ *  replays it with one hipGraphLaunch while those repeat (every residual of
  *  the drivers and of a caller's loop on fixed buffers); 0 turns it off (default), -1 only queries.
  *  *captures / *replays (may be NULL): graphs built and launched so far. Not a reference option: the
  *  reference's MPI step has no counterpart (host enqueue of the step: tools/enqueue_probe.py). */
