@@ -13,7 +13,7 @@ run() {  # name timeout cmd...
   local rc=$?
   echo "rc=$rc"; tail -c 600 "$OUT/$name.log"; echo
   if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then echo "stopping after $name"; exit $rc; fi
-  if grep -q "returncode: -11\|(-11)\|(-6)\|(139)\|(134)" "$OUT/$name.log"; then echo "a child crashed in $name: stopping"; exit 3; fi
+  if grep -q "returncode: -11\|(-11)\|(-6)\|(139)\|(134)" "$OUT/$name.log"; then echo "a child crashed in $name: stopping"; exit 7; fi
 }
 PYT="python3 -u -m pytest -v --timeout 600 --timeout-method thread -s"
 run rccl_ranks 400 $PYT tests/test_gpu_rccl_ranks.py::test_rccl_ranks_on_one_gpu

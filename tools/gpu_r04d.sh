@@ -12,7 +12,7 @@ run() {  # name timeout cmd...
   local rc=$?
   echo "rc=$rc"; tail -c 700 "$OUT/$name.log"; echo
   if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then echo "stopping after $name"; exit $rc; fi
-  if grep -q "returncode: -11\|(-11)\|(-6)\|(139)\|(134)" "$OUT/$name.log"; then echo "a child crashed in $name: stopping"; exit 3; fi
+  if grep -q "returncode: -11\|(-11)\|(-6)\|(139)\|(134)" "$OUT/$name.log"; then echo "a child crashed in $name: stopping"; exit 7; fi
 }
 run rccl_ranks 400 python3 -u -m pytest -v --timeout 300 --timeout-method thread -s tests/test_gpu_rccl_ranks.py::test_rccl_ranks_on_one_gpu
 run suite 900 python3 -u -m pytest tests -m gpu -q -rf --timeout 300 --timeout-method thread -k "not graph_on_one_gpu and not rccl_ranks_on_one_gpu"
