@@ -291,14 +291,17 @@ def free_port():
         return s.getsockname()[1]
 
 
-def rank_launch_plan(n, argv, port=None):
+def rank_launch_plan(n, argv, port=None, rehearse=False):
     """the N child processes of `bench.py --gpus N` started without a torchrun environment: one rank per
     GPU, this script with the same arguments, the torch.distributed env:// variables set (rendezvous on
     127.0.0.1). Returns a list of (command, env additions)."""
     port = int(os.environ.get("MASTER_PORT") or 0) or port or free_port()
     cmd = [sys.executable, "-u", os.path.abspath(__file__)] + list(argv)
+    # rehearsal on one GPU: RCCL refuses two ranks on one device unless each rank reports its own host
+    extra = (lambda r: {"NCCL_HOSTID": "fvhip-rehearsal-%d" % r, "NCCL_SOCKET_IFNAME": "lo", "NCCL_IB_DISABLE": "1"}) \
+        if rehearse else (lambda r: {})
     return [(cmd, {"RANK": str(r), "LOCAL_RANK": str(r), "WORLD_SIZE": str(n), "LOCAL_WORLD_SIZE": str(n),
-                   "GROUP_RANK": "0", "MASTER_ADDR": "127.0.0.1", "MASTER_PORT": str(port)})
+                   "GROUP_RANK": "0", "MASTER_ADDR": "127.0.0.1", "MASTER_PORT": str(port), **extra(r)})
             for r in range(n)]
 
 
@@ -359,6 +362,9 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--launch-timeout", type=float, default=1500.0,
                     help="--gpus N without torchrun: wall-clock limit for the N ranks this script starts")
+    ap.add_argument("--rehearse-one-gpu", action="store_true",
+                    help="testing only: every rank on GPU 0, RCCL over its socket transport (NCCL_HOSTID per rank); "
+                         "checks the N-rank code path on a one-GPU box, its times mean nothing")
     ap.add_argument("--launch-dry-run", action="store_true",
                     help="print the rank processes --gpus N would start (commands, environment) and exit")
     ap.add_argument("--steps", type=int, default=200)
@@ -395,7 +401,7 @@ def main():
                  % (env_world, args.gpus))
     if env_world is None and (args.gpus > 1 or args.launch_dry_run):
         argv = [a for a in sys.argv[1:] if a != "--launch-dry-run"]
-        plan = rank_launch_plan(args.gpus, argv) if args.gpus > 1 else []
+        plan = rank_launch_plan(args.gpus, argv, rehearse=args.rehearse_one_gpu) if args.gpus > 1 else []
         if args.launch_dry_run:
             print(json.dumps({"ranks": [{"cmd": c, "env": e} for c, e in plan],
                               "in_process": args.gpus == 1, "watchdog_s": args.launch_timeout}))
@@ -411,7 +417,7 @@ def main():
     import torch
     if world > 1:
         import torch.distributed as dist
-        torch.cuda.set_device(local_rank)
+        torch.cuda.set_device(0 if args.rehearse_one_gpu else local_rank)
         dist.init_process_group("nccl", init_method="env://")
     else:
         dist = None
@@ -463,7 +469,7 @@ def main():
         torch.cuda.synchronize()
         sp.synchronize()
 
-    def measure(fast, path="default", preheat_ms=0.0, graph=False):
+    def measure(fast, path="default", preheat_ms=0.0):
         """ms per step (timed region bracketed by barrier + sync, max over ranks) and per-kernel ms;
         preheat_ms: after the warm-up steps, further untimed steps for that long (all ranks run the
         same count), outside the timed region"""
@@ -471,8 +477,6 @@ def main():
         if world > 1:
             sp = fa.FlowFV(mesh, p, n, device=torch.cuda.current_device(), partition=part, rank=rank)
             sp.comm_init(world, rank, new_uid())
-            if graph:
-                sp.set_residual_graph(True)
             owned = np.nonzero(part == rank)[0]
         else:
             sp = fa.FlowFV(mesh, p, n, device=torch.cuda.current_device())
@@ -572,16 +576,6 @@ def main():
                      "kernels_ms_summed_over_chunks": {k: round(v, 5) for k, v in pk.items()},
                      "hbm_GBs_both_kernels": round((sweep_algorithmic_bytes(*cnt) + prep_algorithmic_bytes(*cnt))
                                                    / (pms * 1e-3) / 1e9, 1)}
-    # N GPUs: the same step captured in a hipGraph (fvhip_set_residual_graph: pack, RCCL group, ghost
-    # gradients and both fused launches replayed by one hipGraphLaunch)
-    graph_path = None
-    if world > 1:
-        try:
-            gms, gk, _ = measure(False, preheat_ms=args.preheat_ms, graph=True)
-            graph_path = {"ms_per_step": round(gms, 5), "value": round(F / (gms * 1e-3) / 1e6, 3),
-                          "kernels_ms": {k: round(v, 5) for k, v in gk.items()}}
-        except Exception as e:          # report, do not lose the measurement
-            graph_path = {"error": str(e)}
     # the primary measurement: the library's default path for this configuration, after a wall-clock
     # pre-heat (untimed, reported): layout set-up between the secondary measurements leaves the GPU
     # idle for ~1 s, and a 20-step timed region (~6 ms) would otherwise run while the clocks ramp
@@ -687,7 +681,9 @@ def main():
                        "parallelism": (f"dp{world}: {args.partitioner} {world}-way partition, two-layer halo, one RCCL "
                                        f"p2p exchange of u per residual"
                                        if world > 1 else "single GPU"),
-                       "layout": stats, "setup_s": round(t_setup, 2)},
+                       "layout": stats, "setup_s": round(t_setup, 2),
+                       **({"rehearsal_one_gpu": "all ranks on GPU 0, RCCL over sockets: times are not a measurement"}
+                          if args.rehearse_one_gpu else {})},
             "preheat": {**preheat, "note": "untimed steps of the primary path after its warm-up, outside the "
                                            "timed region (--preheat-ms)"},
             "roofline": {"bound": cb["bound"] if cb else None,
@@ -715,7 +711,6 @@ def main():
             "fast_math": fast,
             "staged_path": staged,
             "pipelined_path": pipelined,
-            "graph_path": graph_path,
             "implicit_step": implicit,
             "recorded": recorded,
             "build": fa._ffi.build_info(),

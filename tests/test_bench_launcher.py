@@ -36,6 +36,17 @@ def test_dry_run_lists_n_ranks():
         assert r["cmd"][3:] == ["--gpus", "4", "--steps", "7"]
 
 
+def test_dry_run_rehearsal_sets_host_ids():
+    out = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "3", "--rehearse-one-gpu",
+                          "--launch-dry-run"], env=_env_without_dist(), capture_output=True, text=True, timeout=120)
+    assert out.returncode == 0, out.stderr
+    ranks = json.loads(out.stdout.strip().splitlines()[-1])["ranks"]
+    assert [r["env"]["NCCL_HOSTID"] for r in ranks] == ["fvhip-rehearsal-%d" % i for i in range(3)]
+    assert all(r["env"]["NCCL_SOCKET_IFNAME"] == "lo" for r in ranks)
+    plain = bench.rank_launch_plan(3, [], port=29500)
+    assert all("NCCL_HOSTID" not in e for _, e in plain)
+
+
 def test_dry_run_one_gpu_runs_in_process():
     out = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "1", "--launch-dry-run"],
                          env=_env_without_dist(), capture_output=True, text=True, timeout=120)

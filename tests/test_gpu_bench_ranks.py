@@ -1,0 +1,38 @@
+"""bench.py's N-rank path end to end on ONE GPU (--rehearse-one-gpu): `python bench.py --gpus 2` starts
+its two ranks itself (no torchrun), each on GPU 0 with its own NCCL_HOSTID so RCCL (the library's
+communicator and torch's) runs over its socket transport. What the driver's multi-GPU run executes runs
+here: the partition, the library's RCCL communicator, the overlapped halo residual, halo_parity (every
+rank's owned rows bitwise against the one-GPU residual), the N-rank implicit step, the max-over-ranks
+timing and rank 0's one JSON line. The times mean nothing (one shared GPU, sockets)."""
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def test_bench_two_ranks_on_one_gpu():
+    env = dict(os.environ)
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT"):
+        env.pop(k, None)
+    out = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--rehearse-one-gpu",
+                          "--scale", "4", "--steps", "5", "--warmup", "2", "--no-cpu-baseline", "--no-fast",
+                          "--preheat-ms", "20", "--launch-timeout", "400"],
+                         env=env, capture_output=True, text=True, timeout=450)
+    assert out.returncode == 0, out.stderr[-3000:]
+    lines = [l for l in out.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, out.stdout[-2000:]
+    d = json.loads(lines[0])
+    print(json.dumps({k: d[k] for k in ("n_gpus", "value", "ms_per_step", "halo_parity")}),
+          json.dumps(d["implicit_step"])[:600])
+    assert d["n_gpus"] == 2 and d["config"]["rehearsal_one_gpu"]
+    assert d["halo_parity"] is True, d["multi_gpu"]
+    assert d["multi_gpu"]["layout_per_rank"][0]["neighbours"] == 1
+    im = d["implicit_step"]
+    assert "error" not in im and im["ranks"] == 2 and im["steps"] == 3, im
+    assert im["first_order_start"]["resratio"] < 1.0
