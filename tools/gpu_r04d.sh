@@ -1,5 +1,5 @@
 #!/bin/bash
-# round-4 call d: multi-rank RCCL test, the whole GPU suite, smoke; the hipGraph RCCL test last.
+# round-4 call d: multi-rank RCCL test, the whole GPU suite (2-rank bench rehearsal included), smoke.
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
@@ -15,7 +15,6 @@ run() {  # name timeout cmd...
   if grep -q "returncode: -11\|(-11)\|(-6)\|(139)\|(134)" "$OUT/$name.log"; then echo "a child crashed in $name: stopping"; exit 7; fi
 }
 run rccl_ranks 400 python3 -u -m pytest -v --timeout 300 --timeout-method thread -s tests/test_gpu_rccl_ranks.py::test_rccl_ranks_on_one_gpu
-run suite 900 python3 -u -m pytest tests -m gpu -q -rf --timeout 300 --timeout-method thread -k "not graph_on_one_gpu and not rccl_ranks_on_one_gpu"
+run suite 900 python3 -u -m pytest tests -m gpu -q -rf --timeout 450 --timeout-method thread -k "not rccl_ranks_on_one_gpu"
 run smoke 300 python3 -u -c "import __graft_entry__ as g; g.smoke()"
-run rccl_graph 300 python3 -u -m pytest -v --timeout 250 --timeout-method thread -s tests/test_gpu_rccl_ranks.py::test_rccl_ranks_graph_on_one_gpu
 echo done
