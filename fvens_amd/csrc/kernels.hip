@@ -1072,7 +1072,9 @@ __device__ __forceinline__ void fused_wls_row(const DevMesh& M, const DevPhys& P
 		g[iv*2+0] = V.x*f[iv*2+0] + V.y*f[iv*2+1];
 		g[iv*2+1] = V.z*f[iv*2+0] + V.w*f[iv*2+1];
 	}
+#ifndef FVHIP_PROBE_NOLIM
 	if(LIM) fused_limit_row<LIM, W>(M, P, B, fz, row, c, nb4, gp, eps2, g);
+#endif
 	st8(row + 4, 0, g);
 	fz_row_temperature<W>(P.gas, row, g);
 }
@@ -1431,8 +1433,10 @@ __device__ __forceinline__ void fz_body(const DevMesh& M, const DevPhys& P, cons
 #if !FVHIP_FZ_VGEO
 			const double4 vg = make_double4(ri.x, ri.y, rr.x, rr.y);    // the two centres
 #endif
-			double vf[4];
+			double vf[4] = {0, 0, 0, 0};
+#ifndef FVHIP_PROBE_NOVISC
 			fz_viscous(G, rowi, rowj, gpr, vg, n, muRe, va, vf);
+#endif
 			#pragma unroll
 			for(int k = 0; k < 4; k++) f[k] += vf[k]*flen;
 		}
