@@ -10,7 +10,8 @@ those of the one-GPU-per-rank run. torch.distributed (gloo) only rendezvouses th
 RCCL unique id and the results; the single-GPU reference results are computed by every rank itself.
 
 usage (set by the test): RANK, WORLD_SIZE, MASTER_ADDR, MASTER_PORT, NCCL_HOSTID in the environment;
-argv: <out.json> <mesh key> <partitioner> [graph]  (graph: the hipGraph sections only)
+argv: <out.json> <mesh key> <partitioner> [graph | numerics]  (graph: the hipGraph sections only;
+numerics: "visc" = laminar Roe + WLS + Van Albada + Sutherland, "venkat" = Roe + WLS + Venkatakrishnan)
 """
 import json
 import os
@@ -25,7 +26,8 @@ sys.path.insert(0, HERE)
 
 def main():
     out_path, meshkey, partitioner = sys.argv[1], sys.argv[2], sys.argv[3]
-    graph = len(sys.argv) > 4 and sys.argv[4] == "graph"
+    mode = sys.argv[4] if len(sys.argv) > 4 else ""
+    graph = mode == "graph"
 
     def mark(msg):
         print("[rank %s] %s" % (os.environ["RANK"], msg), flush=True)
@@ -39,8 +41,8 @@ def main():
     from test_gpu_residual import get_mesh
 
     m, _ = get_mesh(meshkey)
-    p = cases.physics("naca")
-    n = cases.numerics("ROE", "LEASTSQUARES", "VANALBADA")
+    p = cases.physics("visc" if mode == "visc" else "naca")
+    n = cases.numerics("ROE", "LEASTSQUARES", "VENKATAKRISHNAN" if mode == "venkat" else "VANALBADA")
     part = fa.partition_graph(m, world, weights="cost") if partitioner == "graph" else fa.partition_rcb(m, world)
 
     def uid():

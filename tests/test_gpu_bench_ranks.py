@@ -16,13 +16,14 @@ pytestmark = pytest.mark.gpu
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
-def test_bench_two_ranks_on_one_gpu():
+@pytest.mark.parametrize("numerics", ["headline", "config5"])
+def test_bench_two_ranks_on_one_gpu(numerics):
     env = dict(os.environ)
     for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT"):
         env.pop(k, None)
     out = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--rehearse-one-gpu",
                           "--scale", "4", "--steps", "5", "--warmup", "2", "--no-cpu-baseline", "--no-fast",
-                          "--preheat-ms", "20", "--launch-timeout", "400"],
+                          "--preheat-ms", "20", "--launch-timeout", "400", "--numerics", numerics],
                          env=env, capture_output=True, text=True, timeout=450)
     assert out.returncode == 0, out.stderr[-3000:]
     lines = [l for l in out.stdout.splitlines() if l.startswith("{")]

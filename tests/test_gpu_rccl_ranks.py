@@ -59,9 +59,14 @@ def _run_ranks(tmp_path, world, meshkey, partitioner, mode=""):
     return reps
 
 
-@pytest.mark.parametrize("world,meshkey,partitioner", [(2, "naca_small", "graph"), (4, "naca_small", "rcb")])
-def test_rccl_ranks_on_one_gpu(tmp_path, world, meshkey, partitioner):
-    for rep in _run_ranks(tmp_path, world, meshkey, partitioner):
+@pytest.mark.parametrize("world,meshkey,partitioner,numerics", [(2, "naca_small", "graph", ""), (4, "naca_small", "rcb", ""),
+                                                              (3, "naca_small", "graph", "visc"),
+                                                              (3, "naca_small", "graph", "venkat")])
+def test_rccl_ranks_on_one_gpu(tmp_path, world, meshkey, partitioner, numerics):
+    """the headline numerics on 2 and 4 ranks; BASELINE config 5's (laminar, Sutherland: the fused viscous
+    kernel on the two-layer halo) and config 4's (Venkatakrishnan: the layer-1 ghosts' limiter values
+    formed locally) on 3 ranks"""
+    for rep in _run_ranks(tmp_path, world, meshkey, partitioner, numerics):
         assert rep["layout"]["neighbours"] > 0 and rep["layout"]["ghosts"] > 0
         assert rep["residual_mismatched_rows"] == 0, rep
         for key in ("implicit_pbj", "implicit_lines"):
