@@ -32,3 +32,15 @@ def test_fixture_mesh_layout():
     st = _probe(m)
     assert st["cells"] == m.nelem
     assert st["patches"] >= (m.naface + st["slots_per_patch"] - 1) // st["slots_per_patch"]
+
+
+def test_fused_row_caps_fit_the_lds_budget():
+    """the staged rows per patch fit the LDS each fused instantiation is launched with: inviscid
+    unlimited 14-double rows x 284 (five blocks of 31.8 KB per CU), viscous 18-double rows x 284 (the
+    per-row temperature terms: four blocks of 40.9 KB), limited 14-double rows x 352 (four of 39.4 KB)"""
+    m = fa.UMesh.naca_ogrid(512, 32, 96, 20.0, 1e-5)
+    for kind, rec, rows, width, blocks in (("naca", "VANALBADA", 284, 14, 5), ("visc", "VANALBADA", 284, 18, 4),
+                                           ("naca", "VENKATAKRISHNAN", 352, 14, 4)):
+        st = _probe(m, kind, rec)
+        assert 0 < st["max_staged_cells"] <= rows, (kind, rec, st)
+        assert blocks * rows * width * 8 <= 160 * 1024
