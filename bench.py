@@ -97,7 +97,7 @@ def kernel_bytes(label, N, F, Fb, numerics="headline"):
     for the one-launch residual and for the staged sweep -- they perform the same operation; the
     one-launch kernel's own compulsory traffic is lower (residual_algorithmic_bytes: gradients stay
     in LDS), which is why it is faster, not a different amount of algorithmic work"""
-    if numerics == "config4":
+    if numerics in ("config3", "config4"):
         return config4_algorithmic_bytes(N, F, Fb)
     return sweep_algorithmic_bytes(N, F, Fb)
 
@@ -106,9 +106,11 @@ def kernel_symbol(label, numerics="headline"):
     """profiling label -> rocprofv3 kernel symbol suffix of the Roe/MUSCL/dt (headline), Roe/linear/
     Venkatakrishnan/dt (config4) or Roe/MUSCL/Sutherland/dt (config5) instantiation"""
     if label.startswith("k_residual_wls"):
-        return {"headline": "k_residual_wls<4, 1, true, 0, 0>", "config4": "k_residual_wls<4, 2, true, 0, 2>",
+        return {"headline": "k_residual_wls<4, 1, true, 0, 0>", "config2": "k_residual_wls<4, 1, true, 0, 0>",
+                "config3": "k_residual_wls<6, 2, true, 1, 0>", "config4": "k_residual_wls<4, 2, true, 0, 2>",
                 "config5": "k_residual_wls<4, 1, true, 1, 0>"}[numerics]
-    return {"headline": "k_sweep<4, 1, 0, true, false>", "config4": "k_sweep<4, 2, 0, true, true>",
+    return {"headline": "k_sweep<4, 1, 0, true, false>", "config2": "k_sweep<4, 1, 0, true, false>",
+            "config3": "k_sweep<6, 2, 1, true, false>", "config4": "k_sweep<4, 2, 0, true, true>",
             "config5": "k_sweep<4, 1, 1, true, false>"}[numerics]
 
 
@@ -194,7 +196,7 @@ def host_cpu_info():
             "affinity_cpus": aff, "cgroup_cpu_quota": quota, "physical_cores_used": cores}
 
 
-def cpu_baseline(mesh, u, nrep, rec="VANALBADA", kind="naca"):
+def cpu_baseline(mesh, u, nrep, rec="VANALBADA", kind="naca", flux="ROE"):
     """BASELINE.md's CPU baseline: the oracle's OpenMP restatement (the reference's omp parallel for /
     omp atomic structure) on this host's physical cores, in a child process so that OMP_PROC_BIND /
     OMP_PLACES take effect (torch has already loaded the OpenMP runtime here); median of `nrep` sweeps
@@ -212,7 +214,7 @@ def cpu_baseline(mesh, u, nrep, rec="VANALBADA", kind="naca"):
         for threads, reps in ((nt, nrep), (1, max(3, nrep // 4))):
             env = dict(os.environ, OMP_NUM_THREADS=str(threads), OMP_PROC_BIND="close", OMP_PLACES="cores")
             out = subprocess.run([sys.executable, os.path.abspath(__file__), "--cpu-child", path, str(threads),
-                                  str(reps), rec, kind], env=env, capture_output=True, text=True, timeout=900)
+                                  str(reps), rec, kind, flux], env=env, capture_output=True, text=True, timeout=900)
             if out.returncode != 0:
                 raise RuntimeError("cpu baseline child failed: " + out.stderr[-2000:])
             res[threads] = json.loads(out.stdout.strip().splitlines()[-1])
@@ -229,14 +231,14 @@ def cpu_baseline(mesh, u, nrep, rec="VANALBADA", kind="naca"):
                       f"{med_1:.3f} s"}
 
 
-def cpu_child(path, threads, nrep, rec="VANALBADA", kind="naca"):
+def cpu_child(path, threads, nrep, rec="VANALBADA", kind="naca", flux="ROE"):
     """child of cpu_baseline: builds the oracle from the saved mesh and times it (prints one JSON line)"""
     import _oracle as orc
     import cases
     d = np.load(path)
     raw = {k: (int(d[k]) if d[k].ndim == 0 else d[k]) for k in d.files if k != "u"}
     om = orc.OracleMesh.from_raw(raw)
-    ref = orc.OracleSpatial(om, cases.physics(kind), cases.numerics("ROE", "LEASTSQUARES", rec))
+    ref = orc.OracleSpatial(om, cases.physics(kind), cases.numerics(flux, "LEASTSQUARES", rec))
     med, times = ref.time_residual(np.ascontiguousarray(d["u"]), nrep, True, threads=threads, nwarm=3)
     print(json.dumps({"median_s": med, "nrep": nrep, "threads": threads, "min_s": float(times.min()),
                       "max_s": float(times.max())}))
@@ -384,9 +386,12 @@ def main():
     ap.add_argument("--preheat-ms", type=float, default=400.0,
                     help="untimed steps for this long (wall clock) after the warm-up steps of the primary path, "
                          "so the timed steps run at the clock the GPU holds under this load (reported)")
-    ap.add_argument("--numerics", choices=["headline", "config4", "config5"], default="headline",
+    ap.add_argument("--numerics", choices=["headline", "config2", "config3", "config4", "config5"], default="headline",
                     help="headline: Roe + WLS + MUSCL/Van Albada (north_star's sweep); config4: BASELINE config 4's "
-                         "Roe + WLS + Venkatakrishnan (K = 20); config5: BASELINE config 5, the laminar NACA0012 "
+                         "Roe + WLS + Venkatakrishnan (K = 20); config2: BASELINE config 2, the headline numerics on the "
+                         "~250k-cell member of the C4 family (C4 / 4); config3: BASELINE config 3, the laminar flat plate "
+                         "(1024 x 1024 quads, M 0.2, Re 8.7e5), HLLC + WLS + unlimited linear + Sutherland viscous flux, "
+                         "implicit figure matrix-free; config5: BASELINE config 5, the laminar NACA0012 "
                          "(M 0.5, Re 5000) on the 8.1M-cell C5 O-grid (C4 with 4096 cells around), Roe + WLS + "
                          "MUSCL/Van Albada + Sutherland viscous flux")
     args = ap.parse_args()
@@ -430,11 +435,17 @@ def main():
     mult = world if (world > 1 and args.scaling == "weak") else 1
     if args.numerics == "config5":
         mult *= 2
-    mesh, dims = c4_mesh(fa, args.scale, mult)
-    kind = "visc" if args.numerics == "config5" else "naca"
+    if args.numerics == "config3":       # BASELINE config 3: ~1M-cell laminar flat plate (tests/visc-flatplate)
+        nx = 1024 * mult // args.scale
+        ny = 1024 // args.scale
+        mesh, dims = fa.UMesh.flat_plate(nx, ny), dict(nx=nx, ny=ny)
+    else:
+        mesh, dims = c4_mesh(fa, args.scale * (4 if args.numerics == "config2" else 1), mult)
+    kind = {"config5": "visc", "config3": "plate"}.get(args.numerics, "naca")
     p = cases.physics(kind)
-    rec = "VENKATAKRISHNAN" if args.numerics == "config4" else "VANALBADA"
-    n = cases.numerics("ROE", "LEASTSQUARES", rec)
+    rec = {"config4": "VENKATAKRISHNAN", "config3": "NONE"}.get(args.numerics, "VANALBADA")
+    flux = "HLLC" if args.numerics == "config3" else "ROE"
+    n = cases.numerics(flux, "LEASTSQUARES", rec)
     u = cases.state(mesh, p, seed=42)
     N, F, Fb = mesh.nelem, mesh.naface, mesh.nbface
     part = None
@@ -621,8 +632,10 @@ def main():
                 return float(t.item())
             kw = dict(part=part, rank=rank, world=world, new_uid=new_uid, allmax=allmax)
         try:
-            implicit = next(implicit_steps(mesh, "visc-c5" if args.numerics == "config5" else "naca", steps=3, warmup=1,
-                                           sweeps=1, lines=True, operators=(False,), **IMPLICIT_START, **kw))
+            implicit = next(implicit_steps(mesh, {"config5": "visc-c5", "config3": "plate"}.get(args.numerics, "naca"),
+                                           steps=3, warmup=1, sweeps=1, lines=True,
+                                           operators=((True,) if args.numerics == "config3" else (False,)),
+                                           **IMPLICIT_START, **kw))
             implicit.pop("faces", None)
         except Exception as e:          # N GPUs: report, do not lose the residual measurement
             if world == 1:
@@ -631,7 +644,7 @@ def main():
     # recorded (NOT measured by this run): the committed full-size convergence runs of the same
     # device solver (~10 min each), kept apart from the measured figures
     recorded = None
-    if world == 1 and not args.no_implicit and args.numerics != "config5":
+    if world == 1 and not args.no_implicit and args.numerics in ("headline", "config4"):
         recorded = {"note": "read from committed profiles, not re-run here"}
         runs = (("c4_first_order_converged_bench_mesh.txt",
                  "first-order LLF, line-implicit preconditioner, GMRES(40), expResidualRamp CFL 5 -> 1000"),
@@ -650,7 +663,7 @@ def main():
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        cpu = cpu_baseline(mesh, u, args.cpu_sweeps, rec, kind)
+        cpu = cpu_baseline(mesh, u, args.cpu_sweeps, rec, kind, flux)
 
     if rank == 0:
         # template of the timed sweep: k_residual_wls<FLUX=ROE(4), REC=MUSCL(1), DT, VISC=none(0), LIM=0>
@@ -658,6 +671,10 @@ def main():
         tr = pmc_traffic("exact::" + kernel_symbol(sweep_name[0], args.numerics), N) if world == 1 else None
         cb = counter_bound(tr[3] if tr else None, sweep_ms)
         wl = {"headline": "C4 mesh, Roe + WLS gradients + MUSCL/Van Albada",
+              "config2": "C4 / 4 mesh (~254k cells, the ~250k-cell hybrid NACA0012), Roe + WLS gradients + "
+                         "MUSCL/Van Albada, BASELINE config 2's numerics",
+              "config3": "flat plate (1024 x 1024 quads), laminar M 0.2 Re 8.7e5, HLLC + WLS gradients + unlimited "
+                         "linear + Sutherland viscous flux, BASELINE config 3's numerics",
               "config4": "C4 mesh, Roe + WLS gradients + Venkatakrishnan (K = 20), BASELINE config 4's numerics",
               "config5": "C5 mesh (8.1M cells), laminar M 0.5 Re 5000, Roe + WLS gradients + MUSCL/Van Albada + "
                          "Sutherland viscous flux, BASELINE config 5's numerics"}[args.numerics]
@@ -674,7 +691,9 @@ def main():
             "scaling": args.scaling,
             "vs_baseline": None,
             "dtype": "f64",
-            "data": "synthetic (generated C4 NACA0012 hybrid O-grid; seeded perturbed free stream)",
+            "data": ("synthetic (generated structured flat-plate quad mesh; seeded perturbed free stream)"
+                     if args.numerics == "config3" else
+                     "synthetic (generated C4-family NACA0012 hybrid O-grid; seeded perturbed free stream)"),
             "config": {"workload": f"{wl}, 2nd-order residual sweep with local time steps "
                                    "(explicit pseudo-time step)",
                        "cells": N, "faces": F, "boundary_faces": Fb, **dims,
@@ -697,8 +716,9 @@ def main():
                          "kernel": sweep_name[0] if sweep_name else None,
                          "kernel_ms": round(sweep_ms, 5), "algorithmic_bytes": ab,
                          "bytes_basis": ("SURVEY.md 8(d) 32F + 144N + 48Fb (124.0 B/face) + 8N time step"
-                                         if args.numerics != "config4" else
-                                         "SURVEY.md 8(d) Roe + linear/Venkatakrishnan: 48F + 144N + 48Fb + 8N time step"),
+                                         if args.numerics not in ("config3", "config4") else
+                                         "SURVEY.md 8(d) linear reconstruction (config4: + Venkatakrishnan): "
+                                         "48F + 144N + 48Fb + 8N time step"),
                          "frac_area_dt_basis": round(sweep_bytes_area_dt(*cnt) / (sweep_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
                          "area_dt_basis": "same + 8N (time step as area read 8 + dtm write 8 = 16 B/cell)",
                          "compulsory_bytes_one_launch": residual_algorithmic_bytes(*cnt),
@@ -721,7 +741,7 @@ def main():
 
 
 if __name__ == "__main__":
-    if len(sys.argv) == 7 and sys.argv[1] == "--cpu-child":
-        cpu_child(sys.argv[2], int(sys.argv[3]), int(sys.argv[4]), sys.argv[5], sys.argv[6])
+    if len(sys.argv) == 8 and sys.argv[1] == "--cpu-child":
+        cpu_child(sys.argv[2], int(sys.argv[3]), int(sys.argv[4]), sys.argv[5], sys.argv[6], sys.argv[7])
     else:
         main()

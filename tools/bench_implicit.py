@@ -32,8 +32,8 @@ CASES = {   # physics, flux, gradients, reconstruction
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--case", default="naca", choices=sorted(CASES),
-                    help="naca: bench.py's C4 workload; naca-venkat: BASELINE config 3 numerics on it; "
-                         "plate: config 2, laminar flat plate, ~1M quads; visc-c5: config 5, laminar NACA0012, 8.1M cells")
+                    help="naca: bench.py's C4 workload; naca-venkat: BASELINE config 4 numerics on it; "
+                         "plate: config 3, laminar flat plate, ~1M quads; visc-c5: config 5, laminar NACA0012, 8.1M cells")
     ap.add_argument("--scale", type=int, default=1, help="divide the mesh dimensions by this")
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
