@@ -103,8 +103,9 @@ def kernel_bytes(label, N, F, Fb, numerics="headline"):
 
 
 def kernel_symbol(label, numerics="headline"):
-    """profiling label -> rocprofv3 kernel symbol suffix of the Roe/MUSCL/dt (headline), Roe/linear/
-    Venkatakrishnan/dt (config4) or Roe/MUSCL/Sutherland/dt (config5) instantiation"""
+    """profiling label -> rocprofv3 kernel symbol suffix of the Roe/MUSCL/dt (headline, config2), HLLC/linear/
+    Sutherland/dt (config3), Roe/linear/Venkatakrishnan/dt (config4) or Roe/MUSCL/Sutherland/dt (config5)
+    instantiation (template arguments: include/fvhip.h's flux codes, kernels.hpp's SweepRec / SweepVisc)"""
     if label.startswith("k_residual_wls"):
         return {"headline": "k_residual_wls<4, 1, true, 0, 0>", "config2": "k_residual_wls<4, 1, true, 0, 0>",
                 "config3": "k_residual_wls<6, 2, true, 1, 0>", "config4": "k_residual_wls<4, 2, true, 0, 2>",
@@ -116,13 +117,14 @@ def kernel_symbol(label, numerics="headline"):
 
 def pmc_traffic(kernel_symbol, workload_cells):
     """HBM bytes per launch of `kernel_symbol` from the newest committed rocprofv3 PMC summary
-    (profiles/r*/pmc_traffic.json; pmc_schemes.json / pmc_config5.json for the limited and viscous
+    (profiles/r*/pmc_traffic.json; pmc_schemes.json / pmc_config3.json / pmc_config5.json for the limited and viscous
     instantiations: FETCH_SIZE x2 + WRITE_SIZE, calibrated as MI355X_MICROARCH.md prescribes), if it was
     measured on the same workload; else None."""
     import glob
     best = None
     files = [f for r in sorted(glob.glob(os.path.join(ROOT, "profiles", "r*")))
-             for f in (os.path.join(r, n) for n in ("pmc_schemes.json", "pmc_config5.json", "pmc_traffic.json"))
+             for f in (os.path.join(r, n) for n in ("pmc_schemes.json", "pmc_config3.json", "pmc_config5.json",
+                                                            "pmc_traffic.json"))
              if os.path.exists(f)]
     for f in files:
         try:
