@@ -602,6 +602,15 @@ FVHIP_HD void viscous_face_terms(const Gas& G, const double* ul, const double* u
 	va[0] = 0.5*( div_rn(ul[1], ul[0]) + div_rn(ur[1], ur[0]) );
 	va[1] = 0.5*( div_rn(ul[2], ul[0]) + div_rn(ur[2], ur[0]) );
 }
+/// the same with the two face states' Sutherland viscosities already formed (mul = sutherland(G, ul),
+/// mur = sutherland(G, ur); ignored for constant viscosity)
+template <bool CONSTVISC>
+FVHIP_HD void viscous_face_terms_mu(const Gas& G, const double* ul, const double* ur, double mul, double mur,
+                                    double& muRe, double* va) {
+	muRe = CONSTVISC ? G.rReinf : 0.5*( mul + mur );
+	va[0] = 0.5*( div_rn(ul[1], ul[0]) + div_rn(ur[1], ur[0]) );
+	va[1] = 0.5*( div_rn(ul[2], ul[0]) + div_rn(ur[2], ur[0]) );
+}
 template <bool ORDER2>
 FVHIP_HD void viscous_flux_core(const Gas& G, const double* n, const double* rcl, const double* rcr,
                                 const double* pl, const double* pr, const double* gl, const double* grr,

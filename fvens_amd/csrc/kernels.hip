@@ -1400,6 +1400,13 @@ __device__ __forceinline__ void fz_body(const DevMesh& M, const DevPhys& P, cons
 			}
 		}
 		inviscid_flux_len<FLUX>(G, ul, ur, n, flen, f);
+		// Sutherland viscosities of the two face states: the time step's and the viscous flux's
+		// (viscous_face_terms forms the same two values), formed once
+		double mui = 0, muj = 0;
+		if(VISC != SV_NONE) {
+			mui = VISC == SV_CONST ? G.rReinf : sutherland(G, ul);
+			muj = VISC == SV_CONST ? G.rReinf : sutherland(G, ur);
+		}
 		if(DT) {
 			const double ci = sound_speed_cons(G, ul), cj = sound_speed_cons(G, ur);
 			const double vni = div_rn(dot2(&ul[1],n), ul[0]);
@@ -1407,8 +1414,6 @@ __device__ __forceinline__ void fz_body(const DevMesh& M, const DevPhys& P, cons
 			sri = (fabs(vni)+ci)*flen;
 			srj = (fabs(vnj)+cj)*flen;
 			if(VISC != SV_NONE) {
-				const double mui = VISC == SV_CONST ? G.rReinf : sutherland(G, ul);
-				const double muj = VISC == SV_CONST ? G.rReinf : sutherland(G, ur);
 				const double coi = visc_coef(G, ul[0]), coj = visc_coef(G, ur[0]);   // std::max(4/(3 rho), g/rho)
 				// a ghost cell's spectral radius is never summed (and its area is not stored)
 				const int2 g = M.slot_LR[s];
@@ -1424,7 +1429,7 @@ __device__ __forceinline__ void fz_body(const DevMesh& M, const DevPhys& P, cons
 			// used the face states too), and the fence makes the cell rows fresh LDS reads instead of
 			// the reconstruction's copies kept live through the inviscid flux -- 4 waves per SIMD
 			double muRe, va[2];
-			viscous_face_terms<VISC == SV_CONST>(G, ul, ur, muRe, va);
+			viscous_face_terms_mu<VISC == SV_CONST>(G, ul, ur, mui, muj, muRe, va);
 			double4 gpr = make_double4(0, 0, 0, 0);
 			const double* rowj = nullptr;
 			double2 rr;
