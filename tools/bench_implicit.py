@@ -47,6 +47,7 @@ def main():
     ap.add_argument("--lines", action="store_true", help="line-implicit preconditioner")
     ap.add_argument("--ilu", action="store_true", help="block ILU(0) in multicolour order")
     ap.add_argument("--operators", default="assembled,matrix-free")
+    ap.add_argument("--second-from", default="start", choices=["start", "freestream"])
     args = ap.parse_args()
 
     import torch
@@ -67,16 +68,21 @@ def main():
     for out in implicit_steps(mesh, args.case, steps=args.steps, warmup=args.warmup, init_steps=args.init_steps,
                               cfl=args.cfl, restart=args.restart, lin_maxit=args.lin_maxit, sweeps=args.sweeps,
                               single=args.prec_single, gs=args.gs, lines=args.lines, ilu=args.ilu,
-                              operators=tuple(o == "matrix-free" for o in args.operators.split(","))):
+                              operators=tuple(o == "matrix-free" for o in args.operators.split(",")),
+                              second_from=args.second_from):
         out["dims"] = dims
         print(json.dumps(out), flush=True)
 
 
 def implicit_steps(mesh, case="naca", steps=5, warmup=2, init_steps=10, cfl=25.0, restart=30, lin_maxit=30,
                    sweeps=4, single=False, gs=False, operators=(False, True), lines=False, ilu=False,
-                   init_cfl=None, part=None, rank=0, world=1, new_uid=None, allmax=None):
+                   init_cfl=None, part=None, rank=0, world=1, new_uid=None, allmax=None, second_from="start"):
     """time `steps` second-order backward-Euler steps per operator kind (False: assembled, True:
     matrix-free) after a first-order start; yields one dict per operator.
+    second_from: "start" -- the second-order steps continue from the first-order start's state (the
+    reference's two-stage schedule); "freestream" -- they start from the free stream themselves (the first
+    second-order steps of a cold start, where the residual still falls; the first-order start is timed
+    all the same)
     init_cfl: (cfl_min, cfl_max) of the first-order start's expResidualRamp (aodesolver.cpp:110-120,
     462; default: `cfl` held fixed). part/rank/world/new_uid: this rank's piece of a partition, its
     handles on the library's RCCL communicator (new_uid() -> a fresh unique id, the same on every rank);
@@ -135,12 +141,14 @@ def implicit_steps(mesh, case="naca", steps=5, warmup=2, init_steps=10, cfl=25.0
              "note": "the first-order start from the free stream (the reference's initialization solve): "
                      "residual + first-order Jacobian + GMRES + update per step, the residual falls"}
     sp1.close()
+    dfree = torch.tensor(u0, dtype=torch.float64, device="cuda")
+    dstart = dinit if second_from == "start" else dfree
     for mf in operators:
-        du = dinit.clone()
+        du = dstart.clone()
         torch.cuda.synchronize()  # torch's stream vs the library's (non-blocking) streams
         cfg = fa.ImplicitConfig(cflinit=cfl, cflfin=cfl, tol=0.0, maxiter=warmup, matrix_free=mf, **lin)
         sp.steady_backward_euler_device(du.data_ptr(), cfg)      # warm-up: allocations, clocks
-        du = dinit.clone()
+        du = dstart.clone()
         cfg.maxiter = steps
         torch.cuda.synchronize()
         if allmax:
@@ -160,6 +168,8 @@ def implicit_steps(mesh, case="naca", steps=5, warmup=2, init_steps=10, cfl=25.0
                "cells": mesh.nelem, "faces": mesh.naface, "ranks": world,
                "restart": restart, "prec_sweeps": sweeps, "prec_single": single, "prec_gs": gs, "prec_lines": lines,
                "prec_ilu": ilu, "cfl": cfl,
+               "second_order_from": ("the first-order start's state" if second_from == "start" else
+                                     "the free stream (a cold start's first second-order steps)"),
                "init": {"steps": st0["steps"], "resratio": st0["resratio"], "cfl_ramp": [c0, c1],
                         "final_cfl": st0["cfl"]},
                "first_order_start": first}

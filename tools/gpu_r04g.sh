@@ -18,6 +18,8 @@ run smoke 300 python3 -u -c "import __graft_entry__ as g; g.smoke()"
 run config3 400 python3 -u bench.py --numerics config3 --steps 100 --warmup 10
 run config2 300 python3 -u bench.py --numerics config2 --steps 100 --warmup 10
 run bench_driver 400 python3 -u bench.py --steps 20 --warmup 5
+run iprobe 300 python3 -u tools/implicit_probe.py --schedules "0:25:25:6:25:25,0:25:25:6:10:10,3:25:25:6:25:25"
+run bimp_free 300 python3 -u tools/bench_implicit.py --case naca --steps 3 --warmup 1 --init-steps 5 --sweeps 1 --lines --operators assembled --second-from freestream
 A3="--numerics config3 --steps 100 --warmup 10 --no-cpu-baseline --no-pipelined --no-implicit"
 run c3_trace 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/c3/trace -o run -- python3 bench.py $A3
 run c3_fetch 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $OUT/c3/fetch -o run -- python3 bench.py $A3
