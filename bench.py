@@ -390,8 +390,8 @@ def main():
                          "so the timed steps run at the clock the GPU holds under this load (reported)")
     ap.add_argument("--numerics", choices=["headline", "config2", "config3", "config4", "config5"], default="headline",
                     help="headline: Roe + WLS + MUSCL/Van Albada (north_star's sweep); config4: BASELINE config 4's "
-                         "Roe + WLS + Venkatakrishnan (K = 20); config2: BASELINE config 2, the headline numerics on the "
-                         "~250k-cell member of the C4 family (C4 / 4); config3: BASELINE config 3, the laminar flat plate "
+                         "Roe + WLS + Venkatakrishnan (K = 20); config2: BASELINE config 2, the headline numerics on "
+                         "SURVEY's C2 (229,376 cells); config3: BASELINE config 3, the laminar flat plate "
                          "(1024 x 1024 quads, M 0.2, Re 8.7e5), HLLC + WLS + unlimited linear + Sutherland viscous flux, "
                          "implicit figure matrix-free; config5: BASELINE config 5, the laminar NACA0012 "
                          "(M 0.5, Re 5000) on the 8.1M-cell C5 O-grid (C4 with 4096 cells around), Roe + WLS + "
@@ -441,8 +441,12 @@ def main():
         nx = 1024 * mult // args.scale
         ny = 1024 // args.scale
         mesh, dims = fa.UMesh.flat_plate(nx, ny), dict(nx=nx, ny=ny)
+    elif args.numerics == "config2":     # 229,376 cells (the mesh of test_gpu_residual's naca_c2)
+        nt, nq, ntri = 512 * mult // args.scale, 64 // args.scale, 192 // args.scale
+        mesh = fa.UMesh.naca_ogrid(nt, nq, ntri)
+        dims = dict(ntheta=nt, nquad=nq, ntri=ntri, wall_spacing=1e-4, farmap=0)
     else:
-        mesh, dims = c4_mesh(fa, args.scale * (4 if args.numerics == "config2" else 1), mult)
+        mesh, dims = c4_mesh(fa, args.scale, mult)
     kind = {"config5": "visc", "config3": "plate"}.get(args.numerics, "naca")
     p = cases.physics(kind)
     rec = {"config4": "VENKATAKRISHNAN", "config3": "NONE"}.get(args.numerics, "VANALBADA")
@@ -673,7 +677,7 @@ def main():
         tr = pmc_traffic("exact::" + kernel_symbol(sweep_name[0], args.numerics), N) if world == 1 else None
         cb = counter_bound(tr[3] if tr else None, sweep_ms)
         wl = {"headline": "C4 mesh, Roe + WLS gradients + MUSCL/Van Albada",
-              "config2": "C4 / 4 mesh (~254k cells, the ~250k-cell hybrid NACA0012), Roe + WLS gradients + "
+              "config2": "C2 mesh (SURVEY 8(d): 229,376-cell hybrid NACA0012 O-grid), Roe + WLS gradients + "
                          "MUSCL/Van Albada, BASELINE config 2's numerics",
               "config3": "flat plate (1024 x 1024 quads), laminar M 0.2 Re 8.7e5, HLLC + WLS gradients + unlimited "
                          "linear + Sutherland viscous flux, BASELINE config 3's numerics",
@@ -695,7 +699,7 @@ def main():
             "dtype": "f64",
             "data": ("synthetic (generated structured flat-plate quad mesh; seeded perturbed free stream)"
                      if args.numerics == "config3" else
-                     "synthetic (generated C4-family NACA0012 hybrid O-grid; seeded perturbed free stream)"),
+                     "synthetic (generated NACA0012 hybrid O-grid; seeded perturbed free stream)"),
             "config": {"workload": f"{wl}, 2nd-order residual sweep with local time steps "
                                    "(explicit pseudo-time step)",
                        "cells": N, "faces": F, "boundary_faces": Fb, **dims,
