@@ -37,3 +37,24 @@ def test_bench_two_ranks_on_one_gpu(numerics):
     im = d["implicit_step"]
     assert "error" not in im and im["ranks"] == 2 and im["steps"] == 3, im
     assert im["first_order_start"]["resratio"] < 1.0
+
+
+@pytest.mark.parametrize("numerics,flux,operator", [("config2", "ROE", "assembled"), ("config3", "HLLC", "matrix-free")])
+def test_bench_baseline_configs_one_gpu(numerics, flux, operator):
+    """BASELINE configs 2 and 3 through bench.py on one GPU (reduced size): the fused instantiation their
+    numerics select is the timed kernel, and config 3's implicit figure runs the matrix-free operator"""
+    env = dict(os.environ)
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT"):
+        env.pop(k, None)
+    out = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--numerics", numerics, "--scale", "4",
+                          "--steps", "5", "--warmup", "2", "--no-cpu-baseline", "--no-fast", "--preheat-ms", "20"],
+                         env=env, capture_output=True, text=True, timeout=400)
+    assert out.returncode == 0, out.stderr[-3000:]
+    lines = [l for l in out.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, out.stdout[-2000:]
+    d = json.loads(lines[0])
+    print(json.dumps({k: d[k] for k in ("value", "ms_per_step", "roofline")}))
+    assert d["n_gpus"] == 1 and d["value"] > 0
+    assert d["roofline"]["kernel"] == "k_residual_wls<%s>" % flux, d["roofline"]
+    im = d["implicit_step"]
+    assert im["operator"] == operator and im["steps"] == 3, im
