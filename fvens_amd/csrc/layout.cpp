@@ -4,6 +4,7 @@
  *   - WLS normal-matrix inverses, agradientschemes.cpp:218-317 (face-order sums, Eigen 2x2 inverse)
  *   - Venkatakrishnan eps^2 = (K*clength)^3, limitedlinearreconstruction.cpp:178-205, 222
  */
+#include <cstdlib>
 #include "layout.hpp"
 #include "partition.hpp"
 #include <algorithm>
@@ -59,10 +60,21 @@ Layout buildLayout(const fvhip_mesh& m, const fvhip_flow_config& cfg, bool renum
 	return buildLayout(topoFromMesh(m), cfg, renumber);
 }
 
+/// faces per patch the layout aims at: SLOTS_MAX, or FVHIP_PATCH_SLOTS (64..SLOTS_MAX) from the
+/// environment (an experiment knob: fewer slots per patch = more patches for small meshes)
+static int patchSlotCap()
+{
+	const char* e = std::getenv("FVHIP_PATCH_SLOTS");
+	if(!e || !*e) return SLOTS_MAX;
+	const int v = std::atoi(e);
+	return v < 64 ? 64 : (v > SLOTS_MAX ? SLOTS_MAX : v);
+}
+
 Layout buildLayout(const MeshTopo& T, const fvhip_flow_config& cfg, bool renumber)
 {
 	Layout Lo;
 	const int N = T.nown, NT = T.ncell(), nb = T.nbface, F = T.naface;
+	const int SC = patchSlotCap(), CC = std::min(CELLS_MAX, SC);
 	Lo.ncell = N; Lo.nghost = T.nghost; Lo.nbface = nb; Lo.naface = F; Lo.ninface = F - nb;
 
 	Lo.perm = renumber ? hilbertOrder(T.rc.data(), N) : std::vector<int>(N);
@@ -122,7 +134,7 @@ Layout buildLayout(const MeshTopo& T, const fvhip_flow_config& cfg, bool renumbe
 					if(qi == queue.size()) {
 						// the patch's region is exhausted: continue from the next unassigned cell in
 						// Hilbert order (a nearby hole or fresh cells), so every patch fills up
-						if(cc > 0 && cs >= SLOTS_MAX - 4) break;
+						if(cc > 0 && cs >= SC - 4) break;
 						size_t sk = seed;
 						while(sk < static_cast<size_t>(N) && (taken[Lo.perm[sk]] || inq[Lo.perm[sk]] == pid
 						                                      || !allowed(Lo.perm[sk]))) sk++;
@@ -133,7 +145,7 @@ Layout buildLayout(const MeshTopo& T, const fvhip_flow_config& cfg, bool renumbe
 					const int ref = queue[qi++];
 					int nnew = 0;
 					for(int j = 0; j < nf(ref); j++) if(mark[efc(ref,j)] != pid) nnew++;
-					if(cc > 0 && (cs + nnew > SLOTS_MAX || cc + 1 > CELLS_MAX)) continue;   // left for later patches
+					if(cc > 0 && (cs + nnew > SC || cc + 1 > CC)) continue;   // left for later patches
 					for(int j = 0; j < nf(ref); j++) mark[efc(ref,j)] = pid;
 					cs += nnew; cc++;
 					taken[ref] = 1;
@@ -157,7 +169,7 @@ Layout buildLayout(const MeshTopo& T, const fvhip_flow_config& cfg, bool renumbe
 			const int ref = Lo.perm[c];
 			int nnew = 0;
 			for(int j = 0; j < nf(ref); j++) if(mark[efc(ref,j)] != pid) nnew++;
-			if(cc > 0 && (cs + nnew > SLOTS_MAX || cc + 1 > CELLS_MAX)) {
+			if(cc > 0 && (cs + nnew > SC || cc + 1 > CC)) {
 				Lo.patch_cell.push_back(c);
 				pid++; cs = 0; cc = 0; nnew = nf(ref);
 			}
