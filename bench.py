@@ -641,10 +641,16 @@ def main():
                 return float(t.item())
             kw = dict(part=part, rank=rank, world=world, new_uid=new_uid, allmax=allmax)
         try:
+            start = dict(IMPLICIT_START)
+            if args.numerics == "config3":
+                # the flat plate's free stream is a steady state of the density residual up to rounding (its
+                # second-order residual there is ~1e-16): a ratio from it means nothing, so the steps are
+                # timed after the first-order start (one step: its first-order residual is exactly 0)
+                start["second_from"] = "start"
             implicit = next(implicit_steps(mesh, {"config5": "visc-c5", "config3": "plate"}.get(args.numerics, "naca"),
                                            steps=3, warmup=1, sweeps=1, lines=True,
                                            operators=((True,) if args.numerics == "config3" else (False,)),
-                                           **IMPLICIT_START, **kw))
+                                           **start, **kw))
             implicit.pop("faces", None)
         except Exception as e:          # N GPUs: report, do not lose the residual measurement
             if world == 1:
