@@ -27,3 +27,4 @@ for rep in 1 2; do
   done
 done
 echo done
+bash tools/gpu_r04j.sh
