@@ -466,14 +466,19 @@ void k_line_solve(const int* __restrict__ gstart, const int* __restrict__ lcell,
 	double2* G2 = reinterpret_cast<double2*>(G) + 128*r0 + j;     // row k: G2[128k], G2[128k + 64]
 	double Dk[4][4], Lk[4][4];
 	double4 gp = make_double4(0, 0, 0, 0), vk = make_double4(0, 0, 0, 0), s = make_double4(0, 0, 0, 0);
+	// the cells of rows k+1 and k+2 are known before row k's arithmetic: the v row of k+1 is requested
+	// without first waiting for its cell index (one memory round trip per cell instead of two)
+	int c1 = n > 1 ? cl[64] : 0, c2 = n > 2 ? cl[128] : 0;
 	if(n > 0) { vk = v4[cl[0]]; ldP16(D, r0, j, Dk); }
 	for(int k = 0; k < n; k++) {
 		double Dn[4][4], Ln[4][4];
 		double4 vn = make_double4(0, 0, 0, 0);
 		if(k + 1 < n) {
-			vn = v4[cl[64*(k+1)]];
+			vn = v4[c1];
 			ldP16(D, r0 + k + 1, j, Dn);
 			ldP16(Lb, r0 + k + 1, j, Ln);
+			c1 = c2;
+			c2 = k + 3 < n ? cl[64*(k+3)] : 0;
 		}
 		if(tw && k == n - 1) {                         // the twist: this side's term A[t][last] g_last
 			s = make_double4(Lk[0][0]*gp.x + Lk[0][1]*gp.y + Lk[0][2]*gp.z + Lk[0][3]*gp.w,
