@@ -676,6 +676,27 @@ def main():
                 "stage": stage, "steps": st["steps"], "seconds": st["seconds"], "ms_per_step": st["ms_per_step"],
                 "drop_from_peak": st["drop_from_peak"], "drop_from_first": st["drop_from_first"]}
 
+    # the C-ABI's host-pointer entry (fvhip_compute_residual: the reference's own calling convention, u, r
+    # and dtm in host memory in reference order), PCIe and host work included -- reported, never `value`
+    host_boundary = None
+    if world == 1:
+        n.fast_math = False
+        hb = fa.FlowFV(mesh, p, n, device=torch.cuda.current_device())
+        hr = np.zeros((N, 4))
+        hdt = np.zeros(N)
+        hb.compute_residual(u, hr, True, hdt)                       # warm-up: staging buffers
+        reps = 5
+        th = time.perf_counter()
+        for _ in range(reps):
+            hr[:] = 0.0
+            hb.compute_residual(u, hr, True, hdt)
+        hms = (time.perf_counter() - th) / reps * 1e3
+        hb.close()
+        del hr, hdt
+        host_boundary = {"ms_per_call": round(hms, 3), "Mfaces_per_s": round(F / (hms * 1e-3) / 1e6, 3),
+                         "calls": reps,
+                         "note": "fvhip_compute_residual with host arrays in reference order (u, r in; r, dtm out): "
+                                 "PCIe transfers and reordering included; the device-resident residual is `value`"}
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline(mesh, u, args.cpu_sweeps, rec, kind, flux)
@@ -743,6 +764,7 @@ def main():
             "multi_gpu": ({**partinfo, **halo} if world > 1 else None),
             "halo_parity": (halo["halo_parity"] if world > 1 else None),
             "cpu_baseline": cpu,
+            "host_boundary": host_boundary,
             "fast_math": fast,
             "staged_path": staged,
             "pipelined_path": pipelined,

@@ -140,7 +140,18 @@ struct fvhip_ctx
 	JacMesh J{};
 	bool jac_ready = false;
 	double *d_jb = nullptr, *d_jlo = nullptr, *d_jup = nullptr, *d_jdiag = nullptr;
-	std::vector<double> h_stage;
+	/// reference-order rows of the host-pointer entries (fvhip_compute_residual & co.): the host array is
+	/// copied as it is and reordered on the device (k_gather / k_scatter over d_perm)
+	double* d_raw = nullptr;
+	size_t raw_cap = 0;
+	double* rawScratch(size_t doubles) {
+		if(raw_cap < doubles) {
+			if(d_raw) release(d_raw);
+			d_raw = dalloc(doubles, owned);
+			raw_cap = doubles;
+		}
+		return d_raw;
+	}
 	// partitioned meshes: halo exchange with the neighbour ranks (RCCL, or in-process for a group)
 	int rank = 0, nparts = 1;
 	bool rankmesh = false;        ///< one rank's subdomain with connectivity faces (fvhip_create, nconnface > 0)

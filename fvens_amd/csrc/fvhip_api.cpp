@@ -175,7 +175,7 @@ static fvhip_ctx* createCtx(const MeshTopo& T, const fvhip_flow_config* cfg, int
 	if(cfg->reconstruction == FVHIP_REC_WENO) h->d_lgrad = dalloc(8*NT, o);
 	if(cfg->reconstruction == FVHIP_REC_BARTHJESPERSEN || cfg->reconstruction == FVHIP_REC_VENKATAKRISHNAN)
 		h->d_phi = dalloc(4*NT, o);
-	h->h_stage.resize(16*N);
+
 	return h.release();
 }
 
@@ -436,11 +436,28 @@ int fvhip_compute_residual_device(fvhip_handle h, const double* d_u, double* d_r
 	});
 }
 
-static void toInternal(fvhip_ctx* h, const double* src, double* dst, int width) {
-	const int N = h->L.ncell;
-	for(int c = 0; c < N; c++)
-		std::memcpy(dst + static_cast<size_t>(c)*width, src + static_cast<size_t>(h->L.perm[c])*width, width*sizeof(double));
+/// host array in reference order -> device array in internal order, on the handle's stream: the rows are
+/// copied as they are (one contiguous transfer) and reordered by k_gather over d_perm on the device
+static void uploadInternal(fvhip_ctx* h, const double* host_ref, double* d_internal, int width) {
+	const size_t n = static_cast<size_t>(h->L.ncell)*width;
+	if(n == 0) return;
+	double* raw = h->rawScratch(n);
+	HC(hipMemcpyAsync(raw, host_ref, n*sizeof(double), hipMemcpyHostToDevice, h->stream));
+	exact::launch_gather_cells(h->d_perm, raw, d_internal, h->L.ncell, width, h->stream);
+	HC(hipGetLastError());
 }
+/// device array in internal order -> host array in reference order (k_scatter, then one transfer);
+/// returns when the host array holds the values
+static void downloadReference(fvhip_ctx* h, const double* d_internal, double* host_ref, int width) {
+	const size_t n = static_cast<size_t>(h->L.ncell)*width;
+	if(n == 0) return;
+	double* raw = h->rawScratch(n);
+	exact::launch_scatter_cells(h->d_perm, d_internal, raw, h->L.ncell, width, h->stream);
+	HC(hipGetLastError());
+	HC(hipMemcpyAsync(host_ref, raw, n*sizeof(double), hipMemcpyDeviceToHost, h->stream));
+	HC(hipStreamSynchronize(h->stream));
+}
+/// host-side reordering of rows already on the host (internal -> reference)
 static void fromInternal(fvhip_ctx* h, const double* src, double* dst, int width) {
 	const int N = h->L.ncell;
 	for(int c = 0; c < N; c++)
@@ -453,22 +470,11 @@ int fvhip_compute_residual(fvhip_handle h, const double* u, double* r, int getti
 		need(h, "handle");
 		need(u, "u"); need(r, "residual"); if(gettimesteps) need(dtm, "dtm");
 		HC(hipSetDevice(h->device));
-		const size_t N = static_cast<size_t>(h->L.ncell);
-		std::vector<double>& st = h->h_stage;
-		toInternal(h, u, st.data(), 4);
-		HC(hipMemcpyAsync(h->d_u, st.data(), 4*N*sizeof(double), hipMemcpyHostToDevice, h->stream));
-		HC(hipStreamSynchronize(h->stream));
-		toInternal(h, r, st.data(), 4);
-		HC(hipMemcpyAsync(h->d_r, st.data(), 4*N*sizeof(double), hipMemcpyHostToDevice, h->stream));
+		uploadInternal(h, u, h->d_u, 4);
+		uploadInternal(h, r, h->d_r, 4);
 		h->residual(h->d_u, h->d_r, gettimesteps != 0, h->d_dtm, false);
-		HC(hipMemcpyAsync(st.data(), h->d_r, 4*N*sizeof(double), hipMemcpyDeviceToHost, h->stream));
-		HC(hipStreamSynchronize(h->stream));
-		fromInternal(h, st.data(), r, 4);
-		if(gettimesteps) {
-			HC(hipMemcpyAsync(st.data(), h->d_dtm, N*sizeof(double), hipMemcpyDeviceToHost, h->stream));
-			HC(hipStreamSynchronize(h->stream));
-			fromInternal(h, st.data(), dtm, 1);
-		}
+		downloadReference(h, h->d_r, r, 4);
+		if(gettimesteps) downloadReference(h, h->d_dtm, dtm, 1);
 	});
 }
 
@@ -478,10 +484,7 @@ int fvhip_get_gradients(fvhip_handle h, const double* u, double* grads)
 		need(h, "handle");
 		need(u, "u"); need(grads, "grads");
 		HC(hipSetDevice(h->device));
-		const size_t N = static_cast<size_t>(h->L.ncell);
-		std::vector<double>& st = h->h_stage;
-		toInternal(h, u, st.data(), 4);
-		HC(hipMemcpyAsync(h->d_u, st.data(), 4*N*sizeof(double), hipMemcpyHostToDevice, h->stream));
+		uploadInternal(h, u, h->d_u, 4);
 		h->exchange_rccl(h->d_u, 4);   // ghost rows for the border cells (partitioned handles)
 		// ghost states from cell values, then the gradient scheme on CONSERVED variables
 		exact::launch_prep(h->M, h->P, h->d_u, h->d_up, h->d_ubc, h->d_ug, false, h->stream);
@@ -491,9 +494,7 @@ int fvhip_get_gradients(fvhip_handle h, const double* u, double* grads)
 			default: exact::launch_fill(h->d_grad, 0.0, 8LL*h->L.ncell, h->stream);
 		}
 		HC(hipGetLastError());
-		HC(hipMemcpyAsync(st.data(), h->d_grad, 8*N*sizeof(double), hipMemcpyDeviceToHost, h->stream));
-		HC(hipStreamSynchronize(h->stream));
-		fromInternal(h, st.data(), grads, 8);
+		downloadReference(h, h->d_grad, grads, 8);
 	});
 }
 
@@ -587,9 +588,7 @@ int fvhip_assemble_jacobian(fvhip_handle h, const double* u, double* diag, doubl
 		need(u, "u"); need(diag, "diag"); if(h->L.ninface > 0) { need(lower, "lower"); need(upper, "upper"); }
 		HC(hipSetDevice(h->device));
 		const size_t N = static_cast<size_t>(h->L.ncell), Fi = static_cast<size_t>(h->L.ninface);
-		std::vector<double>& st = h->h_stage;
-		toInternal(h, u, st.data(), 4);
-		HC(hipMemcpyAsync(h->d_u, st.data(), 4*N*sizeof(double), hipMemcpyHostToDevice, h->stream));
+		uploadInternal(h, u, h->d_u, 4);
 		h->exchange_rccl(h->d_u, 4);   // ghost rows: the cut-face blocks read them (partitioned handles)
 		HC(hipStreamSynchronize(h->stream));
 		if(!h->d_jdiag) {
@@ -599,14 +598,12 @@ int fvhip_assemble_jacobian(fvhip_handle h, const double* u, double* diag, doubl
 		}
 		h->assemble(h->d_u, h->d_jdiag, h->d_jlo, h->d_jup);
 		// ADD_VALUES into the caller's blocks (the reference's caller zeroes them, aodesolver.cpp:456)
-		std::vector<double> dg(16*N), tmp(16*N), lo(16*Fi), up(16*Fi);
-		HC(hipMemcpyAsync(dg.data(), h->d_jdiag, 16*N*sizeof(double), hipMemcpyDeviceToHost, h->stream));
+		std::vector<double> tmp(16*N), lo(16*Fi), up(16*Fi);
 		if(Fi) {
 			HC(hipMemcpyAsync(lo.data(), h->d_jlo, 16*Fi*sizeof(double), hipMemcpyDeviceToHost, h->stream));
 			HC(hipMemcpyAsync(up.data(), h->d_jup, 16*Fi*sizeof(double), hipMemcpyDeviceToHost, h->stream));
 		}
-		HC(hipStreamSynchronize(h->stream));
-		fromInternal(h, dg.data(), tmp.data(), 16);
+		downloadReference(h, h->d_jdiag, tmp.data(), 16);
 		for(size_t k = 0; k < 16*N; k++) diag[k] += tmp[k];
 		for(size_t k = 0; k < 16*Fi; k++) { lower[k] += lo[k]; upper[k] += up[k]; }
 	});
@@ -698,16 +695,14 @@ int fvhip_matfree_set_state(fvhip_handle h, const double* u, const double* r, co
 {
 	return guard([&] {
 		need(h, "handle");
+		need(u, "u"); need(r, "residual"); need(mdt, "mdt");
 		HC(hipSetDevice(h->device));
 		const size_t N = static_cast<size_t>(h->L.ncell);
 		if(!h->d_mf_u) { h->d_mf_u = dalloc(4*N, h->owned); h->d_mf_r = dalloc(4*N, h->owned); h->d_mf_mdt = dalloc(N, h->owned); }
-		std::vector<double> st(4*N);
-		toInternal(h, u, st.data(), 4);
-		HC(hipMemcpy(h->d_mf_u, st.data(), 4*N*sizeof(double), hipMemcpyHostToDevice));
-		toInternal(h, r, st.data(), 4);
-		HC(hipMemcpy(h->d_mf_r, st.data(), 4*N*sizeof(double), hipMemcpyHostToDevice));
-		toInternal(h, mdt, st.data(), 1);
-		HC(hipMemcpy(h->d_mf_mdt, st.data(), N*sizeof(double), hipMemcpyHostToDevice));
+		uploadInternal(h, u, h->d_mf_u, 4);
+		uploadInternal(h, r, h->d_mf_r, 4);
+		uploadInternal(h, mdt, h->d_mf_mdt, 1);
+		HC(hipStreamSynchronize(h->stream));
 		h->mf_u = h->d_mf_u; h->mf_r = h->d_mf_r; h->mf_mdt = h->d_mf_mdt;
 	});
 }
@@ -718,21 +713,16 @@ int fvhip_matfree_apply(fvhip_handle h, const double* x, double* y)
 		need(h, "handle");
 		need(x, "x"); need(y, "y");
 		HC(hipSetDevice(h->device));
-		const size_t N = static_cast<size_t>(h->L.ncell);
 		if(!h->d_mf_u) throw std::runtime_error("matrix-free operator: state not set");
-		std::vector<double> st(4*N);
-		toInternal(h, x, st.data(), 4);
 		double *dx = h->d_u, *dy = h->d_r;   // scratch: the operator's state lives in d_mf_*
-		HC(hipMemcpyAsync(dx, st.data(), 4*N*sizeof(double), hipMemcpyHostToDevice, h->stream));
+		uploadInternal(h, x, dx, 4);
 		if(h->halo()) {
 			// partitioned: the operator over all ranks (global |x|; ghost rows of the perturbed state
 			// are exchanged inside the residual), as fvhip_matfree_apply_device does
 			if(!h->comm) throw std::runtime_error("partitioned handle: call fvhip_comm_init first");
 			sysMatfree({h}, fvhip_ctx::GroupExchange(), {dx}, {dy});
 		} else h->matfree(dx, dy);
-		HC(hipMemcpyAsync(st.data(), dy, 4*N*sizeof(double), hipMemcpyDeviceToHost, h->stream));
-		HC(hipStreamSynchronize(h->stream));
-		fromInternal(h, st.data(), y, 4);
+		downloadReference(h, dy, y, 4);
 	});
 }
 
@@ -780,10 +770,10 @@ int fvhip_to_internal(fvhip_handle h, const double* host_ref, double* d_internal
 	return guard([&] {
 		need(h, "handle");
 		need(host_ref, "host array"); need(d_internal, "device array");
+		if(width < 1) throw std::invalid_argument("width must be >= 1");
 		HC(hipSetDevice(h->device));
-		std::vector<double> st(static_cast<size_t>(h->L.ncell)*width);
-		toInternal(h, host_ref, st.data(), width);
-		HC(hipMemcpy(d_internal, st.data(), st.size()*sizeof(double), hipMemcpyHostToDevice));
+		uploadInternal(h, host_ref, d_internal, width);
+		HC(hipStreamSynchronize(h->stream));
 	});
 }
 int fvhip_from_internal(fvhip_handle h, const double* d_internal, double* host_ref, int width)
@@ -791,11 +781,9 @@ int fvhip_from_internal(fvhip_handle h, const double* d_internal, double* host_r
 	return guard([&] {
 		need(h, "handle");
 		need(d_internal, "device array"); need(host_ref, "host array");
+		if(width < 1) throw std::invalid_argument("width must be >= 1");
 		HC(hipSetDevice(h->device));
-		HC(hipStreamSynchronize(h->stream));
-		std::vector<double> st(static_cast<size_t>(h->L.ncell)*width);
-		HC(hipMemcpy(st.data(), d_internal, st.size()*sizeof(double), hipMemcpyDeviceToHost));
-		fromInternal(h, st.data(), host_ref, width);
+		downloadReference(h, d_internal, host_ref, width);
 	});
 }
 int fvhip_get_permutation(fvhip_handle h, int* perm)

@@ -1558,6 +1558,15 @@ __global__ void k_gather(const int* perm, const double* src, double* dst, int n,
 	dst[i] = src[static_cast<size_t>(perm[c])*width + w];
 }
 
+/// dst row perm[c] = src row c (internal -> reference order, the inverse of k_gather)
+__global__ void k_scatter(const int* perm, const double* src, double* dst, int n, int width)
+{
+	const long long i = static_cast<long long>(blockIdx.x)*blockDim.x + threadIdx.x;
+	if(i >= static_cast<long long>(n)*width) return;
+	const int c = static_cast<int>(i / width), w = static_cast<int>(i % width);
+	dst[static_cast<size_t>(perm[c])*width + w] = src[i];
+}
+
 // ------------------------------------------------------------------------------------------------
 // launchers
 // ------------------------------------------------------------------------------------------------
@@ -1629,6 +1638,8 @@ void launch_divsqrt_probe(int n, const double* a, const double* b, double* out, 
 
 void launch_gather_cells(const int* perm, const double* src, double* dst, int n, int width, hipStream_t s)
 { if(n > 0) k_gather<<<nblk(static_cast<long long>(n)*width,256), 256, 0, s>>>(perm, src, dst, n, width); }
+void launch_scatter_cells(const int* perm, const double* src, double* dst, int n, int width, hipStream_t s)
+{ if(n > 0) k_scatter<<<nblk(static_cast<long long>(n)*width,256), 256, 0, s>>>(perm, src, dst, n, width); }
 
 // sweep dispatch over (flux, reconstruction, viscous, dt, phi)
 typedef void (*SweepFn)(const DevMesh, const DevPhys, const SweepBuffers);

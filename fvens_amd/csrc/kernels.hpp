@@ -117,6 +117,7 @@ void launch_fill(double* p, double v, long long n, hipStream_t s); \
 void launch_local_flux(int flux, const gd::Gas& G, int nf, const double* ul, const double* ur, \
                        const double* n, double* f, hipStream_t s); \
 void launch_gather_cells(const int* perm, const double* src, double* dst, int n, int width, hipStream_t s); \
+void launch_scatter_cells(const int* perm, const double* src, double* dst, int n, int width, hipStream_t s); \
 void launch_divsqrt_probe(int n, const double* a, const double* b, double* out, hipStream_t s);
 
 namespace exact { FVHIP_SWEEP_LAUNCHERS }
