@@ -209,6 +209,48 @@ void k_jac_diag(JacMesh J, const double* __restrict__ bblk, const double* __rest
 	for(int q = 0; q < 4; q++) o[q] = make_double4(d[4*q], d[4*q+1], d[4*q+2], d[4*q+3]);
 }
 
+#ifndef FVHIP_BLOCK_ROWS
+#define FVHIP_BLOCK_ROWS 1
+#endif
+/// k_jac_diag with four lanes per cell, lane i forming row i of the block: each face block is read as four
+/// consecutive 32-byte rows by four consecutive lanes (one 128-byte segment per block instead of one per
+/// lane and 16-byte piece), and the diagonal block is written the same way. Every entry takes the same
+/// operations in the same order as k_jac_diag's (its terms over the faces in ascending order, then the
+/// pseudo-time term), so the blocks are bitwise the same.
+__global__ __launch_bounds__(256)
+void k_jac_diag_rows(JacMesh J, const double* __restrict__ bblk, const double* __restrict__ lower,
+                     const double* __restrict__ upper, double* __restrict__ diag, const double* __restrict__ area,
+                     double cfl, double* __restrict__ dtm)
+{
+	const long long g = static_cast<long long>(blockIdx.x)*blockDim.x + threadIdx.x;
+	const int c = static_cast<int>(g >> 2), i = static_cast<int>(g & 3);
+	if(c >= J.ncell) return;
+	const int4 fc = J.cell_rfaces[c];
+	const int codes[4] = {fc.x, fc.y, fc.z, fc.w};
+	double4 v[4];
+#pragma unroll
+	for(int j = 0; j < 4; j++) {
+		const int code = codes[j];
+		const int f = code >> 1;
+		const double* blk = code < 0 ? kZeroBlock
+		                  : f < J.nbface ? bblk + 16*static_cast<size_t>(f)
+		                  : ((code & 1) ? upper : lower) + 16*static_cast<size_t>(f - J.nbface);
+		v[j] = reinterpret_cast<const double4*>(blk)[i];
+	}
+	double d[4] = {0, 0, 0, 0};
+#pragma unroll
+	for(int j = 0; j < 4; j++) {
+		d[0] += -1.0*v[j].x; d[1] += -1.0*v[j].y; d[2] += -1.0*v[j].z; d[3] += -1.0*v[j].w;
+	}
+	if(area) {
+		const double m = area[c] / (cfl*dtm[c]);
+#pragma unroll
+		for(int k = 0; k < 4; k++) d[k] += m*(i == k ? 1.0 : 0.0);
+		if(i == 0) dtm[c] = m;            // after all four lanes of the cell (one wavefront) have read it
+	}
+	reinterpret_cast<double4*>(diag + 16*static_cast<size_t>(c))[i] = make_double4(d[0], d[1], d[2], d[3]);
+}
+
 // -------------------------------------------------------------------------------------------------
 // pseudo-time term: dtm <- area/(cfl*dtm); diag += dtm*I (all 16 entries, as MatSetValuesBlocked)
 // -------------------------------------------------------------------------------------------------
@@ -278,6 +320,38 @@ void k_block_apply(JacMesh J, const double* __restrict__ diag, const double* __r
 		for(int i = 0; i < 4; i++) acc[i] += s[i];
 	}
 	reinterpret_cast<double4*>(y)[c] = make_double4(acc[0], acc[1], acc[2], acc[3]);
+}
+
+/// k_block_apply with four lanes per cell, lane i forming y[c][i]: the same row dot products in the same
+/// order (diagonal block first, then the faces ascending), so bitwise the same y; each block is read as four
+/// consecutive 32-byte rows by four consecutive lanes, and y is written as one 32-byte row per cell
+__global__ __launch_bounds__(256)
+void k_block_apply_rows(JacMesh J, const double* __restrict__ diag, const double* __restrict__ lower,
+                        const double* __restrict__ upper, const double* __restrict__ x, double* __restrict__ y)
+{
+	const long long g = static_cast<long long>(blockIdx.x)*blockDim.x + threadIdx.x;
+	const int c = static_cast<int>(g >> 2), i = static_cast<int>(g & 3);
+	if(c >= J.ncell) return;
+	const double4* x4 = reinterpret_cast<const double4*>(x);
+	const int4 fc = J.cell_rfaces[c];
+	const int4 nb = J.cell_nbr_fo[c];
+	const int codes[4] = {fc.x, fc.y, fc.z, fc.w};
+	const int nbrs[4] = {nb.x, nb.y, nb.z, nb.w};
+	double4 r = reinterpret_cast<const double4*>(diag + 16*static_cast<size_t>(c))[i];
+	double4 xv = x4[c];
+	double acc = r.x*xv.x + r.y*xv.y + r.z*xv.z + r.w*xv.w;
+#pragma unroll
+	for(int j = 0; j < 4; j++) {
+		const int code = codes[j];
+		if(code < 0) continue;
+		const int f = code >> 1;
+		if(f < J.nbface) continue;
+		const double* B = ((code & 1) ? lower : upper) + 16*static_cast<size_t>(f - J.nbface);
+		r = reinterpret_cast<const double4*>(B)[i];
+		xv = x4[nbrs[j]];
+		acc += r.x*xv.x + r.y*xv.y + r.z*xv.z + r.w*xv.w;
+	}
+	y[4*static_cast<size_t>(c) + i] = acc;
 }
 
 /// One block-Jacobi sweep fused into one pass: zout = D^-1 (v - sum_faces B zin[nbr]), the
@@ -472,7 +546,11 @@ void launch_jac_faces(const JacMesh& J, const DevPhys& P, int jflux, int visc, c
 void launch_jac_diag(const JacMesh& J, const double* bblk, const double* lower, const double* upper,
                      double* diag, hipStream_t s, const double* area, double cfl, double* dtm)
 {
-	hipLaunchKernelGGL(k_jac_diag, dim3(nblk(J.ncell,256)), dim3(256), 0, s, J, bblk, lower, upper, diag, area, cfl, dtm);
+	if(J.ncell <= 0) return;
+	if(FVHIP_BLOCK_ROWS)
+		hipLaunchKernelGGL(k_jac_diag_rows, dim3(nblk(4LL*J.ncell,256)), dim3(256), 0, s, J, bblk, lower, upper, diag, area, cfl, dtm);
+	else
+		hipLaunchKernelGGL(k_jac_diag, dim3(nblk(J.ncell,256)), dim3(256), 0, s, J, bblk, lower, upper, diag, area, cfl, dtm);
 }
 
 void launch_pseudo_time(int ncell, const double* area, double cfl, double* dtm, double* diag, hipStream_t s)
@@ -483,7 +561,11 @@ void launch_pseudo_time(int ncell, const double* area, double cfl, double* dtm, 
 void launch_block_apply(const JacMesh& J, const double* diag, const double* lower, const double* upper,
                         const double* x, double* y, hipStream_t s)
 {
-	hipLaunchKernelGGL(k_block_apply, dim3(nblk(J.ncell,256)), dim3(256), 0, s, J, diag, lower, upper, x, y);
+	if(J.ncell <= 0) return;
+	if(FVHIP_BLOCK_ROWS)
+		hipLaunchKernelGGL(k_block_apply_rows, dim3(nblk(4LL*J.ncell,256)), dim3(256), 0, s, J, diag, lower, upper, x, y);
+	else
+		hipLaunchKernelGGL(k_block_apply, dim3(nblk(J.ncell,256)), dim3(256), 0, s, J, diag, lower, upper, x, y);
 }
 
 void launch_bjac_sweep(const JacMesh& J, const double* dinv, const double* lower, const double* upper,
