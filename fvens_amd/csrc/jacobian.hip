@@ -389,6 +389,52 @@ void k_bjac_sweep(JacMesh J, const T* __restrict__ dinv, const T* __restrict__ l
 	reinterpret_cast<double4*>(zout)[c] = make_double4(o[0], o[1], o[2], o[3]);
 }
 
+/// row i of a row-major 4x4 block dotted with x, as blk_row_dots forms it (k ascending)
+__device__ __forceinline__ double blk_row_dot(const double* __restrict__ B, int i, const double4 x)
+{
+	const double4 r = reinterpret_cast<const double4*>(B)[i];
+	return r.x*x.x + r.y*x.y + r.z*x.z + r.w*x.w;
+}
+__device__ __forceinline__ double blk_row_dot(const float* __restrict__ B, int i, const double4 x)
+{
+	const float4 r = reinterpret_cast<const float4*>(B)[i];
+	return static_cast<double>(r.x)*x.x + static_cast<double>(r.y)*x.y + static_cast<double>(r.z)*x.z
+	     + static_cast<double>(r.w)*x.w;
+}
+/// k_bjac_sweep with four lanes per cell, lane i forming row i (coalesced block rows, as k_block_apply_rows):
+/// the same row sums in the same order, the four sums exchanged within the cell's lanes for the product
+/// with D^-1, so bitwise k_bjac_sweep's z
+template <typename T>
+__global__ __launch_bounds__(256)
+void k_bjac_sweep_rows(JacMesh J, const T* __restrict__ dinv, const T* __restrict__ lower,
+                       const T* __restrict__ upper, const double* __restrict__ v, const double* __restrict__ zin,
+                       double* __restrict__ zout)
+{
+	const long long g = static_cast<long long>(blockIdx.x)*blockDim.x + threadIdx.x;
+	const int c = static_cast<int>(g >> 2), i = static_cast<int>(g & 3);
+	const bool live = c < J.ncell;
+	const int cc = live ? c : J.ncell - 1;          // lanes past the end compute a copy and store nothing
+	const double4* z4 = reinterpret_cast<const double4*>(zin);
+	double acc = v[4*static_cast<size_t>(cc) + i];
+	const int4 fc = J.cell_rfaces[cc];
+	const int4 nb = J.cell_nbr_fo[cc];
+	const int codes[4] = {fc.x, fc.y, fc.z, fc.w};
+	const int nbrs[4] = {nb.x, nb.y, nb.z, nb.w};
+#pragma unroll
+	for(int j = 0; j < 4; j++) {
+		const int code = codes[j];
+		if(code < 0) continue;
+		const int f = code >> 1;
+		if(f < J.nbface) continue;
+		const T* B = ((code & 1) ? lower : upper) + 16*static_cast<size_t>(f - J.nbface);
+		acc -= blk_row_dot(B, i, z4[nbrs[j]]);
+	}
+	// the cell's four row sums to every lane of the cell (all 64 lanes of the wave take part)
+	const double4 t = make_double4(__shfl(acc, 0, 4), __shfl(acc, 1, 4), __shfl(acc, 2, 4), __shfl(acc, 3, 4));
+	const double o = blk_row_dot(dinv + 16*static_cast<size_t>(cc), i, t);
+	if(live) zout[4*static_cast<size_t>(c) + i] = o;
+}
+
 /// One colour of a multicolour block Gauss-Seidel sweep, in place: z_c = D^-1 (v - sum_faces B z[nbr])
 /// for the listed cells, which share no face, so every neighbour value read is either from an
 /// earlier colour of this sweep or from the previous sweep (ghost rows: from the last exchange).
@@ -571,12 +617,20 @@ void launch_block_apply(const JacMesh& J, const double* diag, const double* lowe
 void launch_bjac_sweep(const JacMesh& J, const double* dinv, const double* lower, const double* upper,
                        const double* v, const double* zin, double* zout, hipStream_t s)
 {
-	hipLaunchKernelGGL(k_bjac_sweep<double>, dim3(nblk(J.ncell,256)), dim3(256), 0, s, J, dinv, lower, upper, v, zin, zout);
+	if(J.ncell <= 0) return;
+	if(FVHIP_BLOCK_ROWS)
+		hipLaunchKernelGGL(k_bjac_sweep_rows<double>, dim3(nblk(4LL*J.ncell,256)), dim3(256), 0, s, J, dinv, lower, upper, v, zin, zout);
+	else
+		hipLaunchKernelGGL(k_bjac_sweep<double>, dim3(nblk(J.ncell,256)), dim3(256), 0, s, J, dinv, lower, upper, v, zin, zout);
 }
 void launch_bjac_sweep(const JacMesh& J, const float* dinv, const float* lower, const float* upper,
                        const double* v, const double* zin, double* zout, hipStream_t s)
 {
-	hipLaunchKernelGGL(k_bjac_sweep<float>, dim3(nblk(J.ncell,256)), dim3(256), 0, s, J, dinv, lower, upper, v, zin, zout);
+	if(J.ncell <= 0) return;
+	if(FVHIP_BLOCK_ROWS)
+		hipLaunchKernelGGL(k_bjac_sweep_rows<float>, dim3(nblk(4LL*J.ncell,256)), dim3(256), 0, s, J, dinv, lower, upper, v, zin, zout);
+	else
+		hipLaunchKernelGGL(k_bjac_sweep<float>, dim3(nblk(J.ncell,256)), dim3(256), 0, s, J, dinv, lower, upper, v, zin, zout);
 }
 
 template <typename T>
