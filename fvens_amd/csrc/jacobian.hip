@@ -470,6 +470,38 @@ void k_bgs_colour(JacMesh J, const T* __restrict__ dinv, const T* __restrict__ l
 	reinterpret_cast<double4*>(z)[c] = make_double4(o[0], o[1], o[2], o[3]);
 }
 
+/// k_bgs_colour with four lanes per cell (k_bjac_sweep_rows' arithmetic, in place): bitwise k_bgs_colour's z.
+/// Every lane of the cell reads its neighbours' rows before any lane writes the cell (cells of a colour
+/// share no face, so no neighbour is written by this launch)
+template <typename T>
+__global__ __launch_bounds__(256)
+void k_bgs_colour_rows(JacMesh J, const T* __restrict__ dinv, const T* __restrict__ lower, const T* __restrict__ upper,
+                       const double* __restrict__ v, double* z, const int* __restrict__ cells, int n)
+{
+	const long long g = static_cast<long long>(blockIdx.x)*blockDim.x + threadIdx.x;
+	const int k = static_cast<int>(g >> 2), i = static_cast<int>(g & 3);
+	const bool live = k < n;
+	const int c = cells[live ? k : n - 1];
+	const double4* z4 = reinterpret_cast<const double4*>(z);
+	double acc = v[4*static_cast<size_t>(c) + i];
+	const int4 fc = J.cell_rfaces[c];
+	const int4 nb = J.cell_nbr_fo[c];
+	const int codes[4] = {fc.x, fc.y, fc.z, fc.w};
+	const int nbrs[4] = {nb.x, nb.y, nb.z, nb.w};
+#pragma unroll
+	for(int j = 0; j < 4; j++) {
+		const int code = codes[j];
+		if(code < 0) continue;
+		const int f = code >> 1;
+		if(f < J.nbface) continue;
+		const T* B = ((code & 1) ? lower : upper) + 16*static_cast<size_t>(f - J.nbface);
+		acc -= blk_row_dot(B, i, z4[nbrs[j]]);
+	}
+	const double4 t = make_double4(__shfl(acc, 0, 4), __shfl(acc, 1, 4), __shfl(acc, 2, 4), __shfl(acc, 3, 4));
+	const double o = blk_row_dot(dinv + 16*static_cast<size_t>(c), i, t);
+	if(live) z[4*static_cast<size_t>(c) + i] = o;
+}
+
 // -------------------------------------------------------------------------------------------------
 // matrix-free pieces
 // -------------------------------------------------------------------------------------------------
@@ -637,7 +669,10 @@ template <typename T>
 void launch_bgs_colour_t(const JacMesh& J, const T* dinv, const T* lower, const T* upper, const double* v,
                          double* z, const int* cells, int n, hipStream_t s)
 {
-	if(n > 0)
+	if(n <= 0) return;
+	if(FVHIP_BLOCK_ROWS)
+		hipLaunchKernelGGL(k_bgs_colour_rows<T>, dim3(nblk(4LL*n,256)), dim3(256), 0, s, J, dinv, lower, upper, v, z, cells, n);
+	else
 		hipLaunchKernelGGL(k_bgs_colour<T>, dim3(nblk(n,256)), dim3(256), 0, s, J, dinv, lower, upper, v, z, cells, n);
 }
 void launch_bgs_colour(const JacMesh& J, const double* dinv, const double* lower, const double* upper,

@@ -183,6 +183,31 @@ void k_bjac_apply(int n, const T* __restrict__ dinv, const double* __restrict__ 
 	reinterpret_cast<double4*>(y)[c] = make_double4(o[0], o[1], o[2], o[3]);
 }
 
+#ifndef FVHIP_BLOCK_ROWS
+#define FVHIP_BLOCK_ROWS 1
+#endif
+/// k_bjac_apply with four lanes per cell, lane i forming y[c][i] = row i of D^-1 . x[c] (the same dot, in the
+/// same order: bitwise k_bjac_apply's y), the block read as four consecutive rows by the cell's four lanes
+template <typename T>
+__global__ __launch_bounds__(256)
+void k_bjac_apply_rows(int n, const T* __restrict__ dinv, const double* __restrict__ x, double* __restrict__ y)
+{
+	const long long g = static_cast<long long>(blockIdx.x)*blockDim.x + threadIdx.x;
+	const int c = static_cast<int>(g >> 2), i = static_cast<int>(g & 3);
+	if(c >= n) return;
+	const double4 xv = reinterpret_cast<const double4*>(x)[c];
+	double o;
+	if constexpr(sizeof(T) == sizeof(double)) {
+		const double4 r = reinterpret_cast<const double4*>(dinv + 16*static_cast<size_t>(c))[i];
+		o = r.x*xv.x + r.y*xv.y + r.z*xv.z + r.w*xv.w;
+	} else {
+		const float4 r = reinterpret_cast<const float4*>(dinv + 16*static_cast<size_t>(c))[i];
+		o = static_cast<double>(r.x)*xv.x + static_cast<double>(r.y)*xv.y + static_cast<double>(r.z)*xv.z
+		  + static_cast<double>(r.w)*xv.w;
+	}
+	y[4*static_cast<size_t>(c) + i] = o;
+}
+
 __global__ __launch_bounds__(256)
 void k_to_single(long long n, const double* __restrict__ a, float* __restrict__ b)
 {
@@ -602,9 +627,17 @@ void launch_ilu_factor_colour(int ncell, int nbface, const int4* rfaces, const i
 	                                                           dinv, cells, n);
 }
 void launch_bjac_apply(int n, const double* dinv, const double* x, double* y, hipStream_t s)
-{ if(n > 0) k_bjac_apply<double><<<nblk(n,256), 256, 0, s>>>(n, dinv, x, y); }
+{
+	if(n <= 0) return;
+	if(FVHIP_BLOCK_ROWS) k_bjac_apply_rows<double><<<nblk(4LL*n,256), 256, 0, s>>>(n, dinv, x, y);
+	else k_bjac_apply<double><<<nblk(n,256), 256, 0, s>>>(n, dinv, x, y);
+}
 void launch_bjac_apply(int n, const float* dinv, const double* x, double* y, hipStream_t s)
-{ if(n > 0) k_bjac_apply<float><<<nblk(n,256), 256, 0, s>>>(n, dinv, x, y); }
+{
+	if(n <= 0) return;
+	if(FVHIP_BLOCK_ROWS) k_bjac_apply_rows<float><<<nblk(4LL*n,256), 256, 0, s>>>(n, dinv, x, y);
+	else k_bjac_apply<float><<<nblk(n,256), 256, 0, s>>>(n, dinv, x, y);
+}
 void launch_to_single(long long n, const double* a, float* b, hipStream_t s)
 { if(n > 0) k_to_single<<<nblk(n/4,256), 256, 0, s>>>(n, a, b); }
 void launch_bjac_correct(int n, const double* dinv, const double* b, const double* y, double* z, hipStream_t s)

@@ -28,16 +28,17 @@ def main():
     mesh, _ = c4_mesh(fa, args.scale)
     p = cases.physics("naca")
     res = {}
-    for lines in (True, False):
+    for key, extra in (("lines", dict(prec_lines=True)), ("pbj", dict()), ("pbj2", dict(prec_sweeps=2)),
+                       ("gs", dict(prec_gs=True, prec_sweeps=2))):
         sp = fa.FlowFV(mesh, p, cases.numerics("ROE", "LEASTSQUARES", "VANALBADA"), device=0)
         u0 = np.tile(cases.freestream(p), (mesh.nelem, 1))[sp.permutation()]
         du = torch.tensor(u0, dtype=torch.float64, device="cuda")
         torch.cuda.synchronize()
+        kw = dict(prec_sweeps=1, **extra) if "prec_sweeps" not in extra else dict(extra)
         cfg = fa.ImplicitConfig(cflinit=25.0, cflfin=25.0, tol=0.0, maxiter=args.steps, lin_rtol=1e-2, lin_maxit=30,
-                                restart=30, prec_sweeps=1, prec_lines=lines)
+                                restart=30, **kw)
         st, hist = sp.steady_backward_euler_device(du.data_ptr(), cfg)
         sp.synchronize()
-        key = "lines" if lines else "pbj"
         res[key + "_u"] = du.cpu().numpy()
         res[key + "_hist"] = np.asarray(hist, dtype=np.float64)
         res[key + "_lin"] = np.asarray([st["lin_iters"]])
