@@ -146,7 +146,7 @@ struct fvhip_ctx
 	size_t raw_cap = 0;
 	double* rawScratch(size_t doubles) {
 		if(raw_cap < doubles) {
-			if(d_raw) release(d_raw);
+			if(d_raw) { HC(hipStreamSynchronize(stream)); release(d_raw); }   // no transfer still reading it
 			d_raw = dalloc(doubles, owned);
 			raw_cap = doubles;
 		}
