@@ -9,7 +9,7 @@ import os
 import sys
 import time
 
-ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 sys.path.insert(0, os.path.join(ROOT, "tests"))
 import numpy as np
@@ -39,6 +39,7 @@ def main():
     sp1 = fa.FlowFV(mesh, p, cases.numerics(args.init_flux, "NONE", "NONE", order2=False))
     sp2 = fa.FlowFV(mesh, p, cases.numerics("ROE", "LEASTSQUARES", args.rec))
     du = torch.tensor(np.tile(cases.freestream(p), (mesh.nelem, 1))[sp2.permutation()], device="cuda")
+    torch.cuda.synchronize()      # torch's stream vs the library's (non-blocking) streams
     lin = dict(lin_rtol=1e-2, lin_maxit=40, restart=40, prec_sweeps=1, min_relax=0.2, prec_lines=args.lines)
     print("cells", mesh.nelem, dims, flush=True)
     t_start = time.perf_counter()
