@@ -666,9 +666,11 @@ def main():
                 ("c4_first_order_converged.txt",
                  "first-order Roe, point-block Jacobi, GMRES(40), expResidualRamp CFL 5 -> 200"))
         for key, (fname, stage) in zip(("c4_converged_run", "c4_converged_run_wall1e-3"), runs):
-            conv = os.path.join(ROOT, "profiles", "r02", fname)
-            if not os.path.exists(conv):
+            import glob
+            found = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*", fname)))   # the newest round's run
+            if not found:
                 continue
+            conv = found[-1]
             last = json.loads(open(conv).read().strip().splitlines()[-1])
             st = last["stages"][0]
             recorded[key] = {
