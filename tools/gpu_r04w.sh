@@ -1,5 +1,5 @@
 #!/bin/bash
-# round-4 call v: the round-2 convergence run of the full C4 at 1e-3 wall spacing repeated on the round-4 code
+# round-4 call w: the round-2 convergence run of the full C4 at 1e-3 wall spacing repeated on the round-4 code
 # (first-order Roe, point-block Jacobi, GMRES(40), expResidualRamp CFL 5 -> 200, to a 1e-6 drop from the peak)
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
