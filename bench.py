@@ -649,7 +649,8 @@ def main():
                 start["second_from"] = "start"
             implicit = next(implicit_steps(mesh, {"config5": "visc-c5", "config3": "plate"}.get(args.numerics, "naca"),
                                            steps=3, warmup=1, sweeps=1, lines=True,
-                                           operators=((True,) if args.numerics == "config3" else (False,)),
+                                           # BASELINE configs 3 and 5 name the matrix-free operator
+                                           operators=((True,) if args.numerics in ("config3", "config5") else (False,)),
                                            **start, **kw))
             implicit.pop("faces", None)
         except Exception as e:          # N GPUs: report, do not lose the residual measurement
