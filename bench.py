@@ -28,6 +28,7 @@ import time
 
 import numpy as np
 
+T_PROCESS = time.time()       # wall-clock phases of the run are reported from here (out["phases_s"])
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 sys.path.insert(0, os.path.join(ROOT, "tests"))
@@ -100,22 +101,23 @@ def kernel_bytes(label, N, F, Fb, numerics="headline"):
     for the one-launch residual and for the staged sweep -- they perform the same operation; the
     one-launch kernel's own compulsory traffic is lower (residual_algorithmic_bytes: gradients stay
     in LDS), which is why it is faster, not a different amount of algorithmic work"""
-    if numerics in ("config3", "config4"):
+    if numerics in ("config3", "config4", "config5"):
         return config4_algorithmic_bytes(N, F, Fb)
     return sweep_algorithmic_bytes(N, F, Fb)
 
 
 def kernel_symbol(label, numerics="headline"):
     """profiling label -> rocprofv3 kernel symbol suffix of the Roe/MUSCL/dt (headline, config2), HLLC/linear/
-    Sutherland/dt (config3), Roe/linear/Venkatakrishnan/dt (config4) or Roe/MUSCL/Sutherland/dt (config5)
+    Sutherland/dt (config3), Roe/linear/Venkatakrishnan/dt (config4) or Roe/linear/Sutherland/dt (config5: the
+    visc-naca0012 deck's `limiter none`)
     instantiation (template arguments: include/fvhip.h's flux codes, kernels.hpp's SweepRec / SweepVisc)"""
     if label.startswith("k_residual_wls"):
         return {"headline": "k_residual_wls<4, 1, true, 0, 0>", "config2": "k_residual_wls<4, 1, true, 0, 0>",
                 "config3": "k_residual_wls<6, 2, true, 1, 0>", "config4": "k_residual_wls<4, 2, true, 0, 2>",
-                "config5": "k_residual_wls<4, 1, true, 1, 0>"}[numerics]
+                "config5": "k_residual_wls<4, 2, true, 1, 0>"}[numerics]
     return {"headline": "k_sweep<4, 1, 0, true, false>", "config2": "k_sweep<4, 1, 0, true, false>",
             "config3": "k_sweep<6, 2, 1, true, false>", "config4": "k_sweep<4, 2, 0, true, true>",
-            "config5": "k_sweep<4, 1, 1, true, false>"}[numerics]
+            "config5": "k_sweep<4, 2, 1, true, false>"}[numerics]
 
 
 def pmc_traffic(kernel_symbol, workload_cells):
@@ -388,6 +390,10 @@ def main():
                          "coordinate bisection")
     ap.add_argument("--no-pipelined", action="store_true", help="skip the pipelined staged path")
     ap.add_argument("--no-implicit", action="store_true", help="skip the implicit-step figure (1 GPU only)")
+    ap.add_argument("--implicit-deadline", type=float, default=300.0,
+                    help="N GPUs: wall-clock seconds the implicit-step section may take; past it (or when any rank "
+                         "fails in it) rank 0 prints the line with implicit_step = {'error': ...} and every rank exits, "
+                         "so a rank stuck in a collective cannot lose the residual measurement")
     ap.add_argument("--preheat-ms", type=float, default=400.0,
                     help="untimed steps for this long (wall clock) after the warm-up steps of the primary path, "
                          "so the timed steps run at the clock the GPU holds under this load (reported)")
@@ -397,8 +403,8 @@ def main():
                          "SURVEY's C2 (229,376 cells); config3: BASELINE config 3, the laminar flat plate "
                          "(1024 x 1024 quads, M 0.2, Re 8.7e5), HLLC + WLS + unlimited linear + Sutherland viscous flux, "
                          "implicit figure matrix-free; config5: BASELINE config 5, the laminar NACA0012 "
-                         "(M 0.5, Re 5000) on the 8.1M-cell C5 O-grid (C4 with 4096 cells around), Roe + WLS + "
-                         "MUSCL/Van Albada + Sutherland viscous flux")
+                         "(M 0.5, Re 5000, alpha 0) on the 8.1M-cell C5 O-grid (C4 with 4096 cells around), Roe + WLS + "
+                         "unlimited linear reconstruction (the deck's limiter none) + Sutherland viscous flux")
     args = ap.parse_args()
 
     # one process per GPU: under torchrun WORLD_SIZE must agree with --gpus; without it, --gpus N > 1
@@ -424,19 +430,31 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    phases = {"start_to_main": round(time.time() - T_PROCESS, 2)}
+
+    def phase(name, t_start):
+        phases[name] = round(time.time() - t_start, 2)
+
+    tl = time.time()
     import torch
+    ctrl = None
     if world > 1:
         import torch.distributed as dist
         torch.cuda.set_device(0 if args.rehearse_one_gpu else local_rank)
         dist.init_process_group("nccl", init_method="env://")
+        # a host-side (gloo) group for agreeing on the implicit section's outcome: it does not queue
+        # behind RCCL work a failed rank left half done
+        ctrl = dist.new_group(backend="gloo")
     else:
         dist = None
         torch.cuda.set_device(0)
+    phase("launch", tl)
 
     import fvens_amd as fa
     import cases
 
     t0 = time.time()
+    tm = time.time()
     mult = world if (world > 1 and args.scaling == "weak") else 1
     if args.numerics == "config5":
         mult *= 2
@@ -452,11 +470,13 @@ def main():
         mesh, dims = c4_mesh(fa, args.scale, mult)
     kind = {"config5": "visc", "config3": "plate"}.get(args.numerics, "naca")
     p = cases.physics(kind)
-    rec = {"config4": "VENKATAKRISHNAN", "config3": "NONE"}.get(args.numerics, "VANALBADA")
+    # config 5 = testcases/visc-naca0012/laminar-implicit.ctrl: limiter none (:72), alpha 0 (:19, cases.physics)
+    rec = {"config4": "VENKATAKRISHNAN", "config3": "NONE", "config5": "NONE"}.get(args.numerics, "VANALBADA")
     flux = "HLLC" if args.numerics == "config3" else "ROE"
     n = cases.numerics(flux, "LEASTSQUARES", rec)
     u = cases.state(mesh, p, seed=42)
     N, F, Fb = mesh.nelem, mesh.naface, mesh.nbface
+    phase("mesh", tm)
     part = None
     partinfo = None
     if world > 1:
@@ -476,6 +496,7 @@ def main():
                     "edge_cut": fa.partition_edge_cut(mesh, part),
                     "edge_cut_rcb": fa.partition_edge_cut(mesh, fa.partition_rcb(mesh, world)),
                     "partition_s": round(tp, 2)}
+        phases["partition"] = round(tp, 2)
 
     def new_uid():
         """a fresh RCCL unique id for every communicator (an id bootstraps exactly one)"""
@@ -494,6 +515,7 @@ def main():
         preheat_ms: after the warm-up steps, further untimed steps for that long (all ranks run the
         same count), outside the timed region"""
         n.fast_math = fast
+        tlay = time.time()
         if world > 1:
             sp = fa.FlowFV(mesh, p, n, device=torch.cuda.current_device(), partition=part, rank=rank)
             sp.comm_init(world, rank, new_uid())
@@ -501,6 +523,7 @@ def main():
         else:
             sp = fa.FlowFV(mesh, p, n, device=torch.cuda.current_device())
             owned = np.arange(N)
+        layout_s = round(time.time() - tlay, 2)
         gint = owned[sp.permutation()]
         du = torch.zeros((sp.nown + sp.nghost, 4), dtype=torch.float64, device="cuda")
         du[:sp.nown] = torch.tensor(u[gint], device="cuda")
@@ -549,7 +572,7 @@ def main():
             step()
         kt = sp.kernel_times()
         sp.profile(False)
-        stats = sp.layout_stats()
+        stats = dict(sp.layout_stats(), layout_s=layout_s)
         if dist is not None:
             dist.barrier()
         sp.close()
@@ -568,7 +591,9 @@ def main():
     # leaves it idle for ~1 s; the primary (library default) path is timed last
     fast = None
     if not args.no_fast:
+        tpa = time.time()
         fms, fk, stats = measure(True, preheat_ms=args.preheat_ms)
+        phase("path_fast", tpa)
         cnt = (stats["cells"], stats["faces"], stats["bfaces"])
         fname, fsms = dominant(fk)
         fab = kernel_bytes(fname, *cnt, args.numerics) / (fsms * 1e-3) / 1e9
@@ -581,7 +606,9 @@ def main():
                              "(tests/test_gpu_residual.py::test_fast_math_within_tolerance)"}
     # the two-kernel path (WLS gradient kernel + face sweep), same results bit for bit: one after
     # the other, and pipelined (gradient chunks overlapped with the sweep groups on a second stream)
+    tpa = time.time()
     sms, sk, stats = measure(False, "staged", preheat_ms=args.preheat_ms)
+    phase("path_staged", tpa)
     # this rank's algorithmic bytes (its owned cells, its faces incl. both copies of cut faces)
     cnt = (stats["cells"], stats["faces"], stats["bfaces"])
     sname, ssweep = [(k, v) for k, v in sk.items() if k.startswith("k_sweep")][0]
@@ -591,7 +618,9 @@ def main():
               "sweep_algorithmic_bytes": sweep_algorithmic_bytes(*cnt)}
     pipelined = None
     if world == 1 and not args.no_pipelined:
+        tpa = time.time()
         pms, pk, _ = measure(False, "pipelined", preheat_ms=args.preheat_ms)
+        phase("path_pipelined", tpa)
         pipelined = {"ms_per_step": round(pms, 5), "value": round(F / (pms * 1e-3) / 1e6, 3),
                      "kernels_ms_summed_over_chunks": {k: round(v, 5) for k, v in pk.items()},
                      "hbm_GBs_both_kernels": round((sweep_algorithmic_bytes(*cnt) + prep_algorithmic_bytes(*cnt))
@@ -599,7 +628,9 @@ def main():
     # the primary measurement: the library's default path for this configuration, after a wall-clock
     # pre-heat (untimed, reported): layout set-up between the secondary measurements leaves the GPU
     # idle for ~1 s, and a 20-step timed region (~6 ms) would otherwise run while the clocks ramp
+    tpa = time.time()
     ms_per_step, kernels_ms, stats = measure(False, preheat_ms=args.preheat_ms)
+    phase("path_primary", tpa)
     preheat = measure.preheat
 
     halo = None
@@ -612,12 +643,14 @@ def main():
         allstats = [None] * world
         dist.all_gather_object(allstats, stats)
         halo["layout_per_rank"] = [{k: st[k] for k in ("cells", "ghosts", "neighbours", "send_rows",
-                                                        "patches", "interior_patches")} for st in allstats]
+                                                        "patches", "interior_patches", "layout_s")} for st in allstats]
         if args.scaling == "strong":
+            thp = time.time()
             try:
                 halo["halo_parity"] = halo_parity(fa, torch, dist, mesh, p, n, u, part, rank, world, new_uid)
             except Exception as e:          # report, do not lose the measurement
                 halo["halo_parity"] = "error: %s" % e
+            phase("halo_parity", thp)
     sweep_name, sweep_ms = dominant(kernels_ms)
     sweep_name = [sweep_name]
 
@@ -625,38 +658,6 @@ def main():
     achieved = ab / (sweep_ms * 1e-3) / 1e9
     value = F / (ms_per_step * 1e-3) / 1e6       # every face of the (global) mesh once per step
 
-    # secondary figure: the device implicit pseudo-time step (SURVEY 8(f) rank 1; BASELINE configs 3-5) on the
-    # same mesh -- residual, analytic Jacobian, GMRES(30) with the line-implicit preconditioner, update --
-    # with a first-order start, from the free stream and after that start (IMPLICIT_START); on N GPUs every rank its partition's piece (lines cut at
-    # rank boundaries, GMRES dot products through ncclAllReduce), the slowest rank's time
-    implicit = None
-    if not args.no_implicit:
-        sys.path.insert(0, os.path.join(ROOT, "tools"))
-        from bench_implicit import implicit_steps
-        kw = {}
-        if world > 1:
-            def allmax(x):
-                t = torch.tensor([x], dtype=torch.float64, device="cuda")
-                dist.all_reduce(t, op=dist.ReduceOp.MAX)
-                return float(t.item())
-            kw = dict(part=part, rank=rank, world=world, new_uid=new_uid, allmax=allmax)
-        try:
-            start = dict(IMPLICIT_START)
-            if args.numerics == "config3":
-                # the flat plate's free stream is a steady state of the density residual up to rounding (its
-                # second-order residual there is ~1e-16): a ratio from it means nothing, so the steps are
-                # timed after the first-order start (one step: its first-order residual is exactly 0)
-                start["second_from"] = "start"
-            implicit = next(implicit_steps(mesh, {"config5": "visc-c5", "config3": "plate"}.get(args.numerics, "naca"),
-                                           steps=3, warmup=1, sweeps=1, lines=True,
-                                           # BASELINE configs 3 and 5 name the matrix-free operator
-                                           operators=((True,) if args.numerics in ("config3", "config5") else (False,)),
-                                           **start, **kw))
-            implicit.pop("faces", None)
-        except Exception as e:          # N GPUs: report, do not lose the residual measurement
-            if world == 1:
-                raise
-            implicit = {"error": str(e)}
     # recorded (NOT measured by this run): the committed full-size convergence runs of the same
     # device solver (~10 min each), kept apart from the measured figures
     recorded = None
@@ -704,6 +705,35 @@ def main():
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline(mesh, u, args.cpu_sweeps, rec, kind, flux)
 
+    # secondary figure: the device implicit pseudo-time step (SURVEY 8(f) rank 1; BASELINE configs 3-5) on the
+    # same mesh -- residual, analytic Jacobian, GMRES(30) with the line-implicit preconditioner, update --
+    # with a first-order start, from the free stream and after that start (IMPLICIT_START); on N GPUs every
+    # rank its partition's piece (lines cut at rank boundaries, GMRES dot products through ncclAllReduce), the
+    # slowest rank's time. It runs last, after the line's other fields are final.
+    def implicit_section():
+        sys.path.insert(0, os.path.join(ROOT, "tools"))
+        from bench_implicit import implicit_steps
+        kw = {}
+        if world > 1:
+            def allmax(x):
+                t = torch.tensor([x], dtype=torch.float64, device="cuda")
+                dist.all_reduce(t, op=dist.ReduceOp.MAX)
+                return float(t.item())
+            kw = dict(part=part, rank=rank, world=world, new_uid=new_uid, allmax=allmax)
+        start = dict(IMPLICIT_START)
+        if args.numerics == "config3":
+            # the flat plate's free stream is a steady state of the density residual up to rounding (its
+            # second-order residual there is ~1e-16): a ratio from it means nothing, so the steps are
+            # timed after the first-order start (one step: its first-order residual is exactly 0)
+            start["second_from"] = "start"
+        im = next(implicit_steps(mesh, {"config5": "visc-c5", "config3": "plate"}.get(args.numerics, "naca"),
+                                 steps=3, warmup=1, sweeps=1, lines=True,
+                                 # BASELINE configs 3 and 5 name the matrix-free operator
+                                 operators=((True,) if args.numerics in ("config3", "config5") else (False,)),
+                                 **start, **kw))
+        im.pop("faces", None)
+        return im
+
     if rank == 0:
         # template of the timed sweep: k_residual_wls<FLUX=ROE(4), REC=MUSCL(1), DT, VISC=none(0), LIM=0>
         # (config4: REC=linear(2), LIM=Venkatakrishnan(2))
@@ -715,8 +745,9 @@ def main():
               "config3": "flat plate (1024 x 1024 quads), laminar M 0.2 Re 8.7e5, HLLC + WLS gradients + unlimited "
                          "linear + Sutherland viscous flux, BASELINE config 3's numerics",
               "config4": "C4 mesh, Roe + WLS gradients + Venkatakrishnan (K = 20), BASELINE config 4's numerics",
-              "config5": "C5 mesh (8.1M cells), laminar M 0.5 Re 5000, Roe + WLS gradients + MUSCL/Van Albada + "
-                         "Sutherland viscous flux, BASELINE config 5's numerics"}[args.numerics]
+              "config5": "C5 mesh (8.1M cells), laminar M 0.5 Re 5000 alpha 0, Roe + WLS gradients + unlimited linear "
+                         "reconstruction + Sutherland viscous flux, BASELINE config 5's numerics "
+                         "(visc-naca0012/laminar-implicit.ctrl)"}[args.numerics]
         out = {
             "metric": "Mfaces/s (flux+residual sweep) + achieved HBM GB/s, 1/2/4/8 MI355X",
             "value": round(value, 3),
@@ -755,7 +786,7 @@ def main():
                          "kernel": sweep_name[0] if sweep_name else None,
                          "kernel_ms": round(sweep_ms, 5), "algorithmic_bytes": ab,
                          "bytes_basis": ("SURVEY.md 8(d) 32F + 144N + 48Fb (124.0 B/face) + 8N time step"
-                                         if args.numerics not in ("config3", "config4") else
+                                         if args.numerics not in ("config3", "config4", "config5") else
                                          "SURVEY.md 8(d) linear reconstruction (config4: + Venkatakrishnan): "
                                          "48F + 144N + 48Fb + 8N time step"),
                          "frac_area_dt_basis": round(sweep_bytes_area_dt(*cnt) / (sweep_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
@@ -771,13 +802,67 @@ def main():
             "fast_math": fast,
             "staged_path": staged,
             "pipelined_path": pipelined,
-            "implicit_step": implicit,
+            "implicit_step": None,
             "recorded": recorded,
             "build": fa._ffi.build_info(),
         }
-        print(json.dumps(out))
+    ti = time.time()
+    if args.no_implicit:
+        implicit = None
+    elif world == 1:
+        implicit = implicit_section()
+    else:
+        implicit = guarded_implicit(implicit_section, args.implicit_deadline, dist, ctrl, rank,
+                                    lambda im: emit(out, im, phases, ti) if rank == 0 else None)
+    if not args.no_implicit:
+        phase("implicit", ti)
+    if rank == 0:
+        emit(out, implicit, phases, None)
     if dist is not None:
         dist.destroy_process_group()
+
+
+def emit(out, implicit, phases, t_implicit):
+    """rank 0's one JSON line: the measurement with the implicit figure (or its error) and the wall-clock
+    phases of this process (t_implicit: start of an implicit section cut short by its deadline)"""
+    if t_implicit is not None:
+        phases = dict(phases, implicit=round(time.time() - t_implicit, 2))
+    out["implicit_step"] = implicit
+    out["phases_s"] = dict(phases, total=round(time.time() - T_PROCESS, 2))
+    print(json.dumps(out), flush=True)
+
+
+def guarded_implicit(section, deadline_s, dist, ctrl, rank, on_deadline):
+    """N ranks: run the implicit section (collectives over RCCL) so that its failure cannot lose the line.
+    A rank whose section raises keeps the error; the ranks then agree over the host-side gloo group `ctrl`
+    (an error anywhere is an error everywhere). A rank stuck in a collective -- its peer failed, or a
+    transport hangs -- never reaches the agreement: when `deadline_s` passes, every rank's timer fires,
+    rank 0 prints the line with the error (on_deadline) and every process exits at once."""
+    import threading
+    import torch
+
+    def expire():
+        try:
+            on_deadline({"error": "implicit section did not finish on every rank within %.0f s" % deadline_s})
+        finally:
+            sys.stdout.flush()
+            sys.stderr.flush()
+            os._exit(0)
+    timer = threading.Timer(deadline_s, expire)
+    timer.daemon = True
+    timer.start()
+    try:
+        im, err = section(), None
+    except Exception as e:
+        im, err = None, "rank %d: %s" % (rank, e)
+    flag = torch.tensor([0.0 if err is None else 1.0 + rank], dtype=torch.float64)
+    dist.all_reduce(flag, op=dist.ReduceOp.MAX, group=ctrl)
+    timer.cancel()
+    if err is not None:
+        return {"error": err}
+    if flag.item() > 0:
+        return {"error": "rank %d failed in the implicit section" % (int(flag.item()) - 1)}
+    return im
 
 
 if __name__ == "__main__":

@@ -19,7 +19,7 @@ def physics(kind, aoa_deg=0.0, Minf=None):
     """Physics + BCs of the reference test decks.
     'cyl'   inviscid cylinder, tests/inv-2dcyl/inv-cyl-base.ctrl (slipwall 2, farfield 4, M 0.38)
     'naca'  transonic NACA0012, testcases/naca0012/transonic-sanity-test-muscl.ctrl (M 0.8, 1.25 deg)
-    'visc'  laminar NACA0012, testcases/visc-naca0012/laminar-implicit.ctrl (Re 5000, M 0.5)
+    'visc'  laminar NACA0012, testcases/visc-naca0012/laminar-implicit.ctrl (Re 5000, M 0.5, alpha 0: :19-31)
     'plate' flat plate, tests/visc-flatplate/flatplate.ctrl (M 0.2, Re 8.7e5, T 290.19 K, Pr 0.708)
     'wall'  tests/flow-general/test.ctrl (farfield 4, adiabatic 2, isothermal 3; M 0.5, Re 5000);
             the deck's wall temperature 290 is used as a non-dimensional value by abc.cpp:349-366,
@@ -34,7 +34,7 @@ def physics(kind, aoa_deg=0.0, Minf=None):
                                  bcconf=[FlowBCConfig("slipwall", 2), FlowBCConfig("farfield", 4)])
     if kind == "visc":
         return FlowPhysicsConfig(gamma=1.4, Minf=Minf or 0.5, Tinf=288.15, Reinf=5000.0, Pr=0.72,
-                                 aoa=1.0 * d2r, viscous_sim=True,
+                                 aoa=aoa_deg * d2r, viscous_sim=True,
                                  bcconf=[FlowBCConfig("adiabaticwall", 2, [0.0]),
                                          FlowBCConfig("inflowoutflow", 4)])
     if kind == "viscconst":

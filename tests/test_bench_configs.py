@@ -12,7 +12,7 @@ import bench  # noqa: E402
 
 # numerics -> (flux code, SweepRec, SweepVisc, limiter): ROE 4, HLLC 6; MUSCL 1, linear 2; Sutherland 1
 EXPECT = {"headline": (4, 1, 0, 0), "config2": (4, 1, 0, 0), "config3": (6, 2, 1, 0),
-          "config4": (4, 2, 0, 2), "config5": (4, 1, 1, 0)}
+          "config4": (4, 2, 0, 2), "config5": (4, 2, 1, 0)}
 
 
 def test_kernel_symbols_match_numerics():

@@ -126,11 +126,12 @@ def test_partitioned_c4_eight_ranks(rec):
 
 def test_partitioned_c5_eight_ranks():
     """BASELINE config 5 at its full size on the partitioned path: the 8,126,464-cell C5 O-grid (4096
-    cells around, 1e-5 wall spacing), laminar Roe + WLS + Van Albada + Sutherland (the fused viscous
-    kernel on the two-layer halo), split 8 ways by the cost-weighted graph partitioner, all ranks in one
+    cells around, 1e-5 wall spacing), laminar Roe + WLS + unlimited linear + Sutherland at alpha 0 (the
+    visc-naca0012 deck's numerics, laminar-implicit.ctrl:19,72; the fused viscous kernel on the two-layer
+    halo), split 8 ways by the cost-weighted graph partitioner, all ranks in one
     process with the overlapped schedule -- every owned row's residual and time step bitwise the
     single-GPU ones (the same device code evaluates Sutherland's law on both sides)"""
-    r, dt, r1, dt1, stats = run_partitioned("naca_c5", "visc", "ROE", "LEASTSQUARES", "VANALBADA", True, 8,
+    r, dt, r1, dt1, stats = run_partitioned("naca_c5", "visc", "ROE", "LEASTSQUARES", "NONE", True, 8,
                                             partitioner="graph-cost")
     assert r.shape[0] == 8126464
     np.testing.assert_array_equal(r, r1)

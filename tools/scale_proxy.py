@@ -60,7 +60,8 @@ def main():
     from bench import c4_mesh
     mesh, dims = c4_mesh(fa, args.scale, 2 if args.config5 else 1)
     p = cases.physics("visc" if args.config5 else "naca")
-    n = cases.numerics("ROE", "LEASTSQUARES", args.rec)
+    # config 5: the visc-naca0012 deck's limiter none (laminar-implicit.ctrl:72)
+    n = cases.numerics("ROE", "LEASTSQUARES", "NONE" if args.config5 else args.rec)
     u = cases.state(mesh, p, seed=42)
     N = mesh.nelem
     one = fa.FlowFV(mesh, p, n)
