@@ -104,7 +104,7 @@ class ImplicitConfig:
 def _solve_stats(st, hist):
     n = int(st.steps)
     return dict(steps=n, converged=bool(st.converged), lin_iters=int(st.lin_iters), resratio=float(st.resratio),
-                cfl=float(st.cfl)), hist[:n]
+                cfl=float(st.cfl), lin_unconverged=int(st.lin_unconverged), lin_worst=float(st.lin_worst)), hist[:n]
 
 
 class UMesh:

@@ -45,7 +45,8 @@ class FvImplicitConfig(ctypes.Structure):
 
 class FvSolveStats(ctypes.Structure):
     _fields_ = [("steps", ctypes.c_int), ("converged", ctypes.c_int), ("lin_iters", ctypes.c_int),
-                ("resratio", ctypes.c_double), ("cfl", ctypes.c_double)]
+                ("resratio", ctypes.c_double), ("cfl", ctypes.c_double), ("lin_unconverged", ctypes.c_int),
+                ("lin_worst", ctypes.c_double)]
 
 
 _vpp = ctypes.POINTER(ctypes.c_void_p)

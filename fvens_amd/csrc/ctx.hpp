@@ -917,8 +917,13 @@ struct fvhip_ctx
 				all.push_back(std::move(piece));
 			}
 		}
+		// longest first; lines of equal length in ascending internal (Hilbert) order of their first cell, so
+		// that the 64 lanes of a group walk neighbouring lines side by side: their k-th cells' rows of v and
+		// z share 128-byte lines (the cells are gathered by index), instead of 64 unrelated places of the mesh.
+		// Each line's recurrence is independent of the lane it runs on: the same z bit for bit.
 		std::stable_sort(all.begin(), all.end(), [](const std::vector<std::pair<int,int>>& a,
-		                                            const std::vector<std::pair<int,int>>& b) { return a.size() > b.size(); });
+		                                            const std::vector<std::pair<int,int>>& b) {
+			return a.size() > b.size() || (a.size() == b.size() && a[0].first < b[0].first); });
 		// lanes: a line of at least LINE_TWIST_MIN cells is solved from both ends (twisted factorisation):
 		// its top half t = (n-1)/2 cells in order, then the twist cell t, on lane j of a twisted group; its
 		// bottom half n-1 .. t+1 in reverse order, then t, on lane j+32. Every other line is one lane of a

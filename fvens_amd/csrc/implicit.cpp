@@ -391,8 +391,8 @@ static void backwardEuler(System& S, const std::vector<double*>& us, const fvhip
 	const ArrayOf bs = [&](size_t i) { return S.hs[i]->d_r; };
 	const ArrayOf xs = [&](size_t i) { return S.hs[i]->iw.du; };
 
-	double curCFL = 0, resi = 1.0, resiold = 1.0, initres = 1.0;
-	int step = 0, lin = 0;
+	double curCFL = 0, resi = 1.0, resiold = 1.0, initres = 1.0, linworst = 0.0;
+	int step = 0, lin = 0, linbad = 0;
 	while(resi/initres > c.tol && step < c.maxiter) {
 		// r = 0 + (-r(u)) with local time steps (:421-452); fills the ghost rows of u
 		fvhip_ctx::residual_seq(S.hs, cu, rs, true, dts, true, S.exg);
@@ -404,6 +404,10 @@ static void backwardEuler(System& S, const std::vector<double*>& us, const fvhip
 			S.each([&](size_t i, fvhip_ctx* h) { h->mf_u = us[i]; h->mf_r = h->d_r; h->mf_mdt = h->d_dtm; });
 		const GmresOut g = gmres(S, A, bs, xs, c.lin_rtol, c.lin_maxit, c.restart);                  // :483
 		lin += g.iters;
+		if(g.rnorm0 > 0.0) {
+			linworst = std::max(linworst, g.rnorm/g.rnorm0);
+			if(g.rnorm > c.lin_rtol*g.rnorm0) linbad++;
+		}
 		S.each([&](size_t i, fvhip_ctx* h) {                                                        // :494-512
 			launch_relaxed_update(h->L.ncell, h->P.gas, c.min_relax, h->iw.du, us[i], h->stream);
 			launch_energy_sumsq(h->L.ncell, h->d_r, h->M.area, h->iw.part, h->iw.red, h->stream);   // :516-526
@@ -423,6 +427,8 @@ static void backwardEuler(System& S, const std::vector<double*>& us, const fvhip
 	st->resratio = resi/initres;
 	st->converged = (step < c.maxiter && resi/initres <= c.tol) ? 1 : 0;                            // :618-632
 	st->cfl = curCFL;
+	st->lin_unconverged = linbad;
+	st->lin_worst = linworst;
 }
 
 /// SteadyForwardEulerSolver::solve (aodesolver.cpp:135-282): u += cflinit dtm/area r (the ramped

@@ -174,8 +174,18 @@ __global__ void __launch_bounds__(256) k_grad_wls(DevMesh M, const double* __res
 /// and 2*dm*dm scale exact products (2 RN(dp dm), 2 RN(dm dm)), so each sum that adds one is an fma with
 /// the factor 2, and dp*dm is formed once for numerator and denominator; the running max / min are
 /// v_max / v_min -- they differ from the reference's compare-and-assign only in the sign of a zero
-/// dmin/dmax (max(+0, -0)), and a signed zero dp gives the same phi (dp*dp = +0, +0 + (+-0) = +0); phi
-/// is never NaN or -0 (its denominator is >= eps2 > 0, its numerator RN(x + eps2) is +0 at x = -eps2)
+/// dmin/dmax (max(+0, -0)), and a signed zero dp gives the same phi (dp*dp = +0, +0 + (+-0) = +0).
+/// FVHIP_VENK_ONEDIV (A/B experiment, off by default): one division per variable instead of one per face: the reference keeps lim = min(1, min_j RN(n_j/d_j))
+/// (`if(phiik < lim)`, NaN never taken), and rounding is monotone, so that is RN(min(1, min_j n_j/d_j)):
+/// the faces' numerators and denominators are compared exactly -- n/d < bn/bd iff n*bd < bn*d for positive
+/// denominators, decided by the rounded products and, where those tie, by their exact residuals
+/// fma(a, b, -RN(ab)) -- and only the winner is divided (the start 1/1 divides to 1 exactly). dp has dm's
+/// sign (dmin <= 0 <= dmax), so dp*dm >= 0 and n, d >= eps2 > 0; a NaN n or d compares false and is never
+/// taken, as in the reference. Exact while the products stay normal, |n|, |d| in [2^-480, 2^500]
+/// (eps2 = (K clength)^3 with K = 20: clength > 1e-48).
+#ifndef FVHIP_VENK_ONEDIV
+#define FVHIP_VENK_ONEDIV 0
+#endif
 template <bool VENK>
 __device__ __forceinline__ void cell_limiter(const double* uc, const double* g, const double (*un)[4],
                                              const double2* gp, const bool* has, double2 r, double eps2,
@@ -195,6 +205,7 @@ __device__ __forceinline__ void cell_limiter(const double* uc, const double* g, 
 			}
 		}
 		double lim = 1.0;
+		double bn = 1.0, bd = 1.0;     // Venkatakrishnan: the smallest quotient so far, 1/1 at the start
 		#pragma unroll
 		for(int j = 0; j < 4; j++) {
 			if(!has[j]) continue;
@@ -207,8 +218,13 @@ __device__ __forceinline__ void cell_limiter(const double* uc, const double* g, 
 				const double dp = dm < 0 ? dmin : dmax;
 				const double pp = dp*dp, pm = dp*dm;
 				// (dp*dp + 2*dp*dm + eps2)/(dp*dp + dp*dm + 2*dm*dm + eps2)
-				ph = div_rn(__builtin_fma(pm, 2.0, pp) + eps2, __builtin_fma(dm*dm, 2.0, pp + pm) + eps2);
-				lim = __builtin_fmin(lim, ph);
+				const double n = __builtin_fma(pm, 2.0, pp) + eps2, d = __builtin_fma(dm*dm, 2.0, pp + pm) + eps2;
+				if(FVHIP_VENK_ONEDIV) {
+					const double p1 = n*bd, p2 = bn*d;
+					bool lt = p1 < p2;
+					if(p1 == p2) lt = __builtin_fma(n, bd, -p1) < __builtin_fma(bn, d, -p2);
+					if(lt) { bn = n; bd = d; }
+				} else lim = __builtin_fmin(lim, div_rn(n, d));
 				continue;
 			} else {
 				const double diff = uf - uc[iv];
@@ -218,7 +234,7 @@ __device__ __forceinline__ void cell_limiter(const double* uc, const double* g, 
 			}
 			if(ph < lim) lim = ph;
 		}
-		out[iv] = lim;
+		out[iv] = VENK && FVHIP_VENK_ONEDIV ? div_rn(bn, bd) : lim;
 	}
 }
 

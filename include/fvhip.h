@@ -321,6 +321,9 @@ typedef struct fvhip_solve_stats {
 	int lin_iters;            /* total Krylov iterations */
 	double resratio;          /* final ||r||/||r0|| */
 	double cfl;               /* CFL of the last step */
+	int lin_unconverged;      /* linear solves that stopped at lin_maxit above lin_rtol (PETSc's
+	                             KSP_DIVERGED_ITS: not fatal, the step goes on with that update) */
+	double lin_worst;         /* largest final |b - A du| / |b| over the steps' linear solves */
 } fvhip_solve_stats;
 
 /** SteadyBackwardEulerSolver::solve (aodesolver.cpp:363-638) with the linear systems solved on the

@@ -50,6 +50,12 @@ def main():
         dist.broadcast_object_list(obj, src=0)
         return obj[0]
 
+    if os.environ.get("FVHIP_CRASHTRACE"):
+        # diagnostic: native backtrace of a crash (tools/probes/crashtrace.c), installed after every
+        # library that might set its own handlers has loaded
+        import ctypes
+        ctypes.CDLL(os.environ["FVHIP_CRASHTRACE"])
+        mark("crash tracer installed")
     rep = {"rank": rank, "world": world}
     owned = np.nonzero(part == rank)[0]
     mark("mesh and partition ready")

@@ -90,13 +90,18 @@ def test_explicit_pseudo_time_matches_oracle(tmp_path, fast):
 @pytest.mark.gpu
 @pytest.mark.parametrize("meshkey,kind,flux,grad,rec,order2", [
     ("2dcylinderhybrid.msh", "cyl", "LLF", "NONE", "NONE", False),        # BASELINE config 1 (C1-like)
+    ("c1", "cyl", "LLF", "NONE", "NONE", False),                         # BASELINE config 1 at its size: 5,120 cells
     ("naca_small", "naca", "ROE", "LEASTSQUARES", "VANALBADA", True)])
 def test_device_forward_euler_matches_oracle(meshkey, kind, flux, grad, rec, order2):
     """Device-resident explicit pseudo-time loop: state after 30 steps bitwise equal to the oracle's
-    forward Euler (the norm reduction order differs, so only the state is compared bitwise)."""
+    forward Euler (the norm reduction order differs, so only the state is compared bitwise). BASELINE
+    config 1 (inviscid cylinder, LLF, first order, explicit; tests/inv-2dcyl/inv-cyl-base.ctrl) runs on
+    SURVEY's 5,120-cell C1 O-grid as well as on the reference's 2dcylinderhybrid fixture."""
     import torch
     from test_gpu_residual import get_mesh
     m, om = get_mesh(meshkey)
+    if meshkey == "c1":
+        assert m.nelem == 5120 and m.naface == 7744
     p = cases.physics(kind)
     n = cases.numerics(flux, grad, rec, order2=order2)
     u0 = np.tile(cases.freestream(p), (m.nelem, 1))

@@ -26,6 +26,7 @@ the reference's viscous functional regression.
     sits 1.3e-6 / 3.1e-6 off in CDp / CDsf, so it runs on to a 1e-8 drop.
 """
 import os
+import sys
 
 import numpy as np
 import pytest
@@ -126,6 +127,24 @@ def test_visc_naca0012_functional_regression(matrix_free):
     assert abs(cl - CL) / abs(CL) <= 1e-3
     start.close()
     main.close()
+
+
+def test_c5_family_converges_to_deck_tolerance():
+    """BASELINE config 5's case solved to the deck's tolerance on a 1/16-size member of the C5 family
+    (tools/visc_converge.py: the C5 O-grid with 1024 cells around, 64 quadrangle and 216 triangle layers,
+    286,720 cells; laminar-implicit.ctrl's schedule -- first-order start CFL 200 -> 1000 to 1e-1, main solve
+    CFL 500 -> 5000 to a 1e-6 drop, 'full' update -- matrix-free operator, line-implicit preconditioner on
+    the first-order Jacobian). The drag components are those of the reference's 13k-cell grid
+    (regr-LeastSquares_Roe.txt) within the discretisation difference of the two meshes (5 %)."""
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tools"))
+    from visc_converge import run
+    r = run(scale=4, matrix_free=True, main_steps=300)
+    print({k: r[k] for k in ("cells", "CL", "CDp", "CDsf")}, {k: r["main"][k] for k in ("steps", "lin_iters", "resratio",
+                                                                                         "seconds", "converged")})
+    assert r["cells"] == 286720 and r["finite"]
+    assert r["main"]["converged"] and r["main"]["resratio"] <= 1e-6, r["main"]
+    CL, CDP, CDSF = REGR
+    assert abs(r["CDp"] - CDP) <= 0.05 * abs(CDP) and abs(r["CDsf"] - CDSF) <= 0.05 * abs(CDSF), (r["CDp"], r["CDsf"])
 
 
 def test_c3_implicit_matrix_free():

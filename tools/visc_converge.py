@@ -1,0 +1,94 @@
+#!/usr/bin/env python3
+"""BASELINE config 5 solved to the visc-naca0012 deck's tolerance on the C5 O-grid family with the device
+solver: testcases/visc-naca0012/laminar-implicit.ctrl's schedule -- first-order initialisation (CFL 200 ->
+1000, tolerance 1e-1, 50 steps), then the second-order main solve (Roe, least squares, limiter none,
+Sutherland; CFL 500 -> 5000 by expResidualRamp, tolerance 1e-6), 'full' nonlinear update -- with the
+matrix-free operator (BASELINE config 5) or the assembled one, preconditioned by the line-implicit
+preconditioner on the assembled first-order Jacobian (the deck's bjacobi/ILU), GMRES rtol 1e-1.
+Prints a heartbeat while the device runs, then one JSON line: the stages' steps, linear iterations,
+residual histories, wall times, and CL / CDp / CDsf on the wall (marker 2).
+usage: python tools/visc_converge.py [--scale S] [--assembled] [--main-steps N] [--lin-maxit K]"""
+import argparse
+import json
+import os
+import sys
+import threading
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, "tests"))
+
+
+def run(scale=1, matrix_free=True, main_steps=400, init_steps=50, lin_maxit=60, restart=60, sweeps=3,
+        tol=1e-6, heartbeat=None):
+    """the deck's two stages on the C5 mesh divided by `scale` in both directions; returns the record"""
+    import torch
+    import fvens_amd as fa
+    import cases
+    from bench import c4_mesh
+    mesh, dims = c4_mesh(fa, scale, 2)
+    p = cases.physics("visc")                                   # alpha 0 (laminar-implicit.ctrl:19)
+    n1 = cases.numerics("ROE", "NONE", "NONE", order2=False)
+    n2 = cases.numerics("ROE", "LEASTSQUARES", "NONE")          # limiter none (:72)
+    start, main = fa.FlowFV(mesh, p, n1), fa.FlowFV(mesh, p, n2)
+    perm = main.permutation()
+    du = torch.tensor(np.tile(cases.freestream(p), (mesh.nelem, 1))[perm], device="cuda")
+    torch.cuda.synchronize()      # torch's stream vs the library's (non-blocking) streams
+    lin = dict(lin_rtol=1e-1, lin_maxit=lin_maxit, restart=restart, prec_lines=True, prec_sweeps=sweeps,
+               min_relax=1.0)
+    rec = {"cells": mesh.nelem, "faces": mesh.naface, "dims": dims, "operator": "matrix-free" if matrix_free else "assembled",
+           "linear": dict(lin, gmres="GMRES(%d) right-preconditioned" % restart)}
+    done = threading.Event()
+
+    def beat():
+        t0 = time.time()
+        while not done.wait(20.0):
+            if heartbeat:
+                heartbeat("running %.0f s" % (time.time() - t0))
+    th = threading.Thread(target=beat, daemon=True)
+    th.start()
+    try:
+        t0 = time.perf_counter()
+        st0, h0 = start.steady_backward_euler_device(du.data_ptr(), fa.ImplicitConfig(
+            cflinit=200.0, cflfin=1000.0, tol=1e-1, maxiter=init_steps, **lin))
+        torch.cuda.synchronize()
+        t1 = time.perf_counter()
+        st, h = main.steady_backward_euler_device(du.data_ptr(), fa.ImplicitConfig(
+            cflinit=500.0, cflfin=5000.0, tol=tol, maxiter=main_steps, matrix_free=matrix_free, **lin))
+        torch.cuda.synchronize()
+        t2 = time.perf_counter()
+    finally:
+        done.set()
+    (cl, cdp, cdsf), _ = main.surface_data_device(du.data_ptr(), 2)
+    finite = bool(torch.isfinite(du).all().item())
+    start.close()
+    main.close()
+    rec.update({
+        "init": {**st0, "seconds": round(t1 - t0, 2), "history": [float(x) for x in h0]},
+        "main": {**st, "seconds": round(t2 - t1, 2), "ms_per_step": round((t2 - t1) / max(st["steps"], 1) * 1e3, 2),
+                 "history": [float(x) for x in h]},
+        "CL": cl, "CDp": cdp, "CDsf": cdsf, "finite": finite})
+    return rec
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--scale", type=int, default=1)
+    ap.add_argument("--assembled", action="store_true")
+    ap.add_argument("--main-steps", type=int, default=400)
+    ap.add_argument("--lin-maxit", type=int, default=60)
+    ap.add_argument("--restart", type=int, default=60)
+    ap.add_argument("--sweeps", type=int, default=3)
+    args = ap.parse_args()
+    import torch
+    torch.cuda.set_device(0)
+    r = run(args.scale, not args.assembled, args.main_steps, lin_maxit=args.lin_maxit, restart=args.restart,
+            sweeps=args.sweeps, heartbeat=lambda s: print(s, flush=True))
+    print(json.dumps(r), flush=True)
+
+
+if __name__ == "__main__":
+    main()
