@@ -1141,6 +1141,12 @@ __device__ __forceinline__ void fused_limit_row(const DevMesh& M, const DevPhys&
 #define FZ_CLOCK(B, k) do {} while(0)
 #endif
 
+#ifndef FVHIP_FZ_FENCE_PROBE
+#define FVHIP_FZ_FENCE_PROBE 0
+#endif
+#if FVHIP_FZ_FENCE_PROBE
+__device__ int g_fz_fence_flag[1 << 16];
+#endif
 #ifndef FVHIP_FZ_VISC_FENCE
 #define FVHIP_FZ_VISC_FENCE 1
 #endif
@@ -1471,6 +1477,16 @@ __device__ __forceinline__ void fz_body(const DevMesh& M, const DevPhys& P, cons
 	double carea = 0.0;
 	if(c < q.c1) { cs = M.fz_cslot16[c]; if(DT) carea = M.area[c]; }
 	__syncthreads();   // all staged rows read: reuse LDS for the face fluxes
+#if FVHIP_FZ_FENCE_PROBE
+	// cost probe of cross-block publication (one-computation cut faces): the agent-scope
+	// release a producer patch needs after storing its cut-face fluxes (buffer_wbl2 sc1: this XCD's dirty L2
+	// lines written back) and the acquire a consumer needs before reading them (buffer_inv sc1), once per
+	// block, with no data and no waiting -- a lower bound on that design's synchronisation cost
+	if(t == 0) {
+		__hip_atomic_store(&g_fz_fence_flag[q.p & 0xFFFF], 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+		(void)__hip_atomic_load(&g_fz_fence_flag[(q.p + 1) & 0xFFFF], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
+	}
+#endif
 	double* sf = fz;
 	double* ssr = fz + 4*SLOTS_MAX;
 	if(s < q.s1) {
