@@ -60,14 +60,17 @@ Layout buildLayout(const fvhip_mesh& m, const fvhip_flow_config& cfg, bool renum
 	return buildLayout(topoFromMesh(m), cfg, renumber);
 }
 
-/// faces per patch the layout aims at: SLOTS_MAX, or FVHIP_PATCH_SLOTS (64..SLOTS_MAX) from the
-/// environment (an experiment knob: fewer slots per patch = more patches for small meshes)
+/// faces per patch the layout aims at: SLOTS_MAX (the block size), or an experiment build's
+/// FVHIP_PATCH_SLOTS (64..SLOTS_MAX: fewer faces per patch in blocks of SLOTS_MAX threads; measured slower on
+/// every mesh, profiles/r04/patch_slots_ab.txt -- the block-matched variant is a build with FVHIP_SLOTS)
+#ifndef FVHIP_PATCH_SLOTS
+#define FVHIP_PATCH_SLOTS SLOTS_MAX
+#endif
 static int patchSlotCap()
 {
-	const char* e = std::getenv("FVHIP_PATCH_SLOTS");
-	if(!e || !*e) return SLOTS_MAX;
-	const int v = std::atoi(e);
-	return v < 64 ? 64 : (v > SLOTS_MAX ? SLOTS_MAX : v);
+	constexpr int v = FVHIP_PATCH_SLOTS;
+	static_assert(v >= 64 && v <= SLOTS_MAX, "FVHIP_PATCH_SLOTS must lie in [64, FVHIP_SLOTS]");
+	return v;
 }
 
 Layout buildLayout(const MeshTopo& T, const fvhip_flow_config& cfg, bool renumber)

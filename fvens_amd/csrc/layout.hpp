@@ -136,7 +136,7 @@ struct Layout
 };
 
 constexpr int FUSED_LDS_CELLS = FVHIP_FUSED_ROWS;   ///< staged cells per patch (rows of 112 B), at most
-constexpr int FUSED_LDS_CELLS_5W = 284;              ///< ... for the 5-wave inviscid kernel: 284 x 112 B = 31,808 B, five blocks within 160 KB at a 1,280-B allocation granule
+constexpr int FUSED_LDS_CELLS_5W = FVHIP_SLOTS*284/256;   ///< ... for the 5-wave inviscid kernel: 284 x 112 B = 31,808 B, five 256-thread blocks within 160 KB at a 1,280-B allocation granule (FVHIP_SLOTS = 128: ten blocks of 142 rows)
 /// the fused kernel's staged-row cap for cfg: 5 blocks of 32 KB per CU for the inviscid unlimited
 /// instantiations (compiled for 5 waves per SIMD), else FUSED_LDS_CELLS (4 blocks of 39 KB)
 int fusedRowCap(const fvhip_flow_config& cfg);
