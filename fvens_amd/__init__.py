@@ -86,6 +86,7 @@ class ImplicitConfig:
     prec_lines: bool = False        # line-implicit (block-tridiagonal along strongly coupled lines)
     line_threshold: float = 0.0     # strongest/weakest coupling ratio for a cell to join a line (0: 4)
     prec_ilu: bool = False          # block ILU(0) in multicolour order (-sub_pc_type ilu)
+    cgs_refine: int = 0             # -ksp_gmres_cgs_refinement_type: 0 never (PETSc default), 1 ifneeded, 2 always
 
     def _struct(self):
         c = _ffi.FvImplicitConfig()
@@ -98,6 +99,7 @@ class ImplicitConfig:
         c.prec_lines = int(self.prec_lines)
         c.line_threshold = float(self.line_threshold)
         c.prec_ilu = int(self.prec_ilu)
+        c.cgs_refine = int(self.cgs_refine)
         return c
 
 
@@ -272,14 +274,6 @@ class FlowFV:
             st = self.layout_stats()
             self.nown, self.nghost = st["cells"], st["ghosts"]
 
-    def set_residual_graph(self, enable=True):
-        """RCCL rank: capture the overlapped residual step in a hipGraph and replay it (fvhip_set_residual_graph);
-        enable None only queries. Returns (graphs captured, graph launches) so far"""
-        c, r = ctypes.c_int(0), ctypes.c_int(0)
-        check(_ffi.lib().fvhip_set_residual_graph(self._h, -1 if enable is None else int(bool(enable)),
-                                                  ctypes.byref(c), ctypes.byref(r)))
-        return c.value, r.value
-
     def set_rank(self, rank, nranks):
         """rank of a per-rank-mesh handle (before group use; comm_init implies it)"""
         check(_ffi.lib().fvhip_set_rank(self._h, int(rank), int(nranks)))
@@ -402,8 +396,13 @@ class FlowFV:
         st = _ffi.FvSolveStats()
         hist = np.zeros(max(int(cfg.maxiter), 1))
         c = cfg._struct()
-        check(_ffi.lib().fvhip_steady_backward_euler_device(self._h, ctypes.c_void_p(d_u), ctypes.byref(c),
-                                                            ctypes.byref(st), dptr(hist)))
+        try:
+            check(_ffi.lib().fvhip_steady_backward_euler_device(self._h, ctypes.c_void_p(d_u), ctypes.byref(c),
+                                                                ctypes.byref(st), dptr(hist)))
+        except RuntimeError as e:
+            # a diverged solve: the residual norms of the steps before the failing one travel with the error
+            e.history = hist[:int(np.count_nonzero(hist))].copy()
+            raise
         return _solve_stats(st, hist)
 
     def gmres_blocks_device(self, d_diag, d_lower, d_upper, d_b, d_x, rtol, maxit, restart=30, sweeps=1):

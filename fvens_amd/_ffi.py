@@ -40,7 +40,7 @@ class FvImplicitConfig(ctypes.Structure):
                 ("lin_rtol", ctypes.c_double), ("lin_maxit", ctypes.c_int), ("restart", ctypes.c_int),
                 ("prec_sweeps", ctypes.c_int), ("min_relax", ctypes.c_double),
                 ("prec_single", ctypes.c_int), ("prec_gs", ctypes.c_int), ("prec_lines", ctypes.c_int),
-                ("line_threshold", ctypes.c_double), ("prec_ilu", ctypes.c_int)]
+                ("line_threshold", ctypes.c_double), ("prec_ilu", ctypes.c_int), ("cgs_refine", ctypes.c_int)]
 
 
 class FvSolveStats(ctypes.Structure):
@@ -60,8 +60,6 @@ _SIGS = {
                                     ctypes.POINTER(ctypes.c_void_p)]),
     "fvhip_destroy": (ctypes.c_int, [ctypes.c_void_p]),
     "fvhip_set_rank": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_int]),
-    "fvhip_set_residual_graph": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.POINTER(ctypes.c_int),
-                                                ctypes.POINTER(ctypes.c_int)]),
     "fvhip_partition_rcb": (ctypes.c_int, [ctypes.POINTER(FvMeshView), ctypes.c_int, c_int_p]),
     "fvhip_partition_graph": (ctypes.c_int, [ctypes.POINTER(FvMeshView), ctypes.c_int, c_int_p]),
     "fvhip_partition_graph_weighted": (ctypes.c_int, [ctypes.POINTER(FvMeshView), ctypes.c_int, c_int_p, c_int_p]),

@@ -178,16 +178,6 @@ struct fvhip_ctx
 	int* d_trace_conn = nullptr;     ///< per-rank meshes: Layout::trace_conn on the device
 	double* d_tracebuf = nullptr;    ///< [nghost][4] received face traces before the unpack
 	int nsend = 0;
-	// hipGraph of the RCCL rank's overlapped residual step (fvhip_set_residual_graph): captured the first
-	// time it runs with given arguments, replayed afterwards as one hipGraphLaunch
-	bool graph_res = false;
-	hipGraphExec_t rg_exec = nullptr;
-	struct RgKey {
-		const double* u; double* r; double* dtm; bool dt, overwrite;
-		bool operator==(const RgKey& o) const { return u == o.u && r == o.r && dtm == o.dtm && dt == o.dt && overwrite == o.overwrite; }
-	} rg_key{}, rg_seen{};
-	bool rg_seen_valid = false;
-	int rg_captures = 0, rg_replays = 0;
 	// profiling
 	bool prof = false;
 	struct Rec { std::string name; hipEvent_t a, b; };
@@ -211,7 +201,6 @@ struct fvhip_ctx
 #ifdef FVHIP_PROBE_PHASES
 		dumpProbe();
 #endif
-		if(rg_exec) (void)hipGraphExecDestroy(rg_exec);
 		if(comm) (void)ncclCommDestroy(comm);
 		for(auto& r : recs) { (void)hipEventDestroy(r.a); (void)hipEventDestroy(r.b); }
 		for(hipEvent_t e : pipe_ev) (void)hipEventDestroy(e);
@@ -522,45 +511,11 @@ struct fvhip_ctx
 	/// are launched on comm_stream right behind the halo, so their blocks fill the interior launch's
 	/// last partial wave instead of forming a fraction-of-a-wave launch after it. The two launches
 	/// write disjoint cells; `stream` joins the comm stream before the residual is complete.
+	/// (Round 4 also captured this step in a hipGraph; the capture of the RCCL p2p group overflows the stack
+	/// inside the HIP runtime's graph code -- profiles/r05/graph_capture_crash.txt, DESIGN.md section 6 -- and
+	/// the host enqueue, ~26 us against ~40 us of kernels per C4/8 rank step, keeps the step GPU-bound
+	/// without it, so the path was removed.)
 	void residual_fused_overlapped(const double* u, double* r, bool dt, double* dtm, bool overwrite) {
-		if(!graph_res || prof) { residual_fused_overlapped_enqueue(u, r, dt, dtm, overwrite); return; }
-		// the step as one graph: event record/wait, pack, the ncclGroupStart..End of the exchange, the
-		// ghost gradients and both fused launches are enqueued once (~26 us of host work per C4/8 rank
-		// step, tools/enqueue_probe.py) and replayed by one hipGraphLaunch while the arguments repeat
-		const RgKey key{u, r, dtm, dt, overwrite};
-		if(!rg_exec || !(key == rg_key)) {
-			// a step with new arguments runs uncaptured once first: RCCL connects to its peers on the
-			// first send/receive (host-side set-up that must not happen inside a capture) and the
-			// launchers configure their kernels; the next call with the same arguments is captured
-			if(!(rg_seen_valid && key == rg_seen)) {
-				rg_seen = key;
-				rg_seen_valid = true;
-				residual_fused_overlapped_enqueue(u, r, dt, dtm, overwrite);
-				return;
-			}
-			if(rg_exec) { HC(hipGraphExecDestroy(rg_exec)); rg_exec = nullptr; }
-			HC(hipStreamSynchronize(stream));      // nothing of the uncaptured steps left in flight
-			ensureOverlap();
-			hipGraph_t g = nullptr;
-			HC(hipStreamBeginCapture(stream, hipStreamCaptureModeRelaxed));
-			try {
-				residual_fused_overlapped_enqueue(u, r, dt, dtm, overwrite);
-			} catch(...) {
-				(void)hipStreamEndCapture(stream, &g);
-				if(g) (void)hipGraphDestroy(g);
-				throw;
-			}
-			HC(hipStreamEndCapture(stream, &g));
-			const hipError_t e = hipGraphInstantiate(&rg_exec, g, nullptr, nullptr, 0);
-			(void)hipGraphDestroy(g);
-			HC(e);
-			rg_key = key;
-			rg_captures++;
-		}
-		HC(hipGraphLaunch(rg_exec, stream));
-		rg_replays++;
-	}
-	void residual_fused_overlapped_enqueue(const double* u, double* r, bool dt, double* dtm, bool overwrite) {
 		ensureOverlap();
 		double* uu = const_cast<double*>(u);
 		HC(hipEventRecord(ev_u, stream));                 // u as the caller left it (and r, dtm free)

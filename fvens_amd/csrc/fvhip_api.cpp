@@ -194,20 +194,6 @@ int fvhip_create(const fvhip_mesh* mesh, const fvhip_flow_config* cfg, int devic
 	});
 }
 
-int fvhip_set_residual_graph(fvhip_handle h, int enable, int* captures, int* replays)
-{
-	return guard([&] {
-		need(h, "handle");
-		if(enable >= 0) {
-			h->graph_res = enable != 0;
-			if(!h->graph_res && h->rg_exec) { HC(hipSetDevice(h->device)); HC(hipGraphExecDestroy(h->rg_exec)); h->rg_exec = nullptr; }
-			if(!h->graph_res) h->rg_seen_valid = false;
-		}
-		if(captures) *captures = h->rg_captures;
-		if(replays) *replays = h->rg_replays;
-	});
-}
-
 int fvhip_set_rank(fvhip_handle h, int rank, int nranks)
 {
 	return guard([&] {

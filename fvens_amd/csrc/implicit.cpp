@@ -40,6 +40,17 @@ struct System
 		if(exg) { exg(arr, width, 1); return; }
 		each([&](size_t i, fvhip_ctx* h) { h->exchange_rccl(arr(i), width); });
 	}
+	/// global sums of k values every handle left in its iw.red, needed on the device only: one handle
+	/// reduces over its ranks in place (ncclAllReduce, or nothing on one GPU) without a host round trip;
+	/// a group sums on the host (allsum)
+	void allsumDevice(int k) {
+		if(hs.size() == 1) {
+			fvhip_ctx* h = hs[0];
+			if(h->comm) { HC(hipSetDevice(h->device)); NC(ncclAllReduce(h->iw.red, h->iw.red, k, ncclDouble, ncclSum, h->comm, h->stream)); }
+			return;
+		}
+		allsum(k, true);
+	}
 	/// global sums of the k values every handle left in its iw.red: returned on the host and, if
 	/// to_device, present in every handle's iw.red afterwards
 	std::vector<double> allsum(int k, bool to_device) {
@@ -72,7 +83,7 @@ static void matfreeApply(System& S, const ArrayOf& x, const ArrayOf& y)
 		if(!h->mf_u || !h->mf_r || !h->mf_mdt) throw std::runtime_error("matrix-free operator: state not set");
 		launch_mdot(4LL*h->L.ncell, 0, nullptr, 0, x(i), true, h->iw.part, h->iw.red, h->stream);
 	});
-	S.allsum(1, true);
+	S.allsumDevice(1);                         // |x|^2 stays on the device (launch_pertmag reads it there)
 	std::vector<const double*> aux;
 	std::vector<double*> yg, none(S.size(), nullptr);
 	S.each([&](size_t i, fvhip_ctx* h) {
@@ -242,8 +253,10 @@ struct GmresOut { int iters; double rnorm0, rnorm; };
 
 /// Restarted GMRES(m) for A x = b, x0 = 0; stops when |b - A x| <= rtol |b| or after maxit
 /// Arnoldi steps in total (KSPSolve with -ksp_rtol, -ksp_max_it, -ksp_gmres_restart)
-static GmresOut gmres(System& S, LinOp& A, const ArrayOf& b, const ArrayOf& x, double rtol, int maxit, int m)
+static GmresOut gmres(System& S, LinOp& A, const ArrayOf& b, const ArrayOf& x, double rtol, int maxit, int m,
+                      int refine = 0)
 {
+	if(refine < 0 || refine > 2) throw std::invalid_argument("cgs_refine must be 0 (never), 1 (ifneeded) or 2 (always)");
 	auto n4 = [&](size_t i) { return 4LL*S.hs[i]->L.ncell; };
 	auto V = [&](size_t i, int j) { return S.hs[i]->iw.V + static_cast<size_t>(j)*static_cast<size_t>(n4(i)); };
 	const ArrayOf z = [&](size_t i) { return S.hs[i]->iw.z; };
@@ -283,27 +296,51 @@ static GmresOut gmres(System& S, LinOp& A, const ArrayOf& b, const ArrayOf& x, d
 		while(j < m && out.iters < maxit) {
 			A.precondition([&](size_t i) { return V(i,j); }, z);
 			A.apply(z, w);
-			// classical Gram-Schmidt with selective (DGKS) reorthogonalisation: every multi-dot pass
-			// also returns |w|^2, so |w - V h|^2 follows by Pythagoras; a second pass runs only when
-			// the projection removed more than half of |w|^2 (loss of orthogonality possible)
-			S.each([&](size_t i, fvhip_ctx* h) {
-				launch_mdot(n4(i), j+1, V(i,0), n4(i), w(i), true, h->iw.part, h->iw.red, h->stream);
-			});
-			const std::vector<double> h1 = S.allsum(j+2, true);
-			S.each([&](size_t i, fvhip_ctx* h) { launch_maxpy(n4(i), j+1, V(i,0), n4(i), h->iw.red, w(i), h->stream); });
-			double corr = 0.0;
-			for(int k = 0; k <= j; k++) { Hij(k,j) = h1[k]; corr += h1[k]*h1[k]; }
-			double hn2 = h1[j+1] - corr;
-			if(!(hn2 > 0.5*h1[j+1])) {
+			// classical Gram-Schmidt (PETSc's KSPGMRESClassicalGramSchmidtOrthogonalization). refine 0
+			// (PETSc's default, KSP_GMRES_CGS_REFINE_NEVER): one projection h = V^T w, w -= V h, and the new
+			// norm computed from the projected w in the same pass (k_maxpy_norm) -- two passes over the
+			// basis per step. refine 1 (ifneeded): the projection pass also returns |w|^2, so |w - V h|^2
+			// follows by Pythagoras and a second projection runs only when the first removed more than half
+			// of |w|^2 (DGKS); refine 2 (always): two projections every step.
+			double hn2 = 0.0;
+			if(refine != 1) {
+				S.each([&](size_t i, fvhip_ctx* h) {
+					launch_mdot(n4(i), j+1, V(i,0), n4(i), w(i), false, h->iw.part, h->iw.red, h->stream);
+				});
+				const std::vector<double> h1 = S.allsum(j+1, true);
+				for(int k = 0; k <= j; k++) Hij(k,j) = h1[k];
+				if(refine == 2) {
+					S.each([&](size_t i, fvhip_ctx* h) { launch_maxpy(n4(i), j+1, V(i,0), n4(i), h->iw.red, w(i), h->stream); });
+					S.each([&](size_t i, fvhip_ctx* h) {
+						launch_mdot(n4(i), j+1, V(i,0), n4(i), w(i), false, h->iw.part, h->iw.red, h->stream);
+					});
+					const std::vector<double> h2 = S.allsum(j+1, true);
+					for(int k = 0; k <= j; k++) Hij(k,j) += h2[k];
+				}
+				S.each([&](size_t i, fvhip_ctx* h) {
+					launch_maxpy_norm(n4(i), j+1, V(i,0), n4(i), h->iw.red, w(i), h->iw.part, h->iw.red, h->stream);
+				});
+				hn2 = S.allsum(1, false)[0];
+			} else {
 				S.each([&](size_t i, fvhip_ctx* h) {
 					launch_mdot(n4(i), j+1, V(i,0), n4(i), w(i), true, h->iw.part, h->iw.red, h->stream);
 				});
-				const std::vector<double> h2 = S.allsum(j+2, true);
+				const std::vector<double> h1 = S.allsum(j+2, true);
 				S.each([&](size_t i, fvhip_ctx* h) { launch_maxpy(n4(i), j+1, V(i,0), n4(i), h->iw.red, w(i), h->stream); });
-				corr = 0.0;
-				for(int k = 0; k <= j; k++) { Hij(k,j) += h2[k]; corr += h2[k]*h2[k]; }
-				hn2 = h2[j+1] - corr;
-				if(!(hn2 > 1e-4*h2[j+1])) { const double t = norm(w); hn2 = t*t; }   // cancellation: measure
+				double corr = 0.0;
+				for(int k = 0; k <= j; k++) { Hij(k,j) = h1[k]; corr += h1[k]*h1[k]; }
+				hn2 = h1[j+1] - corr;
+				if(!(hn2 > 0.5*h1[j+1])) {
+					S.each([&](size_t i, fvhip_ctx* h) {
+						launch_mdot(n4(i), j+1, V(i,0), n4(i), w(i), true, h->iw.part, h->iw.red, h->stream);
+					});
+					const std::vector<double> h2 = S.allsum(j+2, true);
+					S.each([&](size_t i, fvhip_ctx* h) { launch_maxpy(n4(i), j+1, V(i,0), n4(i), h->iw.red, w(i), h->stream); });
+					corr = 0.0;
+					for(int k = 0; k <= j; k++) { Hij(k,j) += h2[k]; corr += h2[k]*h2[k]; }
+					hn2 = h2[j+1] - corr;
+					if(!(hn2 > 1e-4*h2[j+1])) { const double t = norm(w); hn2 = t*t; }   // cancellation: measure
+				}
 			}
 			const double hn = std::sqrt(hn2);
 			Hij(j+1,j) = hn;
@@ -360,6 +397,7 @@ static double expResidualRamp(double cflmin, double cflmax, double prevcfl, doub
 static void checkImplicit(const fvhip_implicit_config& c)
 {
 	if(c.restart < 1 || c.restart > KRY_MAXK) throw std::invalid_argument("restart must be in [1, 128]");
+	if(c.cgs_refine < 0 || c.cgs_refine > 2) throw std::invalid_argument("cgs_refine must be 0 (never), 1 (ifneeded) or 2 (always)");
 	if(c.prec_sweeps < 1) throw std::invalid_argument("prec_sweeps must be >= 1");
 	if(!(c.min_relax > 0.0)) throw std::domain_error("Minimum relaxation factor is invalid!");  // nonlinearrelaxation.cpp:20-21
 	if(c.matrix_free && !(c.mf_eps > 0.0)) throw std::invalid_argument("matrix-free difference step must be positive");
@@ -402,7 +440,7 @@ static void backwardEuler(System& S, const std::vector<double*>& us, const fvhip
 		A.setup();
 		if(A.matfree)                                                                               // :386-394
 			S.each([&](size_t i, fvhip_ctx* h) { h->mf_u = us[i]; h->mf_r = h->d_r; h->mf_mdt = h->d_dtm; });
-		const GmresOut g = gmres(S, A, bs, xs, c.lin_rtol, c.lin_maxit, c.restart);                  // :483
+		const GmresOut g = gmres(S, A, bs, xs, c.lin_rtol, c.lin_maxit, c.restart, c.cgs_refine);    // :483
 		lin += g.iters;
 		if(g.rnorm0 > 0.0) {
 			linworst = std::max(linworst, g.rnorm/g.rnorm0);
@@ -630,8 +668,9 @@ int fvhip_gmres_blocks_device(fvhip_handle h, const double* d_diag, const double
 		A.sweeps = sweeps;
 		A.D = {d_diag}; A.Lo = {d_lower}; A.Up = {d_upper};
 		A.setup();
+		// the standalone solver keeps the selective reorthogonalisation it was pinned with (cgs_refine 1)
 		const GmresOut g = gmres(S, A, [&](size_t) { return const_cast<double*>(d_b); },
-		                         [&](size_t) { return d_x; }, rtol, maxit, restart);
+		                         [&](size_t) { return d_x; }, rtol, maxit, restart, 1);
 		S.sync();
 		if(iters) *iters = g.iters;
 		if(resnorm) *resnorm = g.rnorm;

@@ -555,11 +555,12 @@ void k_mf_combine(int ncell, const double* __restrict__ mdt, const double* __res
 {
 	const int c = blockIdx.x*256 + threadIdx.x;
 	if(c >= ncell) return;
-	const double pert = pm[1];
-	for(int i = 0; i < 4; i++) {
-		const size_t k = 4*static_cast<size_t>(c) + i;
-		y[k] = mdt[c]*x[k] + (-yg[k] + res[k])/pert;
-	}
+	const double pert = pm[1], d = mdt[c];
+	// one 32-byte row per vector and cell; each entry mdt x + (-yg + res)/pert as before
+	const double4 xv = reinterpret_cast<const double4*>(x)[c], gv = reinterpret_cast<const double4*>(yg)[c];
+	const double4 rv = reinterpret_cast<const double4*>(res)[c];
+	reinterpret_cast<double4*>(y)[c] = make_double4(d*xv.x + (-gv.x + rv.x)/pert, d*xv.y + (-gv.y + rv.y)/pert,
+	                                                d*xv.z + (-gv.z + rv.z)/pert, d*xv.w + (-gv.w + rv.w)/pert);
 }
 
 // pointwise flux Jacobians (InviscidFlux::get_jacobian)

@@ -284,6 +284,31 @@ void k_maxpy(long long n, int k, const double* __restrict__ V, long long ld, con
 	w[i] -= s;
 }
 
+/// w -= V h over k basis vectors (k_maxpy's sum, in its order: the same w bit for bit) and |w|^2 of the result,
+/// over the multi-dot's fixed partition and tree: the Arnoldi step's new norm without another pass over w
+__global__ __launch_bounds__(256)
+void k_maxpy_norm(long long n, int k, const double* __restrict__ V, long long ld, const double* __restrict__ h,
+                  double* __restrict__ w, double* __restrict__ part)
+{
+	double acc[1] = {0.0};
+	const long long n2 = n >> 1;
+	double2* w2 = reinterpret_cast<double2*>(w);
+	for(long long i = blockIdx.x*256LL + threadIdx.x; i < n2; i += 256LL*gridDim.x) {
+		double sx = 0.0, sy = 0.0;
+		for(int j = 0; j < k; j++) {
+			const double2 v = reinterpret_cast<const double2*>(V + j*ld)[i];
+			sx += h[j]*v.x;
+			sy += h[j]*v.y;
+		}
+		double2 wi = w2[i];
+		wi.x -= sx; wi.y -= sy;
+		w2[i] = wi;
+		acc[0] += wi.x*wi.x;
+		acc[0] += wi.y*wi.y;
+	}
+	block_sum<1>(acc, part + blockIdx.x, 1);
+}
+
 __global__ __launch_bounds__(256)
 void k_lincomb(long long n, int k, const double* __restrict__ V, long long ld, const double* __restrict__ c,
                double* __restrict__ out)
@@ -659,6 +684,12 @@ void launch_mdot(long long n, int k, const double* V, long long ld, const double
 
 void launch_maxpy(long long n, int k, const double* V, long long ld, const double* h, double* w, hipStream_t s)
 { if(n > 0 && k > 0) k_maxpy<<<nblk(n,256), 256, 0, s>>>(n, k, V, ld, h, w); }
+void launch_maxpy_norm(long long n, int k, const double* V, long long ld, const double* h, double* w, double* part,
+                       double* out, hipStream_t s)
+{
+	k_maxpy_norm<<<KRY_DOT_BLOCKS, 256, 0, s>>>(n, k, V, ld, h, w, part);
+	k_sum_partials<<<1, 256, 0, s>>>(KRY_DOT_BLOCKS, part, out);
+}
 void launch_lincomb(long long n, int k, const double* V, long long ld, const double* c, double* out, hipStream_t s)
 { if(n > 0) k_lincomb<<<nblk(n,256), 256, 0, s>>>(n, k, V, ld, c, out); }
 void launch_axpby(long long n, double a, const double* x, double b, double* y, hipStream_t s)

@@ -99,6 +99,9 @@ void launch_mdot(long long n, int k, const double* V, long long ld, const double
                  double* part, double* out, hipStream_t s);
 /// w -= sum_{j<k} h[j] V_j  (h: k doubles on the device; ascending j for every element)
 void launch_maxpy(long long n, int k, const double* V, long long ld, const double* h, double* w, hipStream_t s);
+/// w -= V h and out[0] = |w|^2 of the result (fixed partition and tree: reproducible); part: kry_scratch(1)
+void launch_maxpy_norm(long long n, int k, const double* V, long long ld, const double* h, double* w, double* part,
+                       double* out, hipStream_t s);
 /// out = sum_{j<k} c[j] V_j  (c on the device)
 void launch_lincomb(long long n, int k, const double* V, long long ld, const double* c, double* out, hipStream_t s);
 /// y = a*x + b*y  (b == 0: y = a*x and y is not read)

@@ -128,15 +128,6 @@ int fvhip_create(const fvhip_mesh* mesh, const fvhip_flow_config* cfg, int devic
 /** Rank of a per-rank-mesh handle within nranks (PETSC_COMM_WORLD's rank in the reference); needed
  *  before fvhip_group_create, implied by fvhip_comm_init */
 int fvhip_set_rank(fvhip_handle h, int rank, int nranks);
-/** Partitioned handle on an RCCL communicator: enable = 1 captures its overlapped residual step (the
- *  halo exchange's pack and ncclSend/ncclRecv group, the ghost gradients, the interior and border fused
- *  launches with their stream/event joins) in a hipGraph the second time it runs with a given (u, r, dtm,
- *  time-step, overwrite) -- the first runs uncaptured (RCCL's peer connections, kernel set-up) -- and
- *  replays it with one hipGraphLaunch while those repeat (every residual of
- *  the drivers and of a caller's loop on fixed buffers); 0 turns it off (default), -1 only queries.
- *  *captures / *replays (may be NULL): graphs built and launched so far. Not a reference option: the
- *  reference's MPI step has no counterpart (host enqueue of the step: tools/enqueue_probe.py). */
-int fvhip_set_residual_graph(fvhip_handle h, int enable, int* captures, int* replays);
 int fvhip_destroy(fvhip_handle h);
 
 /* ---------------------------------------------------------------------------------------------
@@ -313,6 +304,10 @@ typedef struct fvhip_implicit_config {
 	                             order instead of PETSc's row order): one forward and one backward colour pass per
 	                             application, block-Jacobi across ranks; prec_sweeps - 1 further residual-correction
 	                             sweeps. Not combined with prec_gs / prec_lines. */
+	int cgs_refine;           /* -ksp_gmres_cgs_refinement_type of the classical Gram-Schmidt step: 0 = never
+	                             (PETSc's default, KSP_GMRES_CGS_REFINE_NEVER: one projection per Arnoldi step,
+	                             the new vector's norm computed from the projected vector), 1 = ifneeded (a second
+	                             projection when the first removed more than half of |w|^2, DGKS), 2 = always */
 } fvhip_implicit_config;
 
 typedef struct fvhip_solve_stats {

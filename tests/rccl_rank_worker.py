@@ -10,8 +10,8 @@ those of the one-GPU-per-rank run. torch.distributed (gloo) only rendezvouses th
 RCCL unique id and the results; the single-GPU reference results are computed by every rank itself.
 
 usage (set by the test): RANK, WORLD_SIZE, MASTER_ADDR, MASTER_PORT, NCCL_HOSTID in the environment;
-argv: <out.json> <mesh key> <partitioner> [graph | numerics]  (graph: the hipGraph sections only;
-numerics: "visc" = laminar Roe + WLS + Van Albada + Sutherland, "venkat" = Roe + WLS + Venkatakrishnan)
+argv: <out.json> <mesh key> <partitioner> [numerics]  (numerics: "visc" = laminar Roe + WLS + Van Albada +
+Sutherland, "venkat" = Roe + WLS + Venkatakrishnan)
 """
 import json
 import os
@@ -27,7 +27,6 @@ sys.path.insert(0, HERE)
 def main():
     out_path, meshkey, partitioner = sys.argv[1], sys.argv[2], sys.argv[3]
     mode = sys.argv[4] if len(sys.argv) > 4 else ""
-    graph = mode == "graph"
 
     def mark(msg):
         print("[rank %s] %s" % (os.environ["RANK"], msg), flush=True)
@@ -68,7 +67,7 @@ def main():
     g = owned[sp.permutation()]
     p1 = one.permutation()
     bad = 0
-    for k in range(0 if graph else 5):
+    for k in range(5):
         u = cases.state(m, p, seed=20 + k)
         du1 = torch.tensor(u[p1], device="cuda")
         dr1 = torch.zeros_like(du1)
@@ -91,37 +90,6 @@ def main():
     rep["residual_mismatched_rows"] = bad
     rep["layout"] = sp.layout_stats()
     mark("residuals done")
-
-    # 1b. the same step captured in a hipGraph (fvhip_set_residual_graph): fixed buffers, five states
-    #     copied in -> one capture, five replays, every owned row bitwise the single-GPU residual
-    if graph:
-        sp.set_residual_graph(True)
-        mark("graph on")
-    du = torch.full((sp.nown + sp.nghost, 4), float("nan"), dtype=torch.float64, device="cuda")
-    dr = torch.zeros((sp.nown, 4), dtype=torch.float64, device="cuda")
-    dt = torch.zeros(sp.nown, dtype=torch.float64, device="cuda")
-    bad = 0
-    for k in range(5 if graph else 0):
-        u = cases.state(m, p, seed=30 + k)
-        du1 = torch.tensor(u[p1], device="cuda")
-        dr1 = torch.zeros_like(du1)
-        dt1 = torch.zeros(m.nelem, dtype=torch.float64, device="cuda")
-        torch.cuda.synchronize()  # torch's stream vs the library's (non-blocking) streams
-        one.compute_residual_device(du1.data_ptr(), dr1.data_ptr(), dt1.data_ptr(), True, True)
-        one.synchronize()
-        r1 = np.empty((m.nelem, 4))
-        t1 = np.empty(m.nelem)
-        r1[p1] = dr1.cpu().numpy()
-        t1[p1] = dt1.cpu().numpy()
-        du[:sp.nown] = torch.tensor(u[g], device="cuda")
-        du[sp.nown:] = float("nan")
-        torch.cuda.synchronize()
-        mark("graph residual %d" % k)
-        sp.compute_residual_device(du.data_ptr(), dr.data_ptr(), dt.data_ptr(), True, True)
-        sp.synchronize()
-        bad += int((dr.cpu().numpy() != r1[g]).any(axis=1).sum() + (dt.cpu().numpy() != t1[g]).sum())
-    caps, reps_ = sp.set_residual_graph(False)
-    rep["graph"] = {"mismatched_rows": bad, "captures": caps, "replays": reps_}
 
     # 2. implicit steps (GMRES dot products and norms through ncclAllReduce; block-Jacobi across ranks
     #    for the line preconditioner): the same steps as a one-process group of the same partition
@@ -158,19 +126,6 @@ def main():
                     "hist_rel": float(np.max(np.abs(np.asarray(hist) - np.asarray(histg)) / np.abs(histg))),
                     "u_rel": float(np.abs(ur - ug).max() / scale)}
         mark("implicit %s done" % key)
-        if not graph:
-            continue
-        # the same solve with the residual step graphed: the same operations, so the same bits
-        c0, r0 = sp.set_residual_graph(True)
-        du[:sp.nown] = torch.tensor(u0[g], device="cuda")
-        du[sp.nown:] = float("nan")
-        torch.cuda.synchronize()
-        stG, histG = sp.steady_backward_euler_device(du.data_ptr(), cfg)
-        sp.synchronize()
-        caps, reps_ = sp.set_residual_graph(False)
-        rep[key]["graph"] = {"lin_iters": stG["lin_iters"], "hist_equal": bool(np.array_equal(hist, histG)),
-                             "u_equal": bool(np.array_equal(du[:sp.nown].cpu().numpy(), ur)),
-                             "captures": caps - c0, "replays": reps_ - r0}
 
     # 3. TVD-RK: the global dtmin through ncclMin, bitwise the one-GPU steps
     mark("tvdrk")

@@ -117,7 +117,7 @@ def test_one_backward_euler_step_matches_host(min_relax, single, gs, lines, ilu)
     dev = fa.FlowFV(m, p, n)
     perm = dev.permutation()
     dU = to_device(u0, perm)
-    cfg = fa.ImplicitConfig(cflinit=cfl, cflfin=cfl, tol=0.0, maxiter=1, lin_rtol=1e-13, lin_maxit=3000, restart=60,
+    cfg = fa.ImplicitConfig(cgs_refine=1, cflinit=cfl, cflfin=cfl, tol=0.0, maxiter=1, lin_rtol=1e-13, lin_maxit=3000, restart=60,
                             prec_sweeps=2, min_relax=min_relax, prec_single=single, prec_gs=gs, prec_lines=lines,
                             prec_ilu=ilu)
     st, hist = dev.steady_backward_euler_device(dU.data_ptr(), cfg)
@@ -143,7 +143,7 @@ def test_line_preconditioner_cuts_iterations():
     for lines in (False, True):
         dev = fa.FlowFV(m, p, n)
         dU = to_device(u0, dev.permutation())
-        cfg = fa.ImplicitConfig(cflinit=100.0, cflfin=100.0, tol=0.0, maxiter=1, lin_rtol=1e-8, lin_maxit=3000,
+        cfg = fa.ImplicitConfig(cgs_refine=1, cflinit=100.0, cflfin=100.0, tol=0.0, maxiter=1, lin_rtol=1e-8, lin_maxit=3000,
                                 restart=60, prec_sweeps=1, min_relax=1.0, prec_lines=lines)
         st, hist = dev.steady_backward_euler_device(dU.data_ptr(), cfg)
         out[lines] = (st["lin_iters"], dU.cpu().numpy())
@@ -277,7 +277,7 @@ def test_ilu_preconditioner_cuts_iterations():
     for kind in ("jacobi", "gs", "ilu"):
         dev = fa.FlowFV(m, p, n)
         dU = to_device(u0, dev.permutation())
-        cfg = fa.ImplicitConfig(cflinit=100.0, cflfin=100.0, tol=0.0, maxiter=1, lin_rtol=1e-8, lin_maxit=3000,
+        cfg = fa.ImplicitConfig(cgs_refine=1, cflinit=100.0, cflfin=100.0, tol=0.0, maxiter=1, lin_rtol=1e-8, lin_maxit=3000,
                                 restart=60, prec_sweeps=2 if kind == "gs" else 1, min_relax=1.0,
                                 prec_gs=kind == "gs", prec_ilu=kind == "ilu")
         st, hist = dev.steady_backward_euler_device(dU.data_ptr(), cfg)
@@ -372,7 +372,7 @@ def test_partitioned_gauss_seidel_same_solution():
     p = cases.physics("naca")
     n = cases.numerics("ROE", "LEASTSQUARES", "VANALBADA")
     u0 = cases.state(m, p, 2)
-    cfg = fa.ImplicitConfig(cflinit=10.0, cflfin=10.0, tol=0.0, maxiter=1, lin_rtol=1e-11, lin_maxit=400,
+    cfg = fa.ImplicitConfig(cgs_refine=1, cflinit=10.0, cflfin=10.0, tol=0.0, maxiter=1, lin_rtol=1e-11, lin_maxit=400,
                             restart=60, prec_sweeps=2, prec_gs=True)
     one = fa.FlowFV(m, p, n)
     perm = one.permutation()
@@ -404,7 +404,7 @@ def test_partitioned_ilu_same_solution():
     p = cases.physics("naca")
     n = cases.numerics("ROE", "LEASTSQUARES", "VANALBADA")
     u0 = cases.state(m, p, 2)
-    cfg = fa.ImplicitConfig(cflinit=10.0, cflfin=10.0, tol=0.0, maxiter=1, lin_rtol=1e-11, lin_maxit=400,
+    cfg = fa.ImplicitConfig(cgs_refine=1, cflinit=10.0, cflfin=10.0, tol=0.0, maxiter=1, lin_rtol=1e-11, lin_maxit=400,
                             restart=60, prec_sweeps=1, prec_ilu=True)
     one = fa.FlowFV(m, p, n)
     perm = one.permutation()
@@ -458,7 +458,7 @@ def test_partitioned_line_implicit_same_solution(nparts):
     for mf in (False, True):
         for rtol in (TIGHT["mf" if mf else "asm"], 1e-2):
             for lines in ((True, False) if rtol == 1e-2 else (True,)):
-                cfg = fa.ImplicitConfig(cflinit=25.0, cflfin=25.0, tol=0.0, maxiter=1, lin_rtol=rtol,
+                cfg = fa.ImplicitConfig(cgs_refine=1, cflinit=25.0, cflfin=25.0, tol=0.0, maxiter=1, lin_rtol=rtol,
                                         lin_maxit=1000, restart=60, prec_sweeps=1, min_relax=1.0, matrix_free=mf,
                                         mf_eps=1e-7, prec_lines=lines)
                 one = fa.FlowFV(m, p, n)

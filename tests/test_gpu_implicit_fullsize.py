@@ -62,7 +62,7 @@ def test_c4_eight_ranks_line_implicit_matches_one_gpu():
     p = cases.physics("naca")
     n = cases.numerics("ROE", "LEASTSQUARES", "VANALBADA")
     u0 = cases.state(m, p, 8)
-    cfg = fa.ImplicitConfig(cflinit=25.0, cflfin=25.0, tol=0.0, maxiter=1, lin_rtol=1e-11, lin_maxit=2000,
+    cfg = fa.ImplicitConfig(cgs_refine=1, cflinit=25.0, cflfin=25.0, tol=0.0, maxiter=1, lin_rtol=1e-11, lin_maxit=2000,
                             restart=60, prec_sweeps=1, min_relax=1.0, prec_lines=True)
     one = fa.FlowFV(m, p, n)
     perm = one.permutation()

@@ -8,10 +8,9 @@ residual norms; ncclMin of the TVD-RK time step -- checked against one GPU:
   * three implicit steps (point-block Jacobi, and the line-implicit preconditioner whose lines are cut
     at rank boundaries): the same linear iterations, residual history and states as the in-process group
     of the same partition (rounding of the dot-product sums aside: 1e-9);
-  * TVD-RK order 3: bitwise the one-GPU steps and time;
-  * the step captured in a hipGraph (fvhip_set_residual_graph; a new argument set runs uncaptured once,
-    then is captured and replayed): five residuals on fixed buffers = one capture, four graph launches,
-    bitwise; the implicit solve with it graphed: the same bits as without.
+  * TVD-RK order 3: bitwise the one-GPU steps and time.
+(Round 4's hipGraph capture of the rank step was removed in round 5: RCCL's captured p2p group overflows
+the stack in the HIP runtime's graph code, profiles/r05/graph_capture_crash.txt.)
 """
 import json
 import os
@@ -74,16 +73,3 @@ def test_rccl_ranks_on_one_gpu(tmp_path, world, meshkey, partitioner, numerics):
             assert im["steps"] == 3 and im["lin_iters"] == im["group_lin_iters"], (key, im)
             assert im["hist_rel"] <= 1e-9 and im["u_rel"] <= 1e-9, (key, im)
         assert rep["tvdrk"]["steps"] == 3 and rep["tvdrk"]["time_equal"] and rep["tvdrk"]["mismatched_rows"] == 0
-
-
-@pytest.mark.skipif(os.environ.get("FVHIP_TEST_RESIDUAL_GRAPH") != "1",
-                    reason="RCCL 2.26.6 segfaults capturing the ncclSend/ncclRecv group over its socket transport "
-                           "(profiles/r04/rccl_graph_capture.log); opt-in experiment")
-def test_rccl_ranks_graph_on_one_gpu(tmp_path):
-    for rep in _run_ranks(tmp_path, 2, "naca_small", "graph", "graph"):
-        gr = rep["graph"]
-        assert gr["mismatched_rows"] == 0 and gr["captures"] == 1 and gr["replays"] == 4, gr
-        for key in ("implicit_pbj", "implicit_lines"):
-            ig = rep[key]["graph"]
-            assert ig["lin_iters"] == rep[key]["lin_iters"] and ig["hist_equal"] and ig["u_equal"], (key, ig)
-            assert ig["captures"] == 1 and ig["replays"] == 2, (key, ig)

@@ -23,13 +23,15 @@ sys.path.insert(0, os.path.join(ROOT, "tests"))
 
 
 def run(scale=1, matrix_free=True, main_steps=400, init_steps=50, lin_maxit=60, restart=60, sweeps=3,
-        tol=1e-6, heartbeat=None):
-    """the deck's two stages on the C5 mesh divided by `scale` in both directions; returns the record"""
+        tol=1e-6, heartbeat=None, cfl_init=(200.0, 1000.0), cfl_main=(500.0, 5000.0), min_relax=1.0, lin_rtol=1e-1,
+        wall=None):
+    """the deck's two stages on the C5 mesh divided by `scale` in both directions; returns the record (a stage
+    that diverges is recorded with its history and the error; the later stage is then skipped)"""
     import torch
     import fvens_amd as fa
     import cases
     from bench import c4_mesh
-    mesh, dims = c4_mesh(fa, scale, 2)
+    mesh, dims = c4_mesh(fa, scale, 2, wall=wall)
     p = cases.physics("visc")                                   # alpha 0 (laminar-implicit.ctrl:19)
     n1 = cases.numerics("ROE", "NONE", "NONE", order2=False)
     n2 = cases.numerics("ROE", "LEASTSQUARES", "NONE")          # limiter none (:72)
@@ -37,10 +39,11 @@ def run(scale=1, matrix_free=True, main_steps=400, init_steps=50, lin_maxit=60, 
     perm = main.permutation()
     du = torch.tensor(np.tile(cases.freestream(p), (mesh.nelem, 1))[perm], device="cuda")
     torch.cuda.synchronize()      # torch's stream vs the library's (non-blocking) streams
-    lin = dict(lin_rtol=1e-1, lin_maxit=lin_maxit, restart=restart, prec_lines=True, prec_sweeps=sweeps,
-               min_relax=1.0)
+    lin = dict(lin_rtol=lin_rtol, lin_maxit=lin_maxit, restart=restart, prec_lines=True, prec_sweeps=sweeps,
+               min_relax=min_relax)
     rec = {"cells": mesh.nelem, "faces": mesh.naface, "dims": dims, "operator": "matrix-free" if matrix_free else "assembled",
-           "linear": dict(lin, gmres="GMRES(%d) right-preconditioned" % restart)}
+           "linear": dict(lin, gmres="GMRES(%d) right-preconditioned" % restart), "cfl_init": list(cfl_init),
+           "cfl_main": list(cfl_main)}
     done = threading.Event()
 
     def beat():
@@ -50,27 +53,36 @@ def run(scale=1, matrix_free=True, main_steps=400, init_steps=50, lin_maxit=60, 
                 heartbeat("running %.0f s" % (time.time() - t0))
     th = threading.Thread(target=beat, daemon=True)
     th.start()
-    try:
+    def stage(h, cfg):
         t0 = time.perf_counter()
-        st0, h0 = start.steady_backward_euler_device(du.data_ptr(), fa.ImplicitConfig(
-            cflinit=200.0, cflfin=1000.0, tol=1e-1, maxiter=init_steps, **lin))
-        torch.cuda.synchronize()
-        t1 = time.perf_counter()
-        st, h = main.steady_backward_euler_device(du.data_ptr(), fa.ImplicitConfig(
-            cflinit=500.0, cflfin=5000.0, tol=tol, maxiter=main_steps, matrix_free=matrix_free, **lin))
-        torch.cuda.synchronize()
-        t2 = time.perf_counter()
+        try:
+            st, hh = h.steady_backward_euler_device(du.data_ptr(), cfg)
+            torch.cuda.synchronize()
+            return {**st, "seconds": round(time.perf_counter() - t0, 2),
+                    "ms_per_step": round((time.perf_counter() - t0) / max(st["steps"], 1) * 1e3, 2),
+                    "history": [float(x) for x in hh]}
+        except RuntimeError as e:
+            hh = getattr(e, "history", [])
+            return {"error": str(e), "steps": len(hh), "converged": False, "seconds": round(time.perf_counter() - t0, 2),
+                    "history": [float(x) for x in hh]}
+    try:
+        rec["init"] = stage(start, fa.ImplicitConfig(cflinit=cfl_init[0], cflfin=cfl_init[1], tol=1e-1,
+                                                    maxiter=init_steps, **lin))
+        if "error" not in rec["init"]:
+            rec["main"] = stage(main, fa.ImplicitConfig(cflinit=cfl_main[0], cflfin=cfl_main[1], tol=tol,
+                                                        maxiter=main_steps, matrix_free=matrix_free, **lin))
     finally:
         done.set()
+    if "main" not in rec or "error" in rec["main"]:
+        start.close()
+        main.close()
+        rec["finite"] = False
+        return rec
     (cl, cdp, cdsf), _ = main.surface_data_device(du.data_ptr(), 2)
     finite = bool(torch.isfinite(du).all().item())
     start.close()
     main.close()
-    rec.update({
-        "init": {**st0, "seconds": round(t1 - t0, 2), "history": [float(x) for x in h0]},
-        "main": {**st, "seconds": round(t2 - t1, 2), "ms_per_step": round((t2 - t1) / max(st["steps"], 1) * 1e3, 2),
-                 "history": [float(x) for x in h]},
-        "CL": cl, "CDp": cdp, "CDsf": cdsf, "finite": finite})
+    rec.update({"CL": cl, "CDp": cdp, "CDsf": cdsf, "finite": finite})
     return rec
 
 
@@ -82,11 +94,19 @@ def main():
     ap.add_argument("--lin-maxit", type=int, default=60)
     ap.add_argument("--restart", type=int, default=60)
     ap.add_argument("--sweeps", type=int, default=3)
+    ap.add_argument("--cfl-init", type=float, nargs=2, default=(200.0, 1000.0))
+    ap.add_argument("--cfl-main", type=float, nargs=2, default=(500.0, 5000.0))
+    ap.add_argument("--min-relax", type=float, default=1.0, help=">= 1: full update (the deck), else robust_flow")
+    ap.add_argument("--lin-rtol", type=float, default=1e-1)
+    ap.add_argument("--wall", type=float, default=None, help="first-cell wall spacing (default: the C5 mesh's 1e-5)")
+    ap.add_argument("--tag", default="")
     args = ap.parse_args()
     import torch
     torch.cuda.set_device(0)
     r = run(args.scale, not args.assembled, args.main_steps, lin_maxit=args.lin_maxit, restart=args.restart,
-            sweeps=args.sweeps, heartbeat=lambda s: print(s, flush=True))
+            sweeps=args.sweeps, heartbeat=lambda s: print(s, flush=True), cfl_init=args.cfl_init,
+            cfl_main=args.cfl_main, min_relax=args.min_relax, lin_rtol=args.lin_rtol, wall=args.wall)
+    r["tag"] = args.tag
     print(json.dumps(r), flush=True)
 
 
