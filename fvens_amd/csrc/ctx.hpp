@@ -350,6 +350,7 @@ struct fvhip_ctx
 		if(plist && pcount == 0) return;
 		B.grad = d_grad;     // received gradients of ghost cells (partitioned meshes)
 		if(limited()) B.phi = d_phi;   // layer-1 ghosts' limiter values (two-layer halo)
+		B.mfx = mfz.x; B.mfpm = mfz.pm; B.mfres = mfz.res; B.mfmdt = mfz.mdt;
 #ifdef FVHIP_PROBE_PHASES
 		if(!d_probe) d_probe = static_cast<unsigned long long*>(static_cast<void*>(dalloc(8*(static_cast<size_t>(L.patch_cell.size()) + 16), owned)));
 		B.probe = d_probe;
@@ -359,6 +360,21 @@ struct fvhip_ctx
 		                                                                       limKind(), dt, st); });
 		if(prof && !recs.empty() && recs.back().name == "k_residual_wls" && nm) recs.back().name = nm;
 		HC(hipGetLastError());
+	}
+
+	/// the matrix-free operator fused into one launch of the residual kernel (single domain, fused
+	/// configurations): y = mdt x + (r(u) - r(u + pm[1] x))/pm[1] with the perturbed state formed where the
+	/// kernel reads a state row and the combination where it writes a cell -- k_mf_perturb's and
+	/// k_mf_combine's arithmetic, so bitwise the three-launch operator, without its 5 vector passes over HBM
+	struct MfFuse { const double *x = nullptr, *pm = nullptr, *res = nullptr, *mdt = nullptr; } mfz;
+	/// (x and y must not alias: other blocks read x rows while a block writes its cells' y)
+	bool matfreeFusable() const { return fused() && !halo(); }
+	void matfree_fused(const double* u, const double* x, const double* pm, const double* res, const double* mdt, double* y) {
+		if(!matfreeFusable()) throw std::logic_error("matfree_fused: not a fused single-domain configuration");
+		mfz = MfFuse{x, pm, res, mdt};
+		try { stage_fused(u, y, false, nullptr, true); }
+		catch(...) { mfz = MfFuse{}; throw; }
+		mfz = MfFuse{};
 	}
 
 	/// pack the rows of `arr` (width doubles per cell) that the neighbours hold as ghosts
@@ -987,6 +1003,7 @@ struct fvhip_ctx
 		if(!d_part) { d_part = dalloc(mf_partials(), owned); d_pm = dalloc(2, owned); }
 		if(!d_mf_aux) { d_mf_aux = dalloc(4*N, owned); d_mf_y = dalloc(4*N, owned); }
 		timed("k_mf_norm", [&]{ launch_mf_norm(4LL*L.ncell, x, mf_eps, d_part, d_pm, stream); });
+		if(matfreeFusable() && x != y) { matfree_fused(mf_u, x, d_pm, mf_r, mf_mdt, y); HC(hipGetLastError()); return; }
 		timed("k_mf_perturb", [&]{ launch_mf_perturb(4LL*L.ncell, mf_u, x, d_pm, d_mf_aux, stream); });
 		residual(d_mf_aux, d_mf_y, false, nullptr, true);
 		timed("k_mf_combine", [&]{ launch_mf_combine(L.ncell, mf_mdt, x, d_mf_y, mf_r, d_pm, y, stream); });

@@ -84,6 +84,14 @@ static void matfreeApply(System& S, const ArrayOf& x, const ArrayOf& y)
 		launch_mdot(4LL*h->L.ncell, 0, nullptr, 0, x(i), true, h->iw.part, h->iw.red, h->stream);
 	});
 	S.allsumDevice(1);                         // |x|^2 stays on the device (launch_pertmag reads it there)
+	if(S.size() == 1 && !S.exg && S.hs[0]->matfreeFusable() && x(0) != y(0)) {
+		// one launch: the perturbed state and the combination inside the residual kernel (bitwise the same)
+		fvhip_ctx* h = S.hs[0];
+		launch_pertmag(h->iw.red, h->mf_eps, h->iw.pm, h->stream);
+		h->matfree_fused(h->mf_u, x(0), h->iw.pm, h->mf_r, h->mf_mdt, y(0));
+		HC(hipGetLastError());
+		return;
+	}
 	std::vector<const double*> aux;
 	std::vector<double*> yg, none(S.size(), nullptr);
 	S.each([&](size_t i, fvhip_ctx* h) {

@@ -888,12 +888,28 @@ __device__ __forceinline__ void ghost_c(const DevPhys& P, int bc, const double* 
 	const double ui[4] = {P.uinf[0], P.uinf[1], P.uinf[2], P.uinf[3]};
 	ghost_state_common(P.gas, P.bc[bc], ui, ins, n, gs);
 }
-__device__ __forceinline__ double4 ghost_prim_of_cell(const DevMesh& M, const DevPhys& P, const double* u, int cell, int bf)
+/// the conserved state row of cell c the fused residual works on: u[c], or with the fused matrix-free
+/// operator (SweepBuffers::mfx; MF: instantiations without time steps only) the perturbed state
+/// u[c] + pm[1] x[c], k_mf_perturb's arithmetic
+template <bool MF>
+__device__ __forceinline__ void ld_state(const SweepBuffers& B, int c, double* o)
+{
+	ld4(B.u, c, o);
+	if(MF && B.mfx) {
+		double x[4];
+		ld4(B.mfx, c, x);
+		const double s = B.mfpm[1];
+		#pragma unroll
+		for(int i = 0; i < 4; i++) o[i] = o[i] + s*x[i];
+	}
+}
+template <bool MF>
+__device__ __forceinline__ double4 ghost_prim_of_cell(const DevMesh& M, const DevPhys& P, const SweepBuffers& B, int cell, int bf)
 {
 	const double2 nn = M.bf_n[bf];
 	const double n[2] = {nn.x, nn.y};
 	double ucons[4], gs[4], gp[4];
-	ld4(u, cell, ucons);
+	ld_state<MF>(B, cell, ucons);
 	ghost_c(P, M.bf_bc[bf], ucons, n, gs);
 	cons2prim(P.gas, gs, gp);
 	return make_double4(gp[0], gp[1], gp[2], gp[3]);
@@ -950,7 +966,7 @@ __device__ __forceinline__ void fz_face_centres(const DevMesh& M, int c, double2
 	#pragma unroll
 	for(int k = 0; k < 4; k++) gp[k] = sl[k] >= 0 ? M.slot_gr[sl[k] >> 1] : make_double2(0, 0);
 }
-template <int LIM, int W = FZW>
+template <int LIM, int W = FZW, bool MF = false>
 __device__ __forceinline__ void fused_limit_row(const DevMesh& M, const DevPhys& P, const SweepBuffers& B,
                                                 const double* fz, const double* row, int c, int4 nb4,
                                                 const double2* gp, double eps2, double* g);
@@ -968,7 +984,7 @@ __device__ __forceinline__ void fz_row_temperature(const Gas& G, double* row, co
 		row[16] = ty;
 	}
 }
-template <int LIM, int W = FZW>
+template <int LIM, int W = FZW, bool MF = false>
 __device__ __forceinline__ void fused_wls_row(const DevMesh& M, const DevPhys& P, const SweepBuffers& B,
                                               const double* fz, double* row, int c, int4 nb4, double4 V,
                                               const double2* gp = nullptr, double eps2 = 0.0)
@@ -1062,7 +1078,7 @@ __device__ __forceinline__ void fused_wls_row(const DevMesh& M, const DevPhys& P
 		pin_regs(un[0]); pin_regs(un[1]); pin_regs(un[2]); pin_regs(un[3]); pin_regs(rn.x); pin_regs(rn.y);
 		if(nbk < 0) {
 			const int bf = -2 - nbk;
-			const double4 gp = ghost_prim_of_cell(M, P, B.u, c, bf);
+			const double4 gp = ghost_prim_of_cell<MF>(M, P, B, c, bf);
 			un[0] = gp.x; un[1] = gp.y; un[2] = gp.z; un[3] = gp.w;
 			rn = M.bf_rcbp[bf];
 		}
@@ -1089,7 +1105,7 @@ __device__ __forceinline__ void fused_wls_row(const DevMesh& M, const DevPhys& P
 		g[iv*2+1] = V.z*f[iv*2+0] + V.w*f[iv*2+1];
 	}
 #ifndef FVHIP_PROBE_NOLIM
-	if(LIM) fused_limit_row<LIM, W>(M, P, B, fz, row, c, nb4, gp, eps2, g);
+	if(LIM) fused_limit_row<LIM, W, MF>(M, P, B, fz, row, c, nb4, gp, eps2, g);
 #endif
 	st8(row + 4, 0, g);
 	fz_row_temperature<W>(P.gas, row, g);
@@ -1099,7 +1115,7 @@ __device__ __forceinline__ void fused_wls_row(const DevMesh& M, const DevPhys& P
 /// values from the staged neighbour states (boundary: the ghost primitive state, as the staged path)
 /// and its face centres, k_prep_grad_wls<LIM>'s arithmetic; the staged row then holds lim*g, which is
 /// the product linearExtrapolate forms first ((lim*grad)*(gp - rc), reconstruction_utils.hpp:28-30)
-template <int LIM, int W>
+template <int LIM, int W, bool MF>
 __device__ __forceinline__ void fused_limit_row(const DevMesh& M, const DevPhys& P, const SweepBuffers& B,
                                                 const double* fz, const double* row, int c, int4 nb4,
                                                 const double2* gpre, double eps2, double* g)
@@ -1120,7 +1136,7 @@ __device__ __forceinline__ void fused_limit_row(const DevMesh& M, const DevPhys&
 		if(!has[k]) continue;
 		if(nb[k] >= 0) ld4(&fz[nb[k]*W], 0, un[k]);
 		else {
-			const double4 q = ghost_prim_of_cell(M, P, B.u, c, -2 - nb[k]);
+			const double4 q = ghost_prim_of_cell<MF>(M, P, B, c, -2 - nb[k]);
 			un[k][0] = q.x; un[k][1] = q.y; un[k][2] = q.z; un[k][3] = q.w;
 		}
 	}
@@ -1271,11 +1287,12 @@ __device__ __forceinline__ int fz_cell(const DevMesh& M, const FzPatch& q, int i
 	return i < q.nc ? q.c0 + i : M.fz_ext[q.e0 + (i - q.nc)];
 }
 /// the loads of FzPre (a.cf already set): the staged row and the face
+template <bool MF>
 __device__ __forceinline__ void fz_load_rows(const DevMesh& M, const SweepBuffers& B, const FzPatch& q, int t, FzPre& a)
 {
 	a.ua[0] = a.ua[1] = a.ua[2] = a.ua[3] = 0.0;
 	a.rca = make_double2(0, 0);
-	if(t < q.nl) { ld4(B.u, a.cf, a.ua); a.rca = M.rc[a.cf]; }
+	if(t < q.nl) { ld_state<MF>(B, a.cf, a.ua); a.rca = M.rc[a.cf]; }
 	const int s = q.s0 + t;
 	a.lrl = make_int2(0, -1); a.nn = make_double2(0, 0); a.len = 0;
 	if(s < q.s1) {
@@ -1311,7 +1328,7 @@ __device__ __forceinline__ void fz_body(const DevMesh& M, const DevPhys& P, cons
 	for(int i = t + SLOTS_MAX; i < q.nl; i += SLOTS_MAX) {
 		const int c = fz_cell(M, q, i);
 		double b[4];
-		ld4(B.u, c, b);
+		ld_state<!DT>(B, c, b);
 		stage_row(G, &fz[i*W], b, M.rc[c]);
 	}
 	__syncthreads();
@@ -1321,10 +1338,10 @@ __device__ __forceinline__ void fz_body(const DevMesh& M, const DevPhys& P, cons
 	// (k_prep_grad_wls arithmetic, neighbours in the same ascending reference face order)
 	hookA();
 #ifndef FVHIP_PROBE_NOGRAD
-	if(t < q.ng) fused_wls_row<LIM, W>(M, P, B, fz, &fz[t*W], a.cf, a.nb4a, a.Va, LIM && FVHIP_FZ_LIM_PREFETCH ? a.gpa : nullptr, a.eps2a);
+	if(t < q.ng) fused_wls_row<LIM, W, !DT>(M, P, B, fz, &fz[t*W], a.cf, a.nb4a, a.Va, LIM && FVHIP_FZ_LIM_PREFETCH ? a.gpa : nullptr, a.eps2a);
 	for(int i = t + SLOTS_MAX; i < q.ng; i += SLOTS_MAX) {
 		const int c = fz_cell(M, q, i);
-		fused_wls_row<LIM, W>(M, P, B, fz, &fz[i*W], c, c < M.nown ? fz_nbrs(q, i) : make_int4(-1, -1, -1, -1),
+		fused_wls_row<LIM, W, !DT>(M, P, B, fz, &fz[i*W], c, c < M.nown ? fz_nbrs(q, i) : make_int4(-1, -1, -1, -1),
 		              c < M.nown && !FVHIP_FZ_WLSV ? M.wls_V[c] : make_double4(0, 0, 0, 0));
 	}
 #endif
@@ -1379,7 +1396,7 @@ __device__ __forceinline__ void fz_body(const DevMesh& M, const DevPhys& P, cons
 				prim2cons(G, ur, ur);
 			} else {
 				// ghost of the cell value (k_prep_grad_wls / k_prep_bfaces arithmetic)
-				const double4 gp = ghost_prim_of_cell(M, P, B.u, bcell, bf);
+				const double4 gp = ghost_prim_of_cell<!DT>(M, P, B, bcell, bf);
 				const double uj[4] = {gp.x, gp.y, gp.z, gp.w};
 				const double2 rj = M.bf_rcbp[bf];
 				const double dx = rj.x-ri.x, dy = rj.y-ri.y;
@@ -1455,7 +1472,7 @@ __device__ __forceinline__ void fz_body(const DevMesh& M, const DevPhys& P, cons
 			double4 gpr = make_double4(0, 0, 0, 0);
 			const double* rowj = nullptr;
 			double2 rr;
-			if(bnd) { gpr = ghost_prim_of_cell(M, P, B.u, bcell, bf); rr = M.bf_rcbp[bf]; }
+			if(bnd) { gpr = ghost_prim_of_cell<!DT>(M, P, B, bcell, bf); rr = M.bf_rcbp[bf]; }
 			else { rowj = &fz[lrl.y*W]; rr = *reinterpret_cast<const double2*>(rowj + 12); }
 #if !FVHIP_FZ_VGEO
 			const double4 vg = make_double4(ri.x, ri.y, rr.x, rr.y);    // the two centres
@@ -1517,6 +1534,15 @@ __device__ __forceinline__ void fz_body(const DevMesh& M, const DevPhys& P, cons
 				if(DT) integ += ssr[ls];
 			}
 		}
+		if(!DT && B.mfx) {
+			// y = mdt x + (-yg + res)/pert, k_mf_combine's arithmetic, with yg the sum just formed
+			double x[4], rs[4];
+			ld4(B.mfx, c, x);
+			ld4(B.mfres, c, rs);
+			const double d = B.mfmdt[c], pert = B.mfpm[1];
+			#pragma unroll
+			for(int i = 0; i < 4; i++) r[i] = d*x[i] + (-r[i] + rs[i])/pert;
+		}
 		st4(B.r, c, r);
 		if(DT) B.dtm[c] = div_rn(carea, integ);
 	}
@@ -1550,7 +1576,7 @@ __global__ void __launch_bounds__(SLOTS_MAX, VISC != SV_NONE ? FVHIP_FUSED_WAVES
 	const FzPatch cur = fz_patch(M, B, pi);
 	FzPre pre;
 	pre.cf = t < cur.nl ? fz_cell(M, cur, t) : 0;
-	fz_load_rows(M, B, cur, t, pre);
+	fz_load_rows<!DT>(M, B, cur, t, pre);
 	fz_load_grad(M, cur, t, pre);
 	pre.eps2a = 0.0;
 	if(LIM && FVHIP_FZ_LIM_PREFETCH) {   // the first row's face centres and eps^2, requested before the staging barrier

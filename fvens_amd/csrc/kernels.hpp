@@ -87,6 +87,14 @@ struct SweepBuffers
 	int overwrite;
 	const int* plist;     // patches to sweep (pcount of them), or null: all patches
 	int pcount;
+	// matrix-free operator fused into the one-launch residual (k_residual_wls without time steps, single
+	// domain; MatrixFreeSpatialJacobian::apply, alinalg.cpp:142-233): with mfx set, every state row the
+	// kernel reads is u + pm[1] x (k_mf_perturb's arithmetic) and each cell writes, instead of its
+	// residual yg, y = mdt x + (-yg + res)/pm[1] (k_mf_combine's) into r
+	const double* mfx;    // [N][4] x, or null
+	const double* mfpm;   // [2] (|x|, eps/|x|)
+	const double* mfres;  // [N][4] -r(u) of the operator's state
+	const double* mfmdt;  // [N] pseudo-time diagonal
 	unsigned long long* probe;   // diagnostic builds (-DFVHIP_PROBE_PHASES) only: per-block phase stamps
 };
 

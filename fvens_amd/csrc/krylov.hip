@@ -10,7 +10,7 @@ namespace fvhip {
 
 constexpr int KRY_BLOCKS = 512;   ///< partial sums of the energy norm (= ode.hip's ODE_RED_BLOCKS)
 constexpr int KRY_DOT_BLOCKS = 2048;   ///< partial sums per GMRES dot product (8 blocks per CU: enough loads in flight)
-constexpr int KRY_GROUP = 4;      ///< dot products per block row of the multi-dot
+constexpr int KRY_GROUP = 8;      ///< dot products per block row of the multi-dot (w read once per 8 basis vectors)
 
 static inline int nblk(long long n, int b) { return static_cast<int>((n + b - 1)/b); }
 

@@ -649,3 +649,45 @@ def test_naca0012_weno_implicit_functional_regression():
     assert st["converged"], st
     assert abs(cl - 0.151870649085658) / 0.151870649085658 <= 1e-6
     assert abs(cdp - 0.013085625502343) / 0.013085625502343 <= 1e-7
+
+
+@pytest.mark.parametrize("kind,flux,rec", [("naca", "ROE", "VANALBADA"), ("visc", "ROE", "NONE"),
+                                           ("naca", "ROE", "VENKATAKRISHNAN"), ("plate", "HLLC", "NONE")])
+def test_fused_matfree_operator_bitwise(kind, flux, rec):
+    """MatrixFreeSpatialJacobian::apply (alinalg.cpp:142-233) fused into one launch of the residual kernel
+    (single domain: the perturbed state formed where the kernel reads a state row, the combination where it
+    writes a cell) against the three-launch operator (perturb, residual, combine), which a one-handle group
+    still runs: y bitwise equal; and three matrix-free implicit steps on each give the same states bitwise"""
+    import torch
+    from test_gpu_residual import get_mesh
+    m, _ = get_mesh("plate_small" if kind == "plate" else "naca_small")
+    p = cases.physics(kind)
+    n = cases.numerics(flux, "LEASTSQUARES", rec)
+    h1, h2 = fa.FlowFV(m, p, n), fa.FlowFV(m, p, n)
+    grp = fa.FlowFVGroup([h2])
+    perm = h1.permutation()
+    rng = np.random.default_rng(3)
+    du = torch.tensor(cases.state(m, p, 11)[perm], device="cuda")
+    dr = torch.tensor(rng.standard_normal((m.nelem, 4)) * 1e-3, device="cuda")
+    dmdt = torch.tensor(rng.random(m.nelem) + 0.5, device="cuda")
+    dx = torch.tensor(rng.standard_normal((m.nelem, 4)), device="cuda")
+    y1, y2 = torch.zeros_like(dx), torch.zeros_like(dx)
+    torch.cuda.synchronize()
+    h1.matfree_set_state_device(du.data_ptr(), dr.data_ptr(), dmdt.data_ptr())
+    grp.matfree_set_state_device([du.data_ptr()], [dr.data_ptr()], [dmdt.data_ptr()])
+    h1.matfree_apply_device(dx.data_ptr(), y1.data_ptr())
+    grp.matfree_apply_device([dx.data_ptr()], [y2.data_ptr()])
+    h1.synchronize()
+    h2.synchronize()
+    assert torch.equal(y1, y2), float((y1 - y2).abs().max())
+    cfg = fa.ImplicitConfig(cflinit=20.0, cflfin=200.0, tol=0.0, maxiter=3, lin_rtol=1e-2, lin_maxit=40, restart=20,
+                            prec_lines=True, matrix_free=True, min_relax=0.2)
+    u1, u2 = du.clone(), du.clone()
+    torch.cuda.synchronize()
+    st1, hist1 = h1.steady_backward_euler_device(u1.data_ptr(), cfg)
+    st2, hist2 = grp.steady_backward_euler_device([u2.data_ptr()], cfg)
+    assert st1["lin_iters"] == st2["lin_iters"] and np.array_equal(hist1, hist2), (st1, st2)
+    assert torch.equal(u1, u2)
+    grp.close()
+    h1.close()
+    h2.close()
