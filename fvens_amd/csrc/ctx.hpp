@@ -821,7 +821,7 @@ struct fvhip_ctx
 		                     static_cast<const void*>(lines.face), static_cast<const void*>(lines.D),
 		                     static_cast<const void*>(lines.Lb), static_cast<const void*>(lines.W),
 		                     static_cast<const void*>(lines.len),
-		                     static_cast<const void*>(lines.G)}) release(p);
+		                     static_cast<const void*>(lines.G), static_cast<const void*>(lines.zpart)}) release(p);
 		lines = LineSet{};
 		const int N = L.ncell, nb = L.nbface;
 		struct Nb { int c, fi; double w; };
@@ -972,6 +972,7 @@ struct fvhip_ctx
 		lines.Lb = dalloc(1024*rows, owned);
 		lines.W = dalloc(1024*rows, owned);
 		lines.G = dalloc(256*rows, owned);
+		lines.zpart = dalloc(static_cast<size_t>(std::max(ng, 1)), owned);
 		lines_thr = thr;
 	}
 

@@ -77,13 +77,14 @@ typedef fvhip_ctx::ArrayOf ArrayOf;
 
 /// MatrixFreeSpatialJacobian::apply (alinalg.cpp:142-233) over a system: |x| is the global norm,
 /// the perturbed state gets its ghost rows from the residual's own exchange
-static void matfreeApply(System& S, const ArrayOf& x, const ArrayOf& y)
+/// have_norm: |x|^2 is already in iw.red (the line solve that produced x summed it, LinOp::precondition)
+static void matfreeApply(System& S, const ArrayOf& x, const ArrayOf& y, bool have_norm = false)
 {
 	S.each([&](size_t i, fvhip_ctx* h) {
 		if(!h->mf_u || !h->mf_r || !h->mf_mdt) throw std::runtime_error("matrix-free operator: state not set");
-		launch_mdot(4LL*h->L.ncell, 0, nullptr, 0, x(i), true, h->iw.part, h->iw.red, h->stream);
+		if(!have_norm) launch_mdot(4LL*h->L.ncell, 0, nullptr, 0, x(i), true, h->iw.part, h->iw.red, h->stream);
 	});
-	S.allsumDevice(1);                         // |x|^2 stays on the device (launch_pertmag reads it there)
+	if(!have_norm) S.allsumDevice(1);          // |x|^2 stays on the device (launch_pertmag reads it there)
 	if(S.size() == 1 && !S.exg && S.hs[0]->matfreeFusable() && x(0) != y(0)) {
 		// one launch: the perturbed state and the combination inside the residual kernel (bitwise the same)
 		fvhip_ctx* h = S.hs[0];
@@ -127,15 +128,21 @@ struct LinOp
 			h->timed("k_block_apply", [&]{ launch_block_apply(h->J, D[i], Lo[i], Up[i], x(i), y(i), h->stream); });
 		});
 	}
+	/// set by a precondition call asked for the norm of its output (the Arnoldi step's z), consumed by the
+	/// next apply: the matrix-free operator needs |z| and the line solve summed it while writing z
+	bool znorm = false;
 	void apply(const ArrayOf& x, const ArrayOf& y) {
-		if(matfree) matfreeApply(S, x, y);
+		const bool have = znorm;
+		znorm = false;
+		if(matfree) matfreeApply(S, x, y, have);
 		else blocks(x, y);
 	}
 	/// z = M^-1 v: `sweeps` block-Jacobi sweeps on A z = v from z = 0 (z has ghost rows). The iterates
 	/// alternate between z and aux (both with ghost rows) so that the last one lands in z.
-	void precondition(const ArrayOf& v, const ArrayOf& z) {
+	void precondition(const ArrayOf& v, const ArrayOf& z, bool want_norm = false) {
+		znorm = false;
 		if(gs) { gaussSeidel(v, z); return; }
-		if(lines) { lineSweeps(v, z); return; }
+		if(lines) { lineSweeps(v, z, want_norm); return; }
 		if(ilu) { iluSweeps(v, z); return; }
 		const ArrayOf aux = [&](size_t i) { return S.hs[i]->iw.aux; };
 		auto buf = [&](int k) -> const ArrayOf& { return ((sweeps - 1 - k) % 2 == 0) ? z : aux; };
@@ -215,12 +222,15 @@ struct LinOp
 	}
 	/// z = M^-1 v with M the block-tridiagonal line part of A (factorised in setup), then `sweeps` - 1
 	/// corrections z += M^-1 (v - A z) (A with the ghost coupling: block-Jacobi across ranks)
-	void lineSweeps(const ArrayOf& v, const ArrayOf& z) {
+	void lineSweeps(const ArrayOf& v, const ArrayOf& z, bool want_norm = false) {
 		const ArrayOf aux = [&](size_t i) { return S.hs[i]->iw.aux; };
 		const ArrayOf t = [&](size_t i) { return S.hs[i]->iw.t; };
+		// one sweep on one domain for the matrix-free operator: the line solve also returns |z|^2
+		const bool norm = want_norm && matfree && sweeps == 1 && S.size() == 1 && !S.exg && !S.halo();
 		S.each([&](size_t i, fvhip_ctx* h) {
-			h->timed("k_line_solve", [&]{ launch_line_solve(h->lines, v(i), z(i), h->stream); });
+			h->timed("k_line_solve", [&]{ launch_line_solve(h->lines, v(i), z(i), h->stream, norm ? h->iw.red : nullptr); });
 		});
+		znorm = norm;
 		for(int k = 1; k < sweeps; k++) {
 			blocks(z, t);
 			S.each([&](size_t i, fvhip_ctx* h) {
@@ -302,7 +312,7 @@ static GmresOut gmres(System& S, LinOp& A, const ArrayOf& b, const ArrayOf& x, d
 		int j = 0;
 		bool done = false;
 		while(j < m && out.iters < maxit) {
-			A.precondition([&](size_t i) { return V(i,j); }, z);
+			A.precondition([&](size_t i) { return V(i,j); }, z, true);
 			A.apply(z, w);
 			// classical Gram-Schmidt (PETSc's KSPGMRESClassicalGramSchmidtOrthogonalization). refine 0
 			// (PETSc's default, KSP_GMRES_CGS_REFINE_NEVER): one projection h = V^T w, w -= V h, and the new

@@ -499,17 +499,20 @@ void k_line_factor(const int* __restrict__ gstart, const int* __restrict__ lcell
 /// Twisted groups: each half's forward sweep ends at the twist cell t with s = A[t][last] g_last; the
 /// lanes swap s, lane j forms z_t = pivot_t (v_t - s_top - s_bottom) and hands it to lane j+32, and both
 /// sweep back from z_t.
+/// one lane's line of k_line_solve; returns the sum of squares of the z rows this lane wrote
 template <typename T>
-__global__ __launch_bounds__(64)
-void k_line_solve(const int* __restrict__ gstart, const int* __restrict__ lcell, const int* __restrict__ llen,
-                  int twisted_groups, const T* __restrict__ D, const T* __restrict__ Lb,
-                  const T* __restrict__ W, double* __restrict__ G, const double* __restrict__ v, double* __restrict__ z)
+__device__ __forceinline__ double line_solve_lane(const int* __restrict__ gstart, const int* __restrict__ lcell,
+                                                  const int* __restrict__ llen, int twisted_groups,
+                                                  const T* __restrict__ D, const T* __restrict__ Lb,
+                                                  const T* __restrict__ W, double* __restrict__ G,
+                                                  const double* __restrict__ v, double* __restrict__ z)
 {
+	double zz = 0.0;
 	const int g = blockIdx.x, j = threadIdx.x;
 	const long long r0 = gstart[g];
 	const int n = llen[64*g + j];
 	const bool tw = g < twisted_groups;
-	if(n == 0 && !tw) return;
+	if(n == 0 && !tw) return zz;
 	const int* cl = lcell + 64*r0 + j;
 	const double4* v4 = reinterpret_cast<const double4*>(v);
 	double4* z4 = reinterpret_cast<double4*>(z);
@@ -567,13 +570,17 @@ void k_line_solve(const int* __restrict__ gstart, const int* __restrict__ lcell,
 			for(int i = 0; i < 4; i++) y[i] = Dt[i][0]*r[0] + Dt[i][1]*r[1] + Dt[i][2]*r[2] + Dt[i][3]*r[3];
 			x = make_double4(y[0], y[1], y[2], y[3]);
 			z4[cl[64*(n-1)]] = x;
+			zz += x.x*x.x; zz += x.y*x.y; zz += x.z*x.z; zz += x.w*x.w;
 		}
 		const double4 xo = make_double4(__shfl_xor(x.x, 32), __shfl_xor(x.y, 32), __shfl_xor(x.z, 32), __shfl_xor(x.w, 32));
 		if(j >= 32) x = xo;                            // z_t from lane j
-		if(n == 0) return;
+		if(n == 0) return zz;
 	}
-	else z4[cl[64*(n-1)]] = x;
-	if(n == 1) return;
+	else {
+		z4[cl[64*(n-1)]] = x;
+		zz += x.x*x.x; zz += x.y*x.y; zz += x.z*x.z; zz += x.w*x.w;
+	}
+	if(n == 1) return zz;
 	double Wk[4][4];
 	ldP16(W, r0 + n - 2, j, Wk);
 	double2 ga = G2[128*(n-2)], gb = G2[128*(n-2) + 64];
@@ -592,6 +599,7 @@ void k_line_solve(const int* __restrict__ gstart, const int* __restrict__ lcell,
 		for(int i = 0; i < 4; i++) y[i] = Wk[i][0]*x.x + Wk[i][1]*x.y + Wk[i][2]*x.z + Wk[i][3]*x.w;
 		x = make_double4(ga.x - y[0], ga.y - y[1], gb.x - y[2], gb.y - y[3]);
 		z4[ck] = x;
+		zz += x.x*x.x; zz += x.y*x.y; zz += x.z*x.z; zz += x.w*x.w;
 		if(k == 0) break;
 		#pragma unroll
 		for(int i = 0; i < 4; i++)
@@ -599,6 +607,22 @@ void k_line_solve(const int* __restrict__ gstart, const int* __restrict__ lcell,
 			for(int q = 0; q < 4; q++) Wk[i][q] = Wn[i][q];
 		ga = na; gb = nb; ck = cp;
 	}
+	return zz;
+}
+
+template <typename T>
+__global__ __launch_bounds__(64)
+void k_line_solve(const int* __restrict__ gstart, const int* __restrict__ lcell, const int* __restrict__ llen,
+                  int twisted_groups, const T* __restrict__ D, const T* __restrict__ Lb,
+                  const T* __restrict__ W, double* __restrict__ G, const double* __restrict__ v, double* __restrict__ z,
+                  double* __restrict__ zpart)
+{
+	double zz = line_solve_lane<T>(gstart, lcell, llen, twisted_groups, D, Lb, W, G, v, z);
+	if(!zpart) return;
+	// the group's sum of squares: a fixed shuffle tree over the 64 lanes
+	#pragma unroll
+	for(int off = 32; off > 0; off >>= 1) zz += __shfl_xor(zz, off);
+	if(threadIdx.x == 0) zpart[blockIdx.x] = zz;
 }
 
 /// z += e (4 doubles per cell)
@@ -625,16 +649,18 @@ void launch_line_factor(const LineSet& Ls, const double* diag, const double* low
 		                   Ls.twisted_groups, diag, lower, upper, Ls.D, Ls.Lb, Ls.W);
 }
 
-void launch_line_solve(const LineSet& Ls, const double* v, double* z, hipStream_t s)
+void launch_line_solve(const LineSet& Ls, const double* v, double* z, hipStream_t s, double* zsq)
 {
 	if(Ls.ngroups <= 0) return;
+	double* zp = zsq ? Ls.zpart : nullptr;
 	if(Ls.single)
 		hipLaunchKernelGGL(k_line_solve<float>, dim3(Ls.ngroups), dim3(64), 0, s, Ls.gstart, Ls.cell, Ls.len,
 		                   Ls.twisted_groups, reinterpret_cast<const float*>(Ls.D), reinterpret_cast<const float*>(Ls.Lb),
-		                   reinterpret_cast<const float*>(Ls.W), Ls.G, v, z);
+		                   reinterpret_cast<const float*>(Ls.W), Ls.G, v, z, zp);
 	else
 		hipLaunchKernelGGL(k_line_solve<double>, dim3(Ls.ngroups), dim3(64), 0, s, Ls.gstart, Ls.cell, Ls.len,
-		                   Ls.twisted_groups, Ls.D, Ls.Lb, Ls.W, Ls.G, v, z);
+		                   Ls.twisted_groups, Ls.D, Ls.Lb, Ls.W, Ls.G, v, z, zp);
+	if(zp) k_sum_partials<<<1, 256, 0, s>>>(Ls.ngroups, zp, zsq);
 }
 
 void launch_add_rows(int n, const double* e, double* z, hipStream_t s)

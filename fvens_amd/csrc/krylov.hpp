@@ -61,6 +61,7 @@ struct LineSet {
 	const int* len = nullptr;        ///< [64 ngroups]
 	int twisted_groups = 0;          ///< leading groups of 32 lines solved from both ends (lanes j, j+32)
 	double *D = nullptr, *Lb = nullptr, *W = nullptr, *G = nullptr;
+	double* zpart = nullptr;         ///< [ngroups] per-group sums of z.z (launch_line_solve with a norm)
 	bool single = false;             ///< D, Lb, W held in fp32 (prec_single; float4 rows in the same buffers)
 };
 #ifndef FVHIP_LINE_MAX
@@ -73,8 +74,9 @@ constexpr int LINE_MAX_CELLS = FVHIP_LINE_MAX;   ///< longest line piece (ctx.hp
 constexpr int LINE_TWIST_MIN = FVHIP_LINE_TWIST_MIN;   ///< shortest line solved from both ends
 /// block-Thomas factorisation of every line (D, Lb, W of the line set) from the block operator
 void launch_line_factor(const LineSet& Ls, const double* diag, const double* lower, const double* upper, hipStream_t s);
-/// z = (block-tridiagonal line part of A)^-1 v
-void launch_line_solve(const LineSet& Ls, const double* v, double* z, hipStream_t s);
+/// z = (block-tridiagonal line part of A)^-1 v; with zsq, also zsq[0] = z.z over the solved rows (each
+/// lane sums the rows it writes, a fixed shuffle tree per group, a fixed-tree sum over the groups)
+void launch_line_solve(const LineSet& Ls, const double* v, double* z, hipStream_t s, double* zsq = nullptr);
 /// z += e over n cells
 void launch_add_rows(int n, const double* e, double* z, hipStream_t s);
 /// block ILU(0) in multicolour order, colour q's rows: dinv[c] = (A_cc - sum_{earlier-colour owned

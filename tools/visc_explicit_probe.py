@@ -25,14 +25,25 @@ def main():
     ap.add_argument("--steps1", type=int, default=20000)
     ap.add_argument("--steps2", type=int, default=100000)
     ap.add_argument("--chunk", type=int, default=10000)
+    ap.add_argument("--mesh", default="c5", help="c5: the C5 family (--scale, --wall); ref: the reference's "
+                    "NACA0012_lam_hybrid_1.msh")
+    ap.add_argument("--physics", default="visc", help="visc (the deck) or naca0 (inviscid M 0.5, alpha 0)")
     args = ap.parse_args()
     import torch
     torch.cuda.set_device(0)
     import fvens_amd as fa
     import cases
     from bench import c4_mesh
-    mesh, dims = c4_mesh(fa, args.scale, 2, wall=args.wall)
-    p = cases.physics("visc")
+    if args.mesh == "ref":
+        mesh, dims = fa.UMesh.read_gmsh(cases.fixture_mesh("NACA0012_lam_hybrid_1")), {"wall_spacing": "ref"}
+    else:
+        mesh, dims = c4_mesh(fa, args.scale, 2, wall=args.wall)
+    if args.physics == "naca0":
+        p = cases.physics("naca", Minf=0.5)
+        p.aoa = 0.0
+        p.bcconf = [fa.FlowBCConfig("slipwall", 2), fa.FlowBCConfig("farfield", 4)]
+    else:
+        p = cases.physics("visc")
     h1 = fa.FlowFV(mesh, p, cases.numerics("ROE", "NONE", "NONE", order2=False))
     h2 = fa.FlowFV(mesh, p, cases.numerics("ROE", "LEASTSQUARES", "NONE"))
     du = torch.tensor(np.tile(cases.freestream(p), (mesh.nelem, 1))[h2.permutation()], device="cuda")
@@ -44,7 +55,11 @@ def main():
         while done < nsteps:
             k = min(args.chunk, nsteps - done)
             t0 = time.time()
-            steps, ratio, hist = h.steady_forward_euler_device(du.data_ptr(), args.cfl, 0.0, k)
+            try:
+                steps, ratio, hist = h.steady_forward_euler_device(du.data_ptr(), args.cfl, 0.0, k)
+            except RuntimeError as e:
+                print(json.dumps({"stage": name, "steps_before": done, "error": str(e)}), flush=True)
+                break
             if r0 is None:
                 r0 = float(hist[0])
             done += steps
@@ -55,6 +70,18 @@ def main():
                               "CL": cl, "CDp": cdp, "CDsf": cdsf, "seconds": round(time.time() - t0, 1)}), flush=True)
             if not np.isfinite(hist[-1]):
                 break
+            # where the residual sits: the cells with the largest |r_energy| / area
+            dr = torch.zeros((mesh.nelem, 4), dtype=torch.float64, device="cuda")
+            ddt = torch.zeros(mesh.nelem, dtype=torch.float64, device="cuda")
+            h.compute_residual_device(du.data_ptr(), dr.data_ptr(), ddt.data_ptr(), True, True)
+            h.synchronize()
+            perm = h.permutation()
+            r = np.empty((mesh.nelem, 4))
+            r[perm] = dr.cpu().numpy()
+            q = np.abs(r[:, 3]) / mesh.area
+            top = np.argsort(-q)[:6]
+            print(json.dumps({"top_cells": [[int(c), float("%.3e" % q[c]), [round(float(x), 6) for x in mesh.rc[c]],
+                                             float("%.2e" % mesh.area[c])] for c in top]}), flush=True)
     h1.close()
     h2.close()
 
