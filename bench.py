@@ -48,6 +48,10 @@ C4_WALL_SPACING = 1e-5
 # direction map (0) the cosine-clustered trailing-edge points crowd the far field at angle 0, leaving
 # sliver triangles (aspect ratio ~1e3) along the wake line where second-order solves blow up
 C4_FARMAP = 1
+# the viscous C5 family (config 5) adds farmap bit 2: the layers leave the body along its normal. With
+# straight lines the first layers over the last percent of chord were 8-9 degree parallelograms and no
+# second-order solve of the laminar deck converged on them (profiles/r05/c5_family_convergence_probes.jsonl)
+C5_FARMAP = 3
 
 
 def c4_mesh(fa, scale, mult=1, wall=None, farmap=None):
@@ -55,7 +59,7 @@ def c4_mesh(fa, scale, mult=1, wall=None, farmap=None):
     nq = 256 // scale
     ntri = 864 // scale
     ws = C4_WALL_SPACING if wall is None else wall
-    fm = C4_FARMAP if farmap is None else farmap
+    fm = (C4_FARMAP if mult == 1 else C5_FARMAP) if farmap is None else farmap
     return (fa.UMesh.naca_ogrid(nt, nq, ntri, 20.0, ws, farmap=fm),
             dict(ntheta=nt, nquad=nq, ntri=ntri, wall_spacing=ws, farmap=fm))
 

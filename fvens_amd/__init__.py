@@ -152,7 +152,8 @@ class UMesh:
     @classmethod
     def naca_ogrid(cls, ntheta, nquad, ntri, rfar=20.0, wallspacing=1e-4, farmap=0):
         """farmap 0: far-field points in the direction of the surface point from mid-chord; 1: far-field
-        angles uniform in the surface parameter (mesh.cpp generateNacaOgrid)"""
+        angles uniform in the surface parameter; + 2: layers leave the body along its normal (blended into
+        the straight line to the far field; mesh.cpp generateNacaOgrid)"""
         h = ctypes.c_void_p()
         check(_ffi.lib().fvmesh_generate(0, ntheta, nquad, ntri, rfar, wallspacing, float(farmap), ctypes.byref(h)))
         return cls(h.value)

@@ -501,14 +501,13 @@ void k_line_factor(const int* __restrict__ gstart, const int* __restrict__ lcell
 /// sweep back from z_t.
 /// one lane's line of k_line_solve; returns the sum of squares of the z rows this lane wrote
 template <typename T>
-__device__ __forceinline__ double line_solve_lane(const int* __restrict__ gstart, const int* __restrict__ lcell,
+__device__ __forceinline__ double line_solve_lane(int g, int j, const int* __restrict__ gstart, const int* __restrict__ lcell,
                                                   const int* __restrict__ llen, int twisted_groups,
                                                   const T* __restrict__ D, const T* __restrict__ Lb,
                                                   const T* __restrict__ W, double* __restrict__ G,
                                                   const double* __restrict__ v, double* __restrict__ z)
 {
 	double zz = 0.0;
-	const int g = blockIdx.x, j = threadIdx.x;
 	const long long r0 = gstart[g];
 	const int n = llen[64*g + j];
 	const bool tw = g < twisted_groups;
@@ -617,12 +616,181 @@ void k_line_solve(const int* __restrict__ gstart, const int* __restrict__ lcell,
                   const T* __restrict__ W, double* __restrict__ G, const double* __restrict__ v, double* __restrict__ z,
                   double* __restrict__ zpart)
 {
-	double zz = line_solve_lane<T>(gstart, lcell, llen, twisted_groups, D, Lb, W, G, v, z);
+	double zz = line_solve_lane<T>(blockIdx.x, threadIdx.x, gstart, lcell, llen, twisted_groups, D, Lb, W, G, v, z);
 	if(!zpart) return;
 	// the group's sum of squares: a fixed shuffle tree over the 64 lanes
 	#pragma unroll
 	for(int off = 32; off > 0; off >>= 1) zz += __shfl_xor(zz, off);
 	if(threadIdx.x == 0) zpart[blockIdx.x] = zz;
+}
+
+/// Row i (4 values) of slot j's 4x4 block in group row r of the pair-interleaved factor storage (ldP16's
+/// rows q = 2i, 2i+1; fp32: the float4 of row i)
+__device__ __forceinline__ void ldRow(const double* __restrict__ X, long long r, int j, int i, double (&a)[4])
+{
+	const double2* p = reinterpret_cast<const double2*>(X) + 512*r + 128*i + j;
+	const double2 t0 = p[0], t1 = p[64];
+	a[0] = t0.x; a[1] = t0.y; a[2] = t1.x; a[3] = t1.y;
+}
+__device__ __forceinline__ void ldRow(const float* __restrict__ X, long long r, int j, int i, double (&a)[4])
+{
+	const float4 t = reinterpret_cast<const float4*>(X)[256*r + 64*i + j];
+	a[0] = t.x; a[1] = t.y; a[2] = t.z; a[3] = t.w;
+}
+/// lane Q's value of this lane's quad (DPP quad_perm, no LDS crossbar)
+template <int Q>
+__device__ __forceinline__ double quad_bcast(double x)
+{
+	constexpr int ctrl = Q | (Q << 2) | (Q << 4) | (Q << 6);
+	const long long b = __double_as_longlong(x);
+	const int lo = __builtin_amdgcn_update_dpp(0, static_cast<int>(b), ctrl, 0xF, 0xF, false);
+	const int hi = __builtin_amdgcn_update_dpp(0, static_cast<int>(b >> 32), ctrl, 0xF, 0xF, false);
+	return __longlong_as_double((static_cast<long long>(hi) << 32) | static_cast<unsigned int>(lo));
+}
+__device__ __forceinline__ void quad_all(double x, double (&o)[4])
+{
+	o[0] = quad_bcast<0>(x); o[1] = quad_bcast<1>(x); o[2] = quad_bcast<2>(x); o[3] = quad_bcast<3>(x);
+}
+
+/// The line solve with four lanes per line (one block row each) for the twisted groups -- the long lines,
+/// whose one-lane chains of dependent loads bound k_line_solve -- and the one-lane form for the others.
+/// Block b < twisted_groups is twisted group b: wave w takes slots 8w..8w+7 (top halves) and their partners
+/// 32+8w..32+8w+7 (bottom halves), lane 4 q + i row i of the q-th of those 16 slots, so a slot's partner is
+/// lane ^ 32. Per cell a lane loads its rows of D, Lb (W backward) and its component of v (g, z): the
+/// quad's four lanes read whole rows. The rows of the next P cells are in flight while a cell is computed
+/// (a ring of P register slots, the cell ids 2P ahead), and the quad exchanges its four components by DPP.
+/// Each row is computed in the lane that owns it with k_line_solve's expressions, and the z.z sums keep
+/// that kernel's order (a quad's row-0 lane sums the rows its slot writes; the group's 64 slot sums go
+/// through the same butterfly): z and zsq are bitwise k_line_solve's. Blocks past the twisted groups take
+/// four one-lane groups each (a wave per group).
+template <typename T, int P>
+__global__ __launch_bounds__(256)
+void k_line_solve_rows(const int* __restrict__ gstart, const int* __restrict__ lcell, const int* __restrict__ llen,
+                       int twisted_groups, int ngroups, const T* __restrict__ D, const T* __restrict__ Lb,
+                       const T* __restrict__ W, double* __restrict__ G, const double* __restrict__ v,
+                       double* __restrict__ z, double* __restrict__ zpart)
+{
+	const int b = blockIdx.x, w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+	if(b >= twisted_groups) {                             // block-uniform
+		const int g = twisted_groups + 4*(b - twisted_groups) + w;
+		if(g >= ngroups) return;
+		double zz = line_solve_lane<T>(g, lane, gstart, lcell, llen, twisted_groups, D, Lb, W, G, v, z);
+		if(!zpart) return;
+		#pragma unroll
+		for(int off = 32; off > 0; off >>= 1) zz += __shfl_xor(zz, off);
+		if(lane == 0) zpart[g] = zz;
+		return;
+	}
+	__shared__ double zs[64];
+	const int g = b, qd = lane >> 2, i = lane & 3;
+	const bool top = qd < 8;
+	const int j = top ? 8*w + qd : 24 + 8*w + qd;         // 32 + 8w + (qd - 8)
+	const long long r0 = gstart[g];
+	const int n = llen[64*g + j];
+	const int* cl = lcell + 64*r0 + j;
+	auto gix = [&](int k) { return 2*(128*(r0 + k) + 64*(i >> 1) + j) + (i & 1); };
+	double zz = 0.0;
+	double gp[4] = {0.0, 0.0, 0.0, 0.0};
+	double vt = 0.0, s = 0.0;
+	{
+		double Dr[P][4], Lr[P][4], vr[P];
+		int cn[P];
+		#pragma unroll
+		for(int u = 0; u < P; u++) {
+			if(u < n) {
+				ldRow(D, r0 + u, j, i, Dr[u]);
+				if(u > 0) ldRow(Lb, r0 + u, j, i, Lr[u]);
+				else { Lr[u][0] = 0.0; Lr[u][1] = 0.0; Lr[u][2] = 0.0; Lr[u][3] = 0.0; }
+				vr[u] = v[4*static_cast<size_t>(cl[64*u]) + i];
+			}
+			cn[u] = P + u < n ? cl[64*(P + u)] : 0;
+		}
+		bool stop = n == 0;
+		for(int base = 0; base < n && !stop; base += P) {
+			#pragma unroll
+			for(int u = 0; u < P; u++) {
+				const int k = base + u;
+				if(k >= n || stop) break;
+				if(k == n - 1) {                           // the twist: this side's term A[t][last] g_last
+					s = Lr[u][0]*gp[0] + Lr[u][1]*gp[1] + Lr[u][2]*gp[2] + Lr[u][3]*gp[3];
+					vt = vr[u];
+					stop = true;
+					break;
+				}
+				double r = vr[u];
+				if(k > 0) r -= Lr[u][0]*gp[0] + Lr[u][1]*gp[1] + Lr[u][2]*gp[2] + Lr[u][3]*gp[3];
+				double rq[4];
+				quad_all(r, rq);
+				const double y = Dr[u][0]*rq[0] + Dr[u][1]*rq[1] + Dr[u][2]*rq[2] + Dr[u][3]*rq[3];
+				quad_all(y, gp);
+				G[gix(k)] = y;
+				if(k + P < n) {
+					ldRow(D, r0 + k + P, j, i, Dr[u]);
+					ldRow(Lb, r0 + k + P, j, i, Lr[u]);
+					vr[u] = v[4*static_cast<size_t>(cn[u]) + i];
+					cn[u] = k + 2*P < n ? cl[64*(k + 2*P)] : 0;
+				}
+			}
+		}
+	}
+	// the twist cell: the top lane of the pair forms z_t = pivot_t (v_t - s_top - s_bottom), the bottom
+	// lane receives it
+	double x[4];
+	{
+		const double so = __shfl_xor(s, 32);
+		x[0] = 0.0; x[1] = 0.0; x[2] = 0.0; x[3] = 0.0;
+		if(top && n > 0) {
+			double Dt[4];
+			ldRow(D, r0 + n - 1, j, i, Dt);
+			const double r = (vt - s) - so;
+			double rq[4];
+			quad_all(r, rq);
+			const double y = Dt[0]*rq[0] + Dt[1]*rq[1] + Dt[2]*rq[2] + Dt[3]*rq[3];
+			quad_all(y, x);
+			z[4*static_cast<size_t>(cl[64*(n - 1)]) + i] = y;
+			if(i == 0) { zz += x[0]*x[0]; zz += x[1]*x[1]; zz += x[2]*x[2]; zz += x[3]*x[3]; }
+		}
+		double xo[4];
+		#pragma unroll
+		for(int q = 0; q < 4; q++) xo[q] = __shfl_xor(x[q], 32);
+		if(!top) {
+			#pragma unroll
+			for(int q = 0; q < 4; q++) x[q] = xo[q];
+		}
+	}
+	// backward: z_k = g_k - W_k z_{k+1}, k = n-2 .. 0
+	if(n > 1) {
+		double Wr[P][4], gr[P];
+		int zc[P];
+		#pragma unroll
+		for(int u = 0; u < P; u++) {
+			const int k = n - 2 - u;
+			if(k >= 0) { ldRow(W, r0 + k, j, i, Wr[u]); gr[u] = G[gix(k)]; zc[u] = cl[64*k]; }
+		}
+		for(int base = 0; base <= n - 2; base += P) {
+			#pragma unroll
+			for(int u = 0; u < P; u++) {
+				const int k = n - 2 - (base + u);
+				if(k < 0) break;
+				const double y = Wr[u][0]*x[0] + Wr[u][1]*x[1] + Wr[u][2]*x[2] + Wr[u][3]*x[3];
+				const double xi = gr[u] - y;
+				quad_all(xi, x);
+				z[4*static_cast<size_t>(zc[u]) + i] = xi;
+				if(i == 0) { zz += x[0]*x[0]; zz += x[1]*x[1]; zz += x[2]*x[2]; zz += x[3]*x[3]; }
+				const int k2 = k - P;
+				if(k2 >= 0) { ldRow(W, r0 + k2, j, i, Wr[u]); gr[u] = G[gix(k2)]; zc[u] = cl[64*k2]; }
+			}
+		}
+	}
+	if(!zpart) return;                                    // block-uniform
+	if(i == 0) zs[j] = zz;
+	__syncthreads();
+	if(w == 0) {
+		double t = zs[lane];
+		#pragma unroll
+		for(int off = 32; off > 0; off >>= 1) t += __shfl_xor(t, off);
+		if(lane == 0) zpart[g] = t;
+	}
 }
 
 /// z += e (4 doubles per cell)
@@ -649,11 +817,25 @@ void launch_line_factor(const LineSet& Ls, const double* diag, const double* low
 		                   Ls.twisted_groups, diag, lower, upper, Ls.D, Ls.Lb, Ls.W);
 }
 
+#ifndef FVHIP_LINE_ROWS
+#define FVHIP_LINE_ROWS 4
+#endif
 void launch_line_solve(const LineSet& Ls, const double* v, double* z, hipStream_t s, double* zsq)
 {
 	if(Ls.ngroups <= 0) return;
 	double* zp = zsq ? Ls.zpart : nullptr;
-	if(Ls.single)
+	if(FVHIP_LINE_ROWS > 0) {
+		constexpr int P = FVHIP_LINE_ROWS > 0 ? FVHIP_LINE_ROWS : 1;
+		const int T = Ls.twisted_groups, nb = T + (Ls.ngroups - T + 3)/4;
+		if(Ls.single)
+			hipLaunchKernelGGL((k_line_solve_rows<float, P>), dim3(nb), dim3(256), 0, s, Ls.gstart, Ls.cell, Ls.len, T,
+			                   Ls.ngroups, reinterpret_cast<const float*>(Ls.D), reinterpret_cast<const float*>(Ls.Lb),
+			                   reinterpret_cast<const float*>(Ls.W), Ls.G, v, z, zp);
+		else
+			hipLaunchKernelGGL((k_line_solve_rows<double, P>), dim3(nb), dim3(256), 0, s, Ls.gstart, Ls.cell, Ls.len, T,
+			                   Ls.ngroups, Ls.D, Ls.Lb, Ls.W, Ls.G, v, z, zp);
+	}
+	else if(Ls.single)
 		hipLaunchKernelGGL(k_line_solve<float>, dim3(Ls.ngroups), dim3(64), 0, s, Ls.gstart, Ls.cell, Ls.len,
 		                   Ls.twisted_groups, reinterpret_cast<const float*>(Ls.D), reinterpret_cast<const float*>(Ls.Lb),
 		                   reinterpret_cast<const float*>(Ls.W), Ls.G, v, z, zp);

@@ -645,7 +645,7 @@ MeshData generateNacaOgrid(int ntheta, int nquad, int ntri, double rfar, double 
 		// above and below mid-chord fan out to ~1 degree per cell at ntheta 2048); farmap 1: far-field
 		// angles uniform in the surface parameter (lower surface TE -> LE: 0 -> -pi, upper: pi -> 0)
 		double ang = std::atan2(y, x - 0.5);
-		if(farmap == 1) ang = i <= half ? -PI*static_cast<double>(i)/half : PI - PI*static_cast<double>(i-half)/half;
+		if(farmap & 1) ang = i <= half ? -PI*static_cast<double>(i)/half : PI - PI*static_cast<double>(i-half)/half;
 		if(i == 0) ang = 0.0;
 		if(i == half) ang = PI;
 		fx[i] = 0.5 + rfar*std::cos(ang); fy[i] = rfar*std::sin(ang);
@@ -672,11 +672,35 @@ MeshData generateNacaOgrid(int ntheta, int nquad, int ntri, double rfar, double 
 		for(int j = 1; j <= nl; j++) { acc += d; eta[j] = acc; d *= q; }
 		for(int j = 1; j <= nl; j++) eta[j] /= acc;
 	}
+	// farmap bit 2: the layers leave the body along its normal. Straight lines from each surface point
+	// to its far-field point meet the aft surface at a few degrees (the first layers of the C5 family
+	// were 8-9 degree parallelograms over the last percent of chord: a second-order residual on them has no
+	// steady state). Point j of line i sits at the distance eta_j*|f - s| from the surface point along
+	// the direction (1 - w) n + w t, n the outward normal, t the line's own direction, w = smoothstep(d / 3
+	// chords) of that distance d: normal through the boundary layer (w = 0.002 at 0.08 chord), back on the
+	// straight line from three chords out (the cells beyond are those of farmap 0/1). The trailing-edge
+	// point's normal is the bisector (+x), so the corner is a fan of cells. Blending over 1 / 2 / 3 / 5
+	// chords leaves 56 / 8 / 8 / 8 cells skewed by more than 60 degrees (3,390 with straight lines, C5/8).
+	const bool wallnormal = (farmap & 2) != 0;
+	const double blend = 3.0;
 	for(int j = 0; j <= nl; j++)
 		for(int i = 0; i < ntheta; i++) {
 			const size_t p = static_cast<size_t>(j)*ntheta + i;
-			m.coords[2*p] = sx[i] + eta[j]*(fx[i] - sx[i]);
-			m.coords[2*p+1] = sy[i] + eta[j]*(fy[i] - sy[i]);
+			double dx = fx[i] - sx[i], dy = fy[i] - sy[i];
+			const double L = std::sqrt(dx*dx + dy*dy);
+			if(wallnormal && j > 0 && eta[j]*L < blend) {
+				const int ip = (i + 1) % ntheta, im = (i + ntheta - 1) % ntheta;
+				double nx = sy[ip] - sy[im], ny = -(sx[ip] - sx[im]);
+				if(nx*dx + ny*dy < 0) { nx = -nx; ny = -ny; }
+				const double nn = std::sqrt(nx*nx + ny*ny);
+				const double x = eta[j]*L/blend;
+				const double w = x*x*(3.0 - 2.0*x);
+				double ex = (1.0 - w)*nx/nn + w*dx/L, ey = (1.0 - w)*ny/nn + w*dy/L;
+				const double en = std::sqrt(ex*ex + ey*ey);
+				dx = L*ex/en; dy = L*ey/en;
+			}
+			m.coords[2*p] = sx[i] + eta[j]*dx;
+			m.coords[2*p+1] = sy[i] + eta[j]*dy;
 		}
 	addOgridCells(m, ntheta, nquad, ntri, 0);
 	finishOgrid(m, ntheta, nl, 2, 4);

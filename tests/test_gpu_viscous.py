@@ -73,7 +73,7 @@ def _check_vs_oracle(m, p, n, u):
 
 
 def test_c5_residual_full_size():
-    m = fa.UMesh.naca_ogrid(4096, 256, 864, 20.0, 1e-5, farmap=1)       # bench.py --numerics config5's mesh
+    m = fa.UMesh.naca_ogrid(4096, 256, 864, 20.0, 1e-5, farmap=3)       # bench.py --numerics config5's mesh
     assert m.nelem == 8126464 and m.naface == 12718080
     p = cases.physics("visc")
     n = cases.numerics("ROE", "LEASTSQUARES", "NONE")

@@ -37,6 +37,7 @@ def test_gmsh_fixture_indexing(name):
 @pytest.mark.parametrize("gen", [
     lambda: fa.UMesh.naca_ogrid(64, 4, 12),
     lambda: fa.UMesh.naca_ogrid(200, 10, 30, 15.0, 1e-3),
+    lambda: fa.UMesh.naca_ogrid(256, 16, 54, 20.0, 1e-5, farmap=3),
     lambda: fa.UMesh.cylinder_ogrid(48, 12),
     lambda: fa.UMesh.flat_plate(40, 24),
 ])
@@ -86,6 +87,40 @@ def test_c2_naca_size():
     """C2: NACA0012 O-grid Ntheta=512, 64 quad + 192 triangle layers: 229,376 cells, 360,960 faces"""
     m = fa.UMesh.naca_ogrid(512, 64, 192)
     assert (m.nelem, m.naface) == (229376, 360960)
+
+
+def _quad_skew(m):
+    """largest |corner angle - 90 degrees| of each quadrangle"""
+    q = np.where(m.nnode == 4)[0]
+    P = m.coords[m.inpoel[q, :4]]
+    dev = np.zeros(len(q))
+    for i in range(4):
+        a, b = P[:, i - 1] - P[:, i], P[:, (i + 1) % 4] - P[:, i]
+        c = (a * b).sum(1) / np.linalg.norm(a, axis=1) / np.linalg.norm(b, axis=1)
+        dev = np.maximum(dev, np.abs(np.degrees(np.arccos(np.clip(c, -1, 1))) - 90.0))
+    return q, dev
+
+
+def test_naca_wall_normal_layers():
+    """generateNacaOgrid farmap bit 2 (the C5 family): the layers leave the body along its normal. On C5/8
+    (512 x (32 + 108) layers, 1e-5 wall spacing) straight lines to the far field leave 4,922 of the 16,384
+    boundary-layer quadrangles skewed by more than 45 degrees (the aft surface: 8-9 degree parallelograms);
+    normal layers leave only the trailing-edge fan's 28, every cell stays positive, the first layer's
+    normal spacing is the wall spacing, and the cells three chords out are those of farmap 1."""
+    m1 = fa.UMesh.naca_ogrid(512, 32, 108, 20.0, 1e-5, farmap=1)
+    m3 = fa.UMesh.naca_ogrid(512, 32, 108, 20.0, 1e-5, farmap=3)
+    assert (m1.nelem, m1.naface) == (m3.nelem, m3.naface) and np.array_equal(m1.intfac, m3.intfac)
+    assert (m3.area > 0).all()
+    _, d1 = _quad_skew(m1)
+    _, d3 = _quad_skew(m3)
+    assert (d1 > 45).sum() > 4000 and (d3 > 45).sum() <= 28, ((d1 > 45).sum(), (d3 > 45).sum())
+    # first-layer points: distance from the surface point ~ 1e-5 * |f - s| / 20, along the normal
+    s, p1 = m3.coords[:512], m3.coords[512:1024]
+    d = np.linalg.norm(p1 - s, axis=1)
+    assert np.all((d > 0.97e-5) & (d < 1.03e-5))
+    own = np.tile(m1.coords[:512], (141, 1))          # each point's surface point (point j*512 + i)
+    far = np.linalg.norm(m1.coords - own, axis=1) >= 3.0
+    assert far.sum() > 10000 and np.array_equal(m1.coords[far], m3.coords[far])
 
 
 def test_gmsh_roundtrip(tmp_path):

@@ -61,9 +61,7 @@ def main():
         nx = ny = 1024 // args.scale
         mesh, dims = fa.UMesh.flat_plate(nx, ny), dict(nx=nx, ny=ny)
     elif args.case == "visc-c5":    # BASELINE config 5: laminar NACA0012, 8,126,464 cells, 1e-5 wall spacing
-        nt = 4096 // args.scale
-        mesh = fa.UMesh.naca_ogrid(nt, 256 // args.scale, 864 // args.scale, 20.0, 1e-5, farmap=1)
-        dims = dict(ntheta=nt, nquad=256 // args.scale, ntri=864 // args.scale, wall_spacing=1e-5, farmap=1)
+        mesh, dims = c4_mesh(fa, args.scale, 2)
     else:
         mesh, dims = c4_mesh(fa, args.scale)
     for out in implicit_steps(mesh, args.case, steps=args.steps, warmup=args.warmup, init_steps=args.init_steps,

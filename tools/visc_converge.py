@@ -66,9 +66,10 @@ def run(scale=1, matrix_free=True, main_steps=400, init_steps=50, lin_maxit=60, 
             return {"error": str(e), "steps": len(hh), "converged": False, "seconds": round(time.perf_counter() - t0, 2),
                     "history": [float(x) for x in hh]}
     try:
-        rec["init"] = stage(start, fa.ImplicitConfig(cflinit=cfl_init[0], cflfin=cfl_init[1], tol=1e-1,
-                                                    maxiter=init_steps, **lin))
-        if "error" not in rec["init"]:
+        if init_steps > 0:
+            rec["init"] = stage(start, fa.ImplicitConfig(cflinit=cfl_init[0], cflfin=cfl_init[1], tol=1e-1,
+                                                        maxiter=init_steps, **lin))
+        if "error" not in rec.get("init", {}):
             rec["main"] = stage(main, fa.ImplicitConfig(cflinit=cfl_main[0], cflfin=cfl_main[1], tol=tol,
                                                         maxiter=main_steps, matrix_free=matrix_free, **lin))
     finally:
@@ -91,6 +92,7 @@ def main():
     ap.add_argument("--scale", type=int, default=1)
     ap.add_argument("--assembled", action="store_true")
     ap.add_argument("--main-steps", type=int, default=400)
+    ap.add_argument("--init-steps", type=int, default=50, help="0: no first-order start (main from the free stream)")
     ap.add_argument("--lin-maxit", type=int, default=60)
     ap.add_argument("--restart", type=int, default=60)
     ap.add_argument("--sweeps", type=int, default=3)
@@ -103,7 +105,7 @@ def main():
     args = ap.parse_args()
     import torch
     torch.cuda.set_device(0)
-    r = run(args.scale, not args.assembled, args.main_steps, lin_maxit=args.lin_maxit, restart=args.restart,
+    r = run(args.scale, not args.assembled, args.main_steps, init_steps=args.init_steps, lin_maxit=args.lin_maxit, restart=args.restart,
             sweeps=args.sweeps, heartbeat=lambda s: print(s, flush=True), cfl_init=args.cfl_init,
             cfl_main=args.cfl_main, min_relax=args.min_relax, lin_rtol=args.lin_rtol, wall=args.wall)
     r["tag"] = args.tag
