@@ -692,46 +692,52 @@ void k_line_solve_rows(const int* __restrict__ gstart, const int* __restrict__ l
 	double zz = 0.0;
 	double gp[4] = {0.0, 0.0, 0.0, 0.0};
 	double vt = 0.0, s = 0.0;
-	{
+	// forward over cells 0 .. n-2, then the twist cell n-1 (every slot of these groups ends in one). The
+	// loads are unconditional (rows past the end are clamped to the last cell and land in slots whose cell
+	// is done) and the loop runs whole rounds of P cells with the remainder after it: one back edge, no
+	// early exits, so the compiler keeps the ring in flight across steps instead of draining it.
+	auto fwd = [&](int k, double (&Dk)[4], double (&Lk)[4], double& vk, int& ck) {
+		double r = vk;
+		if(k > 0) r -= Lk[0]*gp[0] + Lk[1]*gp[1] + Lk[2]*gp[2] + Lk[3]*gp[3];
+		double rq[4];
+		quad_all(r, rq);
+		const double y = Dk[0]*rq[0] + Dk[1]*rq[1] + Dk[2]*rq[2] + Dk[3]*rq[3];
+		quad_all(y, gp);
+		G[gix(k)] = y;
+		const int kk = min(k + P, n - 1);
+		ldRow(D, r0 + kk, j, i, Dk);
+		ldRow(Lb, r0 + kk, j, i, Lk);
+		vk = v[4*static_cast<size_t>(ck) + i];
+		ck = cl[64*min(k + 2*P, n - 1)];
+		__builtin_amdgcn_sched_barrier(0);              // the machine scheduler would sink these loads to the round's end
+	};
+	if(n > 0) {
 		double Dr[P][4], Lr[P][4], vr[P];
 		int cn[P];
 		#pragma unroll
 		for(int u = 0; u < P; u++) {
-			if(u < n) {
-				ldRow(D, r0 + u, j, i, Dr[u]);
-				if(u > 0) ldRow(Lb, r0 + u, j, i, Lr[u]);
-				else { Lr[u][0] = 0.0; Lr[u][1] = 0.0; Lr[u][2] = 0.0; Lr[u][3] = 0.0; }
-				vr[u] = v[4*static_cast<size_t>(cl[64*u]) + i];
-			}
-			cn[u] = P + u < n ? cl[64*(P + u)] : 0;
+			const int kk = min(u, n - 1);
+			ldRow(D, r0 + kk, j, i, Dr[u]);
+			ldRow(Lb, r0 + kk, j, i, Lr[u]);
+			vr[u] = v[4*static_cast<size_t>(cl[64*kk]) + i];
+			cn[u] = cl[64*min(P + u, n - 1)];
 		}
-		bool stop = n == 0;
-		for(int base = 0; base < n && !stop; base += P) {
+		const int nf = n - 1, full = nf - nf % P;
+		for(int base = 0; base < full; base += P) {
 			#pragma unroll
-			for(int u = 0; u < P; u++) {
-				const int k = base + u;
-				if(k >= n || stop) break;
-				if(k == n - 1) {                           // the twist: this side's term A[t][last] g_last
-					s = Lr[u][0]*gp[0] + Lr[u][1]*gp[1] + Lr[u][2]*gp[2] + Lr[u][3]*gp[3];
-					vt = vr[u];
-					stop = true;
-					break;
-				}
-				double r = vr[u];
-				if(k > 0) r -= Lr[u][0]*gp[0] + Lr[u][1]*gp[1] + Lr[u][2]*gp[2] + Lr[u][3]*gp[3];
-				double rq[4];
-				quad_all(r, rq);
-				const double y = Dr[u][0]*rq[0] + Dr[u][1]*rq[1] + Dr[u][2]*rq[2] + Dr[u][3]*rq[3];
-				quad_all(y, gp);
-				G[gix(k)] = y;
-				if(k + P < n) {
-					ldRow(D, r0 + k + P, j, i, Dr[u]);
-					ldRow(Lb, r0 + k + P, j, i, Lr[u]);
-					vr[u] = v[4*static_cast<size_t>(cn[u]) + i];
-					cn[u] = k + 2*P < n ? cl[64*(k + 2*P)] : 0;
-				}
-			}
+			for(int u = 0; u < P; u++) fwd(base + u, Dr[u], Lr[u], vr[u], cn[u]);
 		}
+		#pragma unroll
+		for(int u = 0; u < P - 1; u++)
+			if(full + u < nf) fwd(full + u, Dr[u], Lr[u], vr[u], cn[u]);
+		// the twist: this side's term A[t][last] g_last, from the ring slot of cell n-1
+		const int ut = nf % P;
+		#pragma unroll
+		for(int u = 0; u < P; u++)
+			if(u == ut) {
+				s = Lr[u][0]*gp[0] + Lr[u][1]*gp[1] + Lr[u][2]*gp[2] + Lr[u][3]*gp[3];
+				vt = vr[u];
+			}
 	}
 	// the twist cell: the top lane of the pair forms z_t = pivot_t (v_t - s_top - s_bottom), the bottom
 	// lane receives it
@@ -758,29 +764,33 @@ void k_line_solve_rows(const int* __restrict__ gstart, const int* __restrict__ l
 			for(int q = 0; q < 4; q++) x[q] = xo[q];
 		}
 	}
-	// backward: z_k = g_k - W_k z_{k+1}, k = n-2 .. 0
+	// backward: z_k = g_k - W_k z_{k+1}, k = n-2 .. 0 (clamped loads, whole rounds, as forward)
+	auto bwd = [&](int k, double (&Wk)[4], double& gk, int& ck) {
+		const double y = Wk[0]*x[0] + Wk[1]*x[1] + Wk[2]*x[2] + Wk[3]*x[3];
+		const double xi = gk - y;
+		quad_all(xi, x);
+		z[4*static_cast<size_t>(ck) + i] = xi;
+		if(i == 0) { zz += x[0]*x[0]; zz += x[1]*x[1]; zz += x[2]*x[2]; zz += x[3]*x[3]; }
+		const int k2 = max(k - P, 0);
+		ldRow(W, r0 + k2, j, i, Wk); gk = G[gix(k2)]; ck = cl[64*k2];
+		__builtin_amdgcn_sched_barrier(0);
+	};
 	if(n > 1) {
 		double Wr[P][4], gr[P];
 		int zc[P];
 		#pragma unroll
 		for(int u = 0; u < P; u++) {
-			const int k = n - 2 - u;
-			if(k >= 0) { ldRow(W, r0 + k, j, i, Wr[u]); gr[u] = G[gix(k)]; zc[u] = cl[64*k]; }
+			const int k = max(n - 2 - u, 0);
+			ldRow(W, r0 + k, j, i, Wr[u]); gr[u] = G[gix(k)]; zc[u] = cl[64*k];
 		}
-		for(int base = 0; base <= n - 2; base += P) {
+		const int nb = n - 1, full = nb - nb % P;
+		for(int base = 0; base < full; base += P) {
 			#pragma unroll
-			for(int u = 0; u < P; u++) {
-				const int k = n - 2 - (base + u);
-				if(k < 0) break;
-				const double y = Wr[u][0]*x[0] + Wr[u][1]*x[1] + Wr[u][2]*x[2] + Wr[u][3]*x[3];
-				const double xi = gr[u] - y;
-				quad_all(xi, x);
-				z[4*static_cast<size_t>(zc[u]) + i] = xi;
-				if(i == 0) { zz += x[0]*x[0]; zz += x[1]*x[1]; zz += x[2]*x[2]; zz += x[3]*x[3]; }
-				const int k2 = k - P;
-				if(k2 >= 0) { ldRow(W, r0 + k2, j, i, Wr[u]); gr[u] = G[gix(k2)]; zc[u] = cl[64*k2]; }
-			}
+			for(int u = 0; u < P; u++) bwd(n - 2 - (base + u), Wr[u], gr[u], zc[u]);
 		}
+		#pragma unroll
+		for(int u = 0; u < P - 1; u++)
+			if(full + u < nb) bwd(n - 2 - (full + u), Wr[u], gr[u], zc[u]);
 	}
 	if(!zpart) return;                                    // block-uniform
 	if(i == 0) zs[j] = zz;
