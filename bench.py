@@ -48,18 +48,24 @@ C4_WALL_SPACING = 1e-5
 # direction map (0) the cosine-clustered trailing-edge points crowd the far field at angle 0, leaving
 # sliver triangles (aspect ratio ~1e3) along the wake line where second-order solves blow up
 C4_FARMAP = 1
-# the viscous C5 family (config 5) adds farmap bit 2: the layers leave the body along its normal. With
-# straight lines the first layers over the last percent of chord were 8-9 degree parallelograms and no
-# second-order solve of the laminar deck converged on them (profiles/r05/c5_family_convergence_probes.jsonl)
-C5_FARMAP = 3
+# the viscous C5 family (config 5) is a C-grid (generateNacaCgrid): on the O-grid the aft boundary layer
+# was 8-9 degree parallelograms (straight lines) or the trailing-edge point's cells fanned over the wake
+# (wall-normal lines, farmap 3), and no second-order solve of the laminar deck converged on either
+# (profiles/r05/c5_family_convergence_probes.jsonl)
 
 
 def c4_mesh(fa, scale, mult=1, wall=None, farmap=None):
+    """C4 (mult 1): the O-grid; C5 (mult 2): the C-grid of the same cell count (4096 columns: 3072 round
+    the body, 512 along each wake), unless an O-grid `farmap` is asked for"""
     nt = 2048 * mult // scale
     nq = 256 // scale
     ntri = 864 // scale
     ws = C4_WALL_SPACING if wall is None else wall
-    fm = (C4_FARMAP if mult == 1 else C5_FARMAP) if farmap is None else farmap
+    if mult == 2 and farmap is None:
+        ns, nw = 3 * nt // 4, nt // 8
+        return (fa.UMesh.naca_cgrid(ns, nw, nq, ntri, 20.0, ws),
+                dict(topology="C-grid", nsurf=ns, nwake=nw, nquad=nq, ntri=ntri, wall_spacing=ws))
+    fm = C4_FARMAP if farmap is None else farmap
     return (fa.UMesh.naca_ogrid(nt, nq, ntri, 20.0, ws, farmap=fm),
             dict(ntheta=nt, nquad=nq, ntri=ntri, wall_spacing=ws, farmap=fm))
 

@@ -159,6 +159,14 @@ class UMesh:
         return cls(h.value)
 
     @classmethod
+    def naca_cgrid(cls, nsurf, nwake, nquad, ntri, rfar=20.0, wallspacing=1e-5):
+        """C-grid round the NACA 0012: (2 nwake + nsurf) columns x (nquad quadrangle + 2 ntri triangle) rows
+        (mesh.cpp generateNacaCgrid; the C5 family)"""
+        h = ctypes.c_void_p()
+        check(_ffi.lib().fvmesh_generate(3, nsurf, nquad, ntri, rfar, wallspacing, float(nwake), ctypes.byref(h)))
+        return cls(h.value)
+
+    @classmethod
     def cylinder_ogrid(cls, ntheta, nr, r0=0.5, r1=20.0):
         h = ctypes.c_void_p()
         check(_ffi.lib().fvmesh_generate(1, ntheta, nr, 0, r0, r1, 0.0, ctypes.byref(h)))

@@ -133,7 +133,7 @@ struct fvhip_ctx
 		double *jd = nullptr, *jlo = nullptr, *jup = nullptr, *dinv = nullptr;            ///< 4x4 blocks
 		float *slo = nullptr, *sup = nullptr, *sdinv = nullptr;   ///< fp32 copies for the preconditioner
 		double *part = nullptr, *red = nullptr, *coef = nullptr, *pm = nullptr;           ///< reductions
-		double *h_red = nullptr, *h_coef = nullptr;                                      ///< pinned host
+		double *h_red = nullptr, *h_coef = nullptr, *h_red2 = nullptr;                  ///< pinned host
 	} iw;
 	std::vector<void*> owned_host;                  ///< pinned host allocations
 	// Jacobian
@@ -671,7 +671,7 @@ struct fvhip_ctx
 		auto& o = owned;
 		iw.red = dalloc(KRY_MAXK + 2, o); iw.coef = dalloc(KRY_MAXK + 2, o); iw.pm = dalloc(2, o);
 		iw.part = dalloc(kry_scratch(2), o);
-		for(double** hp : {&iw.h_red, &iw.h_coef}) {
+		for(double** hp : {&iw.h_red, &iw.h_coef, &iw.h_red2}) {
 			void* p = nullptr;
 			HC(hipHostMalloc(&p, (KRY_MAXK + 2)*sizeof(double), hipHostMallocDefault));
 			owned_host.push_back(p);

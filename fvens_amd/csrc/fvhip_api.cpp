@@ -934,6 +934,7 @@ int fvmesh_generate(int kind, int a, int b, int c, double x, double y, double z,
 		if(kind == 0) m->raw = generateNacaOgrid(a, b, c, x, y, static_cast<int>(z));
 		else if(kind == 1) m->raw = generateCylinderOgrid(a, b, x, y);
 		else if(kind == 2) m->raw = generateFlatPlate(a, b, x, y, z);
+		else if(kind == 3) m->raw = generateNacaCgrid(a, static_cast<int>(z), b, c, x, y);
 		else throw std::invalid_argument("unknown mesh kind");
 		m->mesh = buildMesh(m->raw);
 		*out = m.release();

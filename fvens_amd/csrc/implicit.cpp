@@ -71,6 +71,14 @@ struct System
 		return tot;
 	}
 	void sync() { each([&](size_t, fvhip_ctx* h) { HC(hipStreamSynchronize(h->stream)); }); }
+	/// one handle: the global sums of the k values in iw.red, copied to iw.h_red2 behind the reduction
+	/// without waiting (read them after a later wait on the stream)
+	void allsumQueue(int k) {
+		fvhip_ctx* h = hs[0];
+		HC(hipSetDevice(h->device));
+		if(h->comm) NC(ncclAllReduce(h->iw.red, h->iw.red, k, ncclDouble, ncclSum, h->comm, h->stream));
+		HC(hipMemcpyAsync(h->iw.h_red2, h->iw.red, k*sizeof(double), hipMemcpyDeviceToHost, h->stream));
+	}
 };
 
 typedef fvhip_ctx::ArrayOf ArrayOf;
@@ -321,7 +329,16 @@ static GmresOut gmres(System& S, LinOp& A, const ArrayOf& b, const ArrayOf& x, d
 			// follows by Pythagoras and a second projection runs only when the first removed more than half
 			// of |w|^2 (DGKS); refine 2 (always): two projections every step.
 			double hn2 = 0.0;
-			if(refine != 1) {
+			if(refine == 0 && S.size() == 1) {
+				// one handle: the projection's coefficients stay on the device for k_maxpy_norm and reach
+				// the host with its norm -- one wait per Arnoldi step
+				fvhip_ctx* h = S.hs[0];
+				launch_mdot(n4(0), j+1, V(0,0), n4(0), w(0), false, h->iw.part, h->iw.red, h->stream);
+				S.allsumQueue(j+1);
+				launch_maxpy_norm(n4(0), j+1, V(0,0), n4(0), h->iw.red, w(0), h->iw.part, h->iw.red, h->stream);
+				hn2 = S.allsum(1, false)[0];
+				for(int k = 0; k <= j; k++) Hij(k,j) = h->iw.h_red2[k];
+			} else if(refine != 1) {
 				S.each([&](size_t i, fvhip_ctx* h) {
 					launch_mdot(n4(i), j+1, V(i,0), n4(i), w(i), false, h->iw.part, h->iw.red, h->stream);
 				});

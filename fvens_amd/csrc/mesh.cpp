@@ -707,6 +707,137 @@ MeshData generateNacaOgrid(int ntheta, int nquad, int ntri, double rfar, double 
 	return m;
 }
 
+/// C-grid round the NACA 0012 (the C5 family, BASELINE config 5's viscous case). A sharp trailing edge
+/// in an O-grid either leaves the aft boundary layer as thin parallelograms (straight lines to the far
+/// field) or fans one trailing-edge point's cells over the whole wake (wall-normal lines); the C-grid's
+/// wake cut carries the boundary-layer spacing downstream instead. Columns i = 0 .. ni-1, ni = 2 nwake +
+/// nsurf + 1: the lower wake from the outflow to the trailing edge, the lower surface to the leading edge,
+/// the upper surface, the upper wake to the outflow; row 0 is the body and the cut (both wakes' row-0
+/// points are the same points), rows 1 .. nquad + ntri go out to a C boundary: a half circle of radius rfar
+/// round the trailing edge and the lines y = +-rfar to the outflow at x = 1 + rfar. Surface points are
+/// clustered at the leading edge (half-cosine) and, less, at the trailing edge (half of a full cosine); the
+/// wake spacing grows geometrically from the trailing-edge spacing. Wake lines are vertical; a surface
+/// point's line leaves along the wall normal (turned vertical over the last tenth of the chord, parallel to
+/// the wake lines at the trailing edge) and bends onto the straight line to its far-field point (angles
+/// uniform in the surface parameter) by one chord (smoothstep). Rows grow geometrically from
+/// `wallspacing`. Quadrangles in the first nquad rows, triangles beyond. Markers: wall 2, far field 4.
+MeshData generateNacaCgrid(int nsurf, int nwake, int nquad, int ntri, double rfar, double wallspacing)
+{
+	if(nsurf < 8 || nsurf % 2 || nwake < 2) throw std::invalid_argument("nsurf must be even and >= 8, nwake >= 2");
+	const double PI = 3.14159265358979323846;
+	const int nl = nquad + ntri, ni = 2*nwake + nsurf + 1, half = nsurf/2;
+	// surface, upper side parameter t = 0 (LE) .. 1 (TE)
+	auto xs = [&](double t) { return 0.5*(1.0 - std::cos(0.5*PI*t)) + 0.25*(1.0 - std::cos(PI*t)); };
+	std::vector<double> sx(ni), sy(ni), fx(ni), fy(ni);
+	const double dte = 1.0 - xs(1.0 - 1.0/half);               // trailing-edge spacing
+	// wake stations x = 1 + w_k, k = 1 .. nwake, geometric from dte to the outflow
+	std::vector<double> wx(nwake + 1, 1.0);
+	{
+		const double L = rfar;
+		double lo = 1.0 + 1e-12, hi = 2.0;
+		for(int it = 0; it < 200; it++) {
+			const double q = 0.5*(lo + hi);
+			if(dte*(std::pow(q, nwake) - 1.0)/(q - 1.0) > L) hi = q; else lo = q;
+		}
+		const double q = 0.5*(lo + hi);
+		double acc = 0, d = dte;
+		for(int k = 1; k <= nwake; k++) { acc += d; wx[k] = 1.0 + acc; d *= q; }
+		for(int k = 1; k <= nwake; k++) wx[k] = 1.0 + (wx[k] - 1.0)*L/acc;
+	}
+	for(int i = 0; i < ni; i++) {
+		if(i < nwake || i > nwake + nsurf) {                     // wake: vertical lines
+			const bool lower = i < nwake;
+			const int k = lower ? nwake - i : i - (nwake + nsurf);
+			sx[i] = wx[k]; sy[i] = 0.0;
+			fx[i] = wx[k]; fy[i] = lower ? -rfar : rfar;
+		} else {
+			const int m = i - nwake;                                // 0 .. nsurf: TE lower -> LE -> TE upper
+			const bool lower = m < half;
+			const double t = lower ? static_cast<double>(half - m)/half : static_cast<double>(m - half)/half;
+			const double x = m == 0 || m == nsurf ? 1.0 : xs(t);
+			sx[i] = x; sy[i] = lower ? -naca0012(x) : naca0012(x);
+			if(m == 0 || m == nsurf) sy[i] = 0.0;
+			const double ang = -0.5*PI - PI*static_cast<double>(m)/nsurf;   // -pi/2 (down) .. -3pi/2 (up)
+			fx[i] = 1.0 + rfar*std::cos(ang); fy[i] = rfar*std::sin(ang);
+		}
+	}
+	// rows: geometric growth from the wall spacing over nl layers (normalised to the line length)
+	std::vector<double> eta(nl+1, 0.0);
+	{
+		const double target = rfar/wallspacing;
+		double lo = 1.0 + 1e-12, hi = 2.0;
+		for(int it = 0; it < 200; it++) {
+			const double q = 0.5*(lo+hi);
+			if((std::pow(q, nl) - 1.0)/(q - 1.0) > target) hi = q; else lo = q;
+		}
+		const double q = 0.5*(lo+hi);
+		double acc = 0, d = 1.0;
+		for(int j = 1; j <= nl; j++) { acc += d; eta[j] = acc; d *= q; }
+		for(int j = 1; j <= nl; j++) eta[j] /= acc;
+	}
+	// points: row 0 has nwake + nsurf distinct points (the upper wake's are the lower wake's), rows >= 1 ni
+	const int n0 = nwake + nsurf;
+	auto P = [&](int i, int j) { return j == 0 ? (i < n0 ? i : ni - 1 - i) : n0 + (j-1)*ni + i; };
+	MeshData m;
+	m.npoin = n0 + nl*ni;
+	m.coords.resize(static_cast<size_t>(m.npoin)*2);
+	const double blend = 1.0;
+	for(int j = 0; j <= nl; j++)
+		for(int i = 0; i < ni; i++) {
+			if(j == 0 && i >= n0) continue;
+			double dx = fx[i] - sx[i], dy = fy[i] - sy[i];
+			const double L = std::sqrt(dx*dx + dy*dy);
+			const bool body = i > nwake && i < nwake + nsurf;
+			if(body && j > 0 && eta[j]*L < blend) {
+				double nx = sy[i+1] - sy[i-1], ny = -(sx[i+1] - sx[i-1]);
+				if(nx*dx + ny*dy < 0) { nx = -nx; ny = -ny; }
+				if(sx[i] > 0.9) {                                   // the normal turns vertical at the trailing
+					const double g = (sx[i] - 0.9)/0.1;              // edge, parallel to the wake lines next to it
+					nx *= 1.0 - g*g*(3.0 - 2.0*g);
+				}
+				const double nn = std::sqrt(nx*nx + ny*ny);
+				const double x = eta[j]*L/blend;
+				const double w = x*x*(3.0 - 2.0*x);
+				const double ex = (1.0 - w)*nx/nn + w*dx/L, ey = (1.0 - w)*ny/nn + w*dy/L;
+				const double en = std::sqrt(ex*ex + ey*ey);
+				dx = L*ex/en; dy = L*ey/en;
+			}
+			const size_t p = static_cast<size_t>(P(i, j));
+			m.coords[2*p] = sx[i] + eta[j]*dx;
+			m.coords[2*p+1] = sy[i] + eta[j]*dy;
+		}
+	// cells: (i,j) (i+1,j) (i+1,j+1) (i,j+1) counter-clockwise (i runs clockwise round the body, j outwards)
+	for(int j = 0; j < nl; j++)
+		for(int i = 0; i < ni - 1; i++) {
+			const int a = P(i,j), b = P(i+1,j), c = P(i+1,j+1), d = P(i,j+1);
+			if(j < nquad) {
+				m.inpoel.insert(m.inpoel.end(), {a, b, c, d});
+				m.nnode.push_back(4); m.nfael.push_back(4);
+			} else {
+				if((i + j) % 2 == 0) m.inpoel.insert(m.inpoel.end(), {a, b, c, -1, a, c, d, -1});
+				else m.inpoel.insert(m.inpoel.end(), {a, b, d, -1, b, c, d, -1});
+				m.nnode.push_back(3); m.nfael.push_back(3);
+				m.nnode.push_back(3); m.nfael.push_back(3);
+			}
+		}
+	m.nnofa = 2; m.nbtag = 2; m.ndtag = 2;
+	m.nelem = static_cast<int>(m.nnode.size());
+	m.maxnnode = nquad > 0 ? 4 : 3; m.maxnfael = m.maxnnode;
+	if(m.maxnnode == 3) {
+		std::vector<int> c(static_cast<size_t>(m.nelem)*3);
+		for(int e = 0; e < m.nelem; e++) for(int k = 0; k < 3; k++) c[3*e+k] = m.inpoel[4*e+k];
+		m.inpoel.swap(c);
+	}
+	m.vol_regions.assign(static_cast<size_t>(m.nelem)*2, 1);
+	// boundary faces: the wall (row 0 along the body), the far field (the outer row and both outflow columns)
+	auto bf = [&](int a, int b, int tag) { m.bface.insert(m.bface.end(), {a, b, tag, 1}); };
+	for(int i = nwake; i < nwake + nsurf; i++) bf(P(i,0), P(i+1,0), 2);
+	for(int i = 0; i < ni - 1; i++) bf(P(i+1,nl), P(i,nl), 4);
+	for(int j = 0; j < nl; j++) { bf(P(0,j+1), P(0,j), 4); bf(P(ni-1,j), P(ni-1,j+1), 4); }
+	m.nbface = static_cast<int>(m.bface.size()/4);
+	return m;
+}
+
 MeshData generateCylinderOgrid(int ntheta, int nr, double r0, double r1)
 {
 	MeshData m;

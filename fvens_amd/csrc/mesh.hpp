@@ -85,6 +85,7 @@ Mesh restrictMesh(const Mesh& gm, const int* elemdist, int rank);
 /// outside them, outer circle radius rfar about (0.5,0). Wall marker 2, farfield marker 4.
 /// Cells: ntheta*(nquad + 2*ntri).
 MeshData generateNacaOgrid(int ntheta, int nquad, int ntri, double rfar, double wallspacing, int farmap = 0);
+MeshData generateNacaCgrid(int nsurf, int nwake, int nquad, int ntri, double rfar, double wallspacing);
 
 /// Synthetic O-grid annulus about a cylinder of radius r0 out to r1, all quads split into
 /// triangles (2dcylinder-like). Inner marker 2, outer marker 4. Cells 2*ntheta*nr.

@@ -417,7 +417,9 @@ int fvmesh_read_gmsh(const char* path, fvmesh_handle* out);
 /** kind: 0 = NACA0012 hybrid O-grid (a=ntheta, b=nquad, c=ntri, x=rfar, y=wall spacing, z=far-field map:
  *            0 = direction of the surface point from mid-chord, 1 = angles uniform in the surface parameter)
  *        1 = cylinder triangle O-grid (a=ntheta, b=nr, x=r0, y=r1)
- *        2 = flat plate quads (a=nx, b=ny, x=lead length, y=height, z=wall spacing) */
+ *        2 = flat plate quads (a=nx, b=ny, x=lead length, y=height, z=wall spacing)
+ *        3 = NACA 0012 C-grid (a=nsurf, b=nquad, c=ntri, x=rfar, y=wall spacing, z=nwake: columns along
+ *            each wake; 2 nwake + nsurf columns of cells) */
 int fvmesh_generate(int kind, int a, int b, int c, double x, double y, double z, fvmesh_handle* out);
 int fvmesh_write_gmsh(fvmesh_handle m, const char* path);
 int fvmesh_destroy(fvmesh_handle m);

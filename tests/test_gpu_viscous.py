@@ -1,7 +1,8 @@
 """The viscous configurations of BASELINE.json (C3 flat plate, C5 visc-NACA0012) at their full sizes, and
 the reference's viscous functional regression.
 
-  * C5 (the C4 O-grid with 4096 points around, 8,126,464 cells; Roe + WLS + Sutherland
+  * C5 (SURVEY.md 8(d)'s 8,126,464 cells as a C-grid: 4096 columns, 3072 round the body and 512 along
+    each wake, 256 quadrangle + 2 x 864 triangle rows, 1e-5 wall spacing; Roe + WLS + Sutherland
     viscous flux, laminar-implicit.ctrl's M 0.5, Re 5000, adiabatic wall 2 / inflow-outflow 4) and C3
     (1024 x 1024 flat plate, HLLC + WLS + viscous, flatplate.ctrl): residual and time steps of the
     device sweep against the oracle. Bar: |dr| <= 1e-12 max|r| per variable and |d dt| <= 1e-12 |dt|
@@ -73,8 +74,8 @@ def _check_vs_oracle(m, p, n, u):
 
 
 def test_c5_residual_full_size():
-    m = fa.UMesh.naca_ogrid(4096, 256, 864, 20.0, 1e-5, farmap=3)       # bench.py --numerics config5's mesh
-    assert m.nelem == 8126464 and m.naface == 12718080
+    m = fa.UMesh.naca_cgrid(3072, 512, 256, 864, 20.0, 1e-5)        # bench.py --numerics config5's mesh
+    assert m.nelem == 8126464 and m.naface == 12718688
     p = cases.physics("visc")
     n = cases.numerics("ROE", "LEASTSQUARES", "NONE")
     _check_vs_oracle(m, p, n, cases.state(m, p, seed=42))

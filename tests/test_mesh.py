@@ -38,6 +38,7 @@ def test_gmsh_fixture_indexing(name):
     lambda: fa.UMesh.naca_ogrid(64, 4, 12),
     lambda: fa.UMesh.naca_ogrid(200, 10, 30, 15.0, 1e-3),
     lambda: fa.UMesh.naca_ogrid(256, 16, 54, 20.0, 1e-5, farmap=3),
+    lambda: fa.UMesh.naca_cgrid(96, 16, 8, 24, 20.0, 1e-5),
     lambda: fa.UMesh.cylinder_ogrid(48, 12),
     lambda: fa.UMesh.flat_plate(40, 24),
 ])
@@ -121,6 +122,28 @@ def test_naca_wall_normal_layers():
     own = np.tile(m1.coords[:512], (141, 1))          # each point's surface point (point j*512 + i)
     far = np.linalg.norm(m1.coords - own, axis=1) >= 3.0
     assert far.sum() > 10000 and np.array_equal(m1.coords[far], m3.coords[far])
+
+
+def test_naca_cgrid():
+    """generateNacaCgrid, the C5 family (BASELINE config 5's viscous case): (2 nwake + nsurf) columns x
+    (nquad + 2 ntri) rows of cells; the wake cut is interior (the two wakes' row-0 points are shared), the
+    wall is the body's row 0 (marker 2), the far field the outer row and both outflow columns (marker 4).
+    On C5/8 every cell is positive and no boundary-layer quadrangle is skewed by more than 10 degrees
+    (the straight-line O-grid's: 82, with 4,922 above 45)."""
+    ns, nw, nq, nt = 384, 64, 32, 108
+    m = fa.UMesh.naca_cgrid(ns, nw, nq, nt, 20.0, 1e-5)
+    cols, rows = 2 * nw + ns, nq + 2 * nt
+    assert m.nelem == cols * rows == 126976
+    tags = m.btags[:, 0] if m.btags.ndim > 1 else m.btags
+    assert (tags == 2).sum() == ns and (tags == 4).sum() == cols + 2 * (nq + nt)
+    assert (m.area > 0).all()
+    # interior faces: every cell edge not on the boundary is shared (Euler: 4-sided cells, 3-sided cells)
+    assert m.naface == (4 * (m.nnode == 4).sum() + 3 * (m.nnode == 3).sum() + m.nbface) // 2
+    _, d = _quad_skew(m)
+    assert d.max() < 10.0, d.max()
+    # the first row's points lie ~1e-5 off the wall, the cut's cells are thin (row 1 at 1e-5 above the cut)
+    wall = np.where(tags == 2)[0]
+    assert np.abs(m.gr[wall] - m.rc[m.intfac[wall, 0]]).max() < 1e-4
 
 
 def test_gmsh_roundtrip(tmp_path):

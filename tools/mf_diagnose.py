@@ -22,6 +22,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--scale", type=int, default=8)
     ap.add_argument("--main-steps", type=int, default=30)
+    ap.add_argument("--farmap", type=int, default=None, help="an O-grid with this generateNacaOgrid farmap (default: the C5 C-grid)")
     ap.add_argument("--cfl", type=float, default=None, help="CFL of the diagnosed system (default: the main's last)")
     args = ap.parse_args()
     import torch
@@ -29,7 +30,7 @@ def main():
     import fvens_amd as fa
     import cases
     from bench import c4_mesh
-    mesh, dims = c4_mesh(fa, args.scale, 2)
+    mesh, dims = c4_mesh(fa, args.scale, 2, farmap=args.farmap)
     p = cases.physics("visc")
     h1 = fa.FlowFV(mesh, p, cases.numerics("ROE", "NONE", "NONE", order2=False))
     h2 = fa.FlowFV(mesh, p, cases.numerics("ROE", "LEASTSQUARES", "NONE"))

@@ -24,7 +24,7 @@ sys.path.insert(0, os.path.join(ROOT, "tests"))
 
 def run(scale=1, matrix_free=True, main_steps=400, init_steps=50, lin_maxit=60, restart=60, sweeps=3,
         tol=1e-6, heartbeat=None, cfl_init=(200.0, 1000.0), cfl_main=(500.0, 5000.0), min_relax=1.0, lin_rtol=1e-1,
-        wall=None):
+        wall=None, mf_eps=None):
     """the deck's two stages on the C5 mesh divided by `scale` in both directions; returns the record (a stage
     that diverges is recorded with its history and the error; the later stage is then skipped)"""
     import torch
@@ -37,6 +37,8 @@ def run(scale=1, matrix_free=True, main_steps=400, init_steps=50, lin_maxit=60, 
     n2 = cases.numerics("ROE", "LEASTSQUARES", "NONE")          # limiter none (:72)
     start, main = fa.FlowFV(mesh, p, n1), fa.FlowFV(mesh, p, n2)
     perm = main.permutation()
+    if mf_eps:
+        main.matfree_set_eps(mf_eps)          # -matrix_free_difference_step (alinalg.cpp:127)
     du = torch.tensor(np.tile(cases.freestream(p), (mesh.nelem, 1))[perm], device="cuda")
     torch.cuda.synchronize()      # torch's stream vs the library's (non-blocking) streams
     lin = dict(lin_rtol=lin_rtol, lin_maxit=lin_maxit, restart=restart, prec_lines=True, prec_sweeps=sweeps,
@@ -101,13 +103,14 @@ def main():
     ap.add_argument("--min-relax", type=float, default=1.0, help=">= 1: full update (the deck), else robust_flow")
     ap.add_argument("--lin-rtol", type=float, default=1e-1)
     ap.add_argument("--wall", type=float, default=None, help="first-cell wall spacing (default: the C5 mesh's 1e-5)")
+    ap.add_argument("--mf-eps", type=float, default=None, help="matrix-free difference step (default 1e-7)")
     ap.add_argument("--tag", default="")
     args = ap.parse_args()
     import torch
     torch.cuda.set_device(0)
     r = run(args.scale, not args.assembled, args.main_steps, init_steps=args.init_steps, lin_maxit=args.lin_maxit, restart=args.restart,
             sweeps=args.sweeps, heartbeat=lambda s: print(s, flush=True), cfl_init=args.cfl_init,
-            cfl_main=args.cfl_main, min_relax=args.min_relax, lin_rtol=args.lin_rtol, wall=args.wall)
+            cfl_main=args.cfl_main, min_relax=args.min_relax, lin_rtol=args.lin_rtol, wall=args.wall, mf_eps=args.mf_eps)
     r["tag"] = args.tag
     print(json.dumps(r), flush=True)
 
