@@ -47,3 +47,30 @@ def pytest_collection_modifyitems(config, items):
     # GPU tests fail loudly (not skip) when selected on a machine without a GPU: the product has no
     # CPU fallback. Without -m gpu they are deselected by the driver's -m "not gpu".
     pass
+
+
+@pytest.fixture(autouse=True)
+def _heartbeat(request):
+    """a test that runs for minutes (the full-size partition and implicit tests) prints a line every 60 s
+    past pytest's capture, so a watchdog that takes a silent run for a hung one sees it alive"""
+    import threading
+    import time
+    done = threading.Event()
+    t0 = time.time()
+
+    capman = request.config.pluginmanager.getplugin("capturemanager")
+
+    def beat():
+        while not done.wait(60.0):
+            line = "[heartbeat] %s running %.0f s\n" % (request.node.nodeid, time.time() - t0)
+            if capman is None:
+                sys.__stderr__.write(line)
+                sys.__stderr__.flush()
+                continue
+            with capman.global_and_fixture_disabled():      # past pytest's fd capture
+                sys.stderr.write(line)
+                sys.stderr.flush()
+    th = threading.Thread(target=beat, daemon=True)
+    th.start()
+    yield
+    done.set()

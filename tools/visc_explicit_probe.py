@@ -26,7 +26,7 @@ def main():
     ap.add_argument("--steps2", type=int, default=100000)
     ap.add_argument("--chunk", type=int, default=10000)
     ap.add_argument("--mesh", default="c5", help="c5: the C5 family (--scale, --wall); ref: the reference's "
-                    "NACA0012_lam_hybrid_1.msh")
+                    "NACA0012_lam_hybrid_1.msh; cgrid-quads: the C5 C-grid without triangle rows")
     ap.add_argument("--physics", default="visc", help="visc (the deck) or naca0 (inviscid M 0.5, alpha 0)")
     args = ap.parse_args()
     import torch
@@ -36,6 +36,10 @@ def main():
     from bench import c4_mesh
     if args.mesh == "ref":
         mesh, dims = fa.UMesh.read_gmsh(cases.fixture_mesh("NACA0012_lam_hybrid_1")), {"wall_spacing": "ref"}
+    elif args.mesh == "cgrid-quads":             # the C5/scale C-grid with quadrangles in every row
+        s = args.scale
+        mesh = fa.UMesh.naca_cgrid(3072 // s, 512 // s, (256 + 864) // s, 0, 20.0, args.wall or 1e-5)
+        dims = {"topology": "C-grid, quadrangles only", "wall_spacing": args.wall or 1e-5}
     else:
         mesh, dims = c4_mesh(fa, args.scale, 2, wall=args.wall)
     if args.physics == "naca0":
