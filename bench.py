@@ -48,10 +48,12 @@ C4_WALL_SPACING = 1e-5
 # direction map (0) the cosine-clustered trailing-edge points crowd the far field at angle 0, leaving
 # sliver triangles (aspect ratio ~1e3) along the wake line where second-order solves blow up
 C4_FARMAP = 1
-# the viscous C5 family (config 5) is a C-grid (generateNacaCgrid): on the O-grid the aft boundary layer
-# was 8-9 degree parallelograms (straight lines) or the trailing-edge point's cells fanned over the wake
-# (wall-normal lines, farmap 3), and no second-order solve of the laminar deck converged on either
-# (profiles/r05/c5_family_convergence_probes.jsonl)
+# the viscous C5 family (config 5) is a C-grid of quadrangles (generateNacaCgrid, ntri 0; 4096 columns x 1984
+# rows = the hybrid O-grid's 8,126,464 cells): on the O-grid the aft boundary layer was 8-9 degree
+# parallelograms (straight lines) or the trailing-edge point's cells fanned over the wake (wall-normal lines,
+# farmap 3), and with triangle rows (split stretched quadrangles) on either grid the first-order-
+# preconditioned GMRES of the laminar deck's second-order solve reduced nothing; on the quadrangle C-grid it
+# converges (profiles/r05/c5_family_convergence_probes.jsonl)
 
 
 def c4_mesh(fa, scale, mult=1, wall=None, farmap=None):
@@ -62,9 +64,9 @@ def c4_mesh(fa, scale, mult=1, wall=None, farmap=None):
     ntri = 864 // scale
     ws = C4_WALL_SPACING if wall is None else wall
     if mult == 2 and farmap is None:
-        ns, nw = 3 * nt // 4, nt // 8
-        return (fa.UMesh.naca_cgrid(ns, nw, nq, ntri, 20.0, ws),
-                dict(topology="C-grid", nsurf=ns, nwake=nw, nquad=nq, ntri=ntri, wall_spacing=ws))
+        ns, nw, rows = 3 * nt // 4, nt // 8, nq + 2 * ntri
+        return (fa.UMesh.naca_cgrid(ns, nw, rows, 0, 20.0, ws),
+                dict(topology="C-grid, quadrangles", nsurf=ns, nwake=nw, rows=rows, wall_spacing=ws))
     fm = C4_FARMAP if farmap is None else farmap
     return (fa.UMesh.naca_ogrid(nt, nq, ntri, 20.0, ws, farmap=fm),
             dict(ntheta=nt, nquad=nq, ntri=ntri, wall_spacing=ws, farmap=fm))

@@ -716,8 +716,9 @@ MeshData generateNacaOgrid(int ntheta, int nquad, int ntri, double rfar, double 
 /// points are the same points), rows 1 .. nquad + ntri go out to a C boundary: a half circle of radius rfar
 /// round the trailing edge and the lines y = +-rfar to the outflow at x = 1 + rfar. Surface points are
 /// clustered at the leading edge (half-cosine) and, less, at the trailing edge (half of a full cosine); the
-/// wake spacing grows geometrically from the trailing-edge spacing. Wake lines are vertical; a surface
-/// point's line leaves along the wall normal (turned vertical over the last tenth of the chord, parallel to
+/// wake spacing grows geometrically from the trailing-edge spacing. Wake lines run from the cut to the
+/// far field, where their spacing starts at the half circle's and grows to the outflow, leaving the cut
+/// vertically; a surface point's line leaves along the wall normal (turned vertical over the last tenth of the chord, parallel to
 /// the wake lines at the trailing edge) and bends onto the straight line to its far-field point (angles
 /// uniform in the surface parameter) by one chord (smoothstep). Rows grow geometrically from
 /// `wallspacing`. Quadrangles in the first nquad rows, triangles beyond. Markers: wall 2, far field 4.
@@ -744,12 +745,31 @@ MeshData generateNacaCgrid(int nsurf, int nwake, int nquad, int ntri, double rfa
 		for(int k = 1; k <= nwake; k++) { acc += d; wx[k] = 1.0 + acc; d *= q; }
 		for(int k = 1; k <= nwake; k++) wx[k] = 1.0 + (wx[k] - 1.0)*L/acc;
 	}
+	// the wake lines' far ends along y = +-rfar: spacing from the half circle's (pi rfar / nsurf) growing
+	// geometrically to the outflow, so the columns next to the trailing edge's line widen outwards
+	// instead of running to the far field as slivers of the trailing-edge spacing
+	std::vector<double> ox(nwake + 1, 1.0);
+	{
+		const double L = rfar, s0 = PI*rfar/nsurf;
+		if(s0*nwake >= L) { for(int k = 1; k <= nwake; k++) ox[k] = 1.0 + L*k/nwake; }
+		else {
+			double lo = 1.0 + 1e-12, hi = 2.0;
+			for(int it = 0; it < 200; it++) {
+				const double q = 0.5*(lo + hi);
+				if(s0*(std::pow(q, nwake) - 1.0)/(q - 1.0) > L) hi = q; else lo = q;
+			}
+			const double q = 0.5*(lo + hi);
+			double acc = 0, d = s0;
+			for(int k = 1; k <= nwake; k++) { acc += d; ox[k] = 1.0 + acc; d *= q; }
+			for(int k = 1; k <= nwake; k++) ox[k] = 1.0 + (ox[k] - 1.0)*L/acc;
+		}
+	}
 	for(int i = 0; i < ni; i++) {
-		if(i < nwake || i > nwake + nsurf) {                     // wake: vertical lines
+		if(i < nwake || i > nwake + nsurf) {                     // wake: lines from the cut to y = +-rfar
 			const bool lower = i < nwake;
 			const int k = lower ? nwake - i : i - (nwake + nsurf);
 			sx[i] = wx[k]; sy[i] = 0.0;
-			fx[i] = wx[k]; fy[i] = lower ? -rfar : rfar;
+			fx[i] = ox[k]; fy[i] = lower ? -rfar : rfar;
 		} else {
 			const int m = i - nwake;                                // 0 .. nsurf: TE lower -> LE -> TE upper
 			const bool lower = m < half;
@@ -788,12 +808,16 @@ MeshData generateNacaCgrid(int nsurf, int nwake, int nquad, int ntri, double rfa
 			double dx = fx[i] - sx[i], dy = fy[i] - sy[i];
 			const double L = std::sqrt(dx*dx + dy*dy);
 			const bool body = i > nwake && i < nwake + nsurf;
-			if(body && j > 0 && eta[j]*L < blend) {
-				double nx = sy[i+1] - sy[i-1], ny = -(sx[i+1] - sx[i-1]);
-				if(nx*dx + ny*dy < 0) { nx = -nx; ny = -ny; }
-				if(sx[i] > 0.9) {                                   // the normal turns vertical at the trailing
-					const double g = (sx[i] - 0.9)/0.1;              // edge, parallel to the wake lines next to it
-					nx *= 1.0 - g*g*(3.0 - 2.0*g);
+			const bool te = i == nwake || i == nwake + nsurf;
+			if(!te && j > 0 && eta[j]*L < blend) {
+				double nx = 0.0, ny = fy[i] > 0 ? 1.0 : -1.0;           // wake: the cut's normal
+				if(body) {
+					nx = sy[i+1] - sy[i-1]; ny = -(sx[i+1] - sx[i-1]);
+					if(nx*dx + ny*dy < 0) { nx = -nx; ny = -ny; }
+					if(sx[i] > 0.9) {                               // the normal turns vertical at the trailing
+						const double g = (sx[i] - 0.9)/0.1;          // edge, parallel to the wake lines next to it
+						nx *= 1.0 - g*g*(3.0 - 2.0*g);
+					}
 				}
 				const double nn = std::sqrt(nx*nx + ny*ny);
 				const double x = eta[j]*L/blend;

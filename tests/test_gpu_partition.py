@@ -126,7 +126,7 @@ def test_partitioned_c4_eight_ranks(rec):
 
 def test_partitioned_c5_eight_ranks():
     """BASELINE config 5 at its full size on the partitioned path: the 8,126,464-cell C5 C-grid (4096
-    columns, 1e-5 wall spacing), laminar Roe + WLS + unlimited linear + Sutherland at alpha 0 (the
+    columns x 1984 rows of quadrangles, 1e-5 wall spacing), laminar Roe + WLS + unlimited linear + Sutherland at alpha 0 (the
     visc-naca0012 deck's numerics, laminar-implicit.ctrl:19,72; the fused viscous kernel on the two-layer
     halo), split 8 ways by the cost-weighted graph partitioner, all ranks in one
     process with the overlapped schedule -- every owned row's residual and time step bitwise the

@@ -32,7 +32,7 @@ def get_mesh(key):
         elif key == "naca_c4":                               # the bench's C4 mesh (no oracle mesh)
             m, om = fa.UMesh.naca_ogrid(2048, 256, 864, 20.0, 1e-5, farmap=1), None
         elif key == "naca_c5":                               # BASELINE config 5's 8,126,464-cell C-grid
-            m, om = fa.UMesh.naca_cgrid(3072, 512, 256, 864, 20.0, 1e-5), None
+            m, om = fa.UMesh.naca_cgrid(3072, 512, 1984, 0, 20.0, 1e-5), None
         elif key == "c1":                                    # BASELINE config 1's cylinder
             m = fa.UMesh.cylinder_ogrid(64, 40)
             om = orc.OracleMesh.from_raw(m.raw())

@@ -1,8 +1,8 @@
 """The viscous configurations of BASELINE.json (C3 flat plate, C5 visc-NACA0012) at their full sizes, and
 the reference's viscous functional regression.
 
-  * C5 (SURVEY.md 8(d)'s 8,126,464 cells as a C-grid: 4096 columns, 3072 round the body and 512 along
-    each wake, 256 quadrangle + 2 x 864 triangle rows, 1e-5 wall spacing; Roe + WLS + Sutherland
+  * C5 (SURVEY.md 8(d)'s 8,126,464 cells as a quadrangle C-grid: 4096 columns, 3072 round the body and
+    512 along each wake, 1984 rows, 1e-5 wall spacing; Roe + WLS + Sutherland
     viscous flux, laminar-implicit.ctrl's M 0.5, Re 5000, adiabatic wall 2 / inflow-outflow 4) and C3
     (1024 x 1024 flat plate, HLLC + WLS + viscous, flatplate.ctrl): residual and time steps of the
     device sweep against the oracle. Bar: |dr| <= 1e-12 max|r| per variable and |d dt| <= 1e-12 |dt|
@@ -74,8 +74,8 @@ def _check_vs_oracle(m, p, n, u):
 
 
 def test_c5_residual_full_size():
-    m = fa.UMesh.naca_cgrid(3072, 512, 256, 864, 20.0, 1e-5)        # bench.py --numerics config5's mesh
-    assert m.nelem == 8126464 and m.naface == 12718688
+    m = fa.UMesh.naca_cgrid(3072, 512, 1984, 0, 20.0, 1e-5)         # bench.py --numerics config5's mesh
+    assert m.nelem == 8126464 and m.naface == 16258496
     p = cases.physics("visc")
     n = cases.numerics("ROE", "LEASTSQUARES", "NONE")
     _check_vs_oracle(m, p, n, cases.state(m, p, seed=42))
@@ -131,21 +131,24 @@ def test_visc_naca0012_functional_regression(matrix_free):
 
 
 def test_c5_family_converges_to_deck_tolerance():
-    """BASELINE config 5's case solved to the deck's tolerance on a 1/16-size member of the C5 family
-    (tools/visc_converge.py: the C5 O-grid with 1024 cells around, 64 quadrangle and 216 triangle layers,
-    286,720 cells; laminar-implicit.ctrl's schedule -- first-order start CFL 200 -> 1000 to 1e-1, main solve
-    CFL 500 -> 5000 to a 1e-6 drop, 'full' update -- matrix-free operator, line-implicit preconditioner on
-    the first-order Jacobian). The drag components are those of the reference's 13k-cell grid
-    (regr-LeastSquares_Roe.txt) within the discretisation difference of the two meshes (5 %)."""
+    """BASELINE config 5's case solved to the deck's tolerance on the 1/64-size member of the C5 family
+    (tools/visc_converge.py: the quadrangle C-grid, 384 columns round the body + 2 x 64 along the wake,
+    248 rows, 1e-5 wall spacing, 126,976 cells) with laminar-implicit.ctrl's schedule -- first-order start
+    CFL 200 -> 1000 to 1e-1 (50 steps), main solve CFL 500 -> 5000 (expResidualRamp) to a 1e-6 drop, 'full'
+    update -- matrix-free operator, line-implicit preconditioner on the first-order Jacobian, GMRES(60)
+    rtol 1e-1. Measured on MI355X: 1,055 main steps, 18 s. The drag components are those of the
+    reference's 13k-cell grid (regr-LeastSquares_Roe.txt) within the two meshes' discretisation difference
+    (measured CDp -0.3 %, CDsf -2.2 %; bar 1 % and 5 %); CL is zero by symmetry (alpha 0)."""
     sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tools"))
     from visc_converge import run
-    r = run(scale=4, matrix_free=True, main_steps=300)
+    r = run(scale=8, matrix_free=True, main_steps=1500)
     print({k: r[k] for k in ("cells", "CL", "CDp", "CDsf")}, {k: r["main"][k] for k in ("steps", "lin_iters", "resratio",
                                                                                          "seconds", "converged")})
-    assert r["cells"] == 286720 and r["finite"]
+    assert r["cells"] == 126976 and r["finite"]
     assert r["main"]["converged"] and r["main"]["resratio"] <= 1e-6, r["main"]
     CL, CDP, CDSF = REGR
-    assert abs(r["CDp"] - CDP) <= 0.05 * abs(CDP) and abs(r["CDsf"] - CDSF) <= 0.05 * abs(CDSF), (r["CDp"], r["CDsf"])
+    assert abs(r["CDp"] - CDP) <= 0.01 * abs(CDP) and abs(r["CDsf"] - CDSF) <= 0.05 * abs(CDSF), (r["CDp"], r["CDsf"])
+    assert abs(r["CL"]) <= 1e-6
 
 
 def test_c3_implicit_matrix_free():

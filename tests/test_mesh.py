@@ -39,6 +39,7 @@ def test_gmsh_fixture_indexing(name):
     lambda: fa.UMesh.naca_ogrid(200, 10, 30, 15.0, 1e-3),
     lambda: fa.UMesh.naca_ogrid(256, 16, 54, 20.0, 1e-5, farmap=3),
     lambda: fa.UMesh.naca_cgrid(96, 16, 8, 24, 20.0, 1e-5),
+    lambda: fa.UMesh.naca_cgrid(96, 16, 62, 0, 20.0, 1e-5),
     lambda: fa.UMesh.cylinder_ogrid(48, 12),
     lambda: fa.UMesh.flat_plate(40, 24),
 ])

@@ -24,14 +24,19 @@ sys.path.insert(0, os.path.join(ROOT, "tests"))
 
 def run(scale=1, matrix_free=True, main_steps=400, init_steps=50, lin_maxit=60, restart=60, sweeps=3,
         tol=1e-6, heartbeat=None, cfl_init=(200.0, 1000.0), cfl_main=(500.0, 5000.0), min_relax=1.0, lin_rtol=1e-1,
-        wall=None, mf_eps=None):
+        wall=None, mf_eps=None, quads=False):
     """the deck's two stages on the C5 mesh divided by `scale` in both directions; returns the record (a stage
     that diverges is recorded with its history and the error; the later stage is then skipped)"""
     import torch
     import fvens_amd as fa
     import cases
     from bench import c4_mesh
-    mesh, dims = c4_mesh(fa, scale, 2, wall=wall)
+    if quads:                                   # the C-grid without triangle rows (quadrangles throughout)
+        ws = wall or 1e-5
+        mesh = fa.UMesh.naca_cgrid(3072 // scale, 512 // scale, 1984 // scale, 0, 20.0, ws)
+        dims = {"topology": "C-grid, quadrangles only", "wall_spacing": ws}
+    else:
+        mesh, dims = c4_mesh(fa, scale, 2, wall=wall)
     p = cases.physics("visc")                                   # alpha 0 (laminar-implicit.ctrl:19)
     n1 = cases.numerics("ROE", "NONE", "NONE", order2=False)
     n2 = cases.numerics("ROE", "LEASTSQUARES", "NONE")          # limiter none (:72)
@@ -103,6 +108,7 @@ def main():
     ap.add_argument("--min-relax", type=float, default=1.0, help=">= 1: full update (the deck), else robust_flow")
     ap.add_argument("--lin-rtol", type=float, default=1e-1)
     ap.add_argument("--wall", type=float, default=None, help="first-cell wall spacing (default: the C5 mesh's 1e-5)")
+    ap.add_argument("--quads", action="store_true", help="the C-grid with quadrangles in every row")
     ap.add_argument("--mf-eps", type=float, default=None, help="matrix-free difference step (default 1e-7)")
     ap.add_argument("--tag", default="")
     args = ap.parse_args()
@@ -110,7 +116,7 @@ def main():
     torch.cuda.set_device(0)
     r = run(args.scale, not args.assembled, args.main_steps, init_steps=args.init_steps, lin_maxit=args.lin_maxit, restart=args.restart,
             sweeps=args.sweeps, heartbeat=lambda s: print(s, flush=True), cfl_init=args.cfl_init,
-            cfl_main=args.cfl_main, min_relax=args.min_relax, lin_rtol=args.lin_rtol, wall=args.wall, mf_eps=args.mf_eps)
+            cfl_main=args.cfl_main, min_relax=args.min_relax, lin_rtol=args.lin_rtol, wall=args.wall, mf_eps=args.mf_eps, quads=args.quads)
     r["tag"] = args.tag
     print(json.dumps(r), flush=True)
 

@@ -38,7 +38,7 @@ def main():
         mesh, dims = fa.UMesh.read_gmsh(cases.fixture_mesh("NACA0012_lam_hybrid_1")), {"wall_spacing": "ref"}
     elif args.mesh == "cgrid-quads":             # the C5/scale C-grid with quadrangles in every row
         s = args.scale
-        mesh = fa.UMesh.naca_cgrid(3072 // s, 512 // s, (256 + 864) // s, 0, 20.0, args.wall or 1e-5)
+        mesh = fa.UMesh.naca_cgrid(3072 // s, 512 // s, 1984 // s, 0, 20.0, args.wall or 1e-5)
         dims = {"topology": "C-grid, quadrangles only", "wall_spacing": args.wall or 1e-5}
     else:
         mesh, dims = c4_mesh(fa, args.scale, 2, wall=args.wall)
