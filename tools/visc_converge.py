@@ -48,7 +48,7 @@ def run(scale=1, matrix_free=True, main_steps=400, init_steps=50, lin_maxit=60, 
     torch.cuda.synchronize()      # torch's stream vs the library's (non-blocking) streams
     lin = dict(lin_rtol=lin_rtol, lin_maxit=lin_maxit, restart=restart, prec_lines=True, prec_sweeps=sweeps,
                min_relax=min_relax)
-    rec = {"cells": mesh.nelem, "faces": mesh.naface, "dims": dims, "operator": "matrix-free" if matrix_free else "assembled",
+    rec = {"library": fa._ffi.build_info()["lib_src_hash"], "cells": mesh.nelem, "faces": mesh.naface, "dims": dims, "operator": "matrix-free" if matrix_free else "assembled",
            "linear": dict(lin, gmres="GMRES(%d) right-preconditioned" % restart), "cfl_init": list(cfl_init),
            "cfl_main": list(cfl_main)}
     done = threading.Event()
