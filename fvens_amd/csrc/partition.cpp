@@ -7,6 +7,7 @@
 #include <cstdlib>
 #include <map>
 #include <numeric>
+#include <queue>
 #include <stdexcept>
 #include <string>
 
@@ -259,22 +260,38 @@ void graphBisect(const fvhip_mesh& m, const std::vector<int>& sub, long long tw,
 			if(comp[a] != big[side[a]]) { side[a] = 1 - side[a]; flipped = true; }
 		if(!flipped) break;
 		// restore the balance: move the best-gain cell off the heavier side while that brings side 0's
-		// weight closer to the target
+		// weight closer to the target (ties: the lowest local id). One max-heap of (gain, -id) per side
+		// with lazy entries: a popped entry whose gain is stale goes back with the current one, a move
+		// pushes its neighbours' new gains, and a cell too heavy to bring the weight closer now never will
+		// be (|w0 - tw| only falls) -- the same sequence of moves as a full scan per move, in O(n log n)
 		w0 = 0;
 		for(int a = 0; a < n; a++) if(side[a] == 0) w0 += w(a);
-		while(w0 != tw) {
-			const int from = w0 > tw ? 0 : 1;
-			int best = -1, bg = -1000;
-			for(int a = 0; a < n; a++) {
-				if(side[a] != from) continue;
-				const long long w0n = from == 0 ? w0 - w(a) : w0 + w(a);
-				if(std::llabs(w0n - tw) >= std::llabs(w0 - tw)) continue;
-				const int g = gain(a);
-				if(g > bg) { bg = g; best = a; }
+		if(w0 != tw) {
+			std::priority_queue<std::pair<int,int>> heap[2];
+			for(int a = 0; a < n; a++) heap[side[a]].push({gain(a), -a});
+			while(w0 != tw) {
+				const int from = w0 > tw ? 0 : 1;
+				int best = -1;
+				while(!heap[from].empty()) {
+					const auto top = heap[from].top();
+					const int a = -top.second;
+					heap[from].pop();
+					if(side[a] != from) continue;
+					const int g = gain(a);
+					if(g != top.first) { heap[from].push({g, -a}); continue; }
+					const long long w0n = from == 0 ? w0 - w(a) : w0 + w(a);
+					if(std::llabs(w0n - tw) >= std::llabs(w0 - tw)) continue;
+					best = a;
+					break;
+				}
+				if(best < 0) break;
+				side[best] = 1 - from;
+				w0 += from == 0 ? -w(best) : w(best);
+				heap[side[best]].push({gain(best), -best});
+				int nb[4];
+				const int k = nbrs(sub[best], nb);
+				for(int j = 0; j < k; j++) heap[side[nb[j]]].push({gain(nb[j]), -nb[j]});
 			}
-			if(best < 0) break;
-			side[best] = 1 - from;
-			w0 += from == 0 ? -w(best) : w(best);
 		}
 	}
 	for(int i = 0; i < n; i++) loc[sub[i]] = -1;
