@@ -10,7 +10,7 @@ Linear solver: the reference's inv_cyl.solverc uses FGMRES (rtol 1e-1, 30 its) w
 here device GMRES (same iteration cap) with the preconditioner that converges each case: two multicolour
 block Gauss-Seidel sweeps and rtol 1e-2 (LS+HLLC), point-block Jacobi and rtol 1e-1 (GG+HLLC).
 
-Deviation, measured on MI355X (tools/experiments/conv_probe.py, tools/experiments/conv_probe2.py): the implicit main solves run
+Deviation, measured on MI355X (tools/experiments/conv_probe.py and conv_probe2.py, in git history up to f4c3eb0): the implicit main solves run
 towards a 1e-7 residual drop (1500 steps at most) instead of the decks' 1e-5 and must reach the decks'
 1e-5. Stopped at 1e-5 the device path leaves more algebraic error on the finest mesh (LS+HLLC finest
 slope 1.50); converged, the slopes are the discretisation's own: LS+HLLC 1.864/1.790/1.675, GG+HLLC

@@ -576,7 +576,7 @@ def test_naca0012_implicit_functional_regression():
     Jacobian 'consistent' (HLLC), -ksp_rtol 1e-1, -ksp_max_it 30. The reference preconditions with
     SOR; block-Jacobi sweeps here, so its step count may differ (max_timesteps raised 170 -> 600).
     Bars: CL (the reference's 1e-6) and CDp 1e-7 relative to regr-MUSCL_LeastSquares_HLLC.txt (the
-    reference: 1e-8). Measured on MI355X (tools/experiments/regr_probe.py): 136 steps to the 1e-7 drop, CL 8.2e-8 /
+    reference: 1e-8). Measured on MI355X (tools/experiments/regr_probe.py, in git history up to f4c3eb0): 136 steps to the 1e-7 drop, CL 8.2e-8 /
     CDp 3.3e-8; converged on to a 1e-11 drop, CL 9.07e-8 / CDp 4.65e-8 -- the gap of the file's own
     values to the converged discrete solution, so 1e-8 holds only along the reference's solver path.
     The second solve below converges to the 1e-11 drop and checks that gap."""

@@ -8,7 +8,7 @@ the same 1e-7 drop (28,168 steps on MI355X; the cap is 300,000) and the oracle e
 functionals (flow_spatial.cpp:130-310).
 
 The reference's 1e-8 CDp bar is not reachable by a different solver path, and the measured gap says
-why (tools/experiments/regr_probe.py, MI355X): converged to a 1e-11 drop -- implicitly, or explicitly to the
+why (tools/experiments/regr_probe.py, in git history up to f4c3eb0, MI355X): converged to a 1e-11 drop -- implicitly, or explicitly to the
 800,000-step cap -- this discretisation (bitwise the reference's residual) gives CL 9.07e-8 and CDp
 4.65e-8 relative to the file, so the file's own values carry ~5e-8 of the reference's 1e-7-drop
 convergence error. At the 1e-7 drop the explicit run sits at CL 9.1e-8 / CDp 4.65e-8, the implicit

@@ -22,7 +22,7 @@ the reference's viscous functional regression.
     within 1e-3 of it (the reference's own files span 0.7 %; measured 2.3e-4 matrix-free, 3.2e-4
     assembled). Preconditioner: line-implicit (block-
     tridiagonal along the wall-normal lines) with 3 sweeps, GMRES(60) rtol 1e-1. Measured on MI355X
-    (tools/experiments/visc_probe.py): assembled, 93 steps to the deck's 1e-6 drop, CDp 6.5e-8 / CDsf 4.0e-8 /
+    (tools/experiments/visc_probe.py, in git history up to f4c3eb0): assembled, 93 steps to the deck's 1e-6 drop, CDp 6.5e-8 / CDsf 4.0e-8 /
     CL 3.2e-4 relative to the file; the matrix-free Newton path reaches 1e-6 in 30 steps but there
     sits 1.3e-6 / 3.1e-6 off in CDp / CDsf, so it runs on to a 1e-8 drop.
 """
