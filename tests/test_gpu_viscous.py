@@ -131,20 +131,24 @@ def test_visc_naca0012_functional_regression(matrix_free):
 
 
 def test_c5_family_converges_to_deck_tolerance():
-    """BASELINE config 5's case solved to the deck's tolerance on the 1/64-size member of the C5 family
-    (tools/visc_converge.py: the quadrangle C-grid, 384 columns round the body + 2 x 64 along the wake,
-    248 rows, 1e-5 wall spacing, 126,976 cells) with laminar-implicit.ctrl's schedule -- first-order start
+    """BASELINE config 5's case solved to the deck's tolerance on the 1/16-size member of the C5 family
+    (tools/visc_converge.py: the quadrangle C-grid, 768 columns round the body + 2 x 128 along the wake,
+    496 rows, 1e-5 wall spacing, 507,904 cells) with laminar-implicit.ctrl's schedule -- first-order start
     CFL 200 -> 1000 to 1e-1 (50 steps), main solve CFL 500 -> 5000 (expResidualRamp) to a 1e-6 drop, 'full'
-    update -- matrix-free operator, line-implicit preconditioner on the first-order Jacobian, GMRES(60)
-    rtol 1e-1. Measured on MI355X: 1,055 main steps, 18 s. The drag components are those of the
+    update -- matrix-free operator, line-implicit preconditioner on the first-order Jacobian, GMRES(60).
+    The linear tolerance is tighter than the deck's: 1e-2 instead of opts.solverc's -ksp_rtol 1e-1 (FGMRES(30),
+    block-Jacobi/ILU there, line-implicit GMRES(60) here). At 1e-1 this 1/16-size solve reaches 1.4e-5 and
+    then leaves the symmetric solution (CL grows to 3e-3); the 1/64-size one converges either way
+    (profiles/r05/c5_quad_cgrid_convergence_s4.jsonl, _s8.jsonl). Measured on MI355X: 1,449 main steps, 77 s. The drag components are those of the
     reference's 13k-cell grid (regr-LeastSquares_Roe.txt) within the two meshes' discretisation difference
-    (measured CDp -0.3 %, CDsf -2.2 %; bar 1 % and 5 %); CL is zero by symmetry (alpha 0)."""
+    (measured CDp -0.30 %, CDsf -2.2 %, the same to 5e-4 at 1/64 size; bar 1 % and 5 %); CL is zero by
+    symmetry (alpha 0)."""
     sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tools"))
     from visc_converge import run
-    r = run(scale=8, matrix_free=True, main_steps=1500)
+    r = run(scale=4, matrix_free=True, main_steps=2000, lin_rtol=1e-2)
     print({k: r[k] for k in ("cells", "CL", "CDp", "CDsf")}, {k: r["main"][k] for k in ("steps", "lin_iters", "resratio",
                                                                                          "seconds", "converged")})
-    assert r["cells"] == 126976 and r["finite"]
+    assert r["cells"] == 507904 and r["finite"]
     assert r["main"]["converged"] and r["main"]["resratio"] <= 1e-6, r["main"]
     CL, CDP, CDSF = REGR
     assert abs(r["CDp"] - CDP) <= 0.01 * abs(CDP) and abs(r["CDsf"] - CDSF) <= 0.05 * abs(CDSF), (r["CDp"], r["CDsf"])
