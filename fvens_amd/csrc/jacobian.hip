@@ -30,8 +30,17 @@ using namespace gd;
 #ifndef FVHIP_JAC_WAVES
 #define FVHIP_JAC_WAVES 2
 #endif
+// FVHIP_JAC_SPLIT = 1: the viscous face kernels compute the inviscid columns into the LDS block first and add
+// the viscous terms to them afterwards (jac_face_split), so the inviscid and the viscous working sets are
+// never live together and the kernel fits two waves per SIMD
+#ifndef FVHIP_JAC_SPLIT
+#define FVHIP_JAC_SPLIT 0
+#endif
 template <int FLUX, int VISC>
-constexpr int jacWaves() { return (FLUX == 4 /* Roe */ && VISC) || (FLUX == 6 /* HLLC */ && VISC == 1) ? 1 : FVHIP_JAC_WAVES; }
+constexpr int jacWaves() {
+	return (FVHIP_JAC_SPLIT && VISC) ? 2
+	     : (FLUX == 4 /* Roe */ && VISC) || (FLUX == 6 /* HLLC */ && VISC == 1) ? 1 : FVHIP_JAC_WAVES;
+}
 // FVHIP_JAC_LDS_STORE = 1: where the face-Jacobian kernel runs at <= 2 waves per SIMD anyway (Roe, HLLC
 // and the viscous instantiations: 190-256 VGPRs), the face blocks go through LDS and leave as coalesced
 // 16-byte rows (a block's 256 faces own one contiguous 64 KB range of lower and of upper), instead of 32
@@ -80,6 +89,51 @@ __device__ __forceinline__ void jac_face(const JacMesh& J, const gd::Gas& G, con
 	}
 }
 
+/// jac_face for the viscous kernels in two phases over the LDS block sb (entry-major rows, stride
+/// JAC_LDS_STRIDE, this thread's face in column t): the inviscid columns go in unscaled, then each column is
+/// read back, the viscous terms are added to it in visc_jac_col's order and the face length applied --
+/// the same operations on the same values as jac_face, so the same bits
+template <int FLUX, int VISC>
+__device__ __forceinline__ void jac_face_split(const JacMesh& J, const gd::Gas& G, const double* __restrict__ u, int fi,
+                                               double* sb, int t)
+{
+	const int2 lr = J.if_LR[fi];
+	const double2 nn = J.if_n[fi];
+	const double n[2] = {nn.x, nn.y};
+	double ul[4], ur[4];
+	{
+		const double4* u4 = reinterpret_cast<const double4*>(u);
+		const double4 a = u4[lr.x], b = u4[lr.y];
+		ul[0] = a.x; ul[1] = a.y; ul[2] = a.z; ul[3] = a.w;
+		ur[0] = b.x; ur[1] = b.y; ur[2] = b.z; ur[3] = b.w;
+	}
+	{
+		typename JacOf<FLUX>::T F;
+		jac_prepare<FLUX>(G, ul, ur, n, F);
+#pragma unroll
+		for(int k = 0; k < 4; k++) {
+			double dl[4], dr[4];
+			jac_col<FLUX>(G, F, n, k, dl, dr);
+			for(int i = 0; i < 4; i++) { sb[(i*4+k)*JAC_LDS_STRIDE + t] = dl[i]; sb[(16+i*4+k)*JAC_LDS_STRIDE + t] = dr[i]; }
+		}
+	}
+	__builtin_amdgcn_sched_barrier(0);          // keep the viscous working set out of the inviscid phase
+	const double len = J.if_len[fi];
+	ViscJ V;
+	{
+		const double2 a = J.rc[lr.x], b = J.rc[lr.y];
+		const double cl[2] = {a.x, a.y}, cr[2] = {b.x, b.y};
+		visc_jac_prepare(G, VISC == 2, ul, ur, cl, cr, V);
+	}
+#pragma unroll
+	for(int k = 0; k < 4; k++) {
+		double dl[4], dr[4];
+		for(int i = 0; i < 4; i++) { dl[i] = sb[(i*4+k)*JAC_LDS_STRIDE + t]; dr[i] = sb[(16+i*4+k)*JAC_LDS_STRIDE + t]; }
+		visc_jac_col(G, V, ul, ur, n, k, dl, dr);
+		for(int i = 0; i < 4; i++) { sb[(i*4+k)*JAC_LDS_STRIDE + t] = dl[i]*len; sb[(16+i*4+k)*JAC_LDS_STRIDE + t] = dr[i]*len; }
+	}
+}
+
 template <int FLUX, int VISC>
 __global__ __launch_bounds__(256, (jacWaves<FLUX, VISC>()))
 void k_jac_interior(JacMesh J, gd::Gas G, const double* __restrict__ u,
@@ -92,11 +146,14 @@ void k_jac_interior(JacMesh J, gd::Gas G, const double* __restrict__ u,
 		// sb[side*16 + entry][face in block]: the columns land entry-major (consecutive threads,
 		// consecutive words: no bank conflicts); then each thread writes double2s of the block's range
 		__shared__ double sb[32*JAC_LDS_STRIDE];
-		if(fi < J.ninface)
-			jac_face<FLUX, VISC>(J, G, u, fi, [&](int i, int k, double lo, double up) {
-				sb[(i*4+k)*JAC_LDS_STRIDE + t] = lo;
-				sb[(16+i*4+k)*JAC_LDS_STRIDE + t] = up;
-			});
+		if(fi < J.ninface) {
+			if constexpr(FVHIP_JAC_SPLIT && VISC != 0) jac_face_split<FLUX, VISC>(J, G, u, fi, sb, t);
+			else
+				jac_face<FLUX, VISC>(J, G, u, fi, [&](int i, int k, double lo, double up) {
+					sb[(i*4+k)*JAC_LDS_STRIDE + t] = lo;
+					sb[(16+i*4+k)*JAC_LDS_STRIDE + t] = up;
+				});
+		}
 		__syncthreads();
 		const int nf = min(256, J.ninface - f0);
 		double2* Lo2 = reinterpret_cast<double2*>(lower + 16*static_cast<size_t>(f0));

@@ -24,6 +24,8 @@ def main():
     ap.add_argument("--scale", type=int, default=1)
     ap.add_argument("--reps", type=int, default=20)
     ap.add_argument("--implicit-scale", type=int, default=4, help="the matrix-free solve's mesh: C5 / this")
+    ap.add_argument("--jac-reps", type=int, default=1, help="Jacobian assemblies (the last one is used)")
+    ap.add_argument("--no-implicit", action="store_true")
     args = ap.parse_args()
     import torch
     torch.cuda.set_device(0)
@@ -47,7 +49,11 @@ def main():
     dtm = torch.zeros(N, dtype=torch.float64, device="cuda")
     torch.cuda.synchronize()
     h.compute_residual_device(u.data_ptr(), r.data_ptr(), dtm.data_ptr(), True, True)
-    h.assemble_jacobian_device(u.data_ptr(), diag.data_ptr(), lower.data_ptr(), upper.data_ptr())
+    for _ in range(args.jac_reps):                  # the face-Jacobian kernel's timing (A/B of its builds)
+        h.assemble_jacobian_device(u.data_ptr(), diag.data_ptr(), lower.data_ptr(), upper.data_ptr())
+    h.synchronize()
+    out["jacobian_sha256"] = hashlib.sha256(lower.cpu().numpy().tobytes() + upper.cpu().numpy().tobytes()
+                                            + diag.cpu().numpy().tobytes()).hexdigest()[:16]
     h.add_pseudo_time_term_device(100.0, dtm.data_ptr(), diag.data_ptr())
     v = torch.tensor(rng.standard_normal((N, 4)), device="cuda")
     z = torch.zeros_like(v)
@@ -59,6 +65,9 @@ def main():
     out.update(cells=N, z_sha256=hashlib.sha256(zc.tobytes()).hexdigest()[:16], z_finite=bool(np.isfinite(zc).all()),
                z_absmax=float(np.abs(zc).max()))
     h.close()
+    if args.no_implicit:
+        print(json.dumps(out), flush=True)
+        return
     # matrix-free implicit steps with the line solve's |z| (single domain, one sweep)
     m5, _ = c4_mesh(fa, args.implicit_scale, 2)
     p5 = cases.physics("visc")
