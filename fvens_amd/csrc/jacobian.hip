@@ -32,9 +32,10 @@ using namespace gd;
 #endif
 // FVHIP_JAC_SPLIT = 1: the viscous face kernels compute the inviscid columns into the LDS block first and add
 // the viscous terms to them afterwards (jac_face_split), so the inviscid and the viscous working sets are
-// never live together and the kernel fits two waves per SIMD
+// never live together and the kernel fits two waves per SIMD: the C5 (Roe + Sutherland) face kernel 3.60-3.63
+// -> 2.88-2.89 ms, bitwise the same blocks (profiles/r05/jac_split_ab.txt)
 #ifndef FVHIP_JAC_SPLIT
-#define FVHIP_JAC_SPLIT 0
+#define FVHIP_JAC_SPLIT 1
 #endif
 template <int FLUX, int VISC>
 constexpr int jacWaves() {
