@@ -415,7 +415,7 @@ def main():
                          "SURVEY's C2 (229,376 cells); config3: BASELINE config 3, the laminar flat plate "
                          "(1024 x 1024 quads, M 0.2, Re 8.7e5), HLLC + WLS + unlimited linear + Sutherland viscous flux, "
                          "implicit figure matrix-free; config5: BASELINE config 5, the laminar NACA0012 "
-                         "(M 0.5, Re 5000, alpha 0) on the 8.1M-cell C5 O-grid (C4 with 4096 cells around), Roe + WLS + "
+                         "(M 0.5, Re 5000, alpha 0) on the 8.1M-cell C5 quadrangle C-grid (4096 columns x 1984 rows), Roe + WLS + "
                          "unlimited linear reconstruction (the deck's limiter none) + Sutherland viscous flux")
     args = ap.parse_args()
 

@@ -3,10 +3,11 @@
 combinations of BASELINE.json's configs on one MI355X, each on its own synthetic mesh:
 
   C2/C4 NACA0012 O-grid (bench.py's generator) -- Roe + WLS + MUSCL/Van Albada (the headline path),
-        Roe + WLS + Venkatakrishnan (config 3), Roe + WLS + unlimited linear, HLLC + Green-Gauss +
+        Roe + WLS + Venkatakrishnan (config 4), Roe + WLS + unlimited linear, HLLC + Green-Gauss +
         Barth-Jespersen, first-order LLF;
-  flat plate (config 2) -- laminar, HLLC + WLS + unlimited linear + Sutherland viscous flux;
-  laminar NACA0012 on the O-grid (config 5 numerics) -- Roe + WLS + Van Albada + viscous.
+  flat plate (config 3) -- laminar, HLLC + WLS + unlimited linear + Sutherland viscous flux;
+  laminar NACA0012 on the O-grid -- Roe + WLS + Van Albada + viscous (config 5 itself, on its C-grid with the
+  deck's unlimited reconstruction: bench.py --numerics config5).
 
 Prints one JSON line per case: ms per residual, Gfaces/s, the kernels and their per-call times.
 """

@@ -1,5 +1,6 @@
 #!/usr/bin/env python3
-"""BASELINE config 5 solved to the visc-naca0012 deck's tolerance on the C5 O-grid family with the device
+"""BASELINE config 5 solved to the visc-naca0012 deck's tolerance on the C5 family (the quadrangle C-grid of
+bench.c4_mesh; --quads: the same grid built here) with the device
 solver: testcases/visc-naca0012/laminar-implicit.ctrl's schedule -- first-order initialisation (CFL 200 ->
 1000, tolerance 1e-1, 50 steps), then the second-order main solve (Roe, least squares, limiter none,
 Sutherland; CFL 500 -> 5000 by expResidualRamp, tolerance 1e-6), 'full' nonlinear update -- with the
