@@ -273,6 +273,31 @@ void k_sum_partials(int np, const double* __restrict__ part, double* __restrict_
 	block_sum<1>(acc, out + blockIdx.x, 1);
 }
 
+// FVHIP_KRY_UNROLL = U > 1: the basis loops of k_maxpy, k_maxpy_norm and k_lincomb load U vectors' rows
+// before their (unchanged, sequential) sums -- the same operations in the same order, so the same bits --
+// instead of one load and a full memory wait per basis vector
+#ifndef FVHIP_KRY_UNROLL
+#define FVHIP_KRY_UNROLL 1
+#endif
+constexpr int KRY_UNROLL = FVHIP_KRY_UNROLL;
+/// s += c[j] * X[j*ld + i] over j = 0 .. k-1 in order (X read as T rows: double or double2)
+template <typename T, typename F>
+__device__ __forceinline__ void basis_sum(int k, const double* __restrict__ c, const double* __restrict__ V, long long ld,
+                                          long long i, F&& add)
+{
+	int j = 0;
+	if constexpr(KRY_UNROLL > 1) {
+		for(; j + KRY_UNROLL <= k; j += KRY_UNROLL) {
+			T v[KRY_UNROLL];
+			#pragma unroll
+			for(int q = 0; q < KRY_UNROLL; q++) v[q] = reinterpret_cast<const T*>(V + (j + q)*ld)[i];
+			#pragma unroll
+			for(int q = 0; q < KRY_UNROLL; q++) add(c[j + q], v[q]);
+		}
+	}
+	for(; j < k; j++) add(c[j], reinterpret_cast<const T*>(V + j*ld)[i]);
+}
+
 __global__ __launch_bounds__(256)
 void k_maxpy(long long n, int k, const double* __restrict__ V, long long ld, const double* __restrict__ h,
              double* __restrict__ w)
@@ -280,7 +305,7 @@ void k_maxpy(long long n, int k, const double* __restrict__ V, long long ld, con
 	const long long i = blockIdx.x*256LL + threadIdx.x;
 	if(i >= n) return;
 	double s = 0.0;
-	for(int j = 0; j < k; j++) s += h[j]*V[j*ld + i];
+	basis_sum<double>(k, h, V, ld, i, [&](double c, double v) { s += c*v; });
 	w[i] -= s;
 }
 
@@ -295,11 +320,7 @@ void k_maxpy_norm(long long n, int k, const double* __restrict__ V, long long ld
 	double2* w2 = reinterpret_cast<double2*>(w);
 	for(long long i = blockIdx.x*256LL + threadIdx.x; i < n2; i += 256LL*gridDim.x) {
 		double sx = 0.0, sy = 0.0;
-		for(int j = 0; j < k; j++) {
-			const double2 v = reinterpret_cast<const double2*>(V + j*ld)[i];
-			sx += h[j]*v.x;
-			sy += h[j]*v.y;
-		}
+		basis_sum<double2>(k, h, V, ld, i, [&](double c, double2 v) { sx += c*v.x; sy += c*v.y; });
 		double2 wi = w2[i];
 		wi.x -= sx; wi.y -= sy;
 		w2[i] = wi;
@@ -316,7 +337,7 @@ void k_lincomb(long long n, int k, const double* __restrict__ V, long long ld, c
 	const long long i = blockIdx.x*256LL + threadIdx.x;
 	if(i >= n) return;
 	double s = 0.0;
-	for(int j = 0; j < k; j++) s += c[j]*V[j*ld + i];
+	basis_sum<double>(k, c, V, ld, i, [&](double cj, double v) { s += cj*v; });
 	out[i] = s;
 }
 
