@@ -48,25 +48,32 @@ C4_WALL_SPACING = 1e-5
 # direction map (0) the cosine-clustered trailing-edge points crowd the far field at angle 0, leaving
 # sliver triangles (aspect ratio ~1e3) along the wake line where second-order solves blow up
 C4_FARMAP = 1
-# the viscous C5 family (config 5) is a C-grid of quadrangles (generateNacaCgrid, ntri 0; 4096 columns x 1984
-# rows = the hybrid O-grid's 8,126,464 cells): on the O-grid the aft boundary layer was 8-9 degree
-# parallelograms (straight lines) or the trailing-edge point's cells fanned over the wake (wall-normal lines,
-# farmap 3), and with triangle rows (split stretched quadrangles) on either grid the first-order-
-# preconditioned GMRES of the laminar deck's second-order solve reduced nothing; on the quadrangle C-grid it
-# converges (profiles/r05/c5_family_convergence_probes.jsonl)
+# the viscous C5 family (config 5): the hybrid mesh of the visc-naca0012 grids' topology
+# (testcases/visc-naca0012/grids/naca0012nasa-blcirc.geo, NACA0012_lam_hybrid_1.msh: quadrangles through the
+# boundary layer, triangles outside it), built on the quadrangle C-grid's points (generateNacaHybrid): 3072
+# columns round the body and 384 along each wake, 2048 rows from a 1e-5 wall spacing; quadrangles in the body's
+# first 768 rows and in the wake blocks, near-isotropic triangles (each row resampled to its row distance)
+# above the body's boundary layer: 8,054,644 cells (3,932,160 quadrangles, 4,122,484 triangles), 14,052,330
+# faces. Round 5's quadrangle C-grid (generateNacaCgrid, ntri 0) stays available as topology "cgrid".
+C5_DIMS = dict(nsurf=3072, nwake=384, nquad=768, nrows=2048)
 
 
-def c4_mesh(fa, scale, mult=1, wall=None, farmap=None):
-    """C4 (mult 1): the O-grid; C5 (mult 2): the C-grid of the same cell count (4096 columns: 3072 round
-    the body, 512 along each wake), unless an O-grid `farmap` is asked for"""
+def c4_mesh(fa, scale, mult=1, wall=None, farmap=None, topology="hybrid"):
+    """C4 (mult 1): the O-grid; C5 (mult 2): the hybrid mesh of the visc-naca0012 grids' topology (or, with
+    topology "cgrid", round 5's quadrangle C-grid: 4096 columns, 3072 round the body, 512 along each wake),
+    unless an O-grid `farmap` is asked for"""
     nt = 2048 * mult // scale
     nq = 256 // scale
     ntri = 864 // scale
     ws = C4_WALL_SPACING if wall is None else wall
+    if mult == 2 and farmap is None and topology == "hybrid":
+        d = {k: v // scale for k, v in C5_DIMS.items()}
+        return (fa.UMesh.naca_hybrid(d["nsurf"], d["nwake"], d["nquad"], d["nrows"], 20.0, ws),
+                dict(topology="hybrid", **d, wall_spacing=ws))
     if mult == 2 and farmap is None:
         ns, nw, rows = 3 * nt // 4, nt // 8, nq + 2 * ntri
         return (fa.UMesh.naca_cgrid(ns, nw, rows, 0, 20.0, ws),
-                dict(topology="C-grid, quadrangles", nsurf=ns, nwake=nw, rows=rows, wall_spacing=ws))
+                dict(topology="cgrid", nsurf=ns, nwake=nw, rows=rows, wall_spacing=ws))
     fm = C4_FARMAP if farmap is None else farmap
     return (fa.UMesh.naca_ogrid(nt, nq, ntri, 20.0, ws, farmap=fm),
             dict(ntheta=nt, nquad=nq, ntri=ntri, wall_spacing=ws, farmap=fm))
@@ -869,22 +876,32 @@ def emit(out, implicit, phases, t_implicit):
     print(json.dumps(out), flush=True)
 
 
+GUARD_EXIT = 3     # exit status of a rank whose implicit section missed the deadline
+
+
 def guarded_implicit(section, deadline_s, dist, ctrl, rank, on_deadline):
     """N ranks: run the implicit section (collectives over RCCL) so that its failure cannot lose the line.
     A rank whose section raises keeps the error; the ranks then agree over the host-side gloo group `ctrl`
     (an error anywhere is an error everywhere). A rank stuck in a collective -- its peer failed, or a
     transport hangs -- never reaches the agreement: when `deadline_s` passes, every rank's timer fires,
-    rank 0 prints the line with the error (on_deadline) and every process exits at once."""
+    rank 0 prints the line with the error (on_deadline) and every process exits at once with status
+    GUARD_EXIT (the run did not finish). A lock orders the timer against the agreement: once the ranks have
+    agreed the timer can no longer fire, so exactly one line is printed."""
     import threading
     import torch
+    lock = threading.Lock()
+    state = {"agreed": False}
 
     def expire():
-        try:
-            on_deadline({"error": "implicit section did not finish on every rank within %.0f s" % deadline_s})
-        finally:
-            sys.stdout.flush()
-            sys.stderr.flush()
-            os._exit(0)
+        with lock:
+            if state["agreed"]:
+                return
+            try:
+                on_deadline({"error": "implicit section did not finish on every rank within %.0f s" % deadline_s})
+            finally:
+                sys.stdout.flush()
+                sys.stderr.flush()
+                os._exit(GUARD_EXIT)
     timer = threading.Timer(deadline_s, expire)
     timer.daemon = True
     timer.start()
@@ -894,6 +911,8 @@ def guarded_implicit(section, deadline_s, dist, ctrl, rank, on_deadline):
         im, err = None, "rank %d: %s" % (rank, e)
     flag = torch.tensor([0.0 if err is None else 1.0 + rank], dtype=torch.float64)
     dist.all_reduce(flag, op=dist.ReduceOp.MAX, group=ctrl)
+    with lock:
+        state["agreed"] = True
     timer.cancel()
     if err is not None:
         return {"error": err}

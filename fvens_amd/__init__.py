@@ -87,6 +87,10 @@ class ImplicitConfig:
     line_threshold: float = 0.0     # strongest/weakest coupling ratio for a cell to join a line (0: 4)
     prec_ilu: bool = False          # block ILU(0) in multicolour order (-sub_pc_type ilu)
     cgs_refine: int = 0             # -ksp_gmres_cgs_refinement_type: 0 never (PETSc default), 1 ifneeded, 2 always
+    prec_amg: int = 0               # aggregation multigrid levels (mgopts.solverc -pc_mg_levels; 0 off)
+    amg_sweeps: int = 2             # smoothing sweeps per level (-mg_levels_ksp_max_it)
+    amg_coarse_sweeps: int = 6      # Gauss-Seidel sweeps on the coarsest level (-mg_coarse_ksp_max_it)
+    amg_threshold: float = 0.2      # aggregation strength threshold (-pc_gamg_threshold)
 
     def _struct(self):
         c = _ffi.FvImplicitConfig()
@@ -100,6 +104,8 @@ class ImplicitConfig:
         c.line_threshold = float(self.line_threshold)
         c.prec_ilu = int(self.prec_ilu)
         c.cgs_refine = int(self.cgs_refine)
+        c.prec_amg, c.amg_sweeps, c.amg_coarse_sweeps = int(self.prec_amg), int(self.amg_sweeps), int(self.amg_coarse_sweeps)
+        c.amg_threshold = float(self.amg_threshold)
         return c
 
 
@@ -164,6 +170,16 @@ class UMesh:
         (mesh.cpp generateNacaCgrid; the C5 family)"""
         h = ctypes.c_void_p()
         check(_ffi.lib().fvmesh_generate(3, nsurf, nquad, ntri, rfar, wallspacing, float(nwake), ctypes.byref(h)))
+        return cls(h.value)
+
+    @classmethod
+    def naca_hybrid(cls, nsurf, nwake, nquad, nrows, rfar=20.0, wallspacing=1e-5):
+        """hybrid mesh of the visc-naca0012 grids' topology: the C-grid of `naca_cgrid` with quadrangles in the
+        body's first nquad rows (boundary layer) and in the wake blocks, near-isotropic triangles above the
+        body's quadrangles (mesh.cpp generateNacaHybrid; the C5 family)"""
+        h = ctypes.c_void_p()
+        check(_ffi.lib().fvmesh_generate_hybrid(nsurf, nwake, nquad, nrows, rfar, wallspacing,
+                                                ctypes.byref(h)))
         return cls(h.value)
 
     @classmethod

@@ -40,7 +40,9 @@ class FvImplicitConfig(ctypes.Structure):
                 ("lin_rtol", ctypes.c_double), ("lin_maxit", ctypes.c_int), ("restart", ctypes.c_int),
                 ("prec_sweeps", ctypes.c_int), ("min_relax", ctypes.c_double),
                 ("prec_single", ctypes.c_int), ("prec_gs", ctypes.c_int), ("prec_lines", ctypes.c_int),
-                ("line_threshold", ctypes.c_double), ("prec_ilu", ctypes.c_int), ("cgs_refine", ctypes.c_int)]
+                ("line_threshold", ctypes.c_double), ("prec_ilu", ctypes.c_int), ("cgs_refine", ctypes.c_int),
+                ("prec_amg", ctypes.c_int), ("amg_sweeps", ctypes.c_int), ("amg_coarse_sweeps", ctypes.c_int),
+                ("amg_threshold", ctypes.c_double)]
 
 
 class FvSolveStats(ctypes.Structure):
@@ -148,6 +150,8 @@ _SIGS = {
     "fvmesh_read_gmsh": (ctypes.c_int, [ctypes.c_char_p, ctypes.POINTER(ctypes.c_void_p)]),
     "fvmesh_generate": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_double,
                                        ctypes.c_double, ctypes.c_double, ctypes.POINTER(ctypes.c_void_p)]),
+    "fvmesh_generate_hybrid": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                              ctypes.c_double, ctypes.c_double, ctypes.POINTER(ctypes.c_void_p)]),
     "fvmesh_write_gmsh": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_char_p]),
     "fvmesh_destroy": (ctypes.c_int, [ctypes.c_void_p]),
     "fvmesh_view": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(FvMeshView)]),

@@ -16,6 +16,7 @@
 #include "halo.hpp"
 #include "ode.hpp"
 #include "surface.hpp"
+#include "amg.hpp"
 #include <rccl/rccl.h>
 #include <hip/hip_runtime.h>
 #include <cstring>
@@ -369,6 +370,13 @@ struct fvhip_ctx
 	struct MfFuse { const double *x = nullptr, *pm = nullptr, *res = nullptr, *mdt = nullptr; } mfz;
 	/// (x and y must not alias: other blocks read x rows while a block writes its cells' y)
 	bool matfreeFusable() const { return fused() && !halo(); }
+	/// the fused operator's blocks read rows of x and of the state u that other blocks' cells need while each
+	/// block writes its own cells of y: y must share no byte with x or u (else the three-launch operator runs)
+	bool matfreeNoAlias(const double* u, const double* x, const double* y) const {
+		const size_t n = 4*static_cast<size_t>(L.ncell), nt = 4*static_cast<size_t>(L.ncell + L.nghost);
+		auto apart = [](const double* a, size_t na, const double* b, size_t nb) { return a + na <= b || b + nb <= a; };
+		return apart(y, n, x, nt) && apart(y, n, u, nt);
+	}
 	void matfree_fused(const double* u, const double* x, const double* pm, const double* res, const double* mdt, double* y) {
 		if(!matfreeFusable()) throw std::logic_error("matfree_fused: not a fused single-domain configuration");
 		mfz = MfFuse{x, pm, res, mdt};
@@ -976,6 +984,76 @@ struct fvhip_ctx
 		lines_thr = thr;
 	}
 
+	/// aggregation multigrid hierarchy (fvhip_implicit_config::prec_amg), built on first use from the mesh:
+	/// the finest level's graph is the owned cells over interior faces with couplings face length / centre
+	/// distance (ghost couplings dropped: block-Jacobi across ranks), its block indices those of the
+	/// face-ordered Jacobian (diag c, lower N + fi, upper N + Fi + fi); coarsening stops at `levels` levels
+	/// or when a level has fewer than 64 rows or shrinks by less than 1.25
+	std::vector<AmgLevel> amg;
+	int amg_levels = 0;
+	double amg_thr = -1.0;
+	void ensureAmg(int levels, double thr) {
+		if(levels < 2) throw std::invalid_argument("prec_amg: at least 2 levels");
+		if(!(thr >= 0.0 && thr < 1.0)) throw std::invalid_argument("amg_threshold must be in [0, 1)");
+		if(amg_levels == levels && amg_thr == thr) return;
+		if(!amg.empty()) throw std::runtime_error("prec_amg: the hierarchy is built once per handle (same levels and threshold)");
+		const int N = L.ncell, nb = L.nbface, Fi = L.ninface;
+		AmgGraph g;
+		g.n = N;
+		g.rowptr.assign(static_cast<size_t>(N) + 1, 0);
+		g.dblk.resize(static_cast<size_t>(N));
+		std::vector<std::array<double,3>> row;          // (column, coupling, block)
+		for(int c = 0; c < N; c++) {
+			g.dblk[c] = c;
+			row.clear();
+			for(int j = 0; j < 4; j++) {
+				const int code = L.cell_rfaces[4*static_cast<size_t>(c)+j];
+				if(code < 0 || (code >> 1) < nb) continue;
+				const int o = L.cell_nbr_fo[4*static_cast<size_t>(c)+j];
+				if(o < 0 || o >= N) continue;
+				const int fi = (code >> 1) - nb;
+				const double dx = L.rc[2*static_cast<size_t>(c)] - L.rc[2*static_cast<size_t>(o)];
+				const double dy = L.rc[2*static_cast<size_t>(c)+1] - L.rc[2*static_cast<size_t>(o)+1];
+				const int blk = (code & 1) ? N + fi : N + Fi + fi;     // A[c][o]: c = R reads lower, c = L upper
+				row.push_back({static_cast<double>(o), L.if_len[fi]/std::sqrt(dx*dx + dy*dy), static_cast<double>(blk)});
+			}
+			std::sort(row.begin(), row.end());
+			for(const auto& r : row) {
+				g.col.push_back(static_cast<int>(r[0])); g.w.push_back(r[1]); g.blk.push_back(static_cast<int>(r[2]));
+			}
+			g.rowptr[c+1] = static_cast<int>(g.col.size());
+		}
+		for(int l = 1; l < levels; l++) {
+			if(g.n < 64) break;
+			AmgLevelHost H = amgCoarsen(g, thr);
+			if(H.n*5 > g.n*4) break;                         // shrinks by less than 1.25: stop
+			AmgLevel D;
+			D.n = H.n; D.nnz = H.rowptr[H.n]; D.nfine = g.n;
+			D.rowptr = upload(H.rowptr, owned); D.col = upload(H.col, owned); D.dpos = upload(H.dpos, owned);
+			D.cstart = upload(H.cstart, owned); D.csrc = upload(H.csrc, owned);
+			D.mstart = upload(H.mstart, owned); D.members = upload(H.members, owned); D.agg = upload(H.agg, owned);
+			D.cells = upload(H.cells, owned); D.cstart_colour = H.cstart_colour;
+			D.val = dalloc(16*static_cast<size_t>(D.nnz), owned); D.dinv = dalloc(16*static_cast<size_t>(D.n), owned);
+			D.x = dalloc(4*static_cast<size_t>(D.n), owned); D.b = dalloc(4*static_cast<size_t>(D.n), owned);
+			D.r = dalloc(4*static_cast<size_t>(D.n), owned);
+			amg.push_back(D);
+			g = amgGraphOf(H);
+		}
+		if(amg.empty()) throw std::runtime_error("prec_amg: the mesh does not coarsen");
+		amg_levels = levels;
+		amg_thr = thr;
+	}
+	/// Galerkin operators of every coarse level from the finest blocks, and their diagonal inverses
+	void amgSetup(const double* diag, const double* lower, const double* upper) {
+		timed("k_amg_galerkin", [&]{
+			for(size_t l = 0; l < amg.size(); l++) {
+				if(l == 0) launch_amg_galerkin_fine(amg[0], L.ncell, L.ninface, diag, lower, upper, stream);
+				else launch_amg_galerkin(amg[l], amg[l-1].val, stream);
+				launch_amg_invert(amg[l], stream);
+			}
+		});
+	}
+
 	/// frees one device array of `owned` before the handle's destruction
 	void release(const void* p) {
 		if(!p) return;
@@ -1004,7 +1082,7 @@ struct fvhip_ctx
 		if(!d_part) { d_part = dalloc(mf_partials(), owned); d_pm = dalloc(2, owned); }
 		if(!d_mf_aux) { d_mf_aux = dalloc(4*N, owned); d_mf_y = dalloc(4*N, owned); }
 		timed("k_mf_norm", [&]{ launch_mf_norm(4LL*L.ncell, x, mf_eps, d_part, d_pm, stream); });
-		if(matfreeFusable() && x != y) { matfree_fused(mf_u, x, d_pm, mf_r, mf_mdt, y); HC(hipGetLastError()); return; }
+		if(matfreeFusable() && matfreeNoAlias(mf_u, x, y)) { matfree_fused(mf_u, x, d_pm, mf_r, mf_mdt, y); HC(hipGetLastError()); return; }
 		timed("k_mf_perturb", [&]{ launch_mf_perturb(4LL*L.ncell, mf_u, x, d_pm, d_mf_aux, stream); });
 		residual(d_mf_aux, d_mf_y, false, nullptr, true);
 		timed("k_mf_combine", [&]{ launch_mf_combine(L.ncell, mf_mdt, x, d_mf_y, mf_r, d_pm, y, stream); });

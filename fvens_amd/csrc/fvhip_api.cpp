@@ -941,6 +941,17 @@ int fvmesh_generate(int kind, int a, int b, int c, double x, double y, double z,
 	});
 }
 
+int fvmesh_generate_hybrid(int nsurf, int nwake, int nquad, int nrows, double rfar,
+                           double wallspacing, fvmesh_handle* out)
+{
+	return guard([&] {
+		std::unique_ptr<fvmesh_s> m(new fvmesh_s());
+		m->raw = generateNacaHybrid(nsurf, nwake, nquad, nrows, rfar, wallspacing);
+		m->mesh = buildMesh(m->raw);
+		*out = m.release();
+	});
+}
+
 int fvmesh_write_gmsh(fvmesh_handle m, const char* path) { return guard([&] { writeGmsh2(m->raw, path); }); }
 int fvmesh_destroy(fvmesh_handle m) { return guard([&] { delete m; }); }
 

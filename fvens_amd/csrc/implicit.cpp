@@ -93,7 +93,7 @@ static void matfreeApply(System& S, const ArrayOf& x, const ArrayOf& y, bool hav
 		if(!have_norm) launch_mdot(4LL*h->L.ncell, 0, nullptr, 0, x(i), true, h->iw.part, h->iw.red, h->stream);
 	});
 	if(!have_norm) S.allsumDevice(1);          // |x|^2 stays on the device (launch_pertmag reads it there)
-	if(S.size() == 1 && !S.exg && S.hs[0]->matfreeFusable() && x(0) != y(0)) {
+	if(S.size() == 1 && !S.exg && S.hs[0]->matfreeFusable() && S.hs[0]->matfreeNoAlias(S.hs[0]->mf_u, x(0), y(0))) {
 		// one launch: the perturbed state and the combination inside the residual kernel (bitwise the same)
 		fvhip_ctx* h = S.hs[0];
 		launch_pertmag(h->iw.red, h->mf_eps, h->iw.pm, h->stream);
@@ -127,6 +127,9 @@ struct LinOp
 	bool ilu = false;                         ///< block ILU(0) in multicolour order
 	double line_thr = 0.0;
 	int sweeps = 1;
+	int amg = 0;                              ///< aggregation multigrid levels (0: one-level preconditioner)
+	int amg_sweeps = 2, amg_coarse = 6;
+	double amg_thr = 0.2;
 	std::vector<const double*> D, Lo, Up;     ///< per handle: diagonal / lower / upper blocks
 
 	/// y = A x with the assembled blocks; x has ghost rows, which are filled here
@@ -149,6 +152,7 @@ struct LinOp
 	/// alternate between z and aux (both with ghost rows) so that the last one lands in z.
 	void precondition(const ArrayOf& v, const ArrayOf& z, bool want_norm = false) {
 		znorm = false;
+		if(amg) { amgApply(v, z); return; }
 		if(gs) { gaussSeidel(v, z); return; }
 		if(lines) { lineSweeps(v, z, want_norm); return; }
 		if(ilu) { iluSweeps(v, z); return; }
@@ -248,8 +252,72 @@ struct LinOp
 			});
 		}
 	}
+	/// z = the finest smoother applied to v (line solve, else D^-1 v)
+	void smooth0(fvhip_ctx* h, size_t i, const double* v, double* z) {
+		if(lines) h->timed("k_line_solve", [&]{ launch_line_solve(h->lines, v, z, h->stream); });
+		else launch_bjac_apply(h->L.ncell, h->iw.dinv, v, z, h->stream);
+	}
+	/// t = v - A z (A with the ghost coupling)
+	void residual0(const ArrayOf& v, const ArrayOf& z, const ArrayOf& t) {
+		blocks(z, t);
+		S.each([&](size_t i, fvhip_ctx* h) { launch_axpby(4LL*h->L.ncell, 1.0, v(i), -1.0, t(i), h->stream); });
+	}
+	/// coarse level l of handle h's hierarchy: V-cycle on A_l x_l = b_l from x_l = 0 (colour Gauss-Seidel
+	/// forward before the coarse correction, backward after it; the coarsest level amg_coarse sweeps)
+	void cycle(fvhip_ctx* h, size_t l) {
+		AmgLevel& C = h->amg[l];
+		exact::launch_fill(C.x, 0.0, 4LL*C.n, h->stream);
+		const int nc = static_cast<int>(C.cstart_colour.size()) - 1;
+		auto sweep = [&](bool fwd) {
+			for(int q = 0; q < nc; q++) launch_amg_gs_colour(C, fwd ? q : nc - 1 - q, C.b, C.x, h->stream);
+		};
+		if(l + 1 == h->amg.size()) {
+			for(int k = 0; k < amg_coarse; k++) sweep(k % 2 == 0);
+			return;
+		}
+		for(int k = 0; k < amg_sweeps; k++) sweep(true);
+		launch_amg_residual(C, C.x, C.b, C.r, h->stream);
+		AmgLevel& F = h->amg[l+1];
+		launch_amg_restrict(F, C.r, F.b, h->stream);
+		cycle(h, l + 1);
+		launch_amg_prolong(F, F.x, C.x, h->stream);
+		for(int k = 0; k < amg_sweeps; k++) sweep(false);
+	}
+	/// z = M^-1 v, M one V-cycle of the aggregation multigrid (block-Jacobi across ranks: each handle's hierarchy
+	/// covers its owned cells; the finest residuals include the ghost coupling)
+	void amgApply(const ArrayOf& v, const ArrayOf& z) {
+		const ArrayOf aux = [&](size_t i) { return S.hs[i]->iw.aux; };
+		const ArrayOf t = [&](size_t i) { return S.hs[i]->iw.t; };
+		S.each([&](size_t i, fvhip_ctx* h) { smooth0(h, i, v(i), z(i)); });
+		auto correct = [&]() {             // z += M0^-1 (v - A z)
+			residual0(v, z, t);
+			S.each([&](size_t i, fvhip_ctx* h) { smooth0(h, i, t(i), aux(i)); launch_add_rows(h->L.ncell, aux(i), z(i), h->stream); });
+		};
+		for(int k = 1; k < amg_sweeps; k++) correct();
+		residual0(v, z, t);
+		S.each([&](size_t i, fvhip_ctx* h) {
+			h->timed("k_amg_cycle", [&]{
+				launch_amg_restrict(h->amg[0], t(i), h->amg[0].b, h->stream);
+				cycle(h, 0);
+				launch_amg_prolong(h->amg[0], h->amg[0].x, z(i), h->stream);
+			});
+		});
+		for(int k = 0; k < amg_sweeps; k++) correct();
+	}
 	/// block inverses of the current diagonal blocks (or the line factorisation)
 	void setup() {
+		if(amg) {
+			S.each([&](size_t i, fvhip_ctx* h) {
+				if(lines) {
+					h->ensureLines(line_thr);
+					h->lines.single = false;
+					h->timed("k_line_factor", [&]{ launch_line_factor(h->lines, D[i], Lo[i], Up[i], h->stream); });
+				} else h->timed("k_bjac_invert", [&]{ launch_bjac_invert(h->L.ncell, D[i], h->iw.dinv, h->stream); });
+				h->ensureAmg(amg, amg_thr);
+				h->amgSetup(D[i], Lo[i], Up[i]);
+			});
+			return;
+		}
 		S.each([&](size_t i, fvhip_ctx* h) {
 			if(lines) {
 				h->ensureLines(line_thr);
@@ -434,6 +502,9 @@ static void checkImplicit(const fvhip_implicit_config& c)
 	if(c.restart < 1 || c.restart > KRY_MAXK) throw std::invalid_argument("restart must be in [1, 128]");
 	if(c.cgs_refine < 0 || c.cgs_refine > 2) throw std::invalid_argument("cgs_refine must be 0 (never), 1 (ifneeded) or 2 (always)");
 	if(c.prec_sweeps < 1) throw std::invalid_argument("prec_sweeps must be >= 1");
+	if(c.prec_amg != 0 && c.prec_amg < 2) throw std::invalid_argument("prec_amg must be 0 (off) or >= 2 levels");
+	if(c.amg_sweeps < 0 || c.amg_coarse_sweeps < 0 || !(c.amg_threshold >= 0.0 && c.amg_threshold < 1.0))
+		throw std::invalid_argument("amg_sweeps / amg_coarse_sweeps must be >= 0 and amg_threshold in [0, 1)");
 	if(!(c.min_relax > 0.0)) throw std::domain_error("Minimum relaxation factor is invalid!");  // nonlinearrelaxation.cpp:20-21
 	if(c.matrix_free && !(c.mf_eps > 0.0)) throw std::invalid_argument("matrix-free difference step must be positive");
 	if(!(c.line_threshold >= 0.0) || !std::isfinite(c.line_threshold))
@@ -457,6 +528,12 @@ static void backwardEuler(System& S, const std::vector<double*>& us, const fvhip
 	A.ilu = c.prec_ilu != 0;
 	if(A.lines && A.gs) throw std::invalid_argument("prec_lines does not combine with prec_gs");
 	if(A.ilu && (A.gs || A.lines)) throw std::invalid_argument("prec_ilu does not combine with prec_gs / prec_lines");
+	A.amg = c.prec_amg;
+	A.amg_sweeps = c.amg_sweeps > 0 ? c.amg_sweeps : 2;
+	A.amg_coarse = c.amg_coarse_sweeps > 0 ? c.amg_coarse_sweeps : 6;
+	A.amg_thr = c.amg_threshold > 0.0 ? c.amg_threshold : 0.2;
+	if(A.amg && (A.gs || A.ilu || A.single || A.sweeps != 1))
+		throw std::invalid_argument("prec_amg combines with prec_lines only (prec_gs / prec_ilu / prec_single / prec_sweeps > 1 are one-level options)");
 	for(fvhip_ctx* h : S.hs) { A.D.push_back(h->iw.jd); A.Lo.push_back(h->iw.jlo); A.Up.push_back(h->iw.jup); }
 	std::vector<const double*> cu(us.begin(), us.end());
 	std::vector<double*> rs, dts;

@@ -722,75 +722,139 @@ MeshData generateNacaOgrid(int ntheta, int nquad, int ntri, double rfar, double 
 /// the wake lines at the trailing edge) and bends onto the straight line to its far-field point (angles
 /// uniform in the surface parameter) by one chord (smoothstep). Rows grow geometrically from
 /// `wallspacing`. Quadrangles in the first nquad rows, triangles beyond. Markers: wall 2, far field 4.
-MeshData generateNacaCgrid(int nsurf, int nwake, int nquad, int ntri, double rfar, double wallspacing)
+namespace {
+
+/// The C-grid's mapping (generateNacaCgrid's columns and rows, shared with generateNacaHybrid): column i's
+/// point at the normalised distance eta along its line from the body / wake cut to the far field
+struct CgridMap
 {
-	if(nsurf < 8 || nsurf % 2 || nwake < 2) throw std::invalid_argument("nsurf must be even and >= 8, nwake >= 2");
-	const double PI = 3.14159265358979323846;
-	const int nl = nquad + ntri, ni = 2*nwake + nsurf + 1, half = nsurf/2;
-	// surface, upper side parameter t = 0 (LE) .. 1 (TE)
-	auto xs = [&](double t) { return 0.5*(1.0 - std::cos(0.5*PI*t)) + 0.25*(1.0 - std::cos(PI*t)); };
-	std::vector<double> sx(ni), sy(ni), fx(ni), fy(ni);
-	const double dte = 1.0 - xs(1.0 - 1.0/half);               // trailing-edge spacing
-	// wake stations x = 1 + w_k, k = 1 .. nwake, geometric from dte to the outflow
-	std::vector<double> wx(nwake + 1, 1.0);
+	int nsurf, nwake, ni, half;
+	std::vector<double> sx, sy, fx, fy;
+	double blend = 1.0;
+	CgridMap(int nsurf_, int nwake_, double rfar) : nsurf(nsurf_), nwake(nwake_), ni(2*nwake_ + nsurf_ + 1),
+		half(nsurf_/2), sx(ni), sy(ni), fx(ni), fy(ni)
 	{
-		const double L = rfar;
-		double lo = 1.0 + 1e-12, hi = 2.0;
-		for(int it = 0; it < 200; it++) {
-			const double q = 0.5*(lo + hi);
-			if(dte*(std::pow(q, nwake) - 1.0)/(q - 1.0) > L) hi = q; else lo = q;
-		}
-		const double q = 0.5*(lo + hi);
-		double acc = 0, d = dte;
-		for(int k = 1; k <= nwake; k++) { acc += d; wx[k] = 1.0 + acc; d *= q; }
-		for(int k = 1; k <= nwake; k++) wx[k] = 1.0 + (wx[k] - 1.0)*L/acc;
-	}
-	// the wake lines' far ends along y = +-rfar: spacing from the half circle's (pi rfar / nsurf) growing
-	// geometrically to the outflow, so the columns next to the trailing edge's line widen outwards
-	// instead of running to the far field as slivers of the trailing-edge spacing
-	std::vector<double> ox(nwake + 1, 1.0);
-	{
-		const double L = rfar, s0 = PI*rfar/nsurf;
-		if(s0*nwake >= L) { for(int k = 1; k <= nwake; k++) ox[k] = 1.0 + L*k/nwake; }
-		else {
+		const double PI = 3.14159265358979323846;
+		// surface, upper side parameter t = 0 (LE) .. 1 (TE)
+		auto xs = [&](double t) { return 0.5*(1.0 - std::cos(0.5*PI*t)) + 0.25*(1.0 - std::cos(PI*t)); };
+		const double dte = 1.0 - xs(1.0 - 1.0/half);               // trailing-edge spacing
+		// wake stations x = 1 + w_k, k = 1 .. nwake, geometric from dte to the outflow
+		std::vector<double> wx(nwake + 1, 1.0);
+		{
+			const double L = rfar;
 			double lo = 1.0 + 1e-12, hi = 2.0;
 			for(int it = 0; it < 200; it++) {
 				const double q = 0.5*(lo + hi);
-				if(s0*(std::pow(q, nwake) - 1.0)/(q - 1.0) > L) hi = q; else lo = q;
+				if(dte*(std::pow(q, nwake) - 1.0)/(q - 1.0) > L) hi = q; else lo = q;
 			}
 			const double q = 0.5*(lo + hi);
-			double acc = 0, d = s0;
-			for(int k = 1; k <= nwake; k++) { acc += d; ox[k] = 1.0 + acc; d *= q; }
-			for(int k = 1; k <= nwake; k++) ox[k] = 1.0 + (ox[k] - 1.0)*L/acc;
+			double acc = 0, d = dte;
+			for(int k = 1; k <= nwake; k++) { acc += d; wx[k] = 1.0 + acc; d *= q; }
+			for(int k = 1; k <= nwake; k++) wx[k] = 1.0 + (wx[k] - 1.0)*L/acc;
+		}
+		// the wake lines' far ends along y = +-rfar: spacing from the half circle's (pi rfar / nsurf) growing
+		// geometrically to the outflow, so the columns next to the trailing edge's line widen outwards
+		// instead of running to the far field as slivers of the trailing-edge spacing
+		std::vector<double> ox(nwake + 1, 1.0);
+		{
+			const double L = rfar, s0 = PI*rfar/nsurf;
+			if(s0*nwake >= L) { for(int k = 1; k <= nwake; k++) ox[k] = 1.0 + L*k/nwake; }
+			else {
+				double lo = 1.0 + 1e-12, hi = 2.0;
+				for(int it = 0; it < 200; it++) {
+					const double q = 0.5*(lo + hi);
+					if(s0*(std::pow(q, nwake) - 1.0)/(q - 1.0) > L) hi = q; else lo = q;
+				}
+				const double q = 0.5*(lo + hi);
+				double acc = 0, d = s0;
+				for(int k = 1; k <= nwake; k++) { acc += d; ox[k] = 1.0 + acc; d *= q; }
+				for(int k = 1; k <= nwake; k++) ox[k] = 1.0 + (ox[k] - 1.0)*L/acc;
+			}
+		}
+		for(int i = 0; i < ni; i++) {
+			if(i < nwake || i > nwake + nsurf) {                     // wake: lines from the cut to y = +-rfar
+				const bool lower = i < nwake;
+				const int k = lower ? nwake - i : i - (nwake + nsurf);
+				sx[i] = wx[k]; sy[i] = 0.0;
+				fx[i] = ox[k]; fy[i] = lower ? -rfar : rfar;
+			} else {
+				const int m = i - nwake;                                // 0 .. nsurf: TE lower -> LE -> TE upper
+				const bool lower = m < half;
+				const double t = lower ? static_cast<double>(half - m)/half : static_cast<double>(m - half)/half;
+				const double x = m == 0 || m == nsurf ? 1.0 : xs(t);
+				sx[i] = x; sy[i] = lower ? -naca0012(x) : naca0012(x);
+				if(m == 0 || m == nsurf) sy[i] = 0.0;
+				const double ang = -0.5*PI - PI*static_cast<double>(m)/nsurf;   // -pi/2 (down) .. -3pi/2 (up)
+				fx[i] = 1.0 + rfar*std::cos(ang); fy[i] = rfar*std::sin(ang);
+			}
 		}
 	}
-	for(int i = 0; i < ni; i++) {
-		if(i < nwake || i > nwake + nsurf) {                     // wake: lines from the cut to y = +-rfar
-			const bool lower = i < nwake;
-			const int k = lower ? nwake - i : i - (nwake + nsurf);
-			sx[i] = wx[k]; sy[i] = 0.0;
-			fx[i] = ox[k]; fy[i] = lower ? -rfar : rfar;
-		} else {
-			const int m = i - nwake;                                // 0 .. nsurf: TE lower -> LE -> TE upper
-			const bool lower = m < half;
-			const double t = lower ? static_cast<double>(half - m)/half : static_cast<double>(m - half)/half;
-			const double x = m == 0 || m == nsurf ? 1.0 : xs(t);
-			sx[i] = x; sy[i] = lower ? -naca0012(x) : naca0012(x);
-			if(m == 0 || m == nsurf) sy[i] = 0.0;
-			const double ang = -0.5*PI - PI*static_cast<double>(m)/nsurf;   // -pi/2 (down) .. -3pi/2 (up)
-			fx[i] = 1.0 + rfar*std::cos(ang); fy[i] = rfar*std::sin(ang);
+	/// column i's point at eta (0: body / cut, 1: far field); eta > 0 only off the body
+	void point(int i, double eta, double& x, double& y) const
+	{
+		double dx = fx[i] - sx[i], dy = fy[i] - sy[i];
+		const double L = std::sqrt(dx*dx + dy*dy);
+		const bool body = i > nwake && i < nwake + nsurf;
+		const bool te = i == nwake || i == nwake + nsurf;
+		if(!te && eta > 0.0 && eta*L < blend) {
+			double nx = 0.0, ny = fy[i] > 0 ? 1.0 : -1.0;           // wake: the cut's normal
+			if(body) {
+				nx = sy[i+1] - sy[i-1]; ny = -(sx[i+1] - sx[i-1]);
+				if(nx*dx + ny*dy < 0) { nx = -nx; ny = -ny; }
+				if(sx[i] > 0.9) {                               // the normal turns vertical at the trailing
+					const double g = (sx[i] - 0.9)/0.1;          // edge, parallel to the wake lines next to it
+					nx *= 1.0 - g*g*(3.0 - 2.0*g);
+				}
+			}
+			const double nn = std::sqrt(nx*nx + ny*ny);
+			const double xx = eta*L/blend;
+			const double w = xx*xx*(3.0 - 2.0*xx);
+			const double ex = (1.0 - w)*nx/nn + w*dx/L, ey = (1.0 - w)*ny/nn + w*dy/L;
+			const double en = std::sqrt(ex*ex + ey*ey);
+			dx = L*ex/en; dy = L*ey/en;
 		}
+		x = sx[i] + eta*dx;
+		y = sy[i] + eta*dy;
 	}
+};
+
+/// growth ratio q of nl rows whose first is `first` and whose sum is `total`
+double rowGrowth(int nl, double total_over_first)
+{
+	double lo = 1.0 + 1e-12, hi = 2.0;
+	for(int it = 0; it < 200; it++) {
+		const double q = 0.5*(lo+hi);
+		if((std::pow(q, nl) - 1.0)/(q - 1.0) > total_over_first) hi = q; else lo = q;
+	}
+	return 0.5*(lo+hi);
+}
+
+}
+
+/// C-grid round the NACA 0012 (the quadrangle C-grid of round 5). A sharp trailing edge
+/// in an O-grid either leaves the aft boundary layer as thin parallelograms (straight lines to the far
+/// field) or fans one trailing-edge point's cells over the whole wake (wall-normal lines); the C-grid's
+/// wake cut carries the boundary-layer spacing downstream instead. Columns i = 0 .. ni-1, ni = 2 nwake +
+/// nsurf + 1: the lower wake from the outflow to the trailing edge, the lower surface to the leading edge,
+/// the upper surface, the upper wake to the outflow; row 0 is the body and the cut (both wakes' row-0
+/// points are the same points), rows 1 .. nquad + ntri go out to a C boundary: a half circle of radius rfar
+/// round the trailing edge and the lines y = +-rfar to the outflow at x = 1 + rfar. Surface points are
+/// clustered at the leading edge (half-cosine) and, less, at the trailing edge (half of a full cosine); the
+/// wake spacing grows geometrically from the trailing-edge spacing. Wake lines run from the cut to the
+/// far field, where their spacing starts at the half circle's and grows to the outflow, leaving the cut
+/// vertically; a surface point's line leaves along the wall normal (turned vertical over the last tenth of the chord, parallel to
+/// the wake lines at the trailing edge) and bends onto the straight line to its far-field point (angles
+/// uniform in the surface parameter) by one chord (smoothstep). Rows grow geometrically from
+/// `wallspacing`. Quadrangles in the first nquad rows, triangles beyond. Markers: wall 2, far field 4.
+MeshData generateNacaCgrid(int nsurf, int nwake, int nquad, int ntri, double rfar, double wallspacing)
+{
+	if(nsurf < 8 || nsurf % 2 || nwake < 2) throw std::invalid_argument("nsurf must be even and >= 8, nwake >= 2");
+	const CgridMap map(nsurf, nwake, rfar);
+	const int nl = nquad + ntri, ni = map.ni;
 	// rows: geometric growth from the wall spacing over nl layers (normalised to the line length)
 	std::vector<double> eta(nl+1, 0.0);
 	{
-		const double target = rfar/wallspacing;
-		double lo = 1.0 + 1e-12, hi = 2.0;
-		for(int it = 0; it < 200; it++) {
-			const double q = 0.5*(lo+hi);
-			if((std::pow(q, nl) - 1.0)/(q - 1.0) > target) hi = q; else lo = q;
-		}
-		const double q = 0.5*(lo+hi);
+		const double q = rowGrowth(nl, rfar/wallspacing);
 		double acc = 0, d = 1.0;
 		for(int j = 1; j <= nl; j++) { acc += d; eta[j] = acc; d *= q; }
 		for(int j = 1; j <= nl; j++) eta[j] /= acc;
@@ -801,34 +865,11 @@ MeshData generateNacaCgrid(int nsurf, int nwake, int nquad, int ntri, double rfa
 	MeshData m;
 	m.npoin = n0 + nl*ni;
 	m.coords.resize(static_cast<size_t>(m.npoin)*2);
-	const double blend = 1.0;
 	for(int j = 0; j <= nl; j++)
 		for(int i = 0; i < ni; i++) {
 			if(j == 0 && i >= n0) continue;
-			double dx = fx[i] - sx[i], dy = fy[i] - sy[i];
-			const double L = std::sqrt(dx*dx + dy*dy);
-			const bool body = i > nwake && i < nwake + nsurf;
-			const bool te = i == nwake || i == nwake + nsurf;
-			if(!te && j > 0 && eta[j]*L < blend) {
-				double nx = 0.0, ny = fy[i] > 0 ? 1.0 : -1.0;           // wake: the cut's normal
-				if(body) {
-					nx = sy[i+1] - sy[i-1]; ny = -(sx[i+1] - sx[i-1]);
-					if(nx*dx + ny*dy < 0) { nx = -nx; ny = -ny; }
-					if(sx[i] > 0.9) {                               // the normal turns vertical at the trailing
-						const double g = (sx[i] - 0.9)/0.1;          // edge, parallel to the wake lines next to it
-						nx *= 1.0 - g*g*(3.0 - 2.0*g);
-					}
-				}
-				const double nn = std::sqrt(nx*nx + ny*ny);
-				const double x = eta[j]*L/blend;
-				const double w = x*x*(3.0 - 2.0*x);
-				const double ex = (1.0 - w)*nx/nn + w*dx/L, ey = (1.0 - w)*ny/nn + w*dy/L;
-				const double en = std::sqrt(ex*ex + ey*ey);
-				dx = L*ex/en; dy = L*ey/en;
-			}
 			const size_t p = static_cast<size_t>(P(i, j));
-			m.coords[2*p] = sx[i] + eta[j]*dx;
-			m.coords[2*p+1] = sy[i] + eta[j]*dy;
+			map.point(i, eta[j], m.coords[2*p], m.coords[2*p+1]);
 		}
 	// cells: (i,j) (i+1,j) (i+1,j+1) (i,j+1) counter-clockwise (i runs clockwise round the body, j outwards)
 	for(int j = 0; j < nl; j++)
@@ -857,6 +898,155 @@ MeshData generateNacaCgrid(int nsurf, int nwake, int nquad, int ntri, double rfa
 	auto bf = [&](int a, int b, int tag) { m.bface.insert(m.bface.end(), {a, b, tag, 1}); };
 	for(int i = nwake; i < nwake + nsurf; i++) bf(P(i,0), P(i+1,0), 2);
 	for(int i = 0; i < ni - 1; i++) bf(P(i+1,nl), P(i,nl), 4);
+	for(int j = 0; j < nl; j++) { bf(P(0,j+1), P(0,j), 4); bf(P(ni-1,j), P(ni-1,j+1), 4); }
+	m.nbface = static_cast<int>(m.bface.size()/4);
+	return m;
+}
+
+MeshData generateNacaHybrid(int nsurf, int nwake, int nquad, int nl, double rfar, double wallspacing)
+{
+	if(nsurf < 8 || nsurf % 2 || nwake < 2) throw std::invalid_argument("nsurf must be even and >= 8, nwake >= 2");
+	if(nquad < 1 || nquad >= nl) throw std::invalid_argument("need 1 <= nquad < nrows");
+	const CgridMap map(nsurf, nwake, rfar);
+	const int ni = map.ni, ib0 = nwake, ib1 = nwake + nsurf;      // the body's columns [ib0, ib1]
+	std::vector<double> eta(nl+1, 0.0);                            // generateNacaCgrid's rows
+	{
+		const double q = rowGrowth(nl, rfar/wallspacing);
+		double acc = 0, d = 1.0;
+		for(int j = 1; j <= nl; j++) { acc += d; eta[j] = acc; d *= q; }
+		for(int j = 1; j <= nl; j++) eta[j] /= acc;
+	}
+	MeshData m;
+	// C-grid points: every column of rows 0 .. nquad (row 0: the wake points shared), and above row nquad the
+	// wake blocks' columns [0, ib0] and [ib1, ni-1] (the trailing edge's columns included)
+	const int n0 = nwake + nsurf, nw = nwake + 1;
+	auto P = [&](int i, int j) {
+		if(j == 0) return i < n0 ? i : ni - 1 - i;
+		if(j <= nquad) return n0 + (j-1)*ni + i;
+		return n0 + nquad*ni + (j-nquad-1)*2*nw + (i <= ib0 ? i : nw + (i - ib1));
+	};
+	m.coords.resize(static_cast<size_t>(n0 + nquad*ni + (nl - nquad)*2*nw)*2);
+	for(int j = 0; j <= nl; j++)
+		for(int i = 0; i < ni; i++) {
+			if(j == 0 && i >= n0) continue;
+			if(j > nquad && i > ib0 && i < ib1) continue;
+			const size_t p = static_cast<size_t>(P(i, j));
+			map.point(i, eta[j], m.coords[2*p], m.coords[2*p+1]);
+		}
+	auto quad = [&](int i, int j) {
+		m.inpoel.insert(m.inpoel.end(), {P(i,j), P(i+1,j), P(i+1,j+1), P(i,j+1)});
+		m.nnode.push_back(4); m.nfael.push_back(4);
+	};
+	auto dist = [](double ax, double ay, double bx, double by) { return std::hypot(bx - ax, by - ay); };
+	auto ccw = [&](int p0, int p1, int p2) {
+		return (m.coords[2*p1] - m.coords[2*p0])*(m.coords[2*p2+1] - m.coords[2*p0+1])
+		     - (m.coords[2*p1+1] - m.coords[2*p0+1])*(m.coords[2*p2] - m.coords[2*p0]) > 0.0; };
+	auto tri = [&](int a, int b, int c) {
+		if(!ccw(a, b, c)) throw std::runtime_error("generateNacaHybrid: an inverted triangle");
+		m.inpoel.insert(m.inpoel.end(), {a, b, c, -1});
+		m.nnode.push_back(3); m.nfael.push_back(3);
+	};
+	// zips polylines A (inner) and B (outer) that run the same way, A[0]-B[0] and their last points joined by
+	// the trailing edge's columns: the region between them is cut into triangles, advancing along the one
+	// whose next diagonal is shorter unless that triangle would be inverted or leave an invalid fan to the
+	// other's end
+	auto zip = [&](const std::vector<int>& A, const std::vector<int>& B) {
+		const size_t M = A.size() - 1, N = B.size() - 1;
+		size_t a = 0, b = 0;
+		auto d = [&](int p, int q2) { return dist(m.coords[2*p], m.coords[2*p+1], m.coords[2*q2], m.coords[2*q2+1]); };
+		while(a < M || b < N) {
+			bool advA = a == M ? false : (b == N ? true : d(A[a+1], B[b]) < d(A[a], B[b+1]));
+			auto okA = [&]() {
+				if(!ccw(A[a], A[a+1], B[b])) return false;
+				if(a + 1 == M) for(size_t j = b; j < N; j++) if(!ccw(A[M], B[j+1], B[j])) return false;
+				return true; };
+			auto okB = [&]() {
+				if(!ccw(A[a], B[b+1], B[b])) return false;
+				if(b + 1 == N) for(size_t i = a; i < M; i++) if(!ccw(A[i], A[i+1], B[N])) return false;
+				return true; };
+			if(advA && b < N && !okA()) advA = false;
+			else if(!advA && a < M && !okB()) advA = true;
+			if(advA) { tri(A[a], A[a+1], B[b]); a++; }
+			else { tri(A[a], B[b+1], B[b]); b++; }
+		}
+	};
+	// cells row by row: the wake blocks' quadrangles in every row, the body's in rows below nquad, and above
+	// them the lower half of each body row (trailing edge to leading edge, both end points kept) resampled to
+	// its distance from the row below over 0.87 (equilateral triangles), within a factor 1.25 of the row
+	// below's spacing, and zipped to it; the upper half is its mirror image (y -> -y), so the mesh is
+	// symmetric about the chord line as the C-grid is (CL = 0 at alpha 0 up to rounding)
+	const double gam = 1.25;
+	const int ile = nwake + nsurf/2;                           // the leading edge's column (its own mirror)
+	std::vector<int> mir(m.coords.size()/2, -1);               // mirror image of every point
+	for(int j = 1; j <= nl; j++)
+		for(int i = 0; i < ni; i++) {
+			if(j > nquad && i > ib0 && i < ib1) continue;
+			mir[P(i, j)] = P(ni - 1 - i, j);
+		}
+	std::vector<int> below;                                    // the lower half of the body's row below
+	std::vector<double> bs;                                    // its nodes' column coordinates
+	for(int j = 0; j < nl; j++) {
+		for(int i = 0; i < ib0; i++) quad(i, j);
+		if(j < nquad) for(int i = ib0; i < ib1; i++) quad(i, j);
+		for(int i = ib1; i < ni - 1; i++) quad(i, j);
+		if(j + 1 == nquad) {
+			for(int i = ib0; i <= ile; i++) { below.push_back(P(i, nquad)); bs.push_back(i); }
+		}
+		if(j < nquad) continue;
+		// row j + 1 at the lower half's columns
+		const int nc = ile - ib0 + 1;
+		std::vector<double> cx(nc), cy(nc);
+		for(int i = 0; i < nc; i++) map.point(ib0 + i, eta[j+1], cx[i], cy[i]);
+		std::vector<double> phi(nc, 0.0);
+		size_t jb = 0;
+		for(int i = 0; i + 1 < nc; i++) {
+			const double sm = i + 0.5;
+			while(jb + 2 < bs.size() && bs[jb+1] - ib0 < sm) jb++;
+			const int pa = below[jb], pb = below[jb+1];
+			const double hp = dist(m.coords[2*pa], m.coords[2*pa+1], m.coords[2*pb], m.coords[2*pb+1]);
+			double bx0, by0, bx1, by1;
+			map.point(ib0 + i, eta[j], bx0, by0); map.point(ib0 + i + 1, eta[j], bx1, by1);
+			const double dl = 0.5*(dist(bx0, by0, cx[i], cy[i]) + dist(bx1, by1, cx[i+1], cy[i+1]));
+			const double h = std::min(std::max(dl/0.87, hp/gam), gam*hp);
+			phi[i+1] = phi[i] + dist(cx[i], cy[i], cx[i+1], cy[i+1])/h;
+		}
+		const int n = std::max(1, static_cast<int>(std::lround(phi.back())));
+		auto addPoint = [&](double x, double y) {
+			m.coords.push_back(x); m.coords.push_back(y); mir.push_back(-1);
+			return static_cast<int>(m.coords.size()/2) - 1;
+		};
+		std::vector<int> row(n + 1);
+		std::vector<double> rs(n + 1);
+		row[0] = P(ib0, j+1); rs[0] = ib0;
+		row[n] = addPoint(cx[nc-1], cy[nc-1]); rs[n] = ile;
+		mir[row[n]] = row[n];
+		for(int a2 = 1, i = 0; a2 < n; a2++) {
+			const double target = phi.back()*a2/n;
+			while(phi[i+1] < target) i++;
+			const double f = (target - phi[i])/(phi[i+1] - phi[i]);
+			row[a2] = addPoint(cx[i] + f*(cx[i+1] - cx[i]), cy[i] + f*(cy[i+1] - cy[i])); rs[a2] = ib0 + i + f;
+			const int q = addPoint(m.coords[2*row[a2]], -m.coords[2*row[a2]+1]);
+			mir[row[a2]] = q; mir[q] = row[a2];
+		}
+		const size_t t0 = m.nnode.size();
+		zip(below, row);
+		const size_t t1 = m.nnode.size();
+		for(size_t t = t0; t < t1; t++) {                      // the upper half: mirrored, orientation restored
+			const int* e = &m.inpoel[4*t];
+			tri(mir[e[0]], mir[e[2]], mir[e[1]]);
+		}
+		below.swap(row); bs.swap(rs);
+	}
+	m.npoin = static_cast<int>(m.coords.size()/2);
+	m.nnofa = 2; m.nbtag = 2; m.ndtag = 2;
+	m.nelem = static_cast<int>(m.nnode.size());
+	m.maxnnode = 4; m.maxnfael = 4;
+	m.vol_regions.assign(static_cast<size_t>(m.nelem)*2, 1);
+	auto bf = [&](int a, int b, int tag) { m.bface.insert(m.bface.end(), {a, b, tag, 1}); };
+	for(int i = ib0; i < ib1; i++) bf(P(i,0), P(i+1,0), 2);
+	for(int i = 0; i < ib0; i++) bf(P(i+1,nl), P(i,nl), 4);
+	for(size_t a = 0; a + 1 < below.size(); a++) { bf(below[a+1], below[a], 4); bf(mir[below[a]], mir[below[a+1]], 4); }
+	for(int i = ib1; i < ni - 1; i++) bf(P(i+1,nl), P(i,nl), 4);
 	for(int j = 0; j < nl; j++) { bf(P(0,j+1), P(0,j), 4); bf(P(ni-1,j), P(ni-1,j+1), 4); }
 	m.nbface = static_cast<int>(m.bface.size()/4);
 	return m;

@@ -86,6 +86,12 @@ Mesh restrictMesh(const Mesh& gm, const int* elemdist, int rank);
 /// Cells: ntheta*(nquad + 2*ntri).
 MeshData generateNacaOgrid(int ntheta, int nquad, int ntri, double rfar, double wallspacing, int farmap = 0);
 MeshData generateNacaCgrid(int nsurf, int nwake, int nquad, int ntri, double rfar, double wallspacing);
+/// Hybrid mesh of the reference's visc-naca0012 topology (naca0012nasa-blcirc.geo: a quadrangle block
+/// round the body, triangles outside it): generateNacaCgrid's points with nrows rows; quadrangles in the
+/// body's first nquad rows (the boundary layer) and in the two wake blocks, near-isotropic triangles above
+/// the body's quadrangles: each row there resampled to its distance from the row below (over 0.87, the
+/// equilateral triangle's height), within a factor 1.25 of the row below's spacing, and zipped to it.
+MeshData generateNacaHybrid(int nsurf, int nwake, int nquad, int nrows, double rfar, double wallspacing);
 
 /// Synthetic O-grid annulus about a cylinder of radius r0 out to r1, all quads split into
 /// triangles (2dcylinder-like). Inner marker 2, outer marker 4. Cells 2*ntheta*nr.

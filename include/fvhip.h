@@ -308,6 +308,17 @@ typedef struct fvhip_implicit_config {
 	                             (PETSc's default, KSP_GMRES_CGS_REFINE_NEVER: one projection per Arnoldi step,
 	                             the new vector's norm computed from the projected vector), 1 = ifneeded (a second
 	                             projection when the first removed more than half of |w|^2, DGKS), 2 = always */
+	int prec_amg;             /* >= 2: aggregation multigrid with this many levels (mgopts.solverc: -pc_type gamg
+	                             -pc_gamg_type agg -pc_gamg_agg_nsmooths 0 -pc_mg_levels 3 -pc_mg_cycle_type v),
+	                             one V-cycle per application: the one-level preconditioner (prec_lines, else
+	                             point-block Jacobi) as the finest smoother, multicolour block Gauss-Seidel on the
+	                             coarse levels; the coarse operators are the Galerkin sums over cell aggregates,
+	                             rebuilt from every assembled Jacobian. 0: off */
+	int amg_sweeps;           /* smoothing sweeps before and after the coarse correction on each level
+	                             (-mg_levels_ksp_max_it; 0: the deck's 2) */
+	int amg_coarse_sweeps;    /* Gauss-Seidel sweeps on the coarsest level (-mg_coarse_ksp_max_it; 0: the deck's 6) */
+	double amg_threshold;     /* two cells aggregate when their coupling (face length / centre distance) is at least
+	                             this fraction of both cells' strongest (-pc_gamg_threshold; 0: the deck's 0.2) */
 } fvhip_implicit_config;
 
 typedef struct fvhip_solve_stats {
@@ -358,7 +369,9 @@ int fvhip_lines(fvhip_handle h, double line_threshold, int* nlines, int* start, 
 int fvhip_matfree_set_state(fvhip_handle h, const double* u, const double* r, const double* mdt);
 int fvhip_matfree_apply(fvhip_handle h, const double* x, double* y);
 /** Device variants (internal order). set_state keeps the pointers, as the reference keeps the Vecs.
- *  On a partitioned handle |x| is the global norm and d_u needs room for the ghost rows. */
+ *  On a partitioned handle |x| is the global norm and d_u needs room for the ghost rows. d_y may alias any
+ *  input: the one-launch operator (the residual kernel with the perturbation and the combination fused in)
+ *  runs only when d_y shares no byte with d_x or the state d_u, else the three-launch operator does. */
 int fvhip_matfree_set_state_device(fvhip_handle h, const double* d_u, const double* d_r, const double* d_mdt);
 int fvhip_matfree_apply_device(fvhip_handle h, const double* d_x, double* d_y);
 int fvhip_group_matfree_set_state_device(fvhip_group g, const double* const* d_u, const double* const* d_r,
@@ -421,6 +434,13 @@ int fvmesh_read_gmsh(const char* path, fvmesh_handle* out);
  *        3 = NACA 0012 C-grid (a=nsurf, b=nquad, c=ntri, x=rfar, y=wall spacing, z=nwake: columns along
  *            each wake; 2 nwake + nsurf columns of cells) */
 int fvmesh_generate(int kind, int a, int b, int c, double x, double y, double z, fvmesh_handle* out);
+/** NACA 0012 hybrid mesh of the visc-naca0012 grids' topology (testcases/visc-naca0012/grids/
+ *  naca0012nasa-blcirc.geo, NACA0012_lam_hybrid_1.msh: a quadrangle block round the body, triangles
+ *  outside it): the C-grid of kind 3 with nrows rows; quadrangles in the body's first nquad rows (the
+ *  boundary layer) and in the two wake blocks (nwake columns each), near-isotropic triangles above the
+ *  body's quadrangles out to the far field (radius rfar). Wall marker 2, far field 4. */
+int fvmesh_generate_hybrid(int nsurf, int nwake, int nquad, int nrows, double rfar,
+                           double wallspacing, fvmesh_handle* out);
 int fvmesh_write_gmsh(fvmesh_handle m, const char* path);
 int fvmesh_destroy(fvmesh_handle m);
 /** TrivialReplicatedGlobalMeshPartitioner::compute_partition (meshpartitioning.cpp:354-367): cell i

@@ -1,6 +1,7 @@
 """bench.py's guarded implicit section on N ranks (CPU, gloo, world size 2): the ranks agree on an error
 raised on one of them, and a rank stuck in a collective (its peer failed before joining) cannot lose the
-measurement -- at the deadline rank 0 prints the line with the error and every process exits."""
+measurement -- at the deadline rank 0 prints the line with the error and every process exits with
+bench.GUARD_EXIT (not 0: the run did not finish)."""
 import json
 import os
 import subprocess
@@ -59,8 +60,10 @@ def _run(mode, tmp_path):
 @pytest.mark.parametrize("mode", ["ok", "raise", "hang"])
 def test_guarded_implicit(mode, tmp_path):
     sys.path.insert(0, ROOT)
+    import bench
     codes, outs = _run(mode, tmp_path)
-    assert codes == [0, 0], [o[1][-1500:] for o in outs]
+    want = bench.GUARD_EXIT if mode == "hang" else 0
+    assert codes == [want, want], (codes, [o[1][-1500:] for o in outs])
     lines = [json.loads(l) for l in outs[0][0].splitlines() if l.startswith("{")]
     assert len(lines) == 1, outs[0]
     d = lines[0]

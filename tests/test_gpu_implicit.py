@@ -99,12 +99,20 @@ def test_gmres_blocks_matches_direct_solve():
     dev.close()
 
 
-@pytest.mark.parametrize("min_relax,single,gs,lines,ilu", [(1.0, False, False, False, False), (0.2, False, False, False, False),
-                                                           (1.0, True, False, False, False), (1.0, False, True, False, False),
-                                                           (1.0, True, True, False, False), (1.0, False, False, True, False),
-                                                           (1.0, False, False, False, True), (1.0, True, False, False, True),
-                                                           (1.0, True, False, True, False)])
-def test_one_backward_euler_step_matches_host(min_relax, single, gs, lines, ilu):
+@pytest.mark.parametrize("min_relax,single,gs,lines,ilu,amg,refine", [
+    (1.0, False, False, False, False, 0, 1), (0.2, False, False, False, False, 0, 1),
+    (1.0, True, False, False, False, 0, 1), (1.0, False, True, False, False, 0, 1),
+    (1.0, True, True, False, False, 0, 1), (1.0, False, False, True, False, 0, 1),
+    (1.0, False, False, False, True, 0, 1), (1.0, True, False, False, True, 0, 1),
+    (1.0, True, False, True, False, 0, 1),
+    # PETSc's default Gram-Schmidt (one projection, the bench's and the drivers' default) and always-twice
+    (1.0, False, False, True, False, 0, 0), (1.0, False, False, False, False, 0, 2),
+    # aggregation multigrid (mgopts.solverc): line-implicit or point-block Jacobi finest smoother, 2 / 3 levels
+    (1.0, False, False, True, False, 3, 0), (1.0, False, False, False, False, 3, 1), (1.0, False, False, True, False, 2, 0)])
+def test_one_backward_euler_step_matches_host(min_relax, single, gs, lines, ilu, amg, refine):
+    """one implicit step against the host restatement (oracle residual and Jacobian, scipy's direct solve,
+    the relaxed update) with every preconditioner and Gram-Schmidt variant: GMRES at rtol 1e-13 must land on
+    the direct solution (the preconditioner only changes the path)"""
     m, om = get_mesh("naca_small")
     p = cases.physics("naca")
     n = cases.numerics("ROE", "LEASTSQUARES", "VANALBADA")
@@ -117,9 +125,9 @@ def test_one_backward_euler_step_matches_host(min_relax, single, gs, lines, ilu)
     dev = fa.FlowFV(m, p, n)
     perm = dev.permutation()
     dU = to_device(u0, perm)
-    cfg = fa.ImplicitConfig(cgs_refine=1, cflinit=cfl, cflfin=cfl, tol=0.0, maxiter=1, lin_rtol=1e-13, lin_maxit=3000, restart=60,
-                            prec_sweeps=2, min_relax=min_relax, prec_single=single, prec_gs=gs, prec_lines=lines,
-                            prec_ilu=ilu)
+    cfg = fa.ImplicitConfig(cgs_refine=refine, cflinit=cfl, cflfin=cfl, tol=0.0, maxiter=1, lin_rtol=1e-13, lin_maxit=3000,
+                            restart=60, prec_sweeps=1 if amg else 2, min_relax=min_relax, prec_single=single, prec_gs=gs,
+                            prec_lines=lines, prec_ilu=ilu, prec_amg=amg)
     st, hist = dev.steady_backward_euler_device(dU.data_ptr(), cfg)
     assert st["steps"] == 1 and st["cfl"] == cfl
     u = np.empty_like(u0)

@@ -74,8 +74,11 @@ def _check_vs_oracle(m, p, n, u):
 
 
 def test_c5_residual_full_size():
-    m = fa.UMesh.naca_cgrid(3072, 512, 1984, 0, 20.0, 1e-5)         # bench.py --numerics config5's mesh
-    assert m.nelem == 8126464 and m.naface == 16258496
+    from bench import c4_mesh
+    m, dims = c4_mesh(fa, 1, 2)                     # bench.py --numerics config5's mesh: the hybrid C5
+    assert dims["topology"] == "hybrid"
+    assert m.nelem == 8054616 and m.naface == 14052288
+    assert (m.nnode == 3).sum() == 4122456 and (m.nnode == 4).sum() == 3932160
     p = cases.physics("visc")
     n = cases.numerics("ROE", "LEASTSQUARES", "NONE")
     _check_vs_oracle(m, p, n, cases.state(m, p, seed=42))

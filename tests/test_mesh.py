@@ -40,6 +40,7 @@ def test_gmsh_fixture_indexing(name):
     lambda: fa.UMesh.naca_ogrid(256, 16, 54, 20.0, 1e-5, farmap=3),
     lambda: fa.UMesh.naca_cgrid(96, 16, 8, 24, 20.0, 1e-5),
     lambda: fa.UMesh.naca_cgrid(96, 16, 62, 0, 20.0, 1e-5),
+    lambda: fa.UMesh.naca_hybrid(96, 12, 24, 64, 20.0, 1e-5),
     lambda: fa.UMesh.cylinder_ogrid(48, 12),
     lambda: fa.UMesh.flat_plate(40, 24),
 ])
@@ -145,6 +146,58 @@ def test_naca_cgrid():
     # the first row's points lie ~1e-5 off the wall, the cut's cells are thin (row 1 at 1e-5 above the cut)
     wall = np.where(tags == 2)[0]
     assert np.abs(m.gr[wall] - m.rc[m.intfac[wall, 0]]).max() < 1e-4
+
+
+def _triangle_shapes(m):
+    tri = np.where(m.nnode == 3)[0]
+    P = m.coords[m.inpoel[tri, :3]]
+    e = np.stack([P[:, 1] - P[:, 0], P[:, 2] - P[:, 1], P[:, 0] - P[:, 2]], 1)
+    L = np.linalg.norm(e, axis=2)
+    area = 0.5 * np.abs(e[:, 0, 0] * e[:, 1, 1] - e[:, 0, 1] * e[:, 1, 0])
+    c = [np.einsum("ij,ij->i", -e[:, (k + 2) % 3], e[:, k]) / (L[:, (k + 2) % 3] * L[:, k]) for k in range(3)]
+    return L.max(1) ** 2 / (2 * area), np.degrees(np.arccos(np.clip(np.min(np.stack(c, 1), 1), -1, 1)))
+
+
+def test_naca_hybrid():
+    """generateNacaHybrid, the C5 family since round 6 (BASELINE config 5's hybrid mesh, the topology of
+    testcases/visc-naca0012/grids/naca0012nasa-blcirc.geo: quadrangles through the boundary layer, triangles
+    outside it): the C-grid's points, quadrangles in the body's first nquad rows and in both wake blocks,
+    near-isotropic triangles above the body's quadrangles, mirror-symmetric about the chord line. The 1/8-size
+    member (bench.c4_mesh(fa, 8, 2)): cell and boundary counts, positive cells, the triangles' shape (longest
+    edge over its height <= 6 on 99 %), no skewed boundary-layer
+    quadrangle, and the mirror image of every cell centre is a cell centre with the same area. (The small
+    members' boundary layer is thinner in chords -- the same 1e-5 wall spacing over fewer rows -- so their
+    first triangle rows over mid-chord are flatter: longest edge over height up to 10 at 1/8 size against 3.2
+    at full size, test_naca_hybrid_full_size_shape.)"""
+    ns, nw, nq, nr = 384, 48, 96, 256
+    m = fa.UMesh.naca_hybrid(ns, nw, nq, nr, 20.0, 1e-5)
+    nquads = ns * nq + 2 * nw * nr
+    assert (m.nnode == 4).sum() == nquads and (m.nnode == 3).sum() > nquads
+    tags = m.btags[:, 0] if m.btags.ndim > 1 else m.btags
+    assert (tags == 2).sum() == ns
+    assert (m.area > 0).all()
+    assert m.naface == (4 * (m.nnode == 4).sum() + 3 * (m.nnode == 3).sum() + m.nbface) // 2
+    asp, ang = _triangle_shapes(m)
+    assert np.percentile(asp, 99) <= 6.0 and asp.max() <= 12.0, (np.percentile(asp, 99), asp.max())
+    q, d = _quad_skew(m)
+    bl = (m.rc[q, 0] < 1.0) & (np.abs(m.rc[q, 1]) < 0.1)        # the body's boundary layer
+    assert d[bl].max() < 10.0, d[bl].max()
+    a = np.round(m.rc[:m.nelem], 9)
+    b = a * np.array([1.0, -1.0])
+    ka, kb = np.lexsort((a[:, 1], a[:, 0])), np.lexsort((b[:, 1], b[:, 0]))
+    assert np.array_equal(a[ka], b[kb])
+    assert np.abs(m.area[ka] - m.area[kb]).max() <= 1e-12 * m.area.max()
+
+
+def test_naca_hybrid_full_size_shape():
+    """BASELINE config 5's mesh (bench.c4_mesh(fa, 1, 2)): 8,054,616 cells, 4,122,456 of them triangles, whose
+    longest edge over its height is at most 3.2 (2.66 at the 99.9th percentile; an equilateral triangle's is
+    1.15, a right isosceles one's 2) and whose largest angle is at most 113 degrees."""
+    from bench import c4_mesh
+    m, dims = c4_mesh(fa, 1, 2)
+    assert dims["topology"] == "hybrid" and m.nelem == 8054616 and (m.nnode == 3).sum() == 4122456
+    asp, ang = _triangle_shapes(m)
+    assert asp.max() <= 3.2 and np.percentile(asp, 99.9) <= 2.7 and ang.max() <= 113.0, (asp.max(), ang.max())
 
 
 def test_gmsh_roundtrip(tmp_path):

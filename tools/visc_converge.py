@@ -25,19 +25,14 @@ sys.path.insert(0, os.path.join(ROOT, "tests"))
 
 def run(scale=1, matrix_free=True, main_steps=400, init_steps=50, lin_maxit=60, restart=60, sweeps=3,
         tol=1e-6, heartbeat=None, cfl_init=(200.0, 1000.0), cfl_main=(500.0, 5000.0), min_relax=1.0, lin_rtol=1e-1,
-        wall=None, mf_eps=None, quads=False):
+        wall=None, mf_eps=None, quads=False, amg=0, amg_sweeps=2, amg_coarse=6, amg_thr=0.2, lines=True):
     """the deck's two stages on the C5 mesh divided by `scale` in both directions; returns the record (a stage
     that diverges is recorded with its history and the error; the later stage is then skipped)"""
     import torch
     import fvens_amd as fa
     import cases
     from bench import c4_mesh
-    if quads:                                   # the C-grid without triangle rows (quadrangles throughout)
-        ws = wall or 1e-5
-        mesh = fa.UMesh.naca_cgrid(3072 // scale, 512 // scale, 1984 // scale, 0, 20.0, ws)
-        dims = {"topology": "C-grid, quadrangles only", "wall_spacing": ws}
-    else:
-        mesh, dims = c4_mesh(fa, scale, 2, wall=wall)
+    mesh, dims = c4_mesh(fa, scale, 2, wall=wall, topology="cgrid" if quads else "hybrid")
     p = cases.physics("visc")                                   # alpha 0 (laminar-implicit.ctrl:19)
     n1 = cases.numerics("ROE", "NONE", "NONE", order2=False)
     n2 = cases.numerics("ROE", "LEASTSQUARES", "NONE")          # limiter none (:72)
@@ -47,8 +42,9 @@ def run(scale=1, matrix_free=True, main_steps=400, init_steps=50, lin_maxit=60, 
         main.matfree_set_eps(mf_eps)          # -matrix_free_difference_step (alinalg.cpp:127)
     du = torch.tensor(np.tile(cases.freestream(p), (mesh.nelem, 1))[perm], device="cuda")
     torch.cuda.synchronize()      # torch's stream vs the library's (non-blocking) streams
-    lin = dict(lin_rtol=lin_rtol, lin_maxit=lin_maxit, restart=restart, prec_lines=True, prec_sweeps=sweeps,
-               min_relax=min_relax)
+    lin = dict(lin_rtol=lin_rtol, lin_maxit=lin_maxit, restart=restart, prec_lines=lines, prec_sweeps=sweeps,
+               min_relax=min_relax, prec_amg=amg, amg_sweeps=amg_sweeps, amg_coarse_sweeps=amg_coarse,
+               amg_threshold=amg_thr)
     rec = {"library": fa._ffi.build_info()["lib_src_hash"], "cells": mesh.nelem, "faces": mesh.naface, "dims": dims, "operator": "matrix-free" if matrix_free else "assembled",
            "linear": dict(lin, gmres="GMRES(%d) right-preconditioned" % restart), "cfl_init": list(cfl_init),
            "cfl_main": list(cfl_main)}
@@ -109,15 +105,22 @@ def main():
     ap.add_argument("--min-relax", type=float, default=1.0, help=">= 1: full update (the deck), else robust_flow")
     ap.add_argument("--lin-rtol", type=float, default=1e-1)
     ap.add_argument("--wall", type=float, default=None, help="first-cell wall spacing (default: the C5 mesh's 1e-5)")
-    ap.add_argument("--quads", action="store_true", help="the C-grid with quadrangles in every row")
+    ap.add_argument("--quads", action="store_true", help="round 5's quadrangle C-grid instead of the hybrid mesh")
     ap.add_argument("--mf-eps", type=float, default=None, help="matrix-free difference step (default 1e-7)")
+    ap.add_argument("--amg", type=int, default=0, help="aggregation multigrid levels (0: the one-level preconditioner)")
+    ap.add_argument("--amg-sweeps", type=int, default=2)
+    ap.add_argument("--amg-coarse", type=int, default=6)
+    ap.add_argument("--amg-thr", type=float, default=0.2)
+    ap.add_argument("--no-lines", action="store_true", help="point-block Jacobi instead of the line-implicit preconditioner")
     ap.add_argument("--tag", default="")
     args = ap.parse_args()
     import torch
     torch.cuda.set_device(0)
     r = run(args.scale, not args.assembled, args.main_steps, init_steps=args.init_steps, lin_maxit=args.lin_maxit, restart=args.restart,
             sweeps=args.sweeps, heartbeat=lambda s: print(s, flush=True), cfl_init=args.cfl_init,
-            cfl_main=args.cfl_main, min_relax=args.min_relax, lin_rtol=args.lin_rtol, wall=args.wall, mf_eps=args.mf_eps, quads=args.quads)
+            cfl_main=args.cfl_main, min_relax=args.min_relax, lin_rtol=args.lin_rtol, wall=args.wall, mf_eps=args.mf_eps, quads=args.quads,
+            amg=args.amg, amg_sweeps=args.amg_sweeps, amg_coarse=args.amg_coarse, amg_thr=args.amg_thr,
+            lines=not args.no_lines)
     r["tag"] = args.tag
     print(json.dumps(r), flush=True)
 
