@@ -185,23 +185,8 @@ struct fvhip_ctx
 	std::vector<Rec> recs;
 	std::map<std::string, std::pair<double,int>> acc;
 
-#ifdef FVHIP_PROBE_PHASES
-	unsigned long long* d_probe = nullptr;
-	/// diagnostic build: the phase stamps of the last fused launch to $FVHIP_PROBE_OUT (raw u64 [blocks][8])
-	void dumpProbe() {
-		const char* path = getenv("FVHIP_PROBE_OUT");
-		if(!d_probe || !path) return;
-		std::vector<unsigned long long> h(8*(L.patch_cell.size() + 16));
-		(void)hipStreamSynchronize(stream);
-		(void)hipMemcpy(h.data(), d_probe, h.size()*sizeof(unsigned long long), hipMemcpyDeviceToHost);
-		if(FILE* f = fopen(path, "wb")) { fwrite(h.data(), sizeof(unsigned long long), h.size(), f); fclose(f); }
-	}
-#endif
 	~fvhip_ctx() {
 		(void)hipSetDevice(device);
-#ifdef FVHIP_PROBE_PHASES
-		dumpProbe();
-#endif
 		if(comm) (void)ncclCommDestroy(comm);
 		for(auto& r : recs) { (void)hipEventDestroy(r.a); (void)hipEventDestroy(r.b); }
 		for(hipEvent_t e : pipe_ev) (void)hipEventDestroy(e);
@@ -352,10 +337,6 @@ struct fvhip_ctx
 		B.grad = d_grad;     // received gradients of ghost cells (partitioned meshes)
 		if(limited()) B.phi = d_phi;   // layer-1 ghosts' limiter values (two-layer halo)
 		B.mfx = mfz.x; B.mfpm = mfz.pm; B.mfres = mfz.res; B.mfmdt = mfz.mdt;
-#ifdef FVHIP_PROBE_PHASES
-		if(!d_probe) d_probe = static_cast<unsigned long long*>(static_cast<void*>(dalloc(8*(static_cast<size_t>(L.patch_cell.size()) + 16), owned)));
-		B.probe = d_probe;
-#endif
 		const char* nm = nullptr;
 		timed_on(st, "k_residual_wls", [&]{ nm = KOPS(launch_residual_wls)(M, P, B, cfg.conv_numflux, recKind(), viscKind(),
 		                                                                       limKind(), dt, st); });

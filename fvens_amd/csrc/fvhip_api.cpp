@@ -103,7 +103,6 @@ static fvhip_ctx* createCtx(const MeshTopo& T, const fvhip_flow_config* cfg, int
 	M.slot_n = reinterpret_cast<const double2*>(upload(L.slot_n, o));
 	M.slot_len = upload(L.slot_len, o);
 	M.slot_gr = reinterpret_cast<const double2*>(upload(L.slot_gr, o));
-	M.slot_vg = L.slot_vg.empty() ? nullptr : reinterpret_cast<const double4*>(upload(L.slot_vg, o));
 	M.cell_slots = reinterpret_cast<const int4*>(upload(L.cell_slots, o));
 	M.cell_nbr = reinterpret_cast<const int4*>(upload(L.cell_nbr_local, o));
 	M.cell_face = reinterpret_cast<const int4*>(upload(L.cell_face_local, o));

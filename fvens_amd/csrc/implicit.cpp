@@ -543,6 +543,12 @@ static void backwardEuler(System& S, const std::vector<double*>& us, const fvhip
 
 	double curCFL = 0, resi = 1.0, resiold = 1.0, initres = 1.0, linworst = 0.0;
 	int step = 0, lin = 0, linbad = 0;
+	const bool resume = c.resume_res0 > 0.0;
+	if(resume) {                     // a checkpointed solve: its residuals and CFL, the ramp continues from them
+		if(!(c.resume_res > 0.0 && c.resume_res_prev > 0.0 && c.resume_cfl > 0.0))
+			throw std::invalid_argument("resume: the last residual, the one before and the last CFL must be positive");
+		initres = c.resume_res0; resi = c.resume_res; resiold = c.resume_res_prev; curCFL = c.resume_cfl;
+	}
 	while(resi/initres > c.tol && step < c.maxiter) {
 		// r = 0 + (-r(u)) with local time steps (:421-452); fills the ghost rows of u
 		fvhip_ctx::residual_seq(S.hs, cu, rs, true, dts, true, S.exg);
@@ -567,7 +573,7 @@ static void backwardEuler(System& S, const std::vector<double*>& us, const fvhip
 		resi = std::sqrt(S.allsum(1, false)[0]);                                                    // :528-530
 		if(!std::isfinite(resi))
 			throw std::runtime_error("Steady backward Euler diverged - residual is Nan or inf!");  // :533-534
-		if(step == 0) initres = resi;
+		if(step == 0 && !resume) initres = resi;
 		step++;
 		if(hist) hist[step-1] = resi;
 	}

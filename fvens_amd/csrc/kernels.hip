@@ -175,17 +175,8 @@ __global__ void __launch_bounds__(256) k_grad_wls(DevMesh M, const double* __res
 /// the factor 2, and dp*dm is formed once for numerator and denominator; the running max / min are
 /// v_max / v_min -- they differ from the reference's compare-and-assign only in the sign of a zero
 /// dmin/dmax (max(+0, -0)), and a signed zero dp gives the same phi (dp*dp = +0, +0 + (+-0) = +0).
-/// FVHIP_VENK_ONEDIV (A/B experiment, off by default): one division per variable instead of one per face: the reference keeps lim = min(1, min_j RN(n_j/d_j))
-/// (`if(phiik < lim)`, NaN never taken), and rounding is monotone, so that is RN(min(1, min_j n_j/d_j)):
-/// the faces' numerators and denominators are compared exactly -- n/d < bn/bd iff n*bd < bn*d for positive
-/// denominators, decided by the rounded products and, where those tie, by their exact residuals
-/// fma(a, b, -RN(ab)) -- and only the winner is divided (the start 1/1 divides to 1 exactly). dp has dm's
-/// sign (dmin <= 0 <= dmax), so dp*dm >= 0 and n, d >= eps2 > 0; a NaN n or d compares false and is never
-/// taken, as in the reference. Exact while the products stay normal, |n|, |d| in [2^-480, 2^500]
-/// (eps2 = (K clength)^3 with K = 20: clength > 1e-48).
-#ifndef FVHIP_VENK_ONEDIV
-#define FVHIP_VENK_ONEDIV 0
-#endif
+/// (A one-division-per-variable variant -- exact arg-min by cross-multiplication, only the winner divided --
+/// was bitwise but 1.2-1.7 % slower: DESIGN.md section 8, profiles/r05/venk_onediv_ab.txt.)
 template <bool VENK>
 __device__ __forceinline__ void cell_limiter(const double* uc, const double* g, const double (*un)[4],
                                              const double2* gp, const bool* has, double2 r, double eps2,
@@ -205,7 +196,6 @@ __device__ __forceinline__ void cell_limiter(const double* uc, const double* g, 
 			}
 		}
 		double lim = 1.0;
-		double bn = 1.0, bd = 1.0;     // Venkatakrishnan: the smallest quotient so far, 1/1 at the start
 		#pragma unroll
 		for(int j = 0; j < 4; j++) {
 			if(!has[j]) continue;
@@ -219,12 +209,7 @@ __device__ __forceinline__ void cell_limiter(const double* uc, const double* g, 
 				const double pp = dp*dp, pm = dp*dm;
 				// (dp*dp + 2*dp*dm + eps2)/(dp*dp + dp*dm + 2*dm*dm + eps2)
 				const double n = __builtin_fma(pm, 2.0, pp) + eps2, d = __builtin_fma(dm*dm, 2.0, pp + pm) + eps2;
-				if(FVHIP_VENK_ONEDIV) {
-					const double p1 = n*bd, p2 = bn*d;
-					bool lt = p1 < p2;
-					if(p1 == p2) lt = __builtin_fma(n, bd, -p1) < __builtin_fma(bn, d, -p2);
-					if(lt) { bn = n; bd = d; }
-				} else lim = __builtin_fmin(lim, div_rn(n, d));
+				lim = __builtin_fmin(lim, div_rn(n, d));
 				continue;
 			} else {
 				const double diff = uf - uc[iv];
@@ -234,7 +219,7 @@ __device__ __forceinline__ void cell_limiter(const double* uc, const double* g, 
 			}
 			if(ph < lim) lim = ph;
 		}
-		out[iv] = VENK && FVHIP_VENK_ONEDIV ? div_rn(bn, bd) : lim;
+		out[iv] = lim;
 	}
 }
 
@@ -924,27 +909,20 @@ __device__ __forceinline__ void stage_row(const Gas& G, double* row, const doubl
 	*reinterpret_cast<double2*>(row + 12) = r;
 }
 
-/// FVHIP_FZ_WLSV = 1: the fused residual rebuilds each cell's WLS inverse from the staged centres it
-/// already reads instead of loading the precomputed one (32 B per gradient row less traffic)
-#ifndef FVHIP_FZ_WLSV
-#define FVHIP_FZ_WLSV 1
-#endif
-/// one neighbour's term of the WLS normal matrix, V[2i+j] += w2*dr[i]*dr[j] (agradientschemes.cpp:
+/// The fused residual rebuilds each cell's WLS inverse from the staged centres it already reads instead of
+/// loading the precomputed one (32 B per gradient row less traffic).
+/// One neighbour's term of the WLS normal matrix, V[2i+j] += w2*dr[i]*dr[j] (agradientschemes.cpp:
 /// 218-317 as restated in layout.cpp: w2*dr[i] first, then times dr[j])
 __device__ __forceinline__ void wls_normal_add(double* vm, double w2, double d0, double d1)
 {
-#if FVHIP_FZ_WLSV
 	const double a = w2*d0, b = w2*d1;
 	vm[0] += a*d0; vm[1] += a*d1; vm[2] += b*d0; vm[3] += b*d1;
-#endif
 }
 /// the first neighbour's term, 0 + w2*dr[i]*dr[j] (mul0)
 __device__ __forceinline__ void wls_normal_first(double* vm, double w2, double d0, double d1)
 {
-#if FVHIP_FZ_WLSV
 	const double a = w2*d0, b = w2*d1;
 	vm[0] = mul0(a, d0); vm[1] = mul0(a, d1); vm[2] = mul0(b, d0); vm[3] = mul0(b, d1);
-#endif
 }
 /// its inverse, the host's 2x2 inverse arithmetic (layout.cpp, Eigen's inverse for 2x2)
 __device__ __forceinline__ double4 wls_inverse(const double* v)
@@ -986,7 +964,7 @@ __device__ __forceinline__ void fz_row_temperature(const Gas& G, double* row, co
 }
 template <int LIM, int W = FZW, bool MF = false>
 __device__ __forceinline__ void fused_wls_row(const DevMesh& M, const DevPhys& P, const SweepBuffers& B,
-                                              const double* fz, double* row, int c, int4 nb4, double4 V,
+                                              const double* fz, double* row, int c, int4 nb4,
                                               const double2* gp = nullptr, double eps2 = 0.0)
 {
 	static_assert(!(LIM && W == FZW_VISC), "limited reconstructions are not fused with the viscous flux");
@@ -1009,7 +987,7 @@ __device__ __forceinline__ void fused_wls_row(const DevMesh& M, const DevPhys& P
 	ld4(row, 0, uc);
 	const double2 rcc = *reinterpret_cast<const double2*>(row + 12);
 	double f[8] = {0,0,0,0,0,0,0,0};
-	double vm[4] = {0, 0, 0, 0};     // WLS normal matrix (FVHIP_FZ_WLSV), same terms and order as the host's
+	double vm[4] = {0, 0, 0, 0};     // WLS normal matrix, same terms and order as the host's
 	if(nb4.x >= 0 && nb4.y >= 0 && nb4.z >= 0 && nb4.w >= -1) {
 		// no boundary neighbour (all but ~0.1 % of the rows): every neighbour is an LDS row. The
 		// first three (every triangle and quad has them) are requested at once and their weights
@@ -1095,18 +1073,14 @@ __device__ __forceinline__ void fused_wls_row(const DevMesh& M, const DevPhys& P
 		}
 		wls_normal_add(vm, w2, dr0, dr1);
 	}
-#if FVHIP_FZ_WLSV
-	V = wls_inverse(vm);
-#endif
+	const double4 V = wls_inverse(vm);
 	double g[8];
 	#pragma unroll
 	for(int iv = 0; iv < 4; iv++) {
 		g[iv*2+0] = V.x*f[iv*2+0] + V.y*f[iv*2+1];
 		g[iv*2+1] = V.z*f[iv*2+0] + V.w*f[iv*2+1];
 	}
-#ifndef FVHIP_PROBE_NOLIM
 	if(LIM) fused_limit_row<LIM, W, MF>(M, P, B, fz, row, c, nb4, gp, eps2, g);
-#endif
 	st8(row + 4, 0, g);
 	fz_row_temperature<W>(P.gas, row, g);
 }
@@ -1146,29 +1120,6 @@ __device__ __forceinline__ void fused_limit_row(const DevMesh& M, const DevPhys&
 	for(int iv = 0; iv < 4; iv++) { g[iv*2+0] = lim[iv]*g[iv*2+0]; g[iv*2+1] = lim[iv]*g[iv*2+1]; }
 }
 
-/// diagnostic build (-DFVHIP_PROBE_PHASES): thread 0 of each block records the 100 MHz real-time
-/// counter at the phase boundaries of the fused residual (probe[8*block + k]) and the shader clock at
-/// its start and end, to see where a block's lifetime goes
-#ifdef FVHIP_PROBE_PHASES
-#define FZ_STAMP(B, k) do { if(threadIdx.x == 0 && (B).probe) (B).probe[8*blockIdx.x + (k)] = __builtin_amdgcn_s_memrealtime(); } while(0)
-#define FZ_CLOCK(B, k) do { if(threadIdx.x == 0 && (B).probe) (B).probe[8*blockIdx.x + (k)] = __builtin_amdgcn_s_memtime(); } while(0)
-#else
-#define FZ_STAMP(B, k) do {} while(0)
-#define FZ_CLOCK(B, k) do {} while(0)
-#endif
-
-#ifndef FVHIP_FZ_FENCE_PROBE
-#define FVHIP_FZ_FENCE_PROBE 0
-#endif
-#if FVHIP_FZ_FENCE_PROBE
-__device__ int g_fz_fence_flag[1 << 16];
-#endif
-#ifndef FVHIP_FZ_VISC_FENCE
-#define FVHIP_FZ_VISC_FENCE 1
-#endif
-#ifndef FVHIP_FZ_LIM_PREFETCH
-#define FVHIP_FZ_LIM_PREFETCH 1
-#endif
 /// the modified-average viscous flux of one face in the fused residual (gasdyn.hpp viscous_flux_core's
 /// arithmetic, same operations in the same order, so bitwise its result), streamed from the staged LDS
 /// rows variable by variable: first the temperature terms (density and pressure values and gradients),
@@ -1180,18 +1131,13 @@ __device__ __forceinline__ void fz_viscous(const Gas& G, const double* rowi, con
                                            double4 vg, const double* n, double muRe, const double* va, double* vf)
 {
 	const double* gsrc = rowj ? rowj : rowi;          // right gradient: the boundary cell's own
-	// the face's unit vector between the centres and their distance: formed here, or (FVHIP_FZ_VGEO)
-	// read from Layout::slot_vg, the same operations on the host (0 + dx^2 + dy^2, correctly rounded
-	// root and quotients)
-#if FVHIP_FZ_VGEO
-	const double dr[2] = {vg.x, vg.y}, dist = vg.z;
-#else
+	// the face's unit vector between the centres (vg: left xy, right xy) and their distance (0 + dx^2 + dy^2,
+	// correctly rounded root and quotients; reading them per slot from HBM was slower)
 	double dr[2], dist = 0;
 	dr[0] = vg.z - vg.x; dist += dr[0]*dr[0];
 	dr[1] = vg.w - vg.y; dist += dr[1]*dr[1];
 	dist = sqrt_rn(dist);
 	dr[0] = div_rn(dr[0], dist); dr[1] = div_rn(dr[1], dist);
-#endif
 	double grad[2][4];
 	{   // temperature: T and dT of each side, formed per staged row in phase 1 (fz_row_temperature); a
 		// boundary face's right side is the ghost state with the cell's own gradients, formed here
@@ -1251,7 +1197,7 @@ __device__ __forceinline__ void fz_viscous(const Gas& G, const double* rowi, con
 struct FzPatch { int p, s0, s1, c0, c1, nc, e0, nl, ng; const uint2* gnbr; const int* gbf; };
 /// what one thread loads for its patch before phase 0: its first staged row (state, centre), the
 /// neighbour list and WLS inverse of the gradient it computes first, and the geometry of its face
-struct FzPre { int cf; double ua[4]; double2 rca; int4 nb4a; double4 Va; int2 lrl; double2 nn; double len;
+struct FzPre { int cf; double ua[4]; double2 rca; int4 nb4a; int2 lrl; double2 nn; double len;
                double2 gpa[4]; double eps2a; };     // gpa, eps2a: limited reconstructions' first-row inputs
 
 __device__ __forceinline__ FzPatch fz_patch(const DevMesh& M, const SweepBuffers& B, int pi)
@@ -1305,8 +1251,7 @@ __device__ __forceinline__ void fz_load_rows(const DevMesh& M, const SweepBuffer
 __device__ __forceinline__ void fz_load_grad(const DevMesh& M, const FzPatch& q, int t, FzPre& a)
 {
 	a.nb4a = make_int4(-1, -1, -1, -1);
-	a.Va = make_double4(0, 0, 0, 0);
-	if(t < q.ng && a.cf < M.nown) { a.nb4a = fz_nbrs(q, t); if(!FVHIP_FZ_WLSV) a.Va = M.wls_V[a.cf]; }
+	if(t < q.ng && a.cf < M.nown) a.nb4a = fz_nbrs(q, t);
 }
 
 /// one patch (512 threads): phase 0 stages the primitive states and centres of the patch, ring-1 and
@@ -1332,35 +1277,21 @@ __device__ __forceinline__ void fz_body(const DevMesh& M, const DevPhys& P, cons
 		stage_row(G, &fz[i*W], b, M.rc[c]);
 	}
 	__syncthreads();
-	FZ_STAMP(B, 1);
 
 	// phase 1: WLS gradients of the patch and ring-1 cells from the staged states
 	// (k_prep_grad_wls arithmetic, neighbours in the same ascending reference face order)
 	hookA();
-#ifndef FVHIP_PROBE_NOGRAD
-	if(t < q.ng) fused_wls_row<LIM, W, !DT>(M, P, B, fz, &fz[t*W], a.cf, a.nb4a, a.Va, LIM && FVHIP_FZ_LIM_PREFETCH ? a.gpa : nullptr, a.eps2a);
+	if(t < q.ng) fused_wls_row<LIM, W, !DT>(M, P, B, fz, &fz[t*W], a.cf, a.nb4a, LIM ? a.gpa : nullptr, a.eps2a);
 	for(int i = t + SLOTS_MAX; i < q.ng; i += SLOTS_MAX) {
 		const int c = fz_cell(M, q, i);
-		fused_wls_row<LIM, W, !DT>(M, P, B, fz, &fz[i*W], c, c < M.nown ? fz_nbrs(q, i) : make_int4(-1, -1, -1, -1),
-		              c < M.nown && !FVHIP_FZ_WLSV ? M.wls_V[c] : make_double4(0, 0, 0, 0));
+		fused_wls_row<LIM, W, !DT>(M, P, B, fz, &fz[i*W], c, c < M.nown ? fz_nbrs(q, i) : make_int4(-1, -1, -1, -1));
 	}
-#endif
 	__syncthreads();
-	FZ_STAMP(B, 2);
 
 	// phase 2: one face per thread (k_sweep arithmetic)
 	double f[4] = {0, 0, 0, 0};
 	double sri = 0, srj = 0;
-#ifdef FVHIP_PROBE_NOFACE
-	if(s < q.s1 && a.len == 12345.0) {
-#else
 	if(s < q.s1) {
-#endif
-		// viscous: the slot's centre-to-centre geometry, requested before the reconstruction and the
-		// inviscid flux, used by the viscous term after them
-#if FVHIP_FZ_VGEO
-		const double4 vg = VISC != SV_NONE ? M.slot_vg[s] : make_double4(0, 0, 0, 0);
-#endif
 		const int2 lrl = a.lrl;
 		const double2 nn = a.nn;
 		const double flen = a.len;
@@ -1474,19 +1405,14 @@ __device__ __forceinline__ void fz_body(const DevMesh& M, const DevPhys& P, cons
 			double2 rr;
 			if(bnd) { gpr = ghost_prim_of_cell<!DT>(M, P, B, bcell, bf); rr = M.bf_rcbp[bf]; }
 			else { rowj = &fz[lrl.y*W]; rr = *reinterpret_cast<const double2*>(rowj + 12); }
-#if !FVHIP_FZ_VGEO
 			const double4 vg = make_double4(ri.x, ri.y, rr.x, rr.y);    // the two centres
-#endif
 			double vf[4] = {0, 0, 0, 0};
-#ifndef FVHIP_PROBE_NOVISC
 			fz_viscous(G, rowi, rowj, gpr, vg, n, muRe, va, vf);
-#endif
 			#pragma unroll
 			for(int k = 0; k < 4; k++) f[k] += vf[k]*flen;
 		}
 	}
 	hookB();
-	FZ_STAMP(B, 3);
 	// the cell's face list (and area) are requested before the two barriers of the flux staging,
 	// once the face work no longer holds registers
 	const int c = q.c0 + t;
@@ -1494,16 +1420,6 @@ __device__ __forceinline__ void fz_body(const DevMesh& M, const DevPhys& P, cons
 	double carea = 0.0;
 	if(c < q.c1) { cs = M.fz_cslot16[c]; if(DT) carea = M.area[c]; }
 	__syncthreads();   // all staged rows read: reuse LDS for the face fluxes
-#if FVHIP_FZ_FENCE_PROBE
-	// cost probe of cross-block publication (one-computation cut faces): the agent-scope
-	// release a producer patch needs after storing its cut-face fluxes (buffer_wbl2 sc1: this XCD's dirty L2
-	// lines written back) and the acquire a consumer needs before reading them (buffer_inv sc1), once per
-	// block, with no data and no waiting -- a lower bound on that design's synchronisation cost
-	if(t == 0) {
-		__hip_atomic_store(&g_fz_fence_flag[q.p & 0xFFFF], 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
-		(void)__hip_atomic_load(&g_fz_fence_flag[(q.p + 1) & 0xFFFF], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
-	}
-#endif
 	double* sf = fz;
 	double* ssr = fz + 4*SLOTS_MAX;
 	if(s < q.s1) {
@@ -1512,7 +1428,6 @@ __device__ __forceinline__ void fz_body(const DevMesh& M, const DevPhys& P, cons
 		if(DT) { ssr[t] = sri; ssr[SLOTS_MAX + t] = srj; }
 	}
 	__syncthreads();
-	FZ_STAMP(B, 4);
 
 	if(c < q.c1) {
 		double r[4];
@@ -1546,8 +1461,6 @@ __device__ __forceinline__ void fz_body(const DevMesh& M, const DevPhys& P, cons
 		st4(B.r, c, r);
 		if(DT) B.dtm[c] = div_rn(carea, integ);
 	}
-	FZ_STAMP(B, 5);
-	FZ_CLOCK(B, 7);
 }
 
 // waves per SIMD the fused instantiations are compiled for (VGPR budgets 96 / 128 / 168); the layout
@@ -1571,15 +1484,13 @@ __global__ void __launch_bounds__(SLOTS_MAX, VISC != SV_NONE ? FVHIP_FUSED_WAVES
 	const int q = (np + 7) >> 3;
 	const int pi = (blockIdx.x & 7) * q + (blockIdx.x >> 3);
 	if(pi >= np) return;
-	FZ_STAMP(B, 0);
-	FZ_CLOCK(B, 6);
 	const FzPatch cur = fz_patch(M, B, pi);
 	FzPre pre;
 	pre.cf = t < cur.nl ? fz_cell(M, cur, t) : 0;
 	fz_load_rows<!DT>(M, B, cur, t, pre);
 	fz_load_grad(M, cur, t, pre);
 	pre.eps2a = 0.0;
-	if(LIM && FVHIP_FZ_LIM_PREFETCH) {   // the first row's face centres and eps^2, requested before the staging barrier
+	if(LIM) {   // the first row's face centres and eps^2, requested before the staging barrier
 		// (owned gradient rows only: a ghost row's limiter values come with its gradient)
 		const bool own = t < cur.ng && pre.cf < M.nown;
 		fz_face_centres(M, own ? pre.cf : 0, pre.gpa);
@@ -1741,11 +1652,6 @@ const char* launch_sweep(const DevMesh& M, const DevPhys& P, const SweepBuffers&
 {
 	const bool phi = B.phi != nullptr;
 	SweepFn fn;
-#ifdef FVHIP_EXPERIMENT_FLUX
-	// ISA experiments: one flux instantiated (every request takes it; results of others are wrong)
-	fn = pick2<FVHIP_EXPERIMENT_FLUX>(rec, visc, dt, phi);
-	(void)flux;
-#else
 	switch(flux) {
 		case 0: fn = pick2<0>(rec, visc, dt, phi); break;
 		case 1: fn = pick2<1>(rec, visc, dt, phi); break;
@@ -1755,7 +1661,6 @@ const char* launch_sweep(const DevMesh& M, const DevPhys& P, const SweepBuffers&
 		case 5: fn = pick2<5>(rec, visc, dt, phi); break;
 		default: fn = pick2<6>(rec, visc, dt, phi); break;
 	}
-#endif
 	const int np = B.plist ? B.pcount : M.npatch;
 	if(np > 0) hipLaunchKernelGGL(fn, dim3(8*((np + 7)/8)), dim3(SLOTS_MAX), 0, s, M, P, B);
 	return kSweepNames[flux < 0 || flux > 6 ? 6 : flux];
@@ -1791,11 +1696,6 @@ const char* launch_residual_wls(const DevMesh& M, const DevPhys& P, const SweepB
                                 int visc, int lim, bool dt, hipStream_t s)
 {
 	FusedFn fn;
-#ifdef FVHIP_EXPERIMENT_FLUX
-	// ISA experiments: one flux instantiated (every request takes it; results of others are wrong)
-	fn = pickFused<FVHIP_EXPERIMENT_FLUX>(rec, visc, lim, dt);
-	(void)flux;
-#else
 	switch(flux) {
 		case 0: fn = pickFused<0>(rec, visc, lim, dt); break;
 		case 1: fn = pickFused<1>(rec, visc, lim, dt); break;
@@ -1805,7 +1705,6 @@ const char* launch_residual_wls(const DevMesh& M, const DevPhys& P, const SweepB
 		case 5: fn = pickFused<5>(rec, visc, lim, dt); break;
 		default: fn = pickFused<6>(rec, visc, lim, dt); break;
 	}
-#endif
 	const size_t W = visc != SV_NONE ? FZW_VISC : FZW;
 	const size_t lds = std::max(static_cast<size_t>(M.fz_max_cells)*W, static_cast<size_t>(6*SLOTS_MAX))*sizeof(double);
 	// raise the dynamic-LDS limit once per instantiation and device to the largest patch the layout

@@ -27,7 +27,6 @@ struct DevMesh
 	const double2* slot_n;     // [S]
 	const double* slot_len;    // [S]
 	const double2* slot_gr;    // [S]
-	const double4* slot_vg;    // [S] viscous: unit vector L->R centre, distance (Layout::slot_vg); else null
 	const int4* cell_slots;    // [N] (slot<<1 | isRight), -1 padded, ascending reference face
 	const int4* cell_nbr;      // [N] esuel order neighbours (internal / ncell+bf)
 	const int4* cell_face;     // [N] esuel order slots
@@ -95,7 +94,6 @@ struct SweepBuffers
 	const double* mfpm;   // [2] (|x|, eps/|x|)
 	const double* mfres;  // [N][4] -r(u) of the operator's state
 	const double* mfmdt;  // [N] pseudo-time diagonal
-	unsigned long long* probe;   // diagnostic builds (-DFVHIP_PROBE_PHASES) only: per-block phase stamps
 };
 
 // Host launchers (all asynchronous on stream). kernels.hip is compiled twice: namespace `exact`

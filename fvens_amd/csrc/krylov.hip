@@ -203,29 +203,12 @@ void k_sum_partials(int np, const double* __restrict__ part, double* __restrict_
 	block_sum<1>(acc, out + blockIdx.x, 1);
 }
 
-// FVHIP_KRY_UNROLL = U > 1: the basis loops of k_maxpy, k_maxpy_norm and k_lincomb load U vectors' rows
-// before their (unchanged, sequential) sums -- the same operations in the same order, so the same bits --
-// instead of one load and a full memory wait per basis vector
-#ifndef FVHIP_KRY_UNROLL
-#define FVHIP_KRY_UNROLL 1
-#endif
-constexpr int KRY_UNROLL = FVHIP_KRY_UNROLL;
 /// s += c[j] * X[j*ld + i] over j = 0 .. k-1 in order (X read as T rows: double or double2)
 template <typename T, typename F>
 __device__ __forceinline__ void basis_sum(int k, const double* __restrict__ c, const double* __restrict__ V, long long ld,
                                           long long i, F&& add)
 {
-	int j = 0;
-	if constexpr(KRY_UNROLL > 1) {
-		for(; j + KRY_UNROLL <= k; j += KRY_UNROLL) {
-			T v[KRY_UNROLL];
-			#pragma unroll
-			for(int q = 0; q < KRY_UNROLL; q++) v[q] = reinterpret_cast<const T*>(V + (j + q)*ld)[i];
-			#pragma unroll
-			for(int q = 0; q < KRY_UNROLL; q++) add(c[j + q], v[q]);
-		}
-	}
-	for(; j < k; j++) add(c[j], reinterpret_cast<const T*>(V + j*ld)[i]);
+	for(int j = 0; j < k; j++) add(c[j], reinterpret_cast<const T*>(V + j*ld)[i]);
 }
 
 __global__ __launch_bounds__(256)

@@ -447,23 +447,6 @@ Layout buildLayout(const MeshTopo& T, const fvhip_flow_config& cfg, bool renumbe
 		Lo.venk_eps2.resize(N);
 		for(int c = 0; c < N; c++) Lo.venk_eps2[c] = std::pow(cfg.limiter_param*T.clength[Lo.perm[c]], 3);
 	}
-	// --- viscous face geometry per slot: the modified-average viscous flux's unit vector between the
-	//     two cell centres (ghost centre for a boundary face) and their distance, in fz_viscous' operation
-	//     order (0 + dx*dx + dy*dy, correctly rounded sqrt and divisions: the device's bits) ---
-	if(FVHIP_FZ_VGEO && cfg.viscous_sim) {
-		const size_t S = Lo.slot_L.size();
-		Lo.slot_vg.assign(4*S, 0.0);
-		for(size_t s = 0; s < S; s++) {
-			const int l = Lo.slot_L[s], r = Lo.slot_R[s];
-			const double* ri = &Lo.rc[2*static_cast<size_t>(l)];
-			const double* rr = r >= NT ? &Lo.bf_rcbp[2*static_cast<size_t>(r - NT)] : &Lo.rc[2*static_cast<size_t>(r)];
-			double dr[2], dist = 0;
-			dr[0] = rr[0]-ri[0]; dist += dr[0]*dr[0];
-			dr[1] = rr[1]-ri[1]; dist += dr[1]*dr[1];
-			dist = std::sqrt(dist);
-			Lo.slot_vg[4*s] = dr[0]/dist; Lo.slot_vg[4*s+1] = dr[1]/dist; Lo.slot_vg[4*s+2] = dist;
-		}
-	}
 	if(fused) buildFused(Lo);
 	if(Lo.nghost == 0 && pipelineEligible(cfg)) buildPipeline(Lo, PIPE_CHUNKS);
 	return Lo;

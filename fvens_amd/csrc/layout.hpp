@@ -24,12 +24,6 @@ namespace fvhip {
 #ifndef FVHIP_FUSED_ROWS
 #define FVHIP_FUSED_ROWS (FVHIP_SLOTS*11/8)   // 352 x 112 B = 39 KB for 256-slot patches: 4 blocks = 16 waves per CU, the VGPR-bound occupancy
 #endif
-/// FVHIP_FZ_VGEO = 1: the fused viscous face reads its centre-to-centre unit vector and distance per slot
-/// (Layout::slot_vg, 32 B per slot) instead of forming them (a root and two quotients); measured slower
-/// on C5 (0.670 -> 0.695 ms, profiles/r04/config5_ab.txt), so off
-#ifndef FVHIP_FZ_VGEO
-#define FVHIP_FZ_VGEO 0
-#endif
 constexpr int SLOTS_MAX = FVHIP_SLOTS;   ///< faces per patch = threads per sweep workgroup
 constexpr int CELLS_MAX = FVHIP_SLOTS;
 constexpr int MAXF = 4;          ///< max faces per cell (linear tri/quad)
@@ -50,8 +44,6 @@ struct Layout
 	std::vector<double> slot_n;            ///< [S][2]
 	std::vector<double> slot_len;          ///< [S]
 	std::vector<double> slot_gr;           ///< [S][2]
-	std::vector<double> slot_vg;           ///< [S][4] FVHIP_FZ_VGEO viscous configurations: (rR - rL)/d (2), d = |rR - rL|, 0
-	                                       ///<  (fz_viscous' face geometry, same IEEE operations: bitwise)
 	// cells (internal order)
 	std::vector<int> cell_slots;           ///< [ncell][4]: (slot << 1 | cell-is-right) of the cell's
 	                                       ///<  faces in ascending reference face index, -1 padded;

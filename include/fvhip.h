@@ -319,6 +319,11 @@ typedef struct fvhip_implicit_config {
 	int amg_coarse_sweeps;    /* Gauss-Seidel sweeps on the coarsest level (-mg_coarse_ksp_max_it; 0: the deck's 6) */
 	double amg_threshold;     /* two cells aggregate when their coupling (face length / centre distance) is at least
 	                             this fraction of both cells' strongest (-pc_gamg_threshold; 0: the deck's 0.2) */
+	double resume_res0;       /* > 0: continue a solve stopped earlier (a checkpoint): its first residual norm, so
+	                             that the tolerance stays relative to it (the reference's initres, aodesolver.cpp:537) */
+	double resume_res;        /*   ... its last residual norm and the one before (the CFL ramp's ratio, :462) */
+	double resume_res_prev;
+	double resume_cfl;        /*   ... and the CFL of its last step (the ramp continues from it) */
 } fvhip_implicit_config;
 
 typedef struct fvhip_solve_stats {
