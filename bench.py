@@ -179,7 +179,9 @@ def counter_bound(counters, kernel_ms):
 
 
 HBM_MEASURED_GBS = 6290.0          # MI355X_MICROARCH.md: float4 copy, 79 % of the spec
-FP64_LANE_OPS = 256 * 64 * 2.4e9   # FP64 VALU issue: 64 lanes/CU/clock (78.6 TFLOPS FMA spec) at 2.4 GHz
+SCLK_MEASURED_HZ = 2.19e9         # the shader clock the chip holds under the residual kernels (DESIGN.md section 5:
+                                   # s_memtime cycles over s_memrealtime, round 4), not the 2.4 GHz boost
+FP64_LANE_OPS = 256 * 64 * SCLK_MEASURED_HZ   # FP64 VALU issue: 64 lanes/CU/clock (78.6 TFLOPS FMA spec at 2.4 GHz)
 
 
 def valu_roofline(valu_wave_instrs, kernel_ms):
@@ -422,7 +424,8 @@ def main():
                          "SURVEY's C2 (229,376 cells); config3: BASELINE config 3, the laminar flat plate "
                          "(1024 x 1024 quads, M 0.2, Re 8.7e5), HLLC + WLS + unlimited linear + Sutherland viscous flux, "
                          "implicit figure matrix-free; config5: BASELINE config 5, the laminar NACA0012 "
-                         "(M 0.5, Re 5000, alpha 0) on the 8.1M-cell C5 quadrangle C-grid (4096 columns x 1984 rows), Roe + WLS + "
+                         "(M 0.5, Re 5000, alpha 0) on the 8.1M-cell hybrid C5 mesh (quadrangle boundary layer and wakes, "
+                         "near-isotropic triangles outside: the visc-naca0012 grids' topology), Roe + WLS + "
                          "unlimited linear reconstruction (the deck's limiter none) + Sutherland viscous flux")
     args = ap.parse_args()
 
@@ -801,6 +804,8 @@ def main():
             "dtype": "f64",
             "data": ("synthetic (generated structured flat-plate quad mesh; seeded perturbed free stream)"
                      if args.numerics == "config3" else
+                     "synthetic (generated NACA0012 hybrid mesh: quadrangle boundary layer and wakes, near-isotropic "
+                     "triangles outside; seeded perturbed free stream)" if args.numerics == "config5" else
                      "synthetic (generated NACA0012 hybrid O-grid; seeded perturbed free stream)"),
             "config": {"workload": f"{wl}, 2nd-order residual sweep with local time steps "
                                    "(explicit pseudo-time step)",

@@ -115,6 +115,56 @@ void k_amg_gs(int cnt, const int* __restrict__ cells, const int* __restrict__ ro
 	if(live) x[4*static_cast<size_t>(row) + i] = o;
 }
 
+/// one workgroup of 1024 threads: every sweep, every colour, 256 rows at a time (4 lanes a row), a barrier
+/// after each colour
+__global__ __launch_bounds__(1024)
+void k_amg_gs_block(int n, int ncol, const int* __restrict__ cstart, const int* __restrict__ cells,
+                    const int* __restrict__ rowptr, const int* __restrict__ col, const int* __restrict__ dpos,
+                    const double* __restrict__ val, const double* __restrict__ dinv, const double* __restrict__ b,
+                    double* x, int sweeps, int fwd, int alternate, int zero)
+{
+	const int t = static_cast<int>(threadIdx.x), i = t & 3;
+	if(zero) {
+		for(int k = t; k < 4*n; k += 1024) x[k] = 0.0;
+		__syncthreads();
+	}
+	const double4* x4 = reinterpret_cast<const double4*>(x);
+	for(int sw = 0; sw < sweeps; sw++) {
+		const bool f = alternate ? (sw % 2 == 0) : (fwd != 0);
+		for(int qq = 0; qq < ncol; qq++) {
+			const int q = f ? qq : ncol - 1 - qq;
+			const int b0 = cstart[q], cnt = cstart[q+1] - b0;
+			for(int r0 = 0; r0 < cnt; r0 += 256) {
+				const int rr = r0 + (t >> 2);
+				const bool live = rr < cnt;
+				const int row = cells[b0 + (live ? rr : cnt - 1)];
+				double acc = b[4*static_cast<size_t>(row) + i];
+				const int kd = dpos[row];
+				for(int k = rowptr[row]; k < rowptr[row+1]; k++) {
+					if(k == kd) continue;
+					const double4 a = reinterpret_cast<const double4*>(val + 16*static_cast<size_t>(k))[i];
+					const double4 xv = x4[col[k]];
+					acc -= a.x*xv.x + a.y*xv.y + a.z*xv.z + a.w*xv.w;
+				}
+				const double4 s = make_double4(__shfl(acc, 0, 4), __shfl(acc, 1, 4), __shfl(acc, 2, 4), __shfl(acc, 3, 4));
+				const double4 d = reinterpret_cast<const double4*>(dinv + 16*static_cast<size_t>(row))[i];
+				const double o = d.x*s.x + d.y*s.y + d.z*s.z + d.w*s.w;
+				if(live) x[4*static_cast<size_t>(row) + i] = o;
+			}
+			__syncthreads();
+		}
+	}
+}
+
+void launch_amg_gs_block(const AmgLevel& L, const double* b, double* x, int sweeps, bool fwd, bool alternate,
+                         bool zero, hipStream_t s)
+{
+	if(L.n <= 0 || L.n > AMG_BLOCK_ROWS) return;
+	hipLaunchKernelGGL(k_amg_gs_block, dim3(1), dim3(1024), 0, s, L.n, static_cast<int>(L.cstart_colour.size()) - 1,
+	                   L.d_cstart_colour, L.cells, L.rowptr, L.col, L.dpos, L.val, L.dinv, b, x, sweeps, fwd ? 1 : 0,
+	                   alternate ? 1 : 0, zero ? 1 : 0);
+}
+
 void launch_amg_galerkin_fine(const AmgLevel& L, int nfine, int nif, const double* diag, const double* lower,
                               const double* upper, hipStream_t s)
 {

@@ -68,6 +68,7 @@ struct AmgLevel
 	const int *cstart = nullptr, *csrc = nullptr;
 	const int *mstart = nullptr, *members = nullptr, *agg = nullptr;
 	const int* cells = nullptr;              ///< colour order
+	const int* d_cstart_colour = nullptr;    ///< the colour starts on the device (single-workgroup sweeps)
 	std::vector<int> cstart_colour;          ///< host copy of the colour starts
 	int nfine = 0;                           ///< rows of the finer level
 	double *val = nullptr, *dinv = nullptr;  ///< [nnz][16], [n][16]
@@ -89,6 +90,13 @@ void launch_amg_prolong(const AmgLevel& L, const double* x, double* xfine, hipSt
 void launch_amg_residual(const AmgLevel& L, const double* x, const double* b, double* r, hipStream_t s);
 /// one colour of a block Gauss-Seidel sweep on A x = b, in place: x_i = dinv_i (b_i - sum_{j != i} A_ij x_j)
 void launch_amg_gs_colour(const AmgLevel& L, int q, const double* b, double* x, hipStream_t s);
+/// levels of at most AMG_BLOCK_ROWS rows: `sweeps` whole Gauss-Seidel sweeps (colours forward on even sweeps,
+/// backward on odd ones when `alternate`, else all in direction `fwd`) in one workgroup, a barrier between
+/// colours -- the same row updates in the same order as per-colour launches, without a launch per colour;
+/// zero: x = 0 first
+constexpr int AMG_BLOCK_ROWS = 4096;
+void launch_amg_gs_block(const AmgLevel& L, const double* b, double* x, int sweeps, bool fwd, bool alternate,
+                         bool zero, hipStream_t s);
 
 }
 #endif

@@ -1014,6 +1014,7 @@ struct fvhip_ctx
 			D.cstart = upload(H.cstart, owned); D.csrc = upload(H.csrc, owned);
 			D.mstart = upload(H.mstart, owned); D.members = upload(H.members, owned); D.agg = upload(H.agg, owned);
 			D.cells = upload(H.cells, owned); D.cstart_colour = H.cstart_colour;
+			D.d_cstart_colour = upload(H.cstart_colour, owned);
 			D.val = dalloc(16*static_cast<size_t>(D.nnz), owned); D.dinv = dalloc(16*static_cast<size_t>(D.n), owned);
 			D.x = dalloc(4*static_cast<size_t>(D.n), owned); D.b = dalloc(4*static_cast<size_t>(D.n), owned);
 			D.r = dalloc(4*static_cast<size_t>(D.n), owned);

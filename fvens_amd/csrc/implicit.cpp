@@ -266,22 +266,26 @@ struct LinOp
 	/// forward before the coarse correction, backward after it; the coarsest level amg_coarse sweeps)
 	void cycle(fvhip_ctx* h, size_t l) {
 		AmgLevel& C = h->amg[l];
-		exact::launch_fill(C.x, 0.0, 4LL*C.n, h->stream);
+		const bool small = C.n <= AMG_BLOCK_ROWS;        // one workgroup sweeps the level (no launch per colour)
+		if(!small) exact::launch_fill(C.x, 0.0, 4LL*C.n, h->stream);
 		const int nc = static_cast<int>(C.cstart_colour.size()) - 1;
 		auto sweep = [&](bool fwd) {
 			for(int q = 0; q < nc; q++) launch_amg_gs_colour(C, fwd ? q : nc - 1 - q, C.b, C.x, h->stream);
 		};
 		if(l + 1 == h->amg.size()) {
-			for(int k = 0; k < amg_coarse; k++) sweep(k % 2 == 0);
+			if(small) launch_amg_gs_block(C, C.b, C.x, amg_coarse, true, true, true, h->stream);
+			else for(int k = 0; k < amg_coarse; k++) sweep(k % 2 == 0);
 			return;
 		}
-		for(int k = 0; k < amg_sweeps; k++) sweep(true);
+		if(small) launch_amg_gs_block(C, C.b, C.x, amg_sweeps, true, false, true, h->stream);
+		else for(int k = 0; k < amg_sweeps; k++) sweep(true);
 		launch_amg_residual(C, C.x, C.b, C.r, h->stream);
 		AmgLevel& F = h->amg[l+1];
 		launch_amg_restrict(F, C.r, F.b, h->stream);
 		cycle(h, l + 1);
 		launch_amg_prolong(F, F.x, C.x, h->stream);
-		for(int k = 0; k < amg_sweeps; k++) sweep(false);
+		if(small) launch_amg_gs_block(C, C.b, C.x, amg_sweeps, false, false, false, h->stream);
+		else for(int k = 0; k < amg_sweeps; k++) sweep(false);
 	}
 	/// z = M^-1 v, M one V-cycle of the aggregation multigrid (block-Jacobi across ranks: each handle's hierarchy
 	/// covers its owned cells; the finest residuals include the ghost coupling)

@@ -688,6 +688,20 @@ def test_fused_matfree_operator_bitwise(kind, flux, rec):
     h1.synchronize()
     h2.synchronize()
     assert torch.equal(y1, y2), float((y1 - y2).abs().max())
+    # y aliasing x or the state u: the fused launch would race (its blocks read rows of x and u other blocks'
+    # cells need while writing y), so the three-launch operator runs -- the same bits
+    xa = dx.clone()
+    torch.cuda.synchronize()
+    h1.matfree_apply_device(xa.data_ptr(), xa.data_ptr())
+    h1.synchronize()
+    assert torch.equal(xa, y1), float((xa - y1).abs().max())
+    ua = du.clone()
+    torch.cuda.synchronize()
+    h1.matfree_set_state_device(ua.data_ptr(), dr.data_ptr(), dmdt.data_ptr())
+    h1.matfree_apply_device(dx.data_ptr(), ua.data_ptr())
+    h1.synchronize()
+    assert torch.equal(ua, y1), float((ua - y1).abs().max())
+    h1.matfree_set_state_device(du.data_ptr(), dr.data_ptr(), dmdt.data_ptr())
     # block-Jacobi sweeps: the line preconditioner would hand the single handle |z| from its own sum
     # (test_line_solve_norm_feeds_matrix_free) where the group takes the multi-dot's
     cfg = fa.ImplicitConfig(cflinit=20.0, cflfin=200.0, tol=0.0, maxiter=3, lin_rtol=1e-2, lin_maxit=40, restart=20,

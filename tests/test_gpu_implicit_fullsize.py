@@ -3,7 +3,7 @@ aodesolver.cpp:363-638, with the linear systems on the device; what bench.py's i
 Size-independent properties, checked on the meshes the bench runs:
   * C4 (4,063,232 cells, config 4's mesh), assembled operator, line-implicit preconditioner: three steps
     from the free stream stay finite, every linear solve reaches lin_rtol, the residual falls;
-  * C5 (8,126,464 cells, config 5: the visc-naca0012 deck's numerics -- Roe, WLS, limiter none, Sutherland,
+  * C5 (the 8,054,616-cell hybrid mesh, config 5: the visc-naca0012 deck's numerics -- Roe, WLS, limiter none, Sutherland,
     alpha 0), matrix-free operator (alinalg.cpp:142-233) with the assembled first-order Jacobian as the
     line-implicit preconditioner: the same checks;
   * C4 split 8 ways by the bench's partitioner (all ranks in one process, device copies for RCCL; lines
@@ -52,7 +52,7 @@ def test_c4_assembled_line_implicit_steps():
 def test_c5_matrix_free_steps():
     from bench import c4_mesh
     m = c4_mesh(fa, 1, 2)[0]
-    assert m.nelem == 8126464
+    assert m.nelem == 8054616
     _three_steps(m, cases.physics("visc"), cases.numerics("ROE", "LEASTSQUARES", "NONE"), True)
 
 

@@ -125,15 +125,16 @@ def test_partitioned_c4_eight_ranks(rec):
 
 
 def test_partitioned_c5_eight_ranks():
-    """BASELINE config 5 at its full size on the partitioned path: the 8,126,464-cell C5 C-grid (4096
-    columns x 1984 rows of quadrangles, 1e-5 wall spacing), laminar Roe + WLS + unlimited linear + Sutherland at alpha 0 (the
+    """BASELINE config 5 at its full size on the partitioned path: the 8,054,616-cell hybrid C5 mesh (quadrangle
+    boundary layer and wakes, 4,122,456 near-isotropic triangles outside, 1e-5 wall spacing), laminar Roe + WLS
+    + unlimited linear + Sutherland at alpha 0 (the
     visc-naca0012 deck's numerics, laminar-implicit.ctrl:19,72; the fused viscous kernel on the two-layer
     halo), split 8 ways by the cost-weighted graph partitioner, all ranks in one
     process with the overlapped schedule -- every owned row's residual and time step bitwise the
     single-GPU ones (the same device code evaluates Sutherland's law on both sides)"""
     r, dt, r1, dt1, stats = run_partitioned("naca_c5", "visc", "ROE", "LEASTSQUARES", "NONE", True, 8,
                                             partitioner="graph-cost")
-    assert r.shape[0] == 8126464
+    assert r.shape[0] == 8054616
     np.testing.assert_array_equal(r, r1)
     np.testing.assert_array_equal(dt, dt1)
     for s in stats:

@@ -31,8 +31,9 @@ def get_mesh(key):
             om = orc.OracleMesh.from_raw(m.raw())
         elif key == "naca_c4":                               # the bench's C4 mesh (no oracle mesh)
             m, om = fa.UMesh.naca_ogrid(2048, 256, 864, 20.0, 1e-5, farmap=1), None
-        elif key == "naca_c5":                               # BASELINE config 5's 8,126,464-cell C-grid
-            m, om = fa.UMesh.naca_cgrid(3072, 512, 1984, 0, 20.0, 1e-5), None
+        elif key == "naca_c5":                               # BASELINE config 5's 8,054,616-cell hybrid mesh
+            from bench import c4_mesh
+            m, om = c4_mesh(fa, 1, 2)[0], None
         elif key == "c1":                                    # BASELINE config 1's cylinder
             m = fa.UMesh.cylinder_ogrid(64, 40)
             om = orc.OracleMesh.from_raw(m.raw())

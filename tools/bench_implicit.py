@@ -60,7 +60,7 @@ def main():
     if kind == "plate":
         nx = ny = 1024 // args.scale
         mesh, dims = fa.UMesh.flat_plate(nx, ny), dict(nx=nx, ny=ny)
-    elif args.case == "visc-c5":    # BASELINE config 5: laminar NACA0012, 8,126,464 cells, 1e-5 wall spacing
+    elif args.case == "visc-c5":    # BASELINE config 5: laminar NACA0012, the 8,054,616-cell hybrid C5
         mesh, dims = c4_mesh(fa, args.scale, 2)
     else:
         mesh, dims = c4_mesh(fa, args.scale)

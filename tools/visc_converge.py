@@ -25,9 +25,13 @@ sys.path.insert(0, os.path.join(ROOT, "tests"))
 
 def run(scale=1, matrix_free=True, main_steps=400, init_steps=50, lin_maxit=60, restart=60, sweeps=3,
         tol=1e-6, heartbeat=None, cfl_init=(200.0, 1000.0), cfl_main=(500.0, 5000.0), min_relax=1.0, lin_rtol=1e-1,
-        wall=None, mf_eps=None, quads=False, amg=0, amg_sweeps=2, amg_coarse=6, amg_thr=0.2, lines=True):
+        wall=None, mf_eps=None, quads=False, amg=0, amg_sweeps=2, amg_coarse=6, amg_thr=0.2, lines=True,
+        u0=None, want_state=False):
     """the deck's two stages on the C5 mesh divided by `scale` in both directions; returns the record (a stage
-    that diverges is recorded with its history and the error; the later stage is then skipped)"""
+    that diverges is recorded with its history and the error; the later stage is then skipped). u0: a start
+    state in the mesh's cell order (mesh sequencing: a coarser member's solution carried over) -- the main
+    stage then starts from it, without the first-order stage; want_state: the final state (cell order) and
+    the cell centres go into rec["_state"], rec["_rc"]"""
     import torch
     import fvens_amd as fa
     import cases
@@ -40,7 +44,10 @@ def run(scale=1, matrix_free=True, main_steps=400, init_steps=50, lin_maxit=60, 
     perm = main.permutation()
     if mf_eps:
         main.matfree_set_eps(mf_eps)          # -matrix_free_difference_step (alinalg.cpp:127)
-    du = torch.tensor(np.tile(cases.freestream(p), (mesh.nelem, 1))[perm], device="cuda")
+    ustart = np.tile(cases.freestream(p), (mesh.nelem, 1)) if u0 is None else np.asarray(u0, np.float64)
+    if u0 is not None:
+        init_steps = 0
+    du = torch.tensor(ustart[perm], device="cuda")
     torch.cuda.synchronize()      # torch's stream vs the library's (non-blocking) streams
     lin = dict(lin_rtol=lin_rtol, lin_maxit=lin_maxit, restart=restart, prec_lines=lines, prec_sweeps=sweeps,
                min_relax=min_relax, prec_amg=amg, amg_sweeps=amg_sweeps, amg_coarse_sweeps=amg_coarse,
@@ -85,10 +92,22 @@ def run(scale=1, matrix_free=True, main_steps=400, init_steps=50, lin_maxit=60, 
         return rec
     (cl, cdp, cdsf), _ = main.surface_data_device(du.data_ptr(), 2)
     finite = bool(torch.isfinite(du).all().item())
+    if want_state:
+        us = np.empty((mesh.nelem, 4))
+        us[perm] = du.cpu().numpy()
+        rec["_state"], rec["_rc"] = us, np.asarray(mesh.rc[:mesh.nelem]).copy()
     start.close()
     main.close()
     rec.update({"CL": cl, "CDp": cdp, "CDsf": cdsf, "finite": finite})
     return rec
+
+
+def carry_over(rc_from, u_from, rc_to):
+    """mesh sequencing: each cell of the finer mesh takes the state of the coarser mesh's cell whose centre is
+    nearest to its own (piecewise-constant prolongation; the meshes share their geometry, not their cells)"""
+    from scipy.spatial import cKDTree
+    _, idx = cKDTree(rc_from).query(rc_to, workers=16)
+    return u_from[idx]
 
 
 def main():
@@ -112,10 +131,36 @@ def main():
     ap.add_argument("--amg-coarse", type=int, default=6)
     ap.add_argument("--amg-thr", type=float, default=0.2)
     ap.add_argument("--no-lines", action="store_true", help="point-block Jacobi instead of the line-implicit preconditioner")
+    ap.add_argument("--sequence", type=int, nargs="+", default=None,
+                    help="mesh sequencing: solve these scales in turn (coarsest first, the deck's schedule), each finer "
+                         "one starting from the previous solution carried over (no first-order stage); the last is --scale")
     ap.add_argument("--tag", default="")
     args = ap.parse_args()
     import torch
     torch.cuda.set_device(0)
+    if args.sequence:
+        import fvens_amd as fa
+        from bench import c4_mesh
+        u0, prev, recs = None, None, []
+        for sc in args.sequence:
+            kw = dict(matrix_free=not args.assembled, main_steps=args.main_steps, init_steps=args.init_steps,
+                      lin_maxit=args.lin_maxit, restart=args.restart, sweeps=args.sweeps,
+                      heartbeat=lambda s: print(s, flush=True), cfl_init=args.cfl_init, cfl_main=args.cfl_main,
+                      min_relax=args.min_relax, lin_rtol=args.lin_rtol, wall=args.wall, mf_eps=args.mf_eps,
+                      quads=args.quads, amg=args.amg, amg_sweeps=args.amg_sweeps, amg_coarse=args.amg_coarse,
+                      amg_thr=args.amg_thr, lines=not args.no_lines)
+            if prev is not None:
+                m, _ = c4_mesh(fa, sc, 2, wall=args.wall, topology="cgrid" if args.quads else "hybrid")
+                u0 = carry_over(prev["_rc"], prev["_state"], np.asarray(m.rc[:m.nelem]))
+                del m
+            r = run(sc, u0=u0, want_state=True, **kw)
+            prev = r
+            out = {k: v for k, v in r.items() if not k.startswith("_")}
+            out["tag"], out["sequence_scale"] = args.tag, sc
+            print(json.dumps(out), flush=True)
+            if not r.get("main", {}).get("converged"):
+                break
+        return
     r = run(args.scale, not args.assembled, args.main_steps, init_steps=args.init_steps, lin_maxit=args.lin_maxit, restart=args.restart,
             sweeps=args.sweeps, heartbeat=lambda s: print(s, flush=True), cfl_init=args.cfl_init,
             cfl_main=args.cfl_main, min_relax=args.min_relax, lin_rtol=args.lin_rtol, wall=args.wall, mf_eps=args.mf_eps, quads=args.quads,
