@@ -747,3 +747,28 @@ def test_line_solve_norm_feeds_matrix_free():
     grp.close()
     h1.close()
     h2.close()
+
+
+def test_resumed_solve_matches_one_call():
+    """a checkpointed backward-Euler solve (fvhip_implicit_config resume_*: the first residual, the last two
+    and the last CFL of the stopped solve) continues with exactly the iterates of one uninterrupted call: two
+    calls of two steps against one of four on the same start state -- the same states and residual
+    histories bit for bit, the same final CFL"""
+    import torch
+    m, _ = get_mesh("naca_small")
+    p = cases.physics("visc")
+    n = cases.numerics("ROE", "LEASTSQUARES", "NONE")
+    dev = fa.FlowFV(m, p, n)
+    u0 = torch.tensor(cases.state(m, p, 5)[dev.permutation()], device="cuda")
+    kw = dict(cflinit=50.0, cflfin=2000.0, tol=1e-12, lin_rtol=1e-2, lin_maxit=30, restart=30, prec_lines=True,
+              matrix_free=True)
+    ua, ub = u0.clone(), u0.clone()
+    torch.cuda.synchronize()
+    sa, ha = dev.steady_backward_euler_device(ua.data_ptr(), fa.ImplicitConfig(maxiter=4, **kw))
+    s1, h1 = dev.steady_backward_euler_device(ub.data_ptr(), fa.ImplicitConfig(maxiter=2, **kw))
+    s2, h2 = dev.steady_backward_euler_device(ub.data_ptr(), fa.ImplicitConfig(
+        maxiter=2, resume=(h1[0], h1[-1], h1[-2], s1["cfl"]), **kw))
+    assert np.array_equal(np.concatenate([h1, h2]), ha), (h1, h2, ha)
+    assert s2["cfl"] == sa["cfl"] and s2["resratio"] == sa["resratio"]
+    assert torch.equal(ua, ub)
+    dev.close()

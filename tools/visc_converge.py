@@ -18,6 +18,8 @@ import time
 
 import numpy as np
 
+T0 = time.time()
+
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 sys.path.insert(0, os.path.join(ROOT, "tests"))
@@ -26,12 +28,14 @@ sys.path.insert(0, os.path.join(ROOT, "tests"))
 def run(scale=1, matrix_free=True, main_steps=400, init_steps=50, lin_maxit=60, restart=60, sweeps=3,
         tol=1e-6, heartbeat=None, cfl_init=(200.0, 1000.0), cfl_main=(500.0, 5000.0), min_relax=1.0, lin_rtol=1e-1,
         wall=None, mf_eps=None, quads=False, amg=0, amg_sweeps=2, amg_coarse=6, amg_thr=0.2, lines=True,
-        u0=None, want_state=False):
+        u0=None, want_state=False, chunk=0, deadline=None):
     """the deck's two stages on the C5 mesh divided by `scale` in both directions; returns the record (a stage
     that diverges is recorded with its history and the error; the later stage is then skipped). u0: a start
     state in the mesh's cell order (mesh sequencing: a coarser member's solution carried over) -- the main
     stage then starts from it, without the first-order stage; want_state: the final state (cell order) and
-    the cell centres go into rec["_state"], rec["_rc"]"""
+    the cell centres go into rec["_state"], rec["_rc"]. chunk > 0: the main stage runs in pieces of `chunk`
+    steps, each a fresh call resumed from the last one's residuals and CFL (fvhip_implicit_config resume_*: the
+    same iterates as one call), so that it can stop at the wall-clock `deadline` (time.time()) with its record"""
     import torch
     import fvens_amd as fa
     import cases
@@ -80,9 +84,41 @@ def run(scale=1, matrix_free=True, main_steps=400, init_steps=50, lin_maxit=60, 
         if init_steps > 0:
             rec["init"] = stage(start, fa.ImplicitConfig(cflinit=cfl_init[0], cflfin=cfl_init[1], tol=1e-1,
                                                         maxiter=init_steps, **lin))
-        if "error" not in rec.get("init", {}):
+        if "error" not in rec.get("init", {}) and chunk <= 0:
             rec["main"] = stage(main, fa.ImplicitConfig(cflinit=cfl_main[0], cflfin=cfl_main[1], tol=tol,
                                                         maxiter=main_steps, matrix_free=matrix_free, **lin))
+        elif "error" not in rec.get("init", {}):
+            agg = {"steps": 0, "lin_iters": 0, "lin_unconverged": 0, "lin_worst": 0.0, "seconds": 0.0, "history": [],
+                   "chunks": 0, "converged": False}
+            t_stage = time.perf_counter()
+            while agg["steps"] < main_steps:
+                hh = agg["history"]
+                res = None if len(hh) < 2 else (hh[0], hh[-1], hh[-2], agg["cfl"])
+                n = min(chunk, main_steps - agg["steps"])
+                st = stage(main, fa.ImplicitConfig(cflinit=cfl_main[0], cflfin=cfl_main[1], tol=tol, maxiter=n,
+                                                   matrix_free=matrix_free, resume=res, **lin))
+                agg["chunks"] += 1
+                agg["history"] = hh + st["history"]
+                for k in ("steps", "lin_iters", "lin_unconverged"):
+                    agg[k] += st.get(k, 0)
+                agg["lin_worst"] = max(agg["lin_worst"], st.get("lin_worst", 0.0))
+                agg["cfl"] = st.get("cfl", agg.get("cfl"))
+                if "error" in st:
+                    agg["error"] = st["error"]
+                    break
+                agg["resratio"] = agg["history"][-1] / agg["history"][0]
+                if heartbeat:
+                    heartbeat("main: %d steps, resratio %.3e, %.0f s" % (agg["steps"], agg["resratio"],
+                                                                         time.perf_counter() - t_stage))
+                if st["converged"]:
+                    agg["converged"] = True
+                    break
+                if deadline is not None and time.time() + 1.5*st["seconds"]*chunk/max(n, 1) > deadline:
+                    agg["stopped"] = "wall-clock deadline"
+                    break
+            agg["seconds"] = round(time.perf_counter() - t_stage, 2)
+            agg["ms_per_step"] = round(agg["seconds"]/max(agg["steps"], 1)*1e3, 2)
+            rec["main"] = agg
     finally:
         done.set()
     if "main" not in rec or "error" in rec["main"]:
@@ -134,6 +170,14 @@ def main():
     ap.add_argument("--sequence", type=int, nargs="+", default=None,
                     help="mesh sequencing: solve these scales in turn (coarsest first, the deck's schedule), each finer "
                          "one starting from the previous solution carried over (no first-order stage); the last is --scale")
+    ap.add_argument("--save-state", default=None, help="with --sequence: the last stage's converged state to this "
+                    ".npz (compressed, float64, the mesh's cell order)")
+    ap.add_argument("--load-state", default=None, help="with --sequence: start the first stage from this .npz "
+                    "(carried over to its mesh) instead of the deck's first-order stage")
+    ap.add_argument("--load-scale", type=int, default=None, help="the member (scale) the loaded state belongs to")
+    ap.add_argument("--chunk", type=int, default=0, help="run the main stage in resumed pieces of this many steps")
+    ap.add_argument("--deadline", type=float, default=None, help="seconds from start after which a chunked main "
+                    "stage stops (and its record is printed)")
     ap.add_argument("--tag", default="")
     args = ap.parse_args()
     import torch
@@ -142,13 +186,20 @@ def main():
         import fvens_amd as fa
         from bench import c4_mesh
         u0, prev, recs = None, None, []
+        if args.load_state:
+            z = np.load(args.load_state)
+            mz, _ = c4_mesh(fa, args.load_scale, 2, wall=args.wall, topology="cgrid" if args.quads else "hybrid")
+            prev = {"_state": z["u"], "_rc": np.asarray(mz.rc[:mz.nelem]).copy()}
+            assert prev["_state"].shape == (mz.nelem, 4), "the loaded state is not of that member"
+            del mz
         for sc in args.sequence:
             kw = dict(matrix_free=not args.assembled, main_steps=args.main_steps, init_steps=args.init_steps,
                       lin_maxit=args.lin_maxit, restart=args.restart, sweeps=args.sweeps,
                       heartbeat=lambda s: print(s, flush=True), cfl_init=args.cfl_init, cfl_main=args.cfl_main,
                       min_relax=args.min_relax, lin_rtol=args.lin_rtol, wall=args.wall, mf_eps=args.mf_eps,
                       quads=args.quads, amg=args.amg, amg_sweeps=args.amg_sweeps, amg_coarse=args.amg_coarse,
-                      amg_thr=args.amg_thr, lines=not args.no_lines)
+                      amg_thr=args.amg_thr, lines=not args.no_lines, chunk=args.chunk,
+                      deadline=None if args.deadline is None else T0 + args.deadline)
             if prev is not None:
                 m, _ = c4_mesh(fa, sc, 2, wall=args.wall, topology="cgrid" if args.quads else "hybrid")
                 u0 = carry_over(prev["_rc"], prev["_state"], np.asarray(m.rc[:m.nelem]))
@@ -160,6 +211,9 @@ def main():
             print(json.dumps(out), flush=True)
             if not r.get("main", {}).get("converged"):
                 break
+        if args.save_state and prev is not None and "_state" in prev:
+            np.savez_compressed(args.save_state, u=prev["_state"])
+            print(json.dumps({"saved": args.save_state, "bytes": os.path.getsize(args.save_state)}), flush=True)
         return
     r = run(args.scale, not args.assembled, args.main_steps, init_steps=args.init_steps, lin_maxit=args.lin_maxit, restart=args.restart,
             sweeps=args.sweeps, heartbeat=lambda s: print(s, flush=True), cfl_init=args.cfl_init,
