@@ -91,6 +91,7 @@ class ImplicitConfig:
     amg_sweeps: int = 2             # smoothing sweeps per level (-mg_levels_ksp_max_it)
     amg_coarse_sweeps: int = 6      # Gauss-Seidel sweeps on the coarsest level (-mg_coarse_ksp_max_it)
     amg_threshold: float = 0.2      # aggregation strength threshold (-pc_gamg_threshold)
+    amg_fine_sweeps: int = 0        # finest-level smoothing sweeps (0: amg_sweeps)
     resume: tuple = None            # continue a checkpointed solve: (first residual, last, the one before, last CFL)
 
     def _struct(self):
@@ -107,6 +108,7 @@ class ImplicitConfig:
         c.cgs_refine = int(self.cgs_refine)
         c.prec_amg, c.amg_sweeps, c.amg_coarse_sweeps = int(self.prec_amg), int(self.amg_sweeps), int(self.amg_coarse_sweeps)
         c.amg_threshold = float(self.amg_threshold)
+        c.amg_fine_sweeps = int(self.amg_fine_sweeps)
         if self.resume is not None:
             c.resume_res0, c.resume_res, c.resume_res_prev, c.resume_cfl = (float(x) for x in self.resume)
         return c

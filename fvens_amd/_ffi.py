@@ -42,7 +42,7 @@ class FvImplicitConfig(ctypes.Structure):
                 ("prec_single", ctypes.c_int), ("prec_gs", ctypes.c_int), ("prec_lines", ctypes.c_int),
                 ("line_threshold", ctypes.c_double), ("prec_ilu", ctypes.c_int), ("cgs_refine", ctypes.c_int),
                 ("prec_amg", ctypes.c_int), ("amg_sweeps", ctypes.c_int), ("amg_coarse_sweeps", ctypes.c_int),
-                ("amg_threshold", ctypes.c_double), ("resume_res0", ctypes.c_double), ("resume_res", ctypes.c_double),
+                ("amg_threshold", ctypes.c_double), ("amg_fine_sweeps", ctypes.c_int), ("resume_res0", ctypes.c_double), ("resume_res", ctypes.c_double),
                 ("resume_res_prev", ctypes.c_double), ("resume_cfl", ctypes.c_double)]
 
 

@@ -128,7 +128,7 @@ struct LinOp
 	double line_thr = 0.0;
 	int sweeps = 1;
 	int amg = 0;                              ///< aggregation multigrid levels (0: one-level preconditioner)
-	int amg_sweeps = 2, amg_coarse = 6;
+	int amg_sweeps = 2, amg_coarse = 6, amg_fine = 2;
 	double amg_thr = 0.2;
 	std::vector<const double*> D, Lo, Up;     ///< per handle: diagonal / lower / upper blocks
 
@@ -259,8 +259,10 @@ struct LinOp
 	}
 	/// t = v - A z (A with the ghost coupling)
 	void residual0(const ArrayOf& v, const ArrayOf& z, const ArrayOf& t) {
-		blocks(z, t);
-		S.each([&](size_t i, fvhip_ctx* h) { launch_axpby(4LL*h->L.ncell, 1.0, v(i), -1.0, t(i), h->stream); });
+		S.exchange(z, 4);
+		S.each([&](size_t i, fvhip_ctx* h) {
+			h->timed("k_block_residual", [&]{ launch_block_residual(h->J, D[i], Lo[i], Up[i], z(i), v(i), t(i), h->stream); });
+		});
 	}
 	/// coarse level l of handle h's hierarchy: V-cycle on A_l x_l = b_l from x_l = 0 (colour Gauss-Seidel
 	/// forward before the coarse correction, backward after it; the coarsest level amg_coarse sweeps)
@@ -297,7 +299,7 @@ struct LinOp
 			residual0(v, z, t);
 			S.each([&](size_t i, fvhip_ctx* h) { smooth0(h, i, t(i), aux(i)); launch_add_rows(h->L.ncell, aux(i), z(i), h->stream); });
 		};
-		for(int k = 1; k < amg_sweeps; k++) correct();
+		for(int k = 1; k < amg_fine; k++) correct();
 		residual0(v, z, t);
 		S.each([&](size_t i, fvhip_ctx* h) {
 			h->timed("k_amg_cycle", [&]{
@@ -306,7 +308,7 @@ struct LinOp
 				launch_amg_prolong(h->amg[0], h->amg[0].x, z(i), h->stream);
 			});
 		});
-		for(int k = 0; k < amg_sweeps; k++) correct();
+		for(int k = 0; k < amg_fine; k++) correct();
 	}
 	/// block inverses of the current diagonal blocks (or the line factorisation)
 	void setup() {
@@ -507,7 +509,7 @@ static void checkImplicit(const fvhip_implicit_config& c)
 	if(c.cgs_refine < 0 || c.cgs_refine > 2) throw std::invalid_argument("cgs_refine must be 0 (never), 1 (ifneeded) or 2 (always)");
 	if(c.prec_sweeps < 1) throw std::invalid_argument("prec_sweeps must be >= 1");
 	if(c.prec_amg != 0 && c.prec_amg < 2) throw std::invalid_argument("prec_amg must be 0 (off) or >= 2 levels");
-	if(c.amg_sweeps < 0 || c.amg_coarse_sweeps < 0 || !(c.amg_threshold >= 0.0 && c.amg_threshold < 1.0))
+	if(c.amg_sweeps < 0 || c.amg_coarse_sweeps < 0 || c.amg_fine_sweeps < 0 || !(c.amg_threshold >= 0.0 && c.amg_threshold < 1.0))
 		throw std::invalid_argument("amg_sweeps / amg_coarse_sweeps must be >= 0 and amg_threshold in [0, 1)");
 	if(!(c.min_relax > 0.0)) throw std::domain_error("Minimum relaxation factor is invalid!");  // nonlinearrelaxation.cpp:20-21
 	if(c.matrix_free && !(c.mf_eps > 0.0)) throw std::invalid_argument("matrix-free difference step must be positive");
@@ -535,6 +537,7 @@ static void backwardEuler(System& S, const std::vector<double*>& us, const fvhip
 	A.amg = c.prec_amg;
 	A.amg_sweeps = c.amg_sweeps > 0 ? c.amg_sweeps : 2;
 	A.amg_coarse = c.amg_coarse_sweeps > 0 ? c.amg_coarse_sweeps : 6;
+	A.amg_fine = c.amg_fine_sweeps > 0 ? c.amg_fine_sweeps : A.amg_sweeps;
 	A.amg_thr = c.amg_threshold > 0.0 ? c.amg_threshold : 0.2;
 	if(A.amg && (A.gs || A.ilu || A.single || A.sweeps != 1))
 		throw std::invalid_argument("prec_amg combines with prec_lines only (prec_gs / prec_ilu / prec_single / prec_sweeps > 1 are one-level options)");

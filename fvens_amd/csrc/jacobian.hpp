@@ -36,6 +36,9 @@ void launch_jac_diag(const JacMesh& J, const double* bblk, const double* lower, 
 void launch_pseudo_time(int ncell, const double* area, double cfl, double* dtm, double* diag, hipStream_t s);
 void launch_block_apply(const JacMesh& J, const double* diag, const double* lower, const double* upper,
                         const double* x, double* y, hipStream_t s);
+/// t = v - A x (A with the ghost coupling: x needs its ghost rows), one pass
+void launch_block_residual(const JacMesh& J, const double* diag, const double* lower, const double* upper,
+                           const double* x, const double* v, double* t, hipStream_t s);
 /// zout = D^-1 (v - (A - D) zin): one block-Jacobi sweep (dinv: inverted diagonal blocks)
 void launch_bjac_sweep(const JacMesh& J, const double* dinv, const double* lower, const double* upper,
                        const double* v, const double* zin, double* zout, hipStream_t s);

@@ -319,6 +319,8 @@ typedef struct fvhip_implicit_config {
 	int amg_coarse_sweeps;    /* Gauss-Seidel sweeps on the coarsest level (-mg_coarse_ksp_max_it; 0: the deck's 6) */
 	double amg_threshold;     /* two cells aggregate when their coupling (face length / centre distance) is at least
 	                             this fraction of both cells' strongest (-pc_gamg_threshold; 0: the deck's 0.2) */
+	int amg_fine_sweeps;      /* smoothing sweeps of the finest level before and after the coarse correction
+	                             (0: amg_sweeps); each costs a residual with the finest blocks and a line solve */
 	double resume_res0;       /* > 0: continue a solve stopped earlier (a checkpoint): its first residual norm, so
 	                             that the tolerance stays relative to it (the reference's initres, aodesolver.cpp:537) */
 	double resume_res;        /*   ... its last residual norm and the one before (the CFL ramp's ratio, :462) */
