@@ -756,12 +756,12 @@ def test_resumed_solve_matches_one_call():
     histories bit for bit, the same final CFL"""
     import torch
     m, _ = get_mesh("naca_small")
-    p = cases.physics("visc")
-    n = cases.numerics("ROE", "LEASTSQUARES", "NONE")
+    p = cases.physics("naca")
+    n = cases.numerics("ROE", "LEASTSQUARES", "VANALBADA")
     dev = fa.FlowFV(m, p, n)
-    u0 = torch.tensor(cases.state(m, p, 5)[dev.permutation()], device="cuda")
-    kw = dict(cflinit=50.0, cflfin=2000.0, tol=1e-12, lin_rtol=1e-2, lin_maxit=30, restart=30, prec_lines=True,
-              matrix_free=True)
+    u0 = torch.tensor(cases.state(m, p, 8)[dev.permutation()], device="cuda")
+    kw = dict(cflinit=5.0, cflfin=50.0, tol=1e-12, lin_rtol=1e-2, lin_maxit=40, restart=20, prec_sweeps=2,
+              min_relax=0.2, matrix_free=True)
     ua, ub = u0.clone(), u0.clone()
     torch.cuda.synchronize()
     sa, ha = dev.steady_backward_euler_device(ua.data_ptr(), fa.ImplicitConfig(maxiter=4, **kw))

@@ -176,6 +176,9 @@ def main():
     ap.add_argument("--load-state", default=None, help="with --sequence: start the first stage from this .npz "
                     "(carried over to its mesh) instead of the deck's first-order stage")
     ap.add_argument("--load-scale", type=int, default=None, help="the member (scale) the loaded state belongs to")
+    ap.add_argument("--final-lin-rtol", type=float, default=None, help="with --sequence: the last stage's linear tolerance")
+    ap.add_argument("--final-lin-maxit", type=int, default=None, help="with --sequence: the last stage's GMRES "
+                    "iteration cap and restart length")
     ap.add_argument("--chunk", type=int, default=0, help="run the main stage in resumed pieces of this many steps")
     ap.add_argument("--deadline", type=float, default=None, help="seconds from start after which a chunked main "
                     "stage stops (and its record is printed)")
@@ -201,6 +204,10 @@ def main():
                       quads=args.quads, amg=args.amg, amg_sweeps=args.amg_sweeps, amg_coarse=args.amg_coarse,
                       amg_thr=args.amg_thr, lines=not args.no_lines, amg_fine=args.amg_fine, chunk=args.chunk,
                       deadline=None if args.deadline is None else T0 + args.deadline)
+            if sc == args.sequence[-1] and args.final_lin_rtol:
+                kw["lin_rtol"] = args.final_lin_rtol
+            if sc == args.sequence[-1] and args.final_lin_maxit:
+                kw["lin_maxit"] = kw["restart"] = args.final_lin_maxit
             if prev is not None:
                 m, _ = c4_mesh(fa, sc, 2, wall=args.wall, topology="cgrid" if args.quads else "hybrid")
                 u0 = carry_over(prev["_rc"], prev["_state"], np.asarray(m.rc[:m.nelem]))
