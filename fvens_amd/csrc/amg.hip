@@ -116,18 +116,18 @@ void k_amg_gs(int cnt, const int* __restrict__ cells, const int* __restrict__ ro
 }
 
 /// one workgroup of 1024 threads: every sweep, every colour, 256 rows at a time (4 lanes a row), a barrier
-/// after each colour
+/// after each colour; the iterate lives in LDS for the whole call (the colour-to-colour chain waits on LDS,
+/// not on L2 round trips), read from / written back to x at the ends
 __global__ __launch_bounds__(1024)
 void k_amg_gs_block(int n, int ncol, const int* __restrict__ cstart, const int* __restrict__ cells,
                     const int* __restrict__ rowptr, const int* __restrict__ col, const int* __restrict__ dpos,
                     const double* __restrict__ val, const double* __restrict__ dinv, const double* __restrict__ b,
-                    double* x, int sweeps, int fwd, int alternate, int zero)
+                    double* xg, int sweeps, int fwd, int alternate, int zero)
 {
+	extern __shared__ __attribute__((aligned(16))) double x[];
 	const int t = static_cast<int>(threadIdx.x), i = t & 3;
-	if(zero) {
-		for(int k = t; k < 4*n; k += 1024) x[k] = 0.0;
-		__syncthreads();
-	}
+	for(int k = t; k < 4*n; k += 1024) x[k] = zero ? 0.0 : xg[k];
+	__syncthreads();
 	const double4* x4 = reinterpret_cast<const double4*>(x);
 	for(int sw = 0; sw < sweeps; sw++) {
 		const bool f = alternate ? (sw % 2 == 0) : (fwd != 0);
@@ -154,13 +154,14 @@ void k_amg_gs_block(int n, int ncol, const int* __restrict__ cstart, const int* 
 			__syncthreads();
 		}
 	}
+	for(int k = t; k < 4*n; k += 1024) xg[k] = x[k];
 }
 
 void launch_amg_gs_block(const AmgLevel& L, const double* b, double* x, int sweeps, bool fwd, bool alternate,
                          bool zero, hipStream_t s)
 {
 	if(L.n <= 0 || L.n > AMG_BLOCK_ROWS) return;
-	hipLaunchKernelGGL(k_amg_gs_block, dim3(1), dim3(1024), 0, s, L.n, static_cast<int>(L.cstart_colour.size()) - 1,
+	hipLaunchKernelGGL(k_amg_gs_block, dim3(1), dim3(1024), 32*static_cast<size_t>(L.n), s, L.n, static_cast<int>(L.cstart_colour.size()) - 1,
 	                   L.d_cstart_colour, L.cells, L.rowptr, L.col, L.dpos, L.val, L.dinv, b, x, sweeps, fwd ? 1 : 0,
 	                   alternate ? 1 : 0, zero ? 1 : 0);
 }

@@ -93,8 +93,8 @@ void launch_amg_gs_colour(const AmgLevel& L, int q, const double* b, double* x, 
 /// levels of at most AMG_BLOCK_ROWS rows: `sweeps` whole Gauss-Seidel sweeps (colours forward on even sweeps,
 /// backward on odd ones when `alternate`, else all in direction `fwd`) in one workgroup, a barrier between
 /// colours -- the same row updates in the same order as per-colour launches, without a launch per colour;
-/// zero: x = 0 first
-constexpr int AMG_BLOCK_ROWS = 4096;
+/// zero: x = 0 first. The iterate is held in LDS (32 B a row: 64 KB at the limit)
+constexpr int AMG_BLOCK_ROWS = 2048;
 void launch_amg_gs_block(const AmgLevel& L, const double* b, double* x, int sweeps, bool fwd, bool alternate,
                          bool zero, hipStream_t s);
 
