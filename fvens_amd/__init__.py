@@ -456,6 +456,29 @@ class FlowFV:
         check(_ffi.lib().fvhip_ilu_precondition_device(self._h, *[ctypes.c_void_p(p) for p in
                                                                   (d_diag, d_lower, d_upper, d_v, d_z)]))
 
+    def amg_precondition_device(self, d_diag, d_lower, d_upper, levels=5, threshold=0.2, sweeps=2, coarse_sweeps=10,
+                                line_threshold=0.0, d_v=None, d_z=None):
+        """the aggregation multigrid on the block operator (prec_amg): builds the hierarchy (once per handle) and
+        the Galerkin coarse operators, then z = M^-1 v by one V-cycle if d_v / d_z are given; returns the number
+        of coarse levels"""
+        nl = np.zeros(1, np.int32)
+        check(_ffi.lib().fvhip_amg_precondition_device(self._h, *[ctypes.c_void_p(p) for p in (d_diag, d_lower, d_upper)],
+                                                       int(levels), float(threshold), int(sweeps), int(coarse_sweeps),
+                                                       float(line_threshold), ctypes.c_void_p(d_v), ctypes.c_void_p(d_z),
+                                                       iptr(nl)))
+        return int(nl[0])
+
+    def amg_level(self, level):
+        """coarse level `level` (1 = first) of the multigrid hierarchy: dict(agg, rowptr, col, val[nnz][4][4])"""
+        n, nnz = np.zeros(1, np.int32), np.zeros(1, np.int32)
+        check(_ffi.lib().fvhip_amg_level(self._h, int(level), iptr(n), iptr(nnz), None, None, None, None))
+        nf = self.nown if level == 1 else self.amg_level(level - 1)["n"]
+        agg, rowptr = np.zeros(nf, np.int32), np.zeros(int(n[0]) + 1, np.int32)
+        col, val = np.zeros(int(nnz[0]), np.int32), np.zeros((int(nnz[0]), 4, 4))
+        check(_ffi.lib().fvhip_amg_level(self._h, int(level), iptr(n), iptr(nnz), iptr(agg), iptr(rowptr), iptr(col),
+                                         dptr(val)))
+        return dict(n=int(n[0]), agg=agg, rowptr=rowptr, col=col, val=val)
+
     def colouring(self):
         """(colour per owned cell in internal order, number of pairwise-adjacent cell triples)"""
         nc = np.zeros(1, np.int32)

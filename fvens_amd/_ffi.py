@@ -124,6 +124,10 @@ _SIGS = {
     "fvhip_lines": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_double, c_int_p, c_int_p, c_int_p, c_int_p]),
     "fvhip_find_lines": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_double, c_int_p, c_int_p, c_int_p, c_int_p]),
     "fvhip_ilu_precondition_device": (ctypes.c_int, [ctypes.c_void_p] * 6),
+    "fvhip_amg_precondition_device": (ctypes.c_int, [ctypes.c_void_p] * 4 + [ctypes.c_int, ctypes.c_double, ctypes.c_int,
+                                                                         ctypes.c_int, ctypes.c_double, ctypes.c_void_p,
+                                                                         ctypes.c_void_p, ctypes.c_void_p]),
+    "fvhip_amg_level": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int] + [ctypes.c_void_p] * 6),
     "fvhip_colouring": (ctypes.c_int, [ctypes.c_void_p, c_int_p, c_int_p, ctypes.POINTER(ctypes.c_longlong)]),
     "fvhip_group_matfree_set_state_device": (ctypes.c_int, [ctypes.c_void_p, _vpp, _vpp, _vpp]),
     "fvhip_group_matfree_apply_device": (ctypes.c_int, [ctypes.c_void_p, _vpp, _vpp]),

@@ -838,6 +838,50 @@ int fvhip_ilu_precondition_device(fvhip_handle h, const double* d_diag, const do
 	});
 }
 
+int fvhip_amg_precondition_device(fvhip_handle h, const double* d_diag, const double* d_lower, const double* d_upper,
+                                  int levels, double threshold, int sweeps, int coarse_sweeps, double line_threshold,
+                                  const double* d_v, double* d_z, int* nlevels)
+{
+	return guard([&] {
+		need(h, "handle");
+		need(d_diag, "diag"); if(h->L.ninface > 0) { need(d_lower, "lower"); need(d_upper, "upper"); }
+		if(levels < 2 || sweeps < 1 || coarse_sweeps < 1) throw std::invalid_argument("levels >= 2, sweeps >= 1, coarse_sweeps >= 1");
+		if((d_v == nullptr) != (d_z == nullptr)) throw std::invalid_argument("v and z go together");
+		System S = single(h);
+		h->ensureImplicit(1);
+		LinOp A{S};
+		A.amg = levels; A.amg_sweeps = A.amg_fine = sweeps; A.amg_coarse = coarse_sweeps; A.amg_thr = threshold;
+		A.lines = line_threshold > 0.0; A.line_thr = line_threshold;
+		A.D = {d_diag}; A.Lo = {d_lower}; A.Up = {d_upper};
+		A.setup();
+		if(d_v) {
+			// z needs ghost rows for the finest residuals: the handle's own operand buffer
+			A.precondition([&](size_t) { return const_cast<double*>(d_v); }, [&](size_t) { return h->iw.z; });
+			HC(hipMemcpyAsync(d_z, h->iw.z, 4*sizeof(double)*static_cast<size_t>(h->L.ncell), hipMemcpyDeviceToDevice, h->stream));
+		}
+		HC(hipGetLastError());
+		S.sync();
+		if(nlevels) *nlevels = static_cast<int>(h->amg.size());
+	});
+}
+
+int fvhip_amg_level(fvhip_handle h, int level, int* n, int* nnz, int* agg, int* rowptr, int* col, double* val)
+{
+	return guard([&] {
+		need(h, "handle");
+		if(level < 1 || level > static_cast<int>(h->amg.size())) throw std::invalid_argument("no such multigrid level");
+		const AmgLevel& L = h->amg[static_cast<size_t>(level) - 1];
+		HC(hipSetDevice(h->device));
+		HC(hipStreamSynchronize(h->stream));
+		if(n) *n = L.n;
+		if(nnz) *nnz = L.nnz;
+		if(agg) HC(hipMemcpy(agg, L.agg, sizeof(int)*static_cast<size_t>(L.nfine), hipMemcpyDeviceToHost));
+		if(rowptr) HC(hipMemcpy(rowptr, L.rowptr, sizeof(int)*(static_cast<size_t>(L.n) + 1), hipMemcpyDeviceToHost));
+		if(col) HC(hipMemcpy(col, L.col, sizeof(int)*static_cast<size_t>(L.nnz), hipMemcpyDeviceToHost));
+		if(val) HC(hipMemcpy(val, L.val, 16*sizeof(double)*static_cast<size_t>(L.nnz), hipMemcpyDeviceToHost));
+	});
+}
+
 int fvhip_colouring(fvhip_handle h, int* ncolours, int* colour, long long* triples)
 {
 	return guard([&] {

@@ -362,6 +362,18 @@ int fvhip_line_precondition_device(fvhip_handle h, const double* d_diag, const d
  *  operator in the colour order of fvhip_colouring, then z = M^-1 v (internal order, [ncell][4]) */
 int fvhip_ilu_precondition_device(fvhip_handle h, const double* d_diag, const double* d_lower, const double* d_upper,
                                   const double* d_v, double* d_z);
+/** The aggregation multigrid (fvhip_implicit_config::prec_amg) alone: builds the hierarchy of `levels` levels
+ *  with strength threshold `threshold` (once per handle), forms the coarse Galerkin operators of the block
+ *  operator (d_diag / d_lower / d_upper as in fvhip_gmres_blocks_device), then, if d_v and d_z are given,
+ *  z = M^-1 v by one V-cycle (the line-implicit finest smoother if line_threshold > 0, else point-block
+ *  Jacobi; `sweeps` per level, `coarse_sweeps` on the coarsest). *nlevels = coarse levels built. */
+int fvhip_amg_precondition_device(fvhip_handle h, const double* d_diag, const double* d_lower, const double* d_upper,
+                                  int levels, double threshold, int sweeps, int coarse_sweeps, double line_threshold,
+                                  const double* d_v, double* d_z, int* nlevels);
+/** Coarse level `level` (1 = the first coarse level) of the hierarchy built by the call above: *n rows, *nnz blocks;
+ *  then, where the arrays are not NULL, agg [rows of the finer level] (its aggregate), rowptr [n+1], col [nnz] and
+ *  val [nnz][16] (the Galerkin blocks, row-major). Rows of level 1 aggregate the internal (Hilbert) cell order. */
+int fvhip_amg_level(fvhip_handle h, int level, int* n, int* nnz, int* agg, int* rowptr, int* col, double* val);
 /** The colouring of the owned cells that prec_gs and prec_ilu use (greedy over interior faces in internal
  *  order): *ncolours, colour [ncell] (internal order; may be NULL), and *triples = the number of owned
  *  cells sharing faces pairwise three at a time (0: the colour-order D-ILU is exactly ILU(0)) */

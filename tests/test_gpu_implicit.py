@@ -772,3 +772,55 @@ def test_resumed_solve_matches_one_call():
     assert s2["cfl"] == sa["cfl"] and s2["resratio"] == sa["resratio"]
     assert torch.equal(ua, ub)
     dev.close()
+
+
+def test_amg_galerkin_operators_and_cycle():
+    """the aggregation multigrid (prec_amg, mgopts.solverc's GAMG): every cell in exactly one aggregate, each
+    level at least 1.25 times smaller; the device's coarse operators equal the Galerkin products P^T A P with
+    the tentative (piecewise-constant) prolongation, formed on the host by scipy from the same blocks (level 1
+    from the finest operator, level 2 from the device's level 1), to 1e-13 of their largest entry (the device
+    sums in a fixed ascending order, scipy in its own); one V-cycle is a fixed linear operator -- the same bits
+    on a second application, M^-1 (a v1 + v2) = a M^-1 v1 + M^-1 v2 to 1e-12"""
+    import torch
+    m, om = get_mesh("naca_small")
+    p = cases.physics("naca")
+    n = cases.numerics("ROE", "LEASTSQUARES", "VANALBADA")
+    u = cases.state(m, p, 4)
+    r, dtm, D, lo, up = pseudo_time_system(m, om, p, n, u, 20.0)
+    N, Fi = m.nelem, m.naface - m.nbface
+    dev = fa.FlowFV(m, p, n)
+    perm = dev.permutation()
+    dd, dl, dup = to_device(D.reshape(N, 16), perm), to_device(lo.reshape(Fi, 16)), to_device(up.reshape(Fi, 16))
+    nlev = dev.amg_precondition_device(dd.data_ptr(), dl.data_ptr(), dup.data_ptr(), levels=3, line_threshold=4.0)
+    assert nlev == 2
+    A = block_matrix(m, D, lo, up).tocsr()
+    iperm = np.argsort(perm)
+    Af = A[np.ravel(4 * perm[:, None] + np.arange(4))][:, np.ravel(4 * perm[:, None] + np.arange(4))]  # internal order
+    nf = N
+    for lev in (1, 2):
+        L = dev.amg_level(lev)
+        agg, nc = L["agg"], L["n"]
+        assert agg.shape == (nf,) and agg.min() == 0 and agg.max() == nc - 1
+        assert len(np.unique(agg)) == nc and nc * 5 <= nf * 4
+        P = sp.csr_matrix((np.ones(4 * nf), (np.arange(4 * nf), np.ravel(4 * agg[:, None] + np.arange(4)))),
+                          shape=(4 * nf, 4 * nc))
+        Ac = (P.T @ Af @ P).toarray()
+        rows = np.repeat(np.arange(nc), np.diff(L["rowptr"]))
+        Ad = np.zeros((4 * nc, 4 * nc))
+        for k in range(len(L["col"])):
+            Ad[4 * rows[k]:4 * rows[k] + 4, 4 * L["col"][k]:4 * L["col"][k] + 4] = L["val"][k]
+        assert np.abs(Ad - Ac).max() <= 1e-13 * np.abs(Ac).max(), (lev, np.abs(Ad - Ac).max())
+        Af = sp.csr_matrix(Ad)             # the next level is formed from the device's level
+        nf = nc
+    rng = np.random.default_rng(7)
+    v1, v2 = rng.standard_normal((N, 4)), rng.standard_normal((N, 4))
+    outs = []
+    for v in (v1, v2, 0.5 * v1 + v2, v1):
+        dv, dz = to_device(v), _torch().zeros((N, 4), dtype=_torch().float64, device="cuda")
+        dev.amg_precondition_device(dd.data_ptr(), dl.data_ptr(), dup.data_ptr(), levels=3, line_threshold=4.0,
+                                    d_v=dv.data_ptr(), d_z=dz.data_ptr())
+        outs.append(dz.cpu().numpy())
+    assert np.array_equal(outs[0], outs[3])
+    lin = 0.5 * outs[0] + outs[1]
+    assert np.abs(outs[2] - lin).max() <= 1e-12 * np.abs(lin).max()
+    dev.close()
