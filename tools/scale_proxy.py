@@ -46,7 +46,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--parts", type=int, nargs="+", default=[2, 4, 8])
     ap.add_argument("--rec", default="VANALBADA")
-    ap.add_argument("--config5", action="store_true", help="BASELINE config 5: the C5 quadrangle C-grid, laminar viscous")
+    ap.add_argument("--config5", action="store_true", help="BASELINE config 5: the hybrid C5 mesh, laminar viscous")
     ap.add_argument("--steps", type=int, default=200)
     ap.add_argument("--preheat", type=float, default=0.3, help="seconds of untimed residuals before each timing")
     ap.add_argument("--scale", type=int, default=1)
