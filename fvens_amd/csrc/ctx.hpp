@@ -133,6 +133,7 @@ struct fvhip_ctx
 		double *w = nullptr, *t = nullptr, *s = nullptr, *du = nullptr, *yg = nullptr;   ///< [4*ncell]
 		double *jd = nullptr, *jlo = nullptr, *jup = nullptr, *dinv = nullptr;            ///< 4x4 blocks
 		float *slo = nullptr, *sup = nullptr, *sdinv = nullptr;   ///< fp32 copies for the preconditioner
+		float* sdiag = nullptr;                     ///< fp32 diagonal blocks (the multigrid's finest residuals)
 		double *part = nullptr, *red = nullptr, *coef = nullptr, *pm = nullptr;           ///< reductions
 		double *h_red = nullptr, *h_coef = nullptr, *h_red2 = nullptr;                  ///< pinned host
 	} iw;
@@ -1053,6 +1054,7 @@ struct fvhip_ctx
 		iw.sdinv = reinterpret_cast<float*>(dalloc(8*N, owned));
 		iw.slo = reinterpret_cast<float*>(dalloc(8*Fi, owned));
 		iw.sup = reinterpret_cast<float*>(dalloc(8*Fi, owned));
+		iw.sdiag = reinterpret_cast<float*>(dalloc(8*N, owned));
 	}
 
 	/// MatrixFreeSpatialJacobian::apply on device vectors (internal order), single domain (the

@@ -255,13 +255,17 @@ struct LinOp
 	/// z = the finest smoother applied to v (line solve, else D^-1 v)
 	void smooth0(fvhip_ctx* h, size_t i, const double* v, double* z) {
 		if(lines) h->timed("k_line_solve", [&]{ launch_line_solve(h->lines, v, z, h->stream); });
+		else if(single) launch_bjac_apply(h->L.ncell, h->iw.sdinv, v, z, h->stream);
 		else launch_bjac_apply(h->L.ncell, h->iw.dinv, v, z, h->stream);
 	}
 	/// t = v - A z (A with the ghost coupling)
 	void residual0(const ArrayOf& v, const ArrayOf& z, const ArrayOf& t) {
 		S.exchange(z, 4);
 		S.each([&](size_t i, fvhip_ctx* h) {
-			h->timed("k_block_residual", [&]{ launch_block_residual(h->J, D[i], Lo[i], Up[i], z(i), v(i), t(i), h->stream); });
+			h->timed("k_block_residual", [&]{
+				if(single) launch_block_residual(h->J, h->iw.sdiag, h->iw.slo, h->iw.sup, z(i), v(i), t(i), h->stream);
+				else launch_block_residual(h->J, D[i], Lo[i], Up[i], z(i), v(i), t(i), h->stream);
+			});
 		});
 	}
 	/// coarse level l of handle h's hierarchy: V-cycle on A_l x_l = b_l from x_l = 0 (colour Gauss-Seidel
@@ -316,9 +320,19 @@ struct LinOp
 			S.each([&](size_t i, fvhip_ctx* h) {
 				if(lines) {
 					h->ensureLines(line_thr);
-					h->lines.single = false;
+					h->lines.single = single;
 					h->timed("k_line_factor", [&]{ launch_line_factor(h->lines, D[i], Lo[i], Up[i], h->stream); });
 				} else h->timed("k_bjac_invert", [&]{ launch_bjac_invert(h->L.ncell, D[i], h->iw.dinv, h->stream); });
+				if(single) {                  // fp32 copies of the finest operator for the smoother's residuals
+					h->ensureSinglePrecond();
+					const long long nf = 16LL*std::max(h->L.ninface, 0);
+					h->timed("k_to_single", [&]{
+						launch_to_single(16LL*h->L.ncell, D[i], h->iw.sdiag, h->stream);
+						launch_to_single(nf, Lo[i], h->iw.slo, h->stream);
+						launch_to_single(nf, Up[i], h->iw.sup, h->stream);
+						if(!lines) launch_to_single(16LL*h->L.ncell, h->iw.dinv, h->iw.sdinv, h->stream);
+					});
+				}
 				h->ensureAmg(amg, amg_thr);
 				h->amgSetup(D[i], Lo[i], Up[i]);
 			});
@@ -539,8 +553,8 @@ static void backwardEuler(System& S, const std::vector<double*>& us, const fvhip
 	A.amg_coarse = c.amg_coarse_sweeps > 0 ? c.amg_coarse_sweeps : 6;
 	A.amg_fine = c.amg_fine_sweeps > 0 ? c.amg_fine_sweeps : A.amg_sweeps;
 	A.amg_thr = c.amg_threshold > 0.0 ? c.amg_threshold : 0.2;
-	if(A.amg && (A.gs || A.ilu || A.single || A.sweeps != 1))
-		throw std::invalid_argument("prec_amg combines with prec_lines only (prec_gs / prec_ilu / prec_single / prec_sweeps > 1 are one-level options)");
+	if(A.amg && (A.gs || A.ilu || A.sweeps != 1))
+		throw std::invalid_argument("prec_amg combines with prec_lines and prec_single only (prec_gs / prec_ilu / prec_sweeps > 1 are one-level options)");
 	for(fvhip_ctx* h : S.hs) { A.D.push_back(h->iw.jd); A.Lo.push_back(h->iw.jlo); A.Up.push_back(h->iw.jup); }
 	std::vector<const double*> cu(us.begin(), us.end());
 	std::vector<double*> rs, dts;

@@ -412,37 +412,6 @@ void k_block_apply_rows(JacMesh J, const double* __restrict__ diag, const double
 	y[4*static_cast<size_t>(c) + i] = acc;
 }
 
-/// t = v - A x in one pass (the multigrid's finest residuals): k_block_apply_rows' row sum, subtracted from v
-__global__ __launch_bounds__(256)
-void k_block_residual_rows(JacMesh J, const double* __restrict__ diag, const double* __restrict__ lower,
-                           const double* __restrict__ upper, const double* __restrict__ x, const double* __restrict__ v,
-                           double* __restrict__ t)
-{
-	const long long g = static_cast<long long>(blockIdx.x)*blockDim.x + threadIdx.x;
-	const int c = static_cast<int>(g >> 2), i = static_cast<int>(g & 3);
-	if(c >= J.ncell) return;
-	const double4* x4 = reinterpret_cast<const double4*>(x);
-	const int4 fc = J.cell_rfaces[c];
-	const int4 nb = J.cell_nbr_fo[c];
-	const int codes[4] = {fc.x, fc.y, fc.z, fc.w};
-	const int nbrs[4] = {nb.x, nb.y, nb.z, nb.w};
-	double4 r = reinterpret_cast<const double4*>(diag + 16*static_cast<size_t>(c))[i];
-	double4 xv = x4[c];
-	double acc = r.x*xv.x + r.y*xv.y + r.z*xv.z + r.w*xv.w;
-#pragma unroll
-	for(int j = 0; j < 4; j++) {
-		const int code = codes[j];
-		if(code < 0) continue;
-		const int f = code >> 1;
-		if(f < J.nbface) continue;
-		const double* B = ((code & 1) ? lower : upper) + 16*static_cast<size_t>(f - J.nbface);
-		r = reinterpret_cast<const double4*>(B)[i];
-		xv = x4[nbrs[j]];
-		acc += r.x*xv.x + r.y*xv.y + r.z*xv.z + r.w*xv.w;
-	}
-	t[4*static_cast<size_t>(c) + i] = v[4*static_cast<size_t>(c) + i] - acc;
-}
-
 /// One block-Jacobi sweep fused into one pass: zout = D^-1 (v - sum_faces B zin[nbr]), the
 /// off-diagonal half of k_block_apply followed by the diagonal solve (zin needs its ghost rows).
 /// Same iterate as zin + D^-1 (v - A zin) up to rounding, without reading D or writing A zin.
@@ -490,6 +459,35 @@ __device__ __forceinline__ double blk_row_dot(const float* __restrict__ B, int i
 	return static_cast<double>(r.x)*x.x + static_cast<double>(r.y)*x.y + static_cast<double>(r.z)*x.z
 	     + static_cast<double>(r.w)*x.w;
 }
+/// t = v - A x in one pass (the multigrid's finest residuals): k_block_apply_rows' row sum, subtracted from v;
+/// T = float: the blocks stored in fp32 (prec_single: the preconditioner's copy), the arithmetic in fp64
+template <typename T>
+__global__ __launch_bounds__(256)
+void k_block_residual_rows(JacMesh J, const T* __restrict__ diag, const T* __restrict__ lower,
+                           const T* __restrict__ upper, const double* __restrict__ x, const double* __restrict__ v,
+                           double* __restrict__ t)
+{
+	const long long g = static_cast<long long>(blockIdx.x)*blockDim.x + threadIdx.x;
+	const int c = static_cast<int>(g >> 2), i = static_cast<int>(g & 3);
+	if(c >= J.ncell) return;
+	const double4* x4 = reinterpret_cast<const double4*>(x);
+	const int4 fc = J.cell_rfaces[c];
+	const int4 nb = J.cell_nbr_fo[c];
+	const int codes[4] = {fc.x, fc.y, fc.z, fc.w};
+	const int nbrs[4] = {nb.x, nb.y, nb.z, nb.w};
+	double acc = blk_row_dot(diag + 16*static_cast<size_t>(c), i, x4[c]);
+#pragma unroll
+	for(int j = 0; j < 4; j++) {
+		const int code = codes[j];
+		if(code < 0) continue;
+		const int f = code >> 1;
+		if(f < J.nbface) continue;
+		const T* B = ((code & 1) ? lower : upper) + 16*static_cast<size_t>(f - J.nbface);
+		acc += blk_row_dot(B, i, x4[nbrs[j]]);
+	}
+	t[4*static_cast<size_t>(c) + i] = v[4*static_cast<size_t>(c) + i] - acc;
+}
+
 /// k_bjac_sweep with four lanes per cell, lane i forming row i (coalesced block rows, as k_block_apply_rows):
 /// the same row sums in the same order, the four sums exchanged within the cell's lanes for the product
 /// with D^-1, so bitwise k_bjac_sweep's z
@@ -740,7 +738,14 @@ void launch_block_residual(const JacMesh& J, const double* diag, const double* l
                            const double* x, const double* v, double* t, hipStream_t s)
 {
 	if(J.ncell <= 0) return;
-	hipLaunchKernelGGL(k_block_residual_rows, dim3(nblk(4LL*J.ncell,256)), dim3(256), 0, s, J, diag, lower, upper, x, v, t);
+	hipLaunchKernelGGL(k_block_residual_rows<double>, dim3(nblk(4LL*J.ncell,256)), dim3(256), 0, s, J, diag, lower, upper, x, v, t);
+}
+
+void launch_block_residual(const JacMesh& J, const float* diag, const float* lower, const float* upper,
+                           const double* x, const double* v, double* t, hipStream_t s)
+{
+	if(J.ncell <= 0) return;
+	hipLaunchKernelGGL(k_block_residual_rows<float>, dim3(nblk(4LL*J.ncell,256)), dim3(256), 0, s, J, diag, lower, upper, x, v, t);
 }
 
 void launch_bjac_sweep(const JacMesh& J, const double* dinv, const double* lower, const double* upper,

@@ -39,6 +39,8 @@ void launch_block_apply(const JacMesh& J, const double* diag, const double* lowe
 /// t = v - A x (A with the ghost coupling: x needs its ghost rows), one pass
 void launch_block_residual(const JacMesh& J, const double* diag, const double* lower, const double* upper,
                            const double* x, const double* v, double* t, hipStream_t s);
+void launch_block_residual(const JacMesh& J, const float* diag, const float* lower, const float* upper,
+                           const double* x, const double* v, double* t, hipStream_t s);
 /// zout = D^-1 (v - (A - D) zin): one block-Jacobi sweep (dinv: inverted diagonal blocks)
 void launch_bjac_sweep(const JacMesh& J, const double* dinv, const double* lower, const double* upper,
                        const double* v, const double* zin, double* zout, hipStream_t s);

@@ -108,7 +108,9 @@ def test_gmres_blocks_matches_direct_solve():
     # PETSc's default Gram-Schmidt (one projection, the bench's and the drivers' default) and always-twice
     (1.0, False, False, True, False, 0, 0), (1.0, False, False, False, False, 0, 2),
     # aggregation multigrid (mgopts.solverc): line-implicit or point-block Jacobi finest smoother, 2 / 3 levels
-    (1.0, False, False, True, False, 3, 0), (1.0, False, False, False, False, 3, 1), (1.0, False, False, True, False, 2, 0)])
+    (1.0, False, False, True, False, 3, 0), (1.0, False, False, False, False, 3, 1), (1.0, False, False, True, False, 2, 0),
+    # ... with its finest smoother's factors and residual blocks in fp32 (prec_single)
+    (1.0, True, False, True, False, 3, 0), (1.0, True, False, False, False, 3, 1)])
 def test_one_backward_euler_step_matches_host(min_relax, single, gs, lines, ilu, amg, refine):
     """one implicit step against the host restatement (oracle residual and Jacobian, scipy's direct solve,
     the relaxed update) with every preconditioner and Gram-Schmidt variant: GMRES at rtol 1e-13 must land on

@@ -27,7 +27,7 @@ sys.path.insert(0, os.path.join(ROOT, "tests"))
 
 def run(scale=1, matrix_free=True, main_steps=400, init_steps=50, lin_maxit=60, restart=60, sweeps=3,
         tol=1e-6, heartbeat=None, cfl_init=(200.0, 1000.0), cfl_main=(500.0, 5000.0), min_relax=1.0, lin_rtol=1e-1,
-        wall=None, mf_eps=None, quads=False, amg=0, amg_sweeps=2, amg_coarse=6, amg_thr=0.2, lines=True, amg_fine=0,
+        wall=None, mf_eps=None, quads=False, amg=0, amg_sweeps=2, amg_coarse=6, amg_thr=0.2, lines=True, amg_fine=0, single=False,
         u0=None, want_state=False, chunk=0, deadline=None):
     """the deck's two stages on the C5 mesh divided by `scale` in both directions; returns the record (a stage
     that diverges is recorded with its history and the error; the later stage is then skipped). u0: a start
@@ -55,7 +55,7 @@ def run(scale=1, matrix_free=True, main_steps=400, init_steps=50, lin_maxit=60, 
     torch.cuda.synchronize()      # torch's stream vs the library's (non-blocking) streams
     lin = dict(lin_rtol=lin_rtol, lin_maxit=lin_maxit, restart=restart, prec_lines=lines, prec_sweeps=sweeps,
                min_relax=min_relax, prec_amg=amg, amg_sweeps=amg_sweeps, amg_coarse_sweeps=amg_coarse,
-               amg_threshold=amg_thr, amg_fine_sweeps=amg_fine)
+               amg_threshold=amg_thr, amg_fine_sweeps=amg_fine, prec_single=single)
     rec = {"library": fa._ffi.build_info()["lib_src_hash"], "cells": mesh.nelem, "faces": mesh.naface, "dims": dims, "operator": "matrix-free" if matrix_free else "assembled",
            "linear": dict(lin, gmres="GMRES(%d) right-preconditioned" % restart), "cfl_init": list(cfl_init),
            "cfl_main": list(cfl_main)}
@@ -167,6 +167,7 @@ def main():
     ap.add_argument("--amg-coarse", type=int, default=6)
     ap.add_argument("--amg-thr", type=float, default=0.2)
     ap.add_argument("--amg-fine", type=int, default=0, help="finest-level sweeps (0: --amg-sweeps)")
+    ap.add_argument("--single", action="store_true", help="preconditioner blocks / line factors in fp32 (prec_single)")
     ap.add_argument("--no-lines", action="store_true", help="point-block Jacobi instead of the line-implicit preconditioner")
     ap.add_argument("--sequence", type=int, nargs="+", default=None,
                     help="mesh sequencing: solve these scales in turn (coarsest first, the deck's schedule), each finer "
@@ -204,7 +205,8 @@ def main():
                       heartbeat=lambda s: print(s, flush=True), cfl_init=args.cfl_init, cfl_main=args.cfl_main,
                       min_relax=args.min_relax, lin_rtol=args.lin_rtol, wall=args.wall, mf_eps=args.mf_eps,
                       quads=args.quads, amg=args.amg, amg_sweeps=args.amg_sweeps, amg_coarse=args.amg_coarse,
-                      amg_thr=args.amg_thr, lines=not args.no_lines, amg_fine=args.amg_fine, chunk=args.chunk,
+                      amg_thr=args.amg_thr, lines=not args.no_lines, amg_fine=args.amg_fine, single=args.single,
+                      chunk=args.chunk,
                       deadline=None if args.deadline is None else T0 + args.deadline)
             if sc == args.sequence[-1] and args.final_lin_rtol:
                 kw["lin_rtol"] = args.final_lin_rtol
@@ -231,7 +233,7 @@ def main():
             sweeps=args.sweeps, heartbeat=lambda s: print(s, flush=True), cfl_init=args.cfl_init,
             cfl_main=args.cfl_main, min_relax=args.min_relax, lin_rtol=args.lin_rtol, wall=args.wall, mf_eps=args.mf_eps, quads=args.quads,
             amg=args.amg, amg_sweeps=args.amg_sweeps, amg_coarse=args.amg_coarse, amg_thr=args.amg_thr,
-            lines=not args.no_lines, amg_fine=args.amg_fine, chunk=args.chunk,
+            lines=not args.no_lines, amg_fine=args.amg_fine, single=args.single, chunk=args.chunk,
             deadline=None if args.deadline is None else T0 + args.deadline)
     r["tag"] = args.tag
     print(json.dumps(r), flush=True)
