@@ -199,6 +199,13 @@ class UMesh:
         check(_ffi.lib().fvmesh_generate(2, nx, ny, 0, xlead, height, wallspacing, ctypes.byref(h)))
         return cls(h.value)
 
+    def amg_aggregates(self, threshold=0.2):
+        """the aggregation multigrid's first coarsening on this mesh's cell order (host only): (aggregates, agg per cell)"""
+        n = np.zeros(1, np.int32)
+        agg = np.zeros(self.nelem, np.int32)
+        check(_ffi.lib().fvmesh_amg_aggregates(self._h, float(threshold), iptr(n), iptr(agg)))
+        return int(n[0]), agg
+
     @staticmethod
     def partition_trivial(nelem, nranks):
         """TrivialReplicatedGlobalMeshPartitioner::compute_partition (meshpartitioning.cpp:354-367)"""

@@ -158,6 +158,7 @@ _SIGS = {
     "fvmesh_generate_hybrid": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
                                               ctypes.c_double, ctypes.c_double, ctypes.POINTER(ctypes.c_void_p)]),
     "fvmesh_write_gmsh": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_char_p]),
+    "fvmesh_amg_aggregates": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_double, ctypes.c_void_p, ctypes.c_void_p]),
     "fvmesh_destroy": (ctypes.c_int, [ctypes.c_void_p]),
     "fvmesh_view": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(FvMeshView)]),
     "fvmesh_partition_trivial": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, c_int_p]),

@@ -951,6 +951,38 @@ int fvmesh_generate_hybrid(int nsurf, int nwake, int nquad, int nrows, double rf
 	});
 }
 
+int fvmesh_amg_aggregates(fvmesh_handle m, double threshold, int* nagg, int* agg)
+{
+	return guard([&] {
+		if(!m || !nagg) throw std::invalid_argument("null argument");
+		if(!(threshold >= 0.0 && threshold < 1.0)) throw std::invalid_argument("threshold must be in [0, 1)");
+		const Mesh& M = m->mesh;
+		const int N = M.md.nelem, nb = M.md.nbface;
+		// the cell graph over interior faces, columns ascending (ctx.hpp ensureAmg's graph in this cell order)
+		std::vector<std::vector<std::pair<int,double>>> adj(static_cast<size_t>(N));
+		for(int f = nb; f < M.naface - M.nconnface; f++) {
+			const int L = M.intfac[4*static_cast<size_t>(f)], R = M.intfac[4*static_cast<size_t>(f)+1];
+			if(R >= N) continue;
+			const double dx = M.rc[2*static_cast<size_t>(L)] - M.rc[2*static_cast<size_t>(R)];
+			const double dy = M.rc[2*static_cast<size_t>(L)+1] - M.rc[2*static_cast<size_t>(R)+1];
+			const double w = M.facemetric[3*static_cast<size_t>(f)+2]/std::sqrt(dx*dx + dy*dy);
+			adj[L].push_back({R, w}); adj[R].push_back({L, w});
+		}
+		AmgGraph g;
+		g.n = N;
+		g.rowptr.assign(static_cast<size_t>(N) + 1, 0);
+		for(int c = 0; c < N; c++) {
+			std::sort(adj[c].begin(), adj[c].end());
+			g.dblk.push_back(c);
+			for(const auto& e : adj[c]) { g.col.push_back(e.first); g.w.push_back(e.second); g.blk.push_back(0); }
+			g.rowptr[c+1] = static_cast<int>(g.col.size());
+		}
+		const AmgLevelHost H = amgCoarsen(g, threshold);
+		*nagg = H.n;
+		if(agg) std::copy(H.agg.begin(), H.agg.end(), agg);
+	});
+}
+
 int fvmesh_write_gmsh(fvmesh_handle m, const char* path) { return guard([&] { writeGmsh2(m->raw, path); }); }
 int fvmesh_destroy(fvmesh_handle m) { return guard([&] { delete m; }); }
 

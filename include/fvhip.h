@@ -462,6 +462,11 @@ int fvmesh_generate_hybrid(int nsurf, int nwake, int nquad, int nrows, double rf
                            double wallspacing, fvmesh_handle* out);
 int fvmesh_write_gmsh(fvmesh_handle m, const char* path);
 int fvmesh_destroy(fvmesh_handle m);
+/** The aggregation multigrid's first coarsening (fvhip_implicit_config::prec_amg) on the mesh's own cell order
+ *  (host only): cells aggregate along couplings face length / centre distance of at least `threshold` of both
+ *  cells' strongest. *nagg = aggregates, agg [nelem] = each cell's aggregate (may be NULL). The device builds the
+ *  same hierarchy over its internal (Hilbert) cell order. */
+int fvmesh_amg_aggregates(fvmesh_handle m, double threshold, int* nagg, int* agg);
 /** TrivialReplicatedGlobalMeshPartitioner::compute_partition (meshpartitioning.cpp:354-367): cell i
  *  goes to rank i/(nelem/nranks), the remainder to the last rank */
 int fvmesh_partition_trivial(int nelem, int nranks, int* elemdist);
