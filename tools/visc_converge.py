@@ -28,14 +28,19 @@ sys.path.insert(0, os.path.join(ROOT, "tests"))
 def run(scale=1, matrix_free=True, main_steps=400, init_steps=50, lin_maxit=60, restart=60, sweeps=3,
         tol=1e-6, heartbeat=None, cfl_init=(200.0, 1000.0), cfl_main=(500.0, 5000.0), min_relax=1.0, lin_rtol=1e-1,
         wall=None, mf_eps=None, quads=False, amg=0, amg_sweeps=2, amg_coarse=6, amg_thr=0.2, lines=True, amg_fine=0, single=False,
-        u0=None, want_state=False, chunk=0, deadline=None):
+        u0=None, want_state=False, chunk=0, deadline=None, symmetrize=False):
     """the deck's two stages on the C5 mesh divided by `scale` in both directions; returns the record (a stage
     that diverges is recorded with its history and the error; the later stage is then skipped). u0: a start
     state in the mesh's cell order (mesh sequencing: a coarser member's solution carried over) -- the main
     stage then starts from it, without the first-order stage; want_state: the final state (cell order) and
     the cell centres go into rec["_state"], rec["_rc"]. chunk > 0: the main stage runs in pieces of `chunk`
     steps, each a fresh call resumed from the last one's residuals and CFL (fvhip_implicit_config resume_*: the
-    same iterates as one call), so that it can stop at the wall-clock `deadline` (time.time()) with its record"""
+    same iterates as one call), so that it can stop at the wall-clock `deadline` (time.time()) with its record.
+    symmetrize (with chunk > 0): between chunks the state is projected onto the mirror-symmetric states of the
+    (exactly mirrored) hybrid mesh, u <- (u + S u)/2 with S the reflection y -> -y (rho v negated); the deck's
+    flow is at alpha 0, so its steady state is symmetric, and the projection removes the antisymmetric mode that
+    the unprojected pseudo-time iteration grows at the full size. The record carries the
+    antisymmetric part's norm removed by each projection"""
     import torch
     import fvens_amd as fa
     import cases
@@ -52,6 +57,12 @@ def run(scale=1, matrix_free=True, main_steps=400, init_steps=50, lin_maxit=60, 
     if u0 is not None:
         init_steps = 0
     du = torch.tensor(ustart[perm], device="cuda")
+    if symmetrize:
+        mir = mirror_map(np.asarray(mesh.rc[:mesh.nelem]))
+        inv = np.empty_like(perm)
+        inv[perm] = np.arange(len(perm))
+        dmir = torch.tensor(inv[mir[perm]], device="cuda")     # device row of each device row's mirror cell
+        sgn = torch.tensor([1.0, 1.0, -1.0, 1.0], device="cuda", dtype=torch.float64)
     torch.cuda.synchronize()      # torch's stream vs the library's (non-blocking) streams
     lin = dict(lin_rtol=lin_rtol, lin_maxit=lin_maxit, restart=restart, prec_lines=lines, prec_sweeps=sweeps,
                min_relax=min_relax, prec_amg=amg, amg_sweeps=amg_sweeps, amg_coarse_sweeps=amg_coarse,
@@ -90,6 +101,8 @@ def run(scale=1, matrix_free=True, main_steps=400, init_steps=50, lin_maxit=60, 
         elif "error" not in rec.get("init", {}):
             agg = {"steps": 0, "lin_iters": 0, "lin_unconverged": 0, "lin_worst": 0.0, "seconds": 0.0, "history": [],
                    "chunks": 0, "converged": False}
+            if symmetrize:
+                agg["antisym_removed"] = []
             t_stage = time.perf_counter()
             while agg["steps"] < main_steps:
                 hh = agg["history"]
@@ -116,6 +129,11 @@ def run(scale=1, matrix_free=True, main_steps=400, init_steps=50, lin_maxit=60, 
                 if deadline is not None and time.time() + 1.5*st["seconds"]*chunk/max(n, 1) > deadline:
                     agg["stopped"] = "wall-clock deadline"
                     break
+                if symmetrize:
+                    us = du[dmir] * sgn
+                    agg["antisym_removed"].append(float((0.5*(du - us)).norm() / du.norm()))
+                    du.copy_(0.5*(du + us))
+                    torch.cuda.synchronize()
             agg["seconds"] = round(time.perf_counter() - t_stage, 2)
             agg["ms_per_step"] = round(agg["seconds"]/max(agg["steps"], 1)*1e3, 2)
             rec["main"] = agg
@@ -136,6 +154,17 @@ def run(scale=1, matrix_free=True, main_steps=400, init_steps=50, lin_maxit=60, 
     main.close()
     rec.update({"CL": cl, "CDp": cdp, "CDsf": cdsf, "finite": finite})
     return rec
+
+
+def mirror_map(rc):
+    """the mirror cell (y -> -y) of every cell of a mirror-symmetric mesh, by its centre; an involution
+    without fixed points, checked"""
+    from scipy.spatial import cKDTree
+    d, mir = cKDTree(rc).query(rc * np.array([1.0, -1.0]), workers=16)
+    scale = np.abs(rc).max()
+    assert d.max() <= 1e-12 * scale, "the mesh is not mirror-symmetric (%g)" % d.max()
+    assert (mir[mir] == np.arange(len(rc))).all() and (mir != np.arange(len(rc))).all()
+    return mir
 
 
 def carry_over(rc_from, u_from, rc_to):
@@ -185,6 +214,8 @@ def main():
     ap.add_argument("--chunk", type=int, default=0, help="run the main stage in resumed pieces of this many steps")
     ap.add_argument("--deadline", type=float, default=None, help="seconds from start after which a chunked main "
                     "stage stops (and its record is printed)")
+    ap.add_argument("--symmetrize", action="store_true", help="with --chunk: project the state onto the "
+                    "mirror-symmetric states between chunks (alpha 0)")
     ap.add_argument("--tag", default="")
     args = ap.parse_args()
     import torch
@@ -206,7 +237,7 @@ def main():
                       min_relax=args.min_relax, lin_rtol=args.lin_rtol, wall=args.wall, mf_eps=args.mf_eps,
                       quads=args.quads, amg=args.amg, amg_sweeps=args.amg_sweeps, amg_coarse=args.amg_coarse,
                       amg_thr=args.amg_thr, lines=not args.no_lines, amg_fine=args.amg_fine, single=args.single,
-                      chunk=args.chunk,
+                      chunk=args.chunk, symmetrize=args.symmetrize and sc == args.sequence[-1],
                       deadline=None if args.deadline is None else T0 + args.deadline)
             if sc == args.sequence[-1] and args.final_lin_rtol:
                 kw["lin_rtol"] = args.final_lin_rtol
@@ -234,7 +265,7 @@ def main():
             cfl_main=args.cfl_main, min_relax=args.min_relax, lin_rtol=args.lin_rtol, wall=args.wall, mf_eps=args.mf_eps, quads=args.quads,
             amg=args.amg, amg_sweeps=args.amg_sweeps, amg_coarse=args.amg_coarse, amg_thr=args.amg_thr,
             lines=not args.no_lines, amg_fine=args.amg_fine, single=args.single, chunk=args.chunk,
-            deadline=None if args.deadline is None else T0 + args.deadline)
+            symmetrize=args.symmetrize, deadline=None if args.deadline is None else T0 + args.deadline)
     r["tag"] = args.tag
     print(json.dumps(r), flush=True)
 
