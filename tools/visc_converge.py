@@ -211,6 +211,8 @@ def main():
                     "iteration cap and restart length")
     ap.add_argument("--final-cfl-main", type=float, nargs=2, default=None, help="with --sequence: the last stage's CFL "
                     "ramp (start, cap)")
+    ap.add_argument("--final-amg-sweeps", type=int, nargs=2, default=None, help="with --sequence: the last stage's "
+                    "multigrid sweeps per level and coarsest-level sweeps")
     ap.add_argument("--chunk", type=int, default=0, help="run the main stage in resumed pieces of this many steps")
     ap.add_argument("--deadline", type=float, default=None, help="seconds from start after which a chunked main "
                     "stage stops (and its record is printed)")
@@ -243,6 +245,8 @@ def main():
                 kw["lin_rtol"] = args.final_lin_rtol
             if sc == args.sequence[-1] and args.final_cfl_main:
                 kw["cfl_main"] = tuple(args.final_cfl_main)
+            if sc == args.sequence[-1] and args.final_amg_sweeps:
+                kw["amg_sweeps"], kw["amg_coarse"] = args.final_amg_sweeps
             if sc == args.sequence[-1] and args.final_lin_maxit:
                 kw["lin_maxit"] = kw["restart"] = args.final_lin_maxit
             if prev is not None:
