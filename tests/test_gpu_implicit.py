@@ -342,7 +342,11 @@ def _gather(u0, sps, dus, glob):
     return u
 
 
-def test_partitioned_backward_euler_matches_single():
+@pytest.mark.parametrize("refine", [0, 2])
+def test_partitioned_backward_euler_matches_single(refine):
+    """a 3-rank group (the multi-handle Gram-Schmidt path: the Hessenberg column summed across handles) against
+    one handle, with the one-projection classical Gram-Schmidt (cgs_refine 0, the default) and with the
+    always-refined one (2)"""
     m, _ = get_mesh("naca_small")
     p = cases.physics("naca")
     n = cases.numerics("ROE", "LEASTSQUARES", "VANALBADA")
@@ -352,7 +356,8 @@ def test_partitioned_backward_euler_matches_single():
     # one matrix-free step, three assembled ones
     for mf, nsteps in ((False, 3), (True, 1)):
         cfg = fa.ImplicitConfig(cflinit=10.0, cflfin=200.0, tol=0.0, maxiter=nsteps, matrix_free=mf, mf_eps=1e-6,
-                                lin_rtol=1e-4, lin_maxit=60, restart=20, prec_sweeps=2, min_relax=0.2)
+                                lin_rtol=1e-4, lin_maxit=60, restart=20, prec_sweeps=2, min_relax=0.2,
+                                cgs_refine=refine)
         one = fa.FlowFV(m, p, n)
         perm = one.permutation()
         dU = to_device(u0, perm)
