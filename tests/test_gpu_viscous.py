@@ -111,8 +111,10 @@ def test_c5_residual_mirror_equivariant():
 def test_symmetry_projection_between_chunks():
     """tools/visc_converge.py's chunked main stage with the symmetry projection (--symmetrize) on the 1/64-size
     hybrid C5 member: the first-order start and two resumed chunks of 25 main steps, projected after each; the
-    part removed is round-off-sized (the projection only holds off the antisymmetric mode) and
-    the final state is mirror-symmetric"""
+    part removed is small (the linear solves are inexact and the aggregation is not mirror-symmetric, so every
+    step's update carries an antisymmetric part of the order of its linear residual: measured 1.4e-6 and 8.1e-7 of
+    the state's norm here in the transient, 5-8e-12 a chunk near the full-size member's converged state) and the
+    final state is mirror-symmetric (the projection's two halves are the same sums, bitwise)"""
     sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tools"))
     from visc_converge import run, mirror_map
     r = run(scale=8, matrix_free=True, main_steps=50, lin_rtol=1e-2, amg=5, sweeps=1, amg_sweeps=2, amg_coarse=10,
@@ -120,10 +122,10 @@ def test_symmetry_projection_between_chunks():
     m = r["main"]
     print({k: m[k] for k in ("steps", "chunks", "resratio", "antisym_removed")})
     assert r["cells"] == 177252 and r["finite"] and m["steps"] == 50 and m["chunks"] == 2
-    assert len(m["antisym_removed"]) == 2 and max(m["antisym_removed"]) <= 1e-8, m["antisym_removed"]
+    assert len(m["antisym_removed"]) == 2 and max(m["antisym_removed"]) <= 1e-5, m["antisym_removed"]
     u, mir = r["_state"], mirror_map(r["_rc"])
     su = u[mir] * np.array([1.0, 1.0, -1.0, 1.0])
-    assert np.abs(u - su).max() <= 1e-14 * np.abs(u).max()
+    assert np.array_equal(u, su)
     assert m["resratio"] < 1.0 and abs(r["CL"]) <= 1e-10
 
 
