@@ -220,6 +220,8 @@ def main():
                     "mirror-symmetric states between chunks (alpha 0)")
     ap.add_argument("--tag", default="")
     args = ap.parse_args()
+    if args.symmetrize and args.chunk <= 0:
+        ap.error("--symmetrize projects between chunks: give --chunk")
     import torch
     torch.cuda.set_device(0)
     if args.sequence:
