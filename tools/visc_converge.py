@@ -45,6 +45,8 @@ def run(scale=1, matrix_free=True, main_steps=400, init_steps=50, lin_maxit=60, 
     import fvens_amd as fa
     import cases
     from bench import c4_mesh
+    if symmetrize and chunk <= 0:
+        raise ValueError("symmetrize projects between chunks: chunk must be > 0")
     mesh, dims = c4_mesh(fa, scale, 2, wall=wall, topology="cgrid" if quads else "hybrid")
     p = cases.physics("visc")                                   # alpha 0 (laminar-implicit.ctrl:19)
     n1 = cases.numerics("ROE", "NONE", "NONE", order2=False)
